@@ -1,0 +1,602 @@
+"""Python side of the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may import this
+module.  It is the parity checker: it never sits on the product path.
+
+It restates, independently of the product library, the host-side half of the reference path:
+
+* segment creation semantics for dictionary-encoded single-value columns: sorted unique
+  dictionary, dictIds by rank, ``bitsPerElement = getNumBitsPerValue(card - 1)``, sortedness
+  detection (SegmentColumnarIndexCreator.java:519-541, PinotDataBitSet.java:59-70);
+* literal -> dictId mapping of the dictionary-based predicate evaluators
+  (EqualsPredicateEvaluatorFactory.java:92-144, NotEqualsPredicateEvaluatorFactory,
+  InPredicateEvaluatorFactory.java:158-210, NotInPredicateEvaluatorFactory.java:158-210,
+  RangePredicateEvaluatorFactory.SortedDictionaryBasedRangePredicateEvaluator :119-232);
+* leaf operator choice and AND/OR simplification (FilterOperatorUtils.java:73-125,
+  FilterPlanNode.java:200-318) -- used for numEntriesScannedInFilter;
+* table-level value union for group keys (the reference merges on ``Key(Object[] values)``,
+  GroupByCombineOperator.java:169-178).
+
+The hot loops (fixed-bit read, scan, group-key generation, aggregation, combine) run in C
+(pinot_oracle.c) through ctypes.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def _load():
+    if not os.path.exists(_LIB_PATH):
+        build()
+    lib = ctypes.CDLL(_LIB_PATH)
+    lib.or_num_bits_per_value.argtypes = [ctypes.c_int32]
+    lib.or_num_bits_per_value.restype = ctypes.c_int
+    lib.or_fixed_bit_num_bytes.argtypes = [ctypes.c_int64, ctypes.c_int]
+    lib.or_fixed_bit_num_bytes.restype = ctypes.c_int64
+    lib.or_fixed_bit_write.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
+    lib.or_fixed_bit_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
+    lib.or_fixed_bit_read.restype = ctypes.c_int32
+    lib.or_fixed_bit_read_range.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int32,
+                                            ctypes.c_void_p]
+    lib.or_murmur_hash_long.argtypes = [ctypes.c_int64]
+    lib.or_murmur_hash_long.restype = ctypes.c_int32
+    lib.or_murmur_hash_bytes.argtypes = [ctypes.c_char_p, ctypes.c_int32, ctypes.c_int32]
+    lib.or_murmur_hash_bytes.restype = ctypes.c_int32
+    lib.or_hll_cardinality.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.or_hll_cardinality.restype = ctypes.c_int64
+    lib.or_execute.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
+    lib.or_execute.restype = ctypes.c_int
+    lib.or_result_free.argtypes = [ctypes.c_void_p]
+    return lib
+
+
+LIB = _load()
+
+
+class _Column(ctypes.Structure):
+    _fields_ = [("cardinality", ctypes.c_int32), ("bits", ctypes.c_int32), ("fwd", ctypes.c_void_p),
+                ("sorted", ctypes.c_void_p), ("values", ctypes.c_void_p), ("hash_longs", ctypes.c_void_p),
+                ("hash_ints", ctypes.c_void_p), ("global_ids", ctypes.c_void_p)]
+
+
+class _Segment(ctypes.Structure):
+    _fields_ = [("num_docs", ctypes.c_int32), ("num_columns", ctypes.c_int32),
+                ("columns", ctypes.POINTER(_Column))]
+
+
+class _FilterOp(ctypes.Structure):
+    _fields_ = [("op", ctypes.c_int32), ("arg", ctypes.c_int32), ("match", ctypes.c_void_p),
+                ("is_scan", ctypes.c_int32)]
+
+
+class _Query(ctypes.Structure):
+    _fields_ = [("num_filter_ops", ctypes.c_int32), ("filter", ctypes.POINTER(_FilterOp)),
+                ("num_group_by", ctypes.c_int32), ("group_cols", ctypes.c_void_p),
+                ("group_global_card", ctypes.c_void_p), ("num_aggs", ctypes.c_int32),
+                ("agg_fn", ctypes.c_void_p), ("agg_col", ctypes.c_void_p), ("log2m", ctypes.c_int32),
+                ("num_groups_limit", ctypes.c_int64)]
+
+
+class _Result(ctypes.Structure):
+    _fields_ = [("num_groups", ctypes.c_int64), ("keys", ctypes.POINTER(ctypes.c_uint64)),
+                ("aggs", ctypes.POINTER(ctypes.c_double)), ("hll", ctypes.POINTER(ctypes.c_uint8)),
+                ("num_hll", ctypes.c_int32), ("num_docs_scanned", ctypes.c_int64),
+                ("num_entries_scanned_in_filter", ctypes.c_int64),
+                ("num_entries_scanned_post_filter", ctypes.c_int64), ("num_total_docs", ctypes.c_int64),
+                ("num_groups_limit_reached", ctypes.c_int32)]
+
+
+OR_F_LEAF, OR_F_AND, OR_F_OR, OR_F_NOT, OR_F_ALL, OR_F_NONE = range(6)
+AGG_CODES = {"COUNT": 0, "SUM": 1, "MIN": 2, "MAX": 3, "DISTINCTCOUNTHLL": 4}
+
+
+# --------------------------------------------------------------------------- codec helpers
+def num_bits_per_value(max_value: int) -> int:
+    return LIB.or_num_bits_per_value(int(max_value))
+
+
+def fixed_bit_pack(values: np.ndarray, bits: int) -> np.ndarray:
+    values = np.ascontiguousarray(values, dtype=np.int32)
+    out = np.zeros(int(LIB.or_fixed_bit_num_bytes(len(values), bits)), dtype=np.uint8)
+    LIB.or_fixed_bit_write(values.ctypes.data, len(values), bits, out.ctypes.data)
+    return out
+
+
+def fixed_bit_unpack(buf: np.ndarray, n: int, bits: int, start: int = 0) -> np.ndarray:
+    # pad so the reader's look-ahead byte stays in bounds
+    b = np.concatenate([np.asarray(buf, dtype=np.uint8), np.zeros(8, np.uint8)])
+    out = np.empty(n, dtype=np.int32)
+    LIB.or_fixed_bit_read_range(b.ctypes.data, start, bits, n, out.ctypes.data)
+    return out
+
+
+def murmur_hash_long(v: int) -> int:
+    return LIB.or_murmur_hash_long(int(v))
+
+
+def murmur_hash_string(s: str) -> int:
+    b = s.encode("utf-8")
+    return LIB.or_murmur_hash_bytes(b, len(b), -1)
+
+
+# --------------------------------------------------------------------------- segments
+@dataclass
+class OracleColumn:
+    name: str
+    data_type: str               # INT | LONG | FLOAT | DOUBLE | STRING
+    dictionary: np.ndarray       # sorted unique values
+    bits: int
+    is_sorted: bool
+    has_inverted: bool = False
+    fwd: Optional[np.ndarray] = None      # packed big-endian fixed-bit bytes (unsorted)
+    sorted_ranges: Optional[np.ndarray] = None  # int32 [card, 2]
+
+    @property
+    def cardinality(self) -> int:
+        return len(self.dictionary)
+
+
+@dataclass
+class OracleSegment:
+    name: str
+    num_docs: int
+    columns: Dict[str, OracleColumn] = field(default_factory=dict)
+
+
+def _np_dtype(data_type):
+    return {"INT": np.int32, "LONG": np.int64, "FLOAT": np.float32, "DOUBLE": np.float64}.get(data_type)
+
+
+def build_column(name: str, values: np.ndarray, data_type: str, inverted: bool = False) -> OracleColumn:
+    if data_type == "STRING":
+        values = np.asarray(values).astype(str)
+    else:
+        values = np.asarray(values, dtype=_np_dtype(data_type))
+    dictionary, dict_ids = np.unique(values, return_inverse=True)
+    dict_ids = dict_ids.astype(np.int32).reshape(-1)
+    card = len(dictionary)
+    bits = num_bits_per_value(card - 1)
+    is_sorted = bool(len(dict_ids) == 0 or np.all(dict_ids[1:] >= dict_ids[:-1]))
+    col = OracleColumn(name, data_type, dictionary, bits, is_sorted, inverted)
+    if is_sorted:
+        starts = np.searchsorted(dict_ids, np.arange(card), side="left")
+        ends = np.searchsorted(dict_ids, np.arange(card), side="right") - 1
+        col.sorted_ranges = np.stack([starts, ends], axis=1).astype(np.int32)
+    else:
+        col.fwd = fixed_bit_pack(dict_ids, bits)
+    return col
+
+
+def build_segment(name: str, columns: Dict[str, tuple], inverted: Sequence[str] = ()) -> OracleSegment:
+    """columns: name -> (values, data_type)"""
+    n = None
+    seg = OracleSegment(name, 0)
+    for c, (vals, dt) in columns.items():
+        col = build_column(c, vals, dt, c in inverted)
+        seg.columns[c] = col
+        n = len(vals) if n is None else n
+        assert n == len(vals)
+    seg.num_docs = n or 0
+    return seg
+
+
+def segment_from_dict_ids(name: str, cols: Dict[str, tuple]) -> OracleSegment:
+    """Build from (dictionary, dict_ids or packed bytes, data_type, bits) -- used for synthetic bench data.
+    cols: name -> dict(dictionary=..., fwd=packed bytes, bits=..., data_type=..., num_docs=...)"""
+    seg = OracleSegment(name, 0)
+    for c, d in cols.items():
+        seg.columns[c] = OracleColumn(c, d["data_type"], d["dictionary"], d["bits"], False, False,
+                                      fwd=np.asarray(d["fwd"], dtype=np.uint8))
+        seg.num_docs = d["num_docs"]
+    return seg
+
+
+# --------------------------------------------------------------------------- predicate evaluation
+def _parse_literal(s: str, data_type: str):
+    if data_type in ("INT", "LONG"):
+        return int(s)
+    if data_type in ("FLOAT", "DOUBLE"):
+        return float(s) if data_type == "DOUBLE" else float(np.float32(float(s)))
+    return s
+
+
+def _index_of(d: np.ndarray, v) -> int:
+    i = int(np.searchsorted(d, v, side="left"))
+    return i if i < len(d) and d[i] == v else -1
+
+
+def _insertion_index_of(d: np.ndarray, v) -> int:
+    """BaseImmutableDictionary.insertionIndexOf: index if found, else -(insertionPoint) - 1."""
+    i = int(np.searchsorted(d, v, side="left"))
+    if i < len(d) and d[i] == v:
+        return i
+    return -(i + 1)
+
+
+def predicate_match(pred, col: OracleColumn):
+    """Returns (match bitset over dictIds as uint8, always_true, always_false)."""
+    d = col.dictionary
+    card = len(d)
+    m = np.zeros(card, dtype=np.uint8)
+    t = pred.TYPE
+    if t == "EQ":
+        i = _index_of(d, _parse_literal(pred.value, col.data_type))
+        if i < 0:
+            return m, False, True
+        m[i] = 1
+        return m, card == 1, False
+    if t == "NOT_EQ":
+        i = _index_of(d, _parse_literal(pred.value, col.data_type))
+        m[:] = 1
+        if i < 0:
+            return m, True, False
+        m[i] = 0
+        return m, False, card == 1
+    if t == "IN":
+        ids = {_index_of(d, _parse_literal(v, col.data_type)) for v in pred.values} - {-1}
+        for i in ids:
+            m[i] = 1
+        return m, len(ids) == card, len(ids) == 0
+    if t == "NOT_IN":
+        ids = {_index_of(d, _parse_literal(v, col.data_type)) for v in pred.values} - {-1}
+        m[:] = 1
+        for i in ids:
+            m[i] = 0
+        return m, len(ids) == 0, len(ids) == card
+    if t == "RANGE":
+        if pred.lower == "*":
+            start = 0
+        else:
+            ii = _insertion_index_of(d, _parse_literal(pred.lower, col.data_type))
+            start = -(ii + 1) if ii < 0 else (ii if pred.lower_inclusive else ii + 1)
+        if pred.upper == "*":
+            end = card
+        else:
+            ii = _insertion_index_of(d, _parse_literal(pred.upper, col.data_type))
+            end = -(ii + 1) if ii < 0 else (ii + 1 if pred.upper_inclusive else ii)
+        if end - start <= 0:
+            return m, False, True
+        m[start:end] = 1
+        return m, end - start == card, False
+    raise ValueError(t)
+
+
+class _Leaf:
+    def __init__(self, kind, col_index=None, match=None, is_scan=False):
+        self.kind = kind  # "leaf" | "all" | "none" | "and" | "or" | "not"
+        self.col_index = col_index
+        self.match = match
+        self.is_scan = is_scan
+        self.children = []
+
+
+def _plan_filter(f, seg: OracleSegment, col_index: Dict[str, int]):
+    """FilterPlanNode.constructPhysicalOperator simplification rules."""
+    if f.type == "PREDICATE":
+        p = f.predicate
+        col = seg.columns[p.column]
+        match, always_true, always_false = predicate_match(p, col)
+        if always_false:
+            return _Leaf("none")
+        if always_true:
+            return _Leaf("all")
+        # FilterOperatorUtils.DefaultImplementation.getLeafFilterOperator
+        if col.is_sorted:
+            is_scan = False
+        elif p.TYPE != "RANGE" and col.has_inverted:
+            is_scan = False
+        else:
+            is_scan = True
+        return _Leaf("leaf", col_index[p.column], match, is_scan)
+    if f.type == "AND":
+        kids = []
+        for c in f.children:
+            k = _plan_filter(c, seg, col_index)
+            if k.kind == "none":
+                return _Leaf("none")
+            if k.kind != "all":
+                kids.append(k)
+        if not kids:
+            return _Leaf("all")
+        if len(kids) == 1:
+            return kids[0]
+        n = _Leaf("and")
+        n.children = kids
+        return n
+    if f.type == "OR":
+        kids = []
+        for c in f.children:
+            k = _plan_filter(c, seg, col_index)
+            if k.kind == "all":
+                return _Leaf("all")
+            if k.kind != "none":
+                kids.append(k)
+        if not kids:
+            return _Leaf("none")
+        if len(kids) == 1:
+            return kids[0]
+        n = _Leaf("or")
+        n.children = kids
+        return n
+    if f.type == "NOT":
+        k = _plan_filter(f.children[0], seg, col_index)
+        if k.kind == "all":
+            return _Leaf("none")
+        if k.kind == "none":
+            return _Leaf("all")
+        n = _Leaf("not")
+        n.children = [k]
+        return n
+    raise ValueError(f.type)
+
+
+def _emit(node: _Leaf, out: list, keep: list):
+    if node.kind == "leaf":
+        keep.append(node.match)
+        out.append((OR_F_LEAF, node.col_index, node.match.ctypes.data, int(node.is_scan)))
+    elif node.kind == "all":
+        out.append((OR_F_ALL, 0, None, 0))
+    elif node.kind == "none":
+        out.append((OR_F_NONE, 0, None, 0))
+    else:
+        for c in node.children:
+            _emit(c, out, keep)
+        code = {"and": OR_F_AND, "or": OR_F_OR, "not": OR_F_NOT}[node.kind]
+        out.append((code, len(node.children), None, 0))
+
+
+# --------------------------------------------------------------------------- execution
+@dataclass
+class OracleStats:
+    num_docs_scanned: int
+    num_entries_scanned_in_filter: int
+    num_entries_scanned_post_filter: int
+    num_total_docs: int
+    num_groups_limit_reached: bool
+
+
+@dataclass
+class OracleResult:
+    keys: List[tuple]
+    aggs: List[list]
+    stats: OracleStats
+
+
+def _hash_arrays(col: OracleColumn):
+    if col.data_type in ("INT", "LONG"):
+        return col.dictionary.astype(np.int64), None
+    if col.data_type == "DOUBLE":
+        return col.dictionary.astype(np.float64).view(np.int64), None
+    if col.data_type == "STRING":
+        return None, np.array([murmur_hash_string(s) for s in col.dictionary], dtype=np.int32)
+    raise NotImplementedError("DISTINCTCOUNTHLL on FLOAT is not pinned")
+
+
+def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> OracleResult:
+    """Run a QueryContext over oracle segments; returns groups (value tuples) and intermediate
+    aggregation results, plus execution statistics."""
+    keep = []  # keep numpy buffers alive
+    used = list(dict.fromkeys(
+        list(q.group_by) + [a.column for a in q.aggregations if a.column] +
+        (q.filter.columns() if q.filter is not None else [])))
+    col_index = {c: i for i, c in enumerate(used)}
+
+    # table-level value unions for group-by columns
+    unions = []
+    for g in q.group_by:
+        unions.append(np.unique(np.concatenate([s.columns[g].dictionary for s in segments]))
+                      if segments else np.array([]))
+    log2m = next((a.log2m for a in q.aggregations if a.function == "DISTINCTCOUNTHLL"), 8)
+
+    seg_structs = (_Segment * max(1, len(segments)))()
+    filter_programs = []
+    for si, s in enumerate(segments):
+        cols = (_Column * len(used))()
+        keep.append(cols)
+        for c, ci in col_index.items():
+            oc = s.columns[c]
+            cs = cols[ci]
+            cs.cardinality = oc.cardinality
+            cs.bits = oc.bits
+            if oc.fwd is not None:
+                fwd = np.concatenate([oc.fwd, np.zeros(8, np.uint8)])
+                keep.append(fwd)
+                cs.fwd = fwd.ctypes.data
+            else:
+                sr = np.ascontiguousarray(oc.sorted_ranges, dtype=np.int32)
+                keep.append(sr)
+                cs.sorted = sr.ctypes.data
+            if oc.data_type != "STRING":
+                vals = oc.dictionary.astype(np.float64)
+                keep.append(vals)
+                cs.values = vals.ctypes.data
+            if any(a.column == c and a.function == "DISTINCTCOUNTHLL" for a in q.aggregations):
+                hl, hi = _hash_arrays(oc)
+                if hl is not None:
+                    keep.append(hl)
+                    cs.hash_longs = hl.ctypes.data
+                else:
+                    keep.append(hi)
+                    cs.hash_ints = hi.ctypes.data
+            if c in q.group_by:
+                gi = np.searchsorted(unions[q.group_by.index(c)], oc.dictionary).astype(np.int32)
+                keep.append(gi)
+                cs.global_ids = gi.ctypes.data
+        seg_structs[si].num_docs = s.num_docs
+        seg_structs[si].num_columns = len(used)
+        seg_structs[si].columns = cols
+        prog = []
+        if q.filter is not None:
+            _emit(_plan_filter(q.filter, s, col_index), prog, keep)
+        filter_programs.append(prog)
+
+    stats = [0, 0, 0, 0, False]
+    group_cols = np.array([col_index[g] for g in q.group_by], dtype=np.int32)
+    gcard = np.array([len(u) for u in unions], dtype=np.int64)
+    agg_fn = np.array([AGG_CODES[a.function] for a in q.aggregations], dtype=np.int32)
+    agg_col = np.array([col_index[a.column] if a.column else -1 for a in q.aggregations], dtype=np.int32)
+    nagg = len(q.aggregations)
+    m = 1 << log2m
+    hll_idx = [k for k, a in enumerate(q.aggregations) if a.function == "DISTINCTCOUNTHLL"]
+    merged_keys: Dict[int, int] = {}
+    merged: List[list] = []
+    key_list: List[int] = []
+    if True:
+        # one or_execute per segment: each segment has its own dictId-space filter program
+        for si in range(len(segments)):
+            prog = filter_programs[si]
+            ops = (_FilterOp * max(1, len(prog)))()
+            for i, (op, arg, ptr, scan) in enumerate(prog):
+                ops[i].op, ops[i].arg, ops[i].match, ops[i].is_scan = op, arg, ptr, scan
+            qs = _Query(len(prog), ops, len(q.group_by), group_cols.ctypes.data, gcard.ctypes.data, nagg,
+                        agg_fn.ctypes.data, agg_col.ctypes.data, log2m, q.num_groups_limit)
+            one = (_Segment * 1)(seg_structs[si])
+            res = _Result()
+            LIB.or_execute(ctypes.byref(qs), one, 1, 1, ctypes.byref(res))
+            _merge(res, q, merged_keys, merged, key_list, nagg, hll_idx, m)
+            stats[0] += res.num_docs_scanned
+            stats[1] += res.num_entries_scanned_in_filter
+            stats[2] += res.num_entries_scanned_post_filter
+            stats[3] += res.num_total_docs
+            stats[4] |= bool(res.num_groups_limit_reached)
+            LIB.or_result_free(ctypes.byref(res))
+    if not q.group_by and not merged:
+        merged.append(_default_row(q, m))
+        key_list.append(0)
+    keys = []
+    for gk in key_list:
+        vals = []
+        for gi, u in enumerate(unions):
+            card = len(u)
+            vals.append(_py(u[gk % card]))
+            gk //= card
+        keys.append(tuple(vals))
+    return OracleResult(keys, merged, OracleStats(*stats))
+
+
+def execute_timed(q, segments: Sequence[OracleSegment], num_threads: int):
+    """Single or_execute call over all segments with a pool of num_threads workers (the timed CPU
+    baseline).  All segments must share one filter plan shape (true for the bench workloads)."""
+    import time
+    keep = []
+    used = list(dict.fromkeys(
+        list(q.group_by) + [a.column for a in q.aggregations if a.column] +
+        (q.filter.columns() if q.filter is not None else [])))
+    col_index = {c: i for i, c in enumerate(used)}
+    unions = [np.unique(np.concatenate([s.columns[g].dictionary for s in segments])) for g in q.group_by]
+    seg_structs = (_Segment * len(segments))()
+    progs = []
+    for si, s in enumerate(segments):
+        cols = (_Column * len(used))()
+        keep.append(cols)
+        for c, ci in col_index.items():
+            oc = s.columns[c]
+            cs = cols[ci]
+            cs.cardinality, cs.bits = oc.cardinality, oc.bits
+            fwd = np.concatenate([oc.fwd, np.zeros(8, np.uint8)])
+            keep.append(fwd)
+            cs.fwd = fwd.ctypes.data
+            vals = oc.dictionary.astype(np.float64)
+            keep.append(vals)
+            cs.values = vals.ctypes.data
+            if c in q.group_by:
+                gi = np.searchsorted(unions[q.group_by.index(c)], oc.dictionary).astype(np.int32)
+                keep.append(gi)
+                cs.global_ids = gi.ctypes.data
+        seg_structs[si].num_docs, seg_structs[si].num_columns, seg_structs[si].columns = s.num_docs, len(used), cols
+        prog = []
+        if q.filter is not None:
+            _emit(_plan_filter(q.filter, s, col_index), prog, keep)
+        progs.append(prog)
+    prog = progs[0]
+    ops = (_FilterOp * max(1, len(prog)))()
+    for i, (op, arg, ptr, scan) in enumerate(prog):
+        ops[i].op, ops[i].arg, ops[i].match, ops[i].is_scan = op, arg, ptr, scan
+    group_cols = np.array([col_index[g] for g in q.group_by], dtype=np.int32)
+    gcard = np.array([len(u) for u in unions], dtype=np.int64)
+    agg_fn = np.array([AGG_CODES[a.function] for a in q.aggregations], dtype=np.int32)
+    agg_col = np.array([col_index[a.column] if a.column else -1 for a in q.aggregations], dtype=np.int32)
+    qs = _Query(len(prog), ops, len(q.group_by), group_cols.ctypes.data, gcard.ctypes.data,
+                len(q.aggregations), agg_fn.ctypes.data, agg_col.ctypes.data, 8, q.num_groups_limit)
+    res = _Result()
+    t0 = time.perf_counter()
+    LIB.or_execute(ctypes.byref(qs), seg_structs, len(segments), num_threads, ctypes.byref(res))
+    dt = time.perf_counter() - t0
+    n = res.num_groups
+    nagg = len(q.aggregations)
+    keys = np.ctypeslib.as_array(res.keys, (n,)).copy() if n else np.zeros(0, np.uint64)
+    aggs = np.ctypeslib.as_array(res.aggs, (n * max(nagg, 1),)).reshape(n, max(nagg, 1)).copy() if n else None
+    LIB.or_result_free(ctypes.byref(res))
+    return dt, keys, aggs
+
+
+def _py(v):
+    if isinstance(v, np.generic):
+        return v.item()
+    return v
+
+
+def _default_row(q, m):
+    row = []
+    for a in q.aggregations:
+        if a.function == "MIN":
+            row.append(float("inf"))
+        elif a.function == "MAX":
+            row.append(float("-inf"))
+        elif a.function == "DISTINCTCOUNTHLL":
+            row.append(np.zeros(1 << a.log2m, np.uint8))
+        elif a.function == "COUNT":
+            row.append(0)
+        else:
+            row.append(0.0)
+    return row
+
+
+def _merge(res, q, merged_keys, merged, key_list, nagg, hll_idx, m):
+    n = res.num_groups
+    if n == 0:
+        return
+    keys = np.ctypeslib.as_array(res.keys, (n,))
+    aggs = np.ctypeslib.as_array(res.aggs, (n * max(nagg, 1),)).reshape(n, max(nagg, 1))
+    hll = None
+    if hll_idx:
+        hll = np.ctypeslib.as_array(res.hll, (n * len(hll_idx) * m,)).reshape(n, len(hll_idx), m)
+    for g in range(n):
+        k = int(keys[g])
+        row = []
+        for j, a in enumerate(q.aggregations):
+            if a.function == "DISTINCTCOUNTHLL":
+                row.append(hll[g, hll_idx.index(j)].copy())
+            elif a.function == "COUNT":
+                row.append(int(aggs[g, j]))
+            else:
+                row.append(float(aggs[g, j]))
+        if k not in merged_keys:
+            merged_keys[k] = len(merged)
+            merged.append(row)
+            key_list.append(k)
+            continue
+        dst = merged[merged_keys[k]]
+        for j, a in enumerate(q.aggregations):
+            f = a.function
+            if f in ("COUNT", "SUM"):
+                dst[j] = dst[j] + row[j]
+            elif f == "MIN":
+                dst[j] = min(dst[j], row[j])
+            elif f == "MAX":
+                dst[j] = max(dst[j], row[j])
+            else:
+                dst[j] = np.maximum(dst[j], row[j])
