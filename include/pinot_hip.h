@@ -1,0 +1,199 @@
+/*
+ * pinot_hip.h -- C-ABI of libpinot_hip.so, the MI355X-native server-side segment execution path
+ * (filter -> aggregation / group-by on immutable, dictionary-encoded segments pinned in HBM).
+ *
+ * Plain C: POD structs, pointers and sizes, int status codes, no C++ or torch types.  Every entry
+ * point is thread-safe.  The Java binding (JNI for JDK 11/17/20, FFM for JDK >= 22) and the Python
+ * ctypes binding both bind exactly these symbols.
+ *
+ * Reference interfaces each entry point replaces (weixiangsun/pinot @ 1.1.0-SNAPSHOT):
+ *   ph_segment_pin / ph_segment_unpin
+ *       ImmutableSegmentLoader.load (pinot-segment-local/.../indexsegment/immutable/
+ *       ImmutableSegmentLoader.java:67-149) and ImmutableSegmentImpl.destroy (:249), hooked from
+ *       BaseTableDataManager.addSegment (pinot-core/.../data/manager/BaseTableDataManager.java:232).
+ *       The column buffers are the PinotDataBuffer slices of columns.psf
+ *       (SingleFileIndexDirectory.java:279-305): fixed-bit forward index, sorted index, dictionary,
+ *       bitmap inverted index, all big-endian exactly as on disk.
+ *   ph_query_execute
+ *       PlanMaker.makeInstancePlan(...).execute() (pinot-core/.../plan/maker/PlanMaker.java:37-67,
+ *       ServerQueryExecutorV1Impl.java:369-376) for the filter -> aggregation / group-by shapes:
+ *       FilterPlanNode.run (:83-114), AggregationPlanNode.run (:75), GroupByPlanNode.run (:57),
+ *       GroupByCombineOperator.mergeResults (:223-252).
+ *   ph_result_*
+ *       GroupByResultsBlock / AggregationResultsBlock contents (GroupByResultsBlock.java:62,86;
+ *       AggregationResultsBlock.java:50) and ExecutionStatistics (GroupByOperator.java:143-148).
+ *   ph_fixed_bit_pack
+ *       FixedBitSVForwardIndexWriter.putDictId (pinot-segment-local/.../io/writer/impl/
+ *       FixedBitSVForwardIndexWriter.java:39-50) -- the on-disk forward-index format.
+ *   ph_last_error
+ *       the message of the Java exception the caller raises (BadQueryRequestException for
+ *       PH_ERR_BAD_QUERY, PredicateEvaluatorProvider.java:92-95; RuntimeException otherwise, which
+ *       GroupByCombineOperator turns into an ExceptionResultsBlock, :236-239).
+ */
+#ifndef PINOT_HIP_H
+#define PINOT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ status codes */
+#define PH_OK 0
+#define PH_ERR_INVALID_ARGUMENT 1 /* caller bug (null pointer, bad size) */
+#define PH_ERR_BAD_QUERY 2        /* BadQueryRequestException: unknown column, unparsable literal */
+#define PH_ERR_UNSUPPORTED 3      /* shape not on the GPU path: caller falls back to the CPU plan */
+#define PH_ERR_DEVICE 4           /* HIP runtime / kernel error */
+#define PH_ERR_OUT_OF_MEMORY 5    /* HBM budget exhausted */
+
+/* ------------------------------------------------------------------ handles */
+typedef struct ph_ctx ph_ctx;         /* one per GPU; owns streams, scratch, pinned-segment registry */
+typedef struct ph_segment ph_segment; /* an immutable segment resident in HBM */
+typedef struct ph_result ph_result;   /* host-side result of one query */
+
+/* Stored data types of dictionary-encoded single-value columns (FieldSpec.DataType). */
+typedef enum { PH_INT = 0, PH_LONG = 1, PH_FLOAT = 2, PH_DOUBLE = 3, PH_STRING = 4 } ph_data_type;
+
+/* ------------------------------------------------------------------ segment description */
+typedef struct {
+  const char* name;
+  int32_t data_type;            /* ph_data_type */
+  int32_t cardinality;          /* column.<c>.cardinality */
+  int32_t bits_per_element;     /* column.<c>.bitsPerElement = getNumBitsPerValue(card - 1) */
+  int32_t is_sorted;            /* column.<c>.isSorted */
+  /* forward_index: unsorted -> fixed-bit packed dictIds, MSB-first, big-endian, ((N*b+7)/8) bytes
+   *                sorted   -> int32 BE (startDocId, endDocId) pairs, 2*card entries
+   *                (SortedIndexReaderImpl.java:37-42) */
+  const void* forward_index;
+  uint64_t forward_index_size;
+  /* dictionary: sorted ascending, fixed width BE (INT 4, LONG 8, FLOAT 4, DOUBLE 8); STRING: UTF-8
+   * zero-padded to dictionary_entry_size (SegmentDictionaryCreator.java:100-276) */
+  const void* dictionary;
+  uint64_t dictionary_size;
+  int32_t dictionary_entry_size;
+  /* optional bitmap inverted index: uint32 BE offsets[card+1] then portable RoaringBitmap blobs
+   * (BitmapInvertedIndexWriter.java:33-96); NULL when the column has none */
+  const void* inverted_index;
+  uint64_t inverted_index_size;
+} ph_column_desc;
+
+typedef struct {
+  const char* name;             /* segment.name */
+  int32_t num_docs;             /* segment.total.docs */
+  int32_t num_columns;
+  const ph_column_desc* columns;
+} ph_segment_desc;
+
+/* ------------------------------------------------------------------ query description */
+typedef enum { PH_PRED_EQ = 0, PH_PRED_NOT_EQ = 1, PH_PRED_IN = 2, PH_PRED_NOT_IN = 3, PH_PRED_RANGE = 4 }
+    ph_predicate_type;
+
+typedef struct {
+  int32_t type;                 /* ph_predicate_type */
+  const char* column;
+  int32_t num_values;           /* EQ / NOT_EQ: 1; IN / NOT_IN: n */
+  const char* const* values;    /* literals as strings, as Pinot's Predicate keeps them */
+  const char* lower;            /* RANGE bounds; "*" = RangePredicate.UNBOUNDED */
+  const char* upper;
+  int32_t lower_inclusive;
+  int32_t upper_inclusive;
+} ph_predicate;
+
+typedef enum { PH_FILTER_AND = 0, PH_FILTER_OR = 1, PH_FILTER_NOT = 2, PH_FILTER_PREDICATE = 3 } ph_filter_type;
+
+typedef struct {
+  int32_t type;                 /* ph_filter_type (FilterContext.Type) */
+  int32_t num_children;
+  const int32_t* children;      /* indices into ph_query.filter_nodes */
+  int32_t predicate;            /* PREDICATE: index into ph_query.predicates */
+} ph_filter_node;
+
+typedef enum { PH_AGG_COUNT = 0, PH_AGG_SUM = 1, PH_AGG_MIN = 2, PH_AGG_MAX = 3, PH_AGG_DISTINCTCOUNTHLL = 4 }
+    ph_aggregation_type;
+
+typedef struct {
+  int32_t type;                 /* ph_aggregation_type */
+  const char* column;           /* NULL for COUNT(*) */
+  int32_t log2m;                /* DISTINCTCOUNTHLL; 0 = default 8 (CommonConstants.java:96-97) */
+} ph_aggregation;
+
+typedef struct {
+  int32_t num_filter_nodes;
+  const ph_filter_node* filter_nodes;
+  int32_t filter_root;          /* -1: no WHERE clause */
+  int32_t num_predicates;
+  const ph_predicate* predicates;
+  int32_t num_group_by;
+  const char* const* group_by;  /* identifiers (DictionaryBasedGroupKeyGenerator columns) */
+  int32_t num_aggregations;
+  const ph_aggregation* aggregations;
+  int64_t num_groups_limit;     /* per-segment numGroupsLimit (InstancePlanMakerImplV2.java:72-73) */
+} ph_query;
+
+typedef struct {
+  int64_t num_docs_scanned;                /* matched docs */
+  int64_t num_entries_scanned_in_filter;   /* full-column entries per scan leaf */
+  int64_t num_entries_scanned_post_filter; /* numDocsScanned x projected columns */
+  int64_t num_total_docs;
+  int64_t num_segments_processed;
+  int64_t num_segments_matched;
+  int32_t num_groups_limit_reached;
+  int32_t sum_precision_flag;              /* 1 if an integer SUM reached 2^53 (double rounding differs) */
+  double device_ms;                        /* kernel time of the query, HIP events */
+  double host_ms;                          /* planning + result materialisation */
+} ph_exec_stats;
+
+/* ------------------------------------------------------------------ context */
+int ph_ctx_create(int32_t device_ordinal, ph_ctx** out);
+int ph_ctx_destroy(ph_ctx* ctx);
+/* Launch on an external HIP stream (e.g. torch's current stream); NULL restores the context's own. */
+int ph_ctx_set_stream(ph_ctx* ctx, void* hip_stream);
+
+/* ------------------------------------------------------------------ segments */
+int ph_segment_pin(ph_ctx* ctx, const ph_segment_desc* desc, ph_segment** out);
+int ph_segment_unpin(ph_segment* seg);
+int64_t ph_segment_device_bytes(const ph_segment* seg);
+int32_t ph_segment_num_docs(const ph_segment* seg);
+
+/* Table-level sorted value union for a column (group keys share ids across segments and GPUs).
+ * Optional: without it the union of the queried segments' dictionaries is used. */
+int ph_table_set_dictionary(ph_ctx* ctx, const char* column, int32_t data_type, const void* values, int64_t count,
+                            int32_t entry_size);
+
+/* ------------------------------------------------------------------ queries */
+int ph_query_execute(ph_ctx* ctx, const ph_query* query, ph_segment* const* segments, int32_t num_segments,
+                     ph_result** out);
+int ph_result_destroy(ph_result* r);
+int ph_result_stats(const ph_result* r, ph_exec_stats* out);
+/* number of result rows: non-empty groups (group-by) or 1 (aggregation-only) */
+int64_t ph_result_num_groups(const ph_result* r);
+/* group-key values of group-by column i for every row, in row order: INT int32, LONG int64,
+ * FLOAT float, DOUBLE double, STRING entry_size-byte zero-padded UTF-8 (entry_size from
+ * ph_result_key_entry_size) */
+int ph_result_key_entry_size(const ph_result* r, int32_t group_by_index);
+/* stored ph_data_type of group-by column i's key values */
+int ph_result_key_type(const ph_result* r, int32_t group_by_index);
+int ph_result_group_keys(const ph_result* r, int32_t group_by_index, void* out);
+/* intermediate result of aggregation i for every row: COUNT int64, SUM/MIN/MAX double,
+ * DISTINCTCOUNTHLL uint8[2^log2m] raw registers (HyperLogLog.addAll = register-wise max) */
+int ph_result_aggregation(const ph_result* r, int32_t aggregation_index, void* out);
+
+/* ------------------------------------------------------------------ segment creation helper */
+/* FixedBitSVForwardIndexWriter: packs n dictIds with `bits` bits, MSB-first big-endian; out_size >=
+ * (n*bits+7)/8 */
+int ph_fixed_bit_pack(const int32_t* dict_ids, int64_t n, int32_t bits, uint8_t* out, uint64_t out_size);
+
+/* Self-test hook: unpack n values of a packed fixed-bit stream on the device with the same routine the
+ * scan kernels use, writing dictIds to host memory `out` (FixedBitIntReaderTest-style parity checks). */
+int ph_selftest_unpack(ph_ctx* ctx, const uint8_t* packed, uint64_t packed_size, int64_t n, int32_t bits,
+                       int32_t* out);
+
+/* thread-local message of the last error on this thread */
+const char* ph_last_error(void);
+const char* ph_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PINOT_HIP_H */

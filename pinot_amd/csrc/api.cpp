@@ -1,0 +1,236 @@
+// api.cpp -- extern "C" entry points of libpinot_hip.so (include/pinot_hip.h).  No C++ exception crosses
+// the ABI: every entry point returns a PH_* status and leaves a thread-local message for ph_last_error().
+#include <cstring>
+#include <new>
+
+#include "ph_internal.h"
+
+namespace ph {
+thread_local std::string g_last_error;
+
+void fail(int code, const std::string& msg) { throw Error{code, msg}; }
+
+ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc);
+ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const* segs, int32_t nseg);
+}  // namespace ph
+
+using namespace ph;
+
+struct ph_ctx {
+  Context c;
+};
+
+template <class F>
+static int guarded(F&& f) {
+  try {
+    f();
+    g_last_error.clear();
+    return PH_OK;
+  } catch (const Error& e) {
+    g_last_error = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_last_error = "host out of memory";
+    return PH_ERR_OUT_OF_MEMORY;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return PH_ERR_INVALID_ARGUMENT;
+  } catch (...) {
+    g_last_error = "unknown error";
+    return PH_ERR_DEVICE;
+  }
+}
+
+extern "C" {
+
+const char* ph_last_error(void) { return g_last_error.c_str(); }
+const char* ph_version(void) { return "pinot_hip 0.1.0 (gfx950)"; }
+
+int ph_ctx_create(int32_t device_ordinal, ph_ctx** out) {
+  return guarded([&] {
+    if (!out) fail(PH_ERR_INVALID_ARGUMENT, "out is null");
+    int n = 0;
+    PH_HIP_CHECK(hipGetDeviceCount(&n));
+    if (device_ordinal < 0 || device_ordinal >= n)
+      fail(PH_ERR_INVALID_ARGUMENT, "device ordinal " + std::to_string(device_ordinal) + " out of range");
+    auto* ctx = new ph_ctx();
+    try {
+      Context& c = ctx->c;
+      c.device = device_ordinal;
+      PH_HIP_CHECK(hipSetDevice(device_ordinal));
+      PH_HIP_CHECK(hipStreamCreateWithFlags(&c.own_stream, hipStreamNonBlocking));
+      c.stream = c.own_stream;
+      PH_HIP_CHECK(hipEventCreate(&c.ev_start));
+      PH_HIP_CHECK(hipEventCreate(&c.ev_stop));
+      hipDeviceProp_t prop;
+      PH_HIP_CHECK(hipGetDeviceProperties(&prop, device_ordinal));
+      c.num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    } catch (...) {
+      delete ctx;
+      throw;
+    }
+    *out = ctx;
+  });
+}
+
+int ph_ctx_destroy(ph_ctx* ctx) {
+  return guarded([&] {
+    if (!ctx) return;
+    Context& c = ctx->c;
+    (void)hipSetDevice(c.device);
+    if (c.own_stream) (void)hipStreamSynchronize(c.own_stream);
+    if (c.ev_start) (void)hipEventDestroy(c.ev_start);
+    if (c.ev_stop) (void)hipEventDestroy(c.ev_stop);
+    if (c.own_stream) (void)hipStreamDestroy(c.own_stream);
+    if (c.pinned) (void)hipHostFree(c.pinned);
+    delete ctx;
+  });
+}
+
+int ph_ctx_set_stream(ph_ctx* ctx, void* hip_stream) {
+  return guarded([&] {
+    if (!ctx) fail(PH_ERR_INVALID_ARGUMENT, "ctx is null");
+    std::lock_guard<std::mutex> g(ctx->c.mu);
+    ctx->c.stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->c.own_stream;
+  });
+}
+
+int ph_segment_pin(ph_ctx* ctx, const ph_segment_desc* desc, ph_segment** out) {
+  return guarded([&] {
+    if (!ctx || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
+    *out = segment_pin_impl(&ctx->c, desc);
+  });
+}
+
+int ph_segment_unpin(ph_segment* seg) {
+  return guarded([&] {
+    if (!seg) return;
+    (void)hipSetDevice(seg->ctx->device);
+    (void)hipStreamSynchronize(seg->ctx->stream);
+    delete seg;
+  });
+}
+
+int64_t ph_segment_device_bytes(const ph_segment* seg) { return seg ? seg->device_bytes : -1; }
+int32_t ph_segment_num_docs(const ph_segment* seg) { return seg ? seg->num_docs : -1; }
+
+int ph_table_set_dictionary(ph_ctx* ctx, const char* column, int32_t data_type, const void* values, int64_t count,
+                            int32_t entry_size) {
+  return guarded([&] {
+    if (!ctx || !column || (count > 0 && !values)) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
+    auto g = std::make_shared<GlobalDict>();
+    Dictionary& d = g->dict;
+    d.type = data_type;
+    d.size = count;
+    const uint8_t* b = static_cast<const uint8_t*>(values);
+    switch (data_type) {
+      case PH_INT:
+        d.ints.resize(count);
+        for (int64_t i = 0; i < count; ++i) d.ints[i] = reinterpret_cast<const int32_t*>(b)[i];
+        break;
+      case PH_LONG:
+        d.ints.assign(reinterpret_cast<const int64_t*>(b), reinterpret_cast<const int64_t*>(b) + count);
+        break;
+      case PH_FLOAT:
+        d.reals.resize(count);
+        for (int64_t i = 0; i < count; ++i) d.reals[i] = reinterpret_cast<const float*>(b)[i];
+        break;
+      case PH_DOUBLE:
+        d.reals.assign(reinterpret_cast<const double*>(b), reinterpret_cast<const double*>(b) + count);
+        break;
+      case PH_STRING:
+        if (entry_size <= 0) fail(PH_ERR_INVALID_ARGUMENT, "entry_size");
+        d.strings.resize(count);
+        for (int64_t i = 0; i < count; ++i) {
+          const char* s = reinterpret_cast<const char*>(b + (size_t)entry_size * i);
+          d.strings[i].assign(s, strnlen(s, entry_size));
+          d.max_string_len = std::max<int32_t>(d.max_string_len, (int32_t)d.strings[i].size());
+        }
+        break;
+      default:
+        fail(PH_ERR_INVALID_ARGUMENT, "data type");
+    }
+    for (int64_t i = 1; i < count; ++i)
+      if (d.compare(i - 1, d, i) >= 0) fail(PH_ERR_INVALID_ARGUMENT, "table dictionary must be sorted and unique");
+    std::lock_guard<std::mutex> lk(ctx->c.mu);
+    g->id = ctx->c.next_id++;
+    ctx->c.table_dicts[column] = g;
+  });
+}
+
+int ph_query_execute(ph_ctx* ctx, const ph_query* query, ph_segment* const* segments, int32_t num_segments,
+                     ph_result** out) {
+  return guarded([&] {
+    if (!ctx || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    *out = query_execute_impl(&ctx->c, query, segments, num_segments);
+  });
+}
+
+int ph_result_destroy(ph_result* r) {
+  delete r;
+  return PH_OK;
+}
+
+int ph_result_stats(const ph_result* r, ph_exec_stats* out) {
+  return guarded([&] {
+    if (!r || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
+    *out = r->stats;
+  });
+}
+
+int64_t ph_result_num_groups(const ph_result* r) { return r ? r->num_groups : -1; }
+
+int ph_result_key_entry_size(const ph_result* r, int32_t i) {
+  if (!r || i < 0 || i >= (int32_t)r->key_entry_size.size()) return -1;
+  return r->key_entry_size[i];
+}
+
+int ph_result_key_type(const ph_result* r, int32_t i) {
+  if (!r || i < 0 || i >= (int32_t)r->key_types.size()) return -1;
+  return r->key_types[i];
+}
+
+int ph_result_group_keys(const ph_result* r, int32_t i, void* out) {
+  return guarded([&] {
+    if (!r || !out || i < 0 || i >= (int32_t)r->keys.size()) fail(PH_ERR_INVALID_ARGUMENT, "bad key index");
+    memcpy(out, r->keys[i].data(), r->keys[i].size());
+  });
+}
+
+int ph_result_aggregation(const ph_result* r, int32_t k, void* out) {
+  return guarded([&] {
+    if (!r || !out || k < 0 || k >= (int32_t)r->aggs.size()) fail(PH_ERR_INVALID_ARGUMENT, "bad aggregation index");
+    memcpy(out, r->aggs[k].data(), r->aggs[k].size());
+  });
+}
+
+int ph_selftest_unpack(ph_ctx* ctx, const uint8_t* packed, uint64_t packed_size, int64_t n, int32_t bits,
+                       int32_t* out) {
+  return guarded([&] {
+    if (!ctx || !packed || !out || n < 0 || bits < 1 || bits > 31) fail(PH_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (packed_size < (uint64_t)((n * bits + 7) / 8)) fail(PH_ERR_INVALID_ARGUMENT, "packed buffer too small");
+    std::lock_guard<std::mutex> lk(ctx->c.mu);
+    PH_HIP_CHECK(hipSetDevice(ctx->c.device));
+    DeviceBuffer in, o;
+    in.alloc(packed_size + kFwdPadBytes, ctx->c.device);
+    o.alloc(sizeof(int32_t) * std::max<int64_t>(1, n), ctx->c.device);
+    PH_HIP_CHECK(hipMemsetAsync(in.ptr, 0, packed_size + kFwdPadBytes, ctx->c.stream));
+    PH_HIP_CHECK(hipMemcpyAsync(in.ptr, packed, packed_size, hipMemcpyHostToDevice, ctx->c.stream));
+    launch_selftest_unpack(in.as<uint32_t>(), n, bits, o.as<int32_t>(), ctx->c.stream);
+    PH_HIP_CHECK(hipMemcpyAsync(out, o.ptr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, ctx->c.stream));
+    PH_HIP_CHECK(hipStreamSynchronize(ctx->c.stream));
+  });
+}
+
+int ph_fixed_bit_pack(const int32_t* dict_ids, int64_t n, int32_t bits, uint8_t* out, uint64_t out_size) {
+  return guarded([&] {
+    if (n < 0 || bits < 1 || bits > 31 || (n > 0 && (!dict_ids || !out)))
+      fail(PH_ERR_INVALID_ARGUMENT, "bad pack arguments");
+    const uint64_t need = (uint64_t)((n * bits + 7) / 8);
+    if (out_size < need) fail(PH_ERR_INVALID_ARGUMENT, "output buffer too small");
+    fixed_bit_pack_host(dict_ids, n, bits, out);
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,342 @@
+// segment.cpp -- pinning immutable segments in HBM (the GPU side of ImmutableSegmentLoader.load).
+//
+// Input buffers are the column slices of the V3 columns.psf exactly as Pinot maps them
+// (SingleFileIndexDirectory.java:279-305, all BIG_ENDIAN):
+//   forward index  FixedBitSVForwardIndexWriter.java:39-50 (unsorted) / SortedIndexReaderImpl.java:37-42 (sorted)
+//   dictionary     SegmentDictionaryCreator.java:100-276 (sorted, fixed width; STRING zero padded)
+//   inverted index BitmapInvertedIndexWriter.java:33-96 (uint32 offsets + portable RoaringBitmap blobs)
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <thread>
+
+#include "ph_internal.h"
+
+namespace ph {
+
+// ------------------------------------------------------------------ device buffer
+DeviceBuffer::~DeviceBuffer() {
+  if (ptr) {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (cur != device) (void)hipSetDevice(device);
+    (void)hipFree(ptr);
+    if (cur != device) (void)hipSetDevice(cur);
+  }
+}
+
+void DeviceBuffer::alloc(size_t n, int dev) {
+  device = dev;
+  bytes = n;
+  if (n == 0) n = 16;
+  hipError_t e = hipMalloc(&ptr, n);
+  if (e != hipSuccess) {
+    ptr = nullptr;
+    fail(e == hipErrorOutOfMemory ? PH_ERR_OUT_OF_MEMORY : PH_ERR_DEVICE,
+         std::string("hipMalloc(") + std::to_string(n) + "): " + hipGetErrorString(e));
+  }
+}
+
+void* Context::host_staging(size_t n) {
+  if (n > pinned_bytes) {
+    if (pinned) PH_HIP_CHECK(hipHostFree(pinned));
+    pinned = nullptr;
+    size_t sz = std::max<size_t>(n, 1 << 20);
+    PH_HIP_CHECK(hipHostMalloc(&pinned, sz, hipHostMallocDefault));
+    pinned_bytes = sz;
+  }
+  return pinned;
+}
+
+// ------------------------------------------------------------------ big-endian readers
+static inline uint32_t be32(const uint8_t* p) {
+  return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
+}
+static inline uint64_t be64(const uint8_t* p) { return ((uint64_t)be32(p) << 32) | be32(p + 4); }
+
+// ------------------------------------------------------------------ fixed-bit pack (FixedBitSVForwardIndexWriter)
+void fixed_bit_pack_host(const int32_t* ids, int64_t n, int bits, uint8_t* out) {
+  // Values are written MSB-first into a big-endian bit stream (PinotDataBitSet.writeInt,
+  // PinotDataBitSet.java:138-165).  Parallel over 32-value groups: a group of 32 values occupies
+  // exactly `bits` 32-bit words, so threads never share an output byte.
+  const int64_t groups = (n + 31) / 32;
+  const int64_t nbytes = (n * bits + 7) / 8;
+  auto work = [&](int64_t g0, int64_t g1) {
+    for (int64_t g = g0; g < g1; ++g) {
+      uint64_t acc = 0;
+      int nacc = 0;
+      int64_t byte = g * 4 * bits;
+      const int64_t i1 = std::min<int64_t>(n, (g + 1) * 32);
+      for (int64_t i = g * 32; i < i1; ++i) {
+        acc = (acc << bits) | ((uint32_t)ids[i] & ((bits == 32) ? 0xffffffffu : ((1u << bits) - 1u)));
+        nacc += bits;
+        while (nacc >= 8) {
+          nacc -= 8;
+          if (byte < nbytes) out[byte] = (uint8_t)(acc >> nacc);
+          byte++;
+        }
+      }
+      if (nacc > 0 && byte < nbytes) out[byte] = (uint8_t)(acc << (8 - nacc));
+    }
+  };
+  const int64_t nthreads = std::min<int64_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
+  if (groups < 65536 || nthreads <= 1) {
+    work(0, groups);
+    return;
+  }
+  std::vector<std::thread> th;
+  const int64_t per = (groups + nthreads - 1) / nthreads;
+  for (int64_t t = 0; t < nthreads; ++t) {
+    const int64_t a = t * per, b = std::min(groups, a + per);
+    if (a < b) th.emplace_back(work, a, b);
+  }
+  for (auto& t : th) t.join();
+}
+
+// clearspring MurmurHash.hash(byte[] data, int length, int seed); Java bytes are signed
+int32_t murmur_hash_bytes(const uint8_t* data, int32_t length, int32_t seed) {
+  const uint32_t m = 0x5bd1e995u;
+  uint32_t h = (uint32_t)(seed ^ length);
+  const int32_t len4 = length >> 2;
+  for (int32_t i = 0; i < len4; i++) {
+    const int32_t i4 = i << 2;
+    uint32_t k = (uint32_t)(int32_t)(int8_t)data[i4 + 3];
+    k = (k << 8) | data[i4 + 2];
+    k = (k << 8) | data[i4 + 1];
+    k = (k << 8) | data[i4 + 0];
+    k *= m;
+    k ^= k >> 24;
+    k *= m;
+    h *= m;
+    h ^= k;
+  }
+  const int32_t left = length - (len4 << 2);
+  if (left != 0) {
+    if (left >= 3) h ^= (uint32_t)((int32_t)(int8_t)data[length - 3] << 16);
+    if (left >= 2) h ^= (uint32_t)((int32_t)(int8_t)data[length - 2] << 8);
+    if (left >= 1) h ^= (uint32_t)(int32_t)(int8_t)data[length - 1];
+    h *= m;
+  }
+  h ^= h >> 13;
+  h *= m;
+  h ^= h >> 15;
+  return (int32_t)h;
+}
+
+// ------------------------------------------------------------------ dictionary
+static bool parse_int64(const std::string& s, int64_t* out) {
+  if (s.empty()) return false;
+  char* end = nullptr;
+  errno = 0;
+  long long v = strtoll(s.c_str(), &end, 10);
+  if (errno != 0 || end != s.c_str() + s.size()) return false;
+  *out = v;
+  return true;
+}
+
+static bool parse_double(const std::string& s, double* out) {
+  if (s.empty()) return false;
+  char* end = nullptr;
+  double v = strtod(s.c_str(), &end);
+  if (end != s.c_str() + s.size()) return false;
+  *out = v;
+  return true;
+}
+
+int64_t Dictionary::insertion_index_of(const std::string& literal) const {
+  // BaseImmutableDictionary.insertionIndexOf / binarySearch (BaseImmutableDictionary.java:124-245):
+  // index when present, else -(insertionPoint) - 1.  Literals are parsed with the column's stored type
+  // (PredicateUtils.getStoredValue).
+  int64_t lo = 0, hi = size - 1;
+  if (type == PH_INT || type == PH_LONG) {
+    int64_t iv;
+    double dv;
+    if (parse_int64(literal, &iv)) {
+      while (lo <= hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (ints[mid] < iv) lo = mid + 1;
+        else if (ints[mid] > iv) hi = mid - 1;
+        else return mid;
+      }
+      return -(lo + 1);
+    }
+    if (!parse_double(literal, &dv)) fail(PH_ERR_BAD_QUERY, "Cannot convert value: '" + literal + "' to type: INT/LONG");
+    while (lo <= hi) {  // non-integral literal: never equal, insertion point by numeric order
+      int64_t mid = (lo + hi) >> 1;
+      if ((double)ints[mid] < dv) lo = mid + 1;
+      else if ((double)ints[mid] > dv) hi = mid - 1;
+      else return mid;
+    }
+    return -(lo + 1);
+  }
+  if (type == PH_FLOAT || type == PH_DOUBLE) {
+    double dv;
+    if (!parse_double(literal, &dv)) fail(PH_ERR_BAD_QUERY, "Cannot convert value: '" + literal + "' to type: DOUBLE");
+    if (type == PH_FLOAT) dv = (double)(float)dv;
+    while (lo <= hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if (reals[mid] < dv) lo = mid + 1;
+      else if (reals[mid] > dv) hi = mid - 1;
+      else return mid;
+    }
+    return -(lo + 1);
+  }
+  while (lo <= hi) {  // STRING: byte order == code point order for UTF-8
+    int64_t mid = (lo + hi) >> 1;
+    int c = strings[mid].compare(literal);
+    if (c < 0) lo = mid + 1;
+    else if (c > 0) hi = mid - 1;
+    else return mid;
+  }
+  return -(lo + 1);
+}
+
+int Dictionary::compare(int64_t i, const Dictionary& o, int64_t j) const {
+  if (type == PH_STRING) return strings[i].compare(o.strings[j]);
+  if (type == PH_INT || type == PH_LONG) return ints[i] < o.ints[j] ? -1 : (ints[i] > o.ints[j] ? 1 : 0);
+  return reals[i] < o.reals[j] ? -1 : (reals[i] > o.reals[j] ? 1 : 0);
+}
+
+static void parse_dictionary(const ph_column_desc& d, Dictionary* out) {
+  const uint8_t* b = static_cast<const uint8_t*>(d.dictionary);
+  const int64_t card = d.cardinality;
+  out->type = d.data_type;
+  out->size = card;
+  int width = 0;
+  switch (d.data_type) {
+    case PH_INT: width = 4; break;
+    case PH_LONG: width = 8; break;
+    case PH_FLOAT: width = 4; break;
+    case PH_DOUBLE: width = 8; break;
+    case PH_STRING: width = d.dictionary_entry_size; break;
+    default: fail(PH_ERR_INVALID_ARGUMENT, "unknown data type for column " + std::string(d.name));
+  }
+  if (width <= 0 || (uint64_t)width * card > d.dictionary_size)
+    fail(PH_ERR_INVALID_ARGUMENT, "dictionary buffer too small for column " + std::string(d.name));
+  switch (d.data_type) {
+    case PH_INT:
+      out->ints.resize(card);
+      for (int64_t i = 0; i < card; ++i) out->ints[i] = (int32_t)be32(b + 4 * i);
+      break;
+    case PH_LONG:
+      out->ints.resize(card);
+      for (int64_t i = 0; i < card; ++i) out->ints[i] = (int64_t)be64(b + 8 * i);
+      break;
+    case PH_FLOAT:
+      out->reals.resize(card);
+      for (int64_t i = 0; i < card; ++i) {
+        uint32_t u = be32(b + 4 * i);
+        float f;
+        memcpy(&f, &u, 4);
+        out->reals[i] = f;
+      }
+      break;
+    case PH_DOUBLE:
+      out->reals.resize(card);
+      for (int64_t i = 0; i < card; ++i) {
+        uint64_t u = be64(b + 8 * i);
+        memcpy(&out->reals[i], &u, 8);
+      }
+      break;
+    case PH_STRING:
+      out->strings.resize(card);
+      for (int64_t i = 0; i < card; ++i) {
+        const char* s = reinterpret_cast<const char*>(b + (int64_t)width * i);
+        size_t len = strnlen(s, width);  // FixedByteValueReaderWriter: value ends at the first 0 byte
+        out->strings[i].assign(s, len);
+        out->max_string_len = std::max<int32_t>(out->max_string_len, (int32_t)len);
+      }
+      break;
+  }
+}
+
+// ------------------------------------------------------------------ pin
+ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
+  if (!desc || desc->num_docs < 0 || desc->num_columns < 0 || (desc->num_columns && !desc->columns))
+    fail(PH_ERR_INVALID_ARGUMENT, "bad segment descriptor");
+  PH_HIP_CHECK(hipSetDevice(ctx->device));
+  auto seg = std::make_unique<ph_segment>();
+  seg->ctx = ctx;
+  seg->name = desc->name ? desc->name : "";
+  seg->num_docs = desc->num_docs;
+  const int64_t n = desc->num_docs;
+  std::vector<int32_t> ids;
+  for (int ci = 0; ci < desc->num_columns; ++ci) {
+    const ph_column_desc& d = desc->columns[ci];
+    if (!d.name) fail(PH_ERR_INVALID_ARGUMENT, "column without a name");
+    auto col = std::make_unique<Column>();
+    col->name = d.name;
+    col->data_type = d.data_type;
+    col->cardinality = d.cardinality;
+    col->is_sorted = d.is_sorted != 0;
+    if (d.cardinality <= 0 && n > 0) fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": cardinality <= 0");
+    if (!d.dictionary) fail(PH_ERR_UNSUPPORTED, "column " + col->name + ": raw (no-dictionary) columns are not on the GPU path");
+    parse_dictionary(d, &col->dict);
+    // PinotDataBitSet.getNumBitsPerValue(cardinality - 1)
+    int bits = 1;
+    while (bits < 31 && ((int64_t)1 << bits) < (int64_t)d.cardinality) bits++;
+    const uint8_t* fwd = static_cast<const uint8_t*>(d.forward_index);
+    if (!fwd) fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": missing forward index");
+    std::vector<uint8_t> packed;
+    const uint8_t* src = fwd;
+    uint64_t src_bytes = d.forward_index_size;
+    if (col->is_sorted) {
+      // SortedIndexReaderImpl: int32 BE (start, end) per dictId; expand to the packed fixed-bit form
+      if (d.forward_index_size < (uint64_t)8 * d.cardinality)
+        fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": sorted index too small");
+      col->sorted_ranges.resize(2 * (size_t)d.cardinality);
+      ids.assign(n, 0);
+      for (int64_t k = 0; k < d.cardinality; ++k) {
+        int32_t s = (int32_t)be32(fwd + 8 * k), e = (int32_t)be32(fwd + 8 * k + 4);
+        col->sorted_ranges[2 * k] = s;
+        col->sorted_ranges[2 * k + 1] = e;
+        for (int64_t doc = std::max<int64_t>(s, 0); doc <= e && doc < n; ++doc) ids[doc] = (int32_t)k;
+      }
+      packed.assign((size_t)((n * bits + 7) / 8), 0);
+      fixed_bit_pack_host(ids.data(), n, bits, packed.data());
+      src = packed.data();
+      src_bytes = packed.size();
+    } else {
+      if (d.bits_per_element != bits)
+        fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": bitsPerElement " + std::to_string(d.bits_per_element) +
+                                          " != getNumBitsPerValue(cardinality - 1) = " + std::to_string(bits));
+      if (src_bytes < (uint64_t)((n * bits + 7) / 8))
+        fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": forward index too small");
+    }
+    col->bits = bits;
+    const size_t fwd_bytes = (size_t)((n * bits + 7) / 8);
+    const size_t alloc = ((fwd_bytes + kFwdPadBytes + 255) / 256) * 256;
+    col->d_fwd.alloc(alloc, ctx->device);
+    PH_HIP_CHECK(hipMemsetAsync(col->d_fwd.ptr, 0, alloc, ctx->stream));
+    PH_HIP_CHECK(hipMemcpyAsync(col->d_fwd.ptr, src, fwd_bytes, hipMemcpyHostToDevice, ctx->stream));
+    seg->device_bytes += alloc;
+    // dictionary values widened for arithmetic
+    if (d.data_type != PH_STRING) {
+      col->d_values.alloc(sizeof(int64_t) * std::max<int64_t>(1, d.cardinality), ctx->device);
+      const void* vsrc = (d.data_type == PH_INT || d.data_type == PH_LONG) ? (const void*)col->dict.ints.data()
+                                                                           : (const void*)col->dict.reals.data();
+      PH_HIP_CHECK(hipMemcpyAsync(col->d_values.ptr, vsrc, sizeof(int64_t) * d.cardinality, hipMemcpyHostToDevice,
+                                  ctx->stream));
+      seg->device_bytes += col->d_values.bytes;
+    }
+    if (d.inverted_index && d.inverted_index_size) {
+      const uint8_t* inv = static_cast<const uint8_t*>(d.inverted_index);
+      if (d.inverted_index_size < (uint64_t)4 * (d.cardinality + 1))
+        fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": inverted index too small");
+      col->inverted.assign(inv, inv + d.inverted_index_size);
+      col->d_inverted.alloc(d.inverted_index_size, ctx->device);
+      PH_HIP_CHECK(hipMemcpyAsync(col->d_inverted.ptr, inv, d.inverted_index_size, hipMemcpyHostToDevice, ctx->stream));
+      seg->device_bytes += d.inverted_index_size;
+    }
+    // the caller's buffers may be released after pin returns
+    PH_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    seg->columns[col->name] = std::move(col);
+  }
+  {
+    std::lock_guard<std::mutex> g(ctx->mu);
+    seg->id = ctx->next_id++;
+  }
+  return seg.release();
+}
+
+}  // namespace ph

@@ -1,0 +1,220 @@
+"""Server-side query execution over HBM-pinned segments (ServerQueryExecutorV1Impl for the filter ->
+aggregation / group-by shapes), followed by the broker reduce (pinot_amd.reduce).
+
+    ctx = GpuContext(0)
+    segs = [ctx.pin(create_segment(...)), ...]
+    table = ctx.query("SELECT g, SUM(m) FROM t WHERE f BETWEEN 0 AND 9 GROUP BY g ORDER BY g", segs)
+
+``execute`` returns the combined intermediate results (what GroupByCombineOperator hands to the
+broker) and the ExecutionStatistics.  Unsupported shapes raise ``UnsupportedError`` -- the
+reference-side plan maker falls back to its CPU plan on that code.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Sequence
+
+import numpy as np
+
+from . import native as N
+from .query import (COUNT, DISTINCTCOUNTHLL, MAX, MIN, SUM, FilterContext, QueryContext, parse_sql)
+from .reduce import ResultTable, reduce_groups
+from .segment import PinnedSegment, SegmentBuffers
+
+_AGG = {COUNT: N.PH_AGG_COUNT, SUM: N.PH_AGG_SUM, MIN: N.PH_AGG_MIN, MAX: N.PH_AGG_MAX,
+        DISTINCTCOUNTHLL: N.PH_AGG_DISTINCTCOUNTHLL}
+_PRED = {"EQ": N.PH_PRED_EQ, "NOT_EQ": N.PH_PRED_NOT_EQ, "IN": N.PH_PRED_IN, "NOT_IN": N.PH_PRED_NOT_IN,
+         "RANGE": N.PH_PRED_RANGE}
+
+
+@dataclass
+class ExecutionStats:
+    num_docs_scanned: int
+    num_entries_scanned_in_filter: int
+    num_entries_scanned_post_filter: int
+    num_total_docs: int
+    num_segments_processed: int
+    num_segments_matched: int
+    num_groups_limit_reached: bool
+    sum_precision_flag: bool
+    device_ms: float
+    host_ms: float
+
+
+@dataclass
+class IntermediateResult:
+    keys: List[tuple]
+    aggs: List[list]
+    stats: ExecutionStats
+
+
+class _QueryStruct:
+    """Builds the ph_query POD graph and keeps every buffer alive while the call runs."""
+
+    def __init__(self, q: QueryContext):
+        self.keep = []
+        nodes: List[N.FilterNode] = []
+        preds: List[N.Predicate] = []
+
+        def s(x):
+            b = x.encode()
+            self.keep.append(b)
+            return b
+
+        def add(f: FilterContext) -> int:
+            if f.type == "PREDICATE":
+                p = f.predicate
+                ps = N.Predicate()
+                ps.type = _PRED[p.TYPE]
+                ps.column = s(p.column)
+                vals = []
+                if p.TYPE in ("EQ", "NOT_EQ"):
+                    vals = [p.value]
+                elif p.TYPE in ("IN", "NOT_IN"):
+                    vals = list(p.values)
+                else:
+                    ps.lower = s(p.lower)
+                    ps.upper = s(p.upper)
+                    ps.lower_inclusive = int(p.lower_inclusive)
+                    ps.upper_inclusive = int(p.upper_inclusive)
+                arr = (ctypes.c_char_p * max(1, len(vals)))(*[s(v) for v in vals])
+                self.keep.append(arr)
+                ps.num_values = len(vals)
+                ps.values = arr
+                preds.append(ps)
+                nodes.append(N.FilterNode(N.PH_FILTER_PREDICATE, 0, None, len(preds) - 1))
+                return len(nodes) - 1
+            kids = [add(c) for c in f.children]
+            arr = (ctypes.c_int32 * max(1, len(kids)))(*kids)
+            self.keep.append(arr)
+            t = {"AND": N.PH_FILTER_AND, "OR": N.PH_FILTER_OR, "NOT": N.PH_FILTER_NOT}[f.type]
+            nodes.append(N.FilterNode(t, len(kids), arr, -1))
+            return len(nodes) - 1
+
+        root = add(q.filter) if q.filter is not None else -1
+        node_arr = (N.FilterNode * max(1, len(nodes)))(*nodes)
+        pred_arr = (N.Predicate * max(1, len(preds)))(*preds)
+        gb = (ctypes.c_char_p * max(1, len(q.group_by)))(*[s(g) for g in q.group_by])
+        aggs = (N.Aggregation * max(1, len(q.aggregations)))(
+            *[N.Aggregation(_AGG[a.function], s(a.column) if a.column else None,
+                            a.log2m if a.function == DISTINCTCOUNTHLL else 0) for a in q.aggregations])
+        self.keep += [node_arr, pred_arr, gb, aggs]
+        self.struct = N.Query(len(nodes), node_arr, root, len(preds), pred_arr, len(q.group_by), gb,
+                              len(q.aggregations), aggs, q.num_groups_limit)
+
+
+_KEY_DTYPE = {N.PH_INT: np.int32, N.PH_LONG: np.int64, N.PH_FLOAT: np.float32, N.PH_DOUBLE: np.float64}
+
+
+class GpuContext:
+    """One context per GPU (ph_ctx)."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        N.check(N.lib().ph_ctx_create(device, ctypes.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            N.lib().ph_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_ptr: int):
+        N.check(N.lib().ph_ctx_set_stream(self.handle, ctypes.c_void_p(stream_ptr)))
+
+    def pin(self, buffers: SegmentBuffers) -> PinnedSegment:
+        return PinnedSegment(self, buffers)
+
+    def set_table_dictionary(self, column: str, data_type: str, values: np.ndarray):
+        dt = N.DATA_TYPES[data_type]
+        if data_type == "STRING":
+            enc = [str(v).encode() for v in values]
+            width = max([len(e) for e in enc] + [1])
+            buf = np.zeros((len(enc), width), np.uint8)
+            for i, e in enumerate(enc):
+                buf[i, :len(e)] = np.frombuffer(e, np.uint8)
+        else:
+            buf = np.ascontiguousarray(values, dtype=_KEY_DTYPE[dt])
+            width = buf.dtype.itemsize
+        N.check(N.lib().ph_table_set_dictionary(self.handle, column.encode(), dt, buf.ctypes.data, len(values), width))
+
+    def execute(self, q: QueryContext, segments: Sequence[PinnedSegment]) -> IntermediateResult:
+        qs = _QueryStruct(q)
+        segs = (ctypes.c_void_p * max(1, len(segments)))(*[s.handle for s in segments])
+        r = ctypes.c_void_p()
+        N.check(N.lib().ph_query_execute(self.handle, ctypes.byref(qs.struct), segs, len(segments), ctypes.byref(r)))
+        try:
+            return self._read_result(q, r)
+        finally:
+            N.lib().ph_result_destroy(r)
+
+    @staticmethod
+    def _read_result(q: QueryContext, r) -> IntermediateResult:
+        L = N.lib()
+        st = N.ExecStats()
+        N.check(L.ph_result_stats(r, ctypes.byref(st)))
+        n = L.ph_result_num_groups(r)
+        cols = []
+        for g in range(len(q.group_by)):
+            es = L.ph_result_key_entry_size(r, g)
+            raw = np.zeros(n * es, np.uint8)
+            if n:
+                N.check(L.ph_result_group_keys(r, g, raw.ctypes.data))
+            cols.append((es, raw))
+        aggs_cols = []
+        for k, a in enumerate(q.aggregations):
+            if a.function == DISTINCTCOUNTHLL:
+                arr = np.zeros((n, 1 << a.log2m), np.uint8)
+            elif a.function == COUNT:
+                arr = np.zeros(n, np.int64)
+            else:
+                arr = np.zeros(n, np.float64)
+            if n:
+                N.check(L.ph_result_aggregation(r, k, arr.ctypes.data))
+            aggs_cols.append(arr)
+        keys = []
+        if q.group_by:
+            decoded = []
+            for g, (es, raw) in enumerate(cols):
+                decoded.append(_decode_keys(raw, es, n, q, g, r))
+            keys = list(zip(*decoded)) if n else []
+        else:
+            keys = [()] * n
+        aggs = []
+        for i in range(n):
+            row = []
+            for k, a in enumerate(q.aggregations):
+                v = aggs_cols[k][i]
+                if a.function == COUNT:
+                    row.append(int(v))
+                elif a.function == DISTINCTCOUNTHLL:
+                    row.append(v)
+                else:
+                    row.append(float(v))
+            aggs.append(row)
+        stats = ExecutionStats(st.num_docs_scanned, st.num_entries_scanned_in_filter,
+                               st.num_entries_scanned_post_filter, st.num_total_docs, st.num_segments_processed,
+                               st.num_segments_matched, bool(st.num_groups_limit_reached),
+                               bool(st.sum_precision_flag), st.device_ms, st.host_ms)
+        return IntermediateResult(keys, aggs, stats)
+
+    def query(self, sql_or_q, segments: Sequence[PinnedSegment]) -> ResultTable:
+        q = parse_sql(sql_or_q) if isinstance(sql_or_q, str) else sql_or_q
+        r = self.execute(q, segments)
+        return reduce_groups(q, r.keys, r.aggs)
+
+
+def _decode_keys(raw: np.ndarray, es: int, n: int, q: QueryContext, g: int, r) -> list:
+    t = N.lib().ph_result_key_type(r, g)
+    if t == N.PH_STRING:
+        m = raw.reshape(n, es)
+        return [bytes(row).rstrip(b"\x00").decode("utf-8") for row in m]
+    return np.frombuffer(raw.tobytes(), dtype=_KEY_DTYPE[t]).tolist()

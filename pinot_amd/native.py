@@ -1,0 +1,147 @@
+"""ctypes binding of libpinot_hip.so (include/pinot_hip.h).
+
+The library is built in-tree (``pinot_amd/libpinot_hip.so``, see ``__graft_entry__.build``).  There is no
+fallback: if the library is missing or a GPU call fails, the error is raised to the caller.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpinot_hip.so")
+
+PH_OK = 0
+PH_ERR_INVALID_ARGUMENT = 1
+PH_ERR_BAD_QUERY = 2
+PH_ERR_UNSUPPORTED = 3
+PH_ERR_DEVICE = 4
+PH_ERR_OUT_OF_MEMORY = 5
+
+PH_INT, PH_LONG, PH_FLOAT, PH_DOUBLE, PH_STRING = range(5)
+DATA_TYPES = {"INT": PH_INT, "LONG": PH_LONG, "FLOAT": PH_FLOAT, "DOUBLE": PH_DOUBLE, "STRING": PH_STRING}
+
+PH_PRED_EQ, PH_PRED_NOT_EQ, PH_PRED_IN, PH_PRED_NOT_IN, PH_PRED_RANGE = range(5)
+PH_FILTER_AND, PH_FILTER_OR, PH_FILTER_NOT, PH_FILTER_PREDICATE = range(4)
+PH_AGG_COUNT, PH_AGG_SUM, PH_AGG_MIN, PH_AGG_MAX, PH_AGG_DISTINCTCOUNTHLL = range(5)
+
+
+class PinotHipError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class BadQueryError(PinotHipError):
+    """BadQueryRequestException (PredicateEvaluatorProvider.java:92-95)."""
+
+
+class UnsupportedError(PinotHipError):
+    """Shape not on the GPU path; the caller falls back to the CPU plan."""
+
+
+class ColumnDesc(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("data_type", ctypes.c_int32), ("cardinality", ctypes.c_int32),
+                ("bits_per_element", ctypes.c_int32), ("is_sorted", ctypes.c_int32),
+                ("forward_index", ctypes.c_void_p), ("forward_index_size", ctypes.c_uint64),
+                ("dictionary", ctypes.c_void_p), ("dictionary_size", ctypes.c_uint64),
+                ("dictionary_entry_size", ctypes.c_int32),
+                ("inverted_index", ctypes.c_void_p), ("inverted_index_size", ctypes.c_uint64)]
+
+
+class SegmentDesc(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("num_docs", ctypes.c_int32), ("num_columns", ctypes.c_int32),
+                ("columns", ctypes.POINTER(ColumnDesc))]
+
+
+class Predicate(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("column", ctypes.c_char_p), ("num_values", ctypes.c_int32),
+                ("values", ctypes.POINTER(ctypes.c_char_p)), ("lower", ctypes.c_char_p),
+                ("upper", ctypes.c_char_p), ("lower_inclusive", ctypes.c_int32),
+                ("upper_inclusive", ctypes.c_int32)]
+
+
+class FilterNode(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("num_children", ctypes.c_int32),
+                ("children", ctypes.POINTER(ctypes.c_int32)), ("predicate", ctypes.c_int32)]
+
+
+class Aggregation(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("column", ctypes.c_char_p), ("log2m", ctypes.c_int32)]
+
+
+class Query(ctypes.Structure):
+    _fields_ = [("num_filter_nodes", ctypes.c_int32), ("filter_nodes", ctypes.POINTER(FilterNode)),
+                ("filter_root", ctypes.c_int32), ("num_predicates", ctypes.c_int32),
+                ("predicates", ctypes.POINTER(Predicate)), ("num_group_by", ctypes.c_int32),
+                ("group_by", ctypes.POINTER(ctypes.c_char_p)), ("num_aggregations", ctypes.c_int32),
+                ("aggregations", ctypes.POINTER(Aggregation)), ("num_groups_limit", ctypes.c_int64)]
+
+
+class ExecStats(ctypes.Structure):
+    _fields_ = [("num_docs_scanned", ctypes.c_int64), ("num_entries_scanned_in_filter", ctypes.c_int64),
+                ("num_entries_scanned_post_filter", ctypes.c_int64), ("num_total_docs", ctypes.c_int64),
+                ("num_segments_processed", ctypes.c_int64), ("num_segments_matched", ctypes.c_int64),
+                ("num_groups_limit_reached", ctypes.c_int32), ("sum_precision_flag", ctypes.c_int32),
+                ("device_ms", ctypes.c_double), ("host_ms", ctypes.c_double)]
+
+
+# every symbol declared in include/pinot_hip.h
+EXPORTED_SYMBOLS = (
+    "ph_ctx_create", "ph_ctx_destroy", "ph_ctx_set_stream", "ph_segment_pin", "ph_segment_unpin",
+    "ph_segment_device_bytes", "ph_segment_num_docs", "ph_table_set_dictionary", "ph_query_execute",
+    "ph_result_destroy", "ph_result_stats", "ph_result_num_groups", "ph_result_key_entry_size", "ph_result_key_type",
+    "ph_result_group_keys", "ph_result_aggregation", "ph_fixed_bit_pack", "ph_selftest_unpack", "ph_last_error", "ph_version",
+)
+
+_lib = None
+
+
+def lib():
+    """Load libpinot_hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    sig = {
+        "ph_ctx_create": ([i32, ctypes.POINTER(vp)], ctypes.c_int),
+        "ph_ctx_destroy": ([vp], ctypes.c_int),
+        "ph_ctx_set_stream": ([vp, vp], ctypes.c_int),
+        "ph_segment_pin": ([vp, ctypes.POINTER(SegmentDesc), ctypes.POINTER(vp)], ctypes.c_int),
+        "ph_segment_unpin": ([vp], ctypes.c_int),
+        "ph_segment_device_bytes": ([vp], i64),
+        "ph_segment_num_docs": ([vp], i32),
+        "ph_table_set_dictionary": ([vp, ctypes.c_char_p, i32, vp, i64, i32], ctypes.c_int),
+        "ph_query_execute": ([vp, ctypes.POINTER(Query), ctypes.POINTER(vp), i32, ctypes.POINTER(vp)], ctypes.c_int),
+        "ph_result_destroy": ([vp], ctypes.c_int),
+        "ph_result_stats": ([vp, ctypes.POINTER(ExecStats)], ctypes.c_int),
+        "ph_result_num_groups": ([vp], i64),
+        "ph_result_key_entry_size": ([vp, i32], ctypes.c_int),
+        "ph_result_key_type": ([vp, i32], ctypes.c_int),
+        "ph_result_group_keys": ([vp, i32, vp], ctypes.c_int),
+        "ph_result_aggregation": ([vp, i32, vp], ctypes.c_int),
+        "ph_fixed_bit_pack": ([vp, i64, i32, vp, ctypes.c_uint64], ctypes.c_int),
+        "ph_selftest_unpack": ([vp, vp, ctypes.c_uint64, i64, i32, vp], ctypes.c_int),
+        "ph_last_error": ([], ctypes.c_char_p),
+        "ph_version": ([], ctypes.c_char_p),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(code: int):
+    if code == PH_OK:
+        return
+    msg = lib().ph_last_error().decode(errors="replace")
+    if code == PH_ERR_BAD_QUERY:
+        raise BadQueryError(code, msg)
+    if code == PH_ERR_UNSUPPORTED:
+        raise UnsupportedError(code, msg)
+    raise PinotHipError(code, msg)

@@ -1,0 +1,252 @@
+"""Segment creation (the writer side of the on-disk format) and HBM pinning.
+
+``create_segment`` produces, for each dictionary-encoded single-value column, the exact byte buffers a
+V3 Pinot segment holds in ``columns.psf`` (all big-endian):
+
+* dictionary       sorted unique values, fixed width (SegmentDictionaryCreator.java:100-276)
+* forward index    unsorted: dictIds packed MSB-first with bitsPerElement = getNumBitsPerValue(card-1)
+                   (FixedBitSVForwardIndexWriter.java:39-50, packed by ph_fixed_bit_pack);
+                   sorted: int32 (startDocId, endDocId) per dictId (SingleValueSortedForwardIndexCreator)
+* inverted index   uint32 offsets[card+1] then one portable-format RoaringBitmap per dictId
+                   (BitmapInvertedIndexWriter.java:33-96; RoaringFormatSpec, RoaringBitmap 0.9.38 serialize())
+
+``pin`` hands those buffers to ``ph_segment_pin`` (the GPU side of ImmutableSegmentLoader.load).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+
+from . import native as N
+
+
+def num_bits_per_value(max_value: int) -> int:
+    """PinotDataBitSet.getNumBitsPerValue (PinotDataBitSet.java:59-70)."""
+    if max_value <= 1:
+        return 1
+    return int(max_value).bit_length()
+
+
+def fixed_bit_pack(dict_ids: np.ndarray, bits: int) -> np.ndarray:
+    ids = np.ascontiguousarray(dict_ids, dtype=np.int32)
+    out = np.zeros((len(ids) * bits + 7) // 8, dtype=np.uint8)
+    N.check(N.lib().ph_fixed_bit_pack(ids.ctypes.data, len(ids), bits, out.ctypes.data, out.nbytes))
+    return out
+
+
+# --------------------------------------------------------------------------- roaring (portable format)
+SERIAL_COOKIE_NO_RUNCONTAINER = 12346
+SERIAL_COOKIE = 12347
+NO_OFFSET_THRESHOLD = 4
+
+
+def roaring_serialize(docs: np.ndarray, run_optimize: bool = False) -> bytes:
+    """Serialize a sorted set of doc ids in RoaringBitmap's portable format.  With ``run_optimize`` each
+    container takes the smallest of array / bitmap / run encodings (RoaringBitmap.runOptimize)."""
+    docs = np.asarray(docs, dtype=np.uint32)
+    if len(docs) == 0:
+        return np.array([SERIAL_COOKIE_NO_RUNCONTAINER, 0], dtype="<u4").tobytes()
+    keys, starts = np.unique(docs >> 16, return_index=True)
+    ends = np.append(starts[1:], len(docs))
+    size = len(keys)
+    kinds, payloads, cards = [], [], []
+    for k, s, e in zip(keys, starts, ends):
+        low = (docs[s:e] & 0xFFFF).astype(np.uint16)
+        card = e - s
+        nruns = 1 + int(np.count_nonzero(np.diff(low.astype(np.int32)) != 1))
+        arr_bytes = 2 * card if card <= 4096 else 1 << 30
+        bmp_bytes = 8192
+        run_bytes = 2 + 4 * nruns if run_optimize else 1 << 30
+        best = min(arr_bytes, bmp_bytes, run_bytes)
+        if best == run_bytes:
+            brk = np.flatnonzero(np.diff(low.astype(np.int32)) != 1)
+            rs = np.concatenate([[0], brk + 1])
+            re = np.concatenate([brk, [card - 1]])
+            runs = np.empty(2 * nruns, dtype="<u2")
+            runs[0::2] = low[rs]
+            runs[1::2] = low[re] - low[rs]
+            payloads.append(np.array([nruns], "<u2").tobytes() + runs.tobytes())
+            kinds.append(2)
+        elif best == arr_bytes:
+            payloads.append(low.astype("<u2").tobytes())
+            kinds.append(0)
+        else:
+            words = np.zeros(1024, dtype=np.uint64)
+            np.bitwise_or.at(words, low >> 6, np.left_shift(np.uint64(1), (low & 63).astype(np.uint64)))
+            payloads.append(words.astype("<u8").tobytes())
+            kinds.append(1)
+        cards.append(card)
+    has_runs = any(k == 2 for k in kinds)
+    head = bytearray()
+    if has_runs:
+        head += np.array([SERIAL_COOKIE | ((size - 1) << 16)], "<u4").tobytes()
+        flags = np.zeros((size + 7) // 8, np.uint8)
+        for i, k in enumerate(kinds):
+            if k == 2:
+                flags[i // 8] |= 1 << (i % 8)
+        head += flags.tobytes()
+        with_offsets = size >= NO_OFFSET_THRESHOLD
+    else:
+        head += np.array([SERIAL_COOKIE_NO_RUNCONTAINER, size], "<u4").tobytes()
+        with_offsets = True
+    desc = np.empty(2 * size, "<u2")
+    desc[0::2] = keys
+    desc[1::2] = np.array(cards) - 1
+    head += desc.tobytes()
+    pos = len(head) + (4 * size if with_offsets else 0)
+    offs = []
+    for p in payloads:
+        offs.append(pos)
+        pos += len(p)
+    if with_offsets:
+        head += np.array(offs, "<u4").tobytes()
+    return bytes(head) + b"".join(payloads)
+
+
+def build_inverted_index(dict_ids: np.ndarray, card: int, run_optimize: bool = False) -> np.ndarray:
+    order = np.argsort(dict_ids, kind="stable")
+    bounds = np.searchsorted(dict_ids[order], np.arange(card + 1), side="left")
+    blobs = [roaring_serialize(order[bounds[i]:bounds[i + 1]], run_optimize) for i in range(card)]
+    base = 4 * (card + 1)
+    offsets = np.empty(card + 1, dtype=np.int64)
+    offsets[0] = base
+    offsets[1:] = base + np.cumsum([len(b) for b in blobs])
+    return np.frombuffer(offsets.astype(">u4").tobytes() + b"".join(blobs), dtype=np.uint8)
+
+
+# --------------------------------------------------------------------------- column / segment buffers
+_NP = {"INT": ">i4", "LONG": ">i8", "FLOAT": ">f4", "DOUBLE": ">f8"}
+_NATIVE = {"INT": np.int32, "LONG": np.int64, "FLOAT": np.float32, "DOUBLE": np.float64}
+
+
+@dataclass
+class ColumnBuffers:
+    name: str
+    data_type: str
+    cardinality: int
+    bits: int
+    is_sorted: bool
+    forward_index: np.ndarray
+    dictionary: np.ndarray          # big-endian bytes
+    entry_size: int
+    dictionary_values: np.ndarray   # native values (for tests / reduce)
+    inverted_index: Optional[np.ndarray] = None
+
+
+@dataclass
+class SegmentBuffers:
+    name: str
+    num_docs: int
+    columns: Dict[str, ColumnBuffers] = field(default_factory=dict)
+
+
+def encode_dictionary(values: np.ndarray, data_type: str):
+    if data_type == "STRING":
+        enc = [str(v).encode("utf-8") for v in values]
+        width = max([len(e) for e in enc] + [1])
+        buf = np.zeros((len(enc), width), dtype=np.uint8)
+        for i, e in enumerate(enc):
+            buf[i, :len(e)] = np.frombuffer(e, dtype=np.uint8)
+        return buf.reshape(-1), width
+    arr = np.asarray(values, dtype=_NP[data_type])
+    return np.frombuffer(arr.tobytes(), dtype=np.uint8), arr.dtype.itemsize
+
+
+def create_column_from_dict_ids(name: str, dictionary: np.ndarray, dict_ids: np.ndarray, data_type: str,
+                                inverted: bool = False, allow_sorted: bool = True,
+                                run_optimize: bool = False) -> ColumnBuffers:
+    card = len(dictionary)
+    dict_ids = np.ascontiguousarray(dict_ids, dtype=np.int32)
+    bits = num_bits_per_value(card - 1)
+    is_sorted = allow_sorted and bool(len(dict_ids) == 0 or np.all(dict_ids[1:] >= dict_ids[:-1]))
+    if is_sorted:
+        starts = np.searchsorted(dict_ids, np.arange(card), side="left")
+        ends = np.searchsorted(dict_ids, np.arange(card), side="right") - 1
+        pairs = np.stack([starts, ends], axis=1).astype(">i4")
+        fwd = np.frombuffer(pairs.tobytes(), dtype=np.uint8)
+    else:
+        fwd = fixed_bit_pack(dict_ids, bits)
+    dbytes, width = encode_dictionary(dictionary, data_type)
+    inv = build_inverted_index(dict_ids, card, run_optimize) if inverted else None
+    return ColumnBuffers(name, data_type, card, bits, is_sorted, fwd, dbytes, width, np.asarray(dictionary), inv)
+
+
+def create_column(name: str, values, data_type: str, inverted: bool = False, run_optimize: bool = False):
+    if data_type == "STRING":
+        values = np.asarray(values).astype(str)
+    else:
+        values = np.asarray(values, dtype=_NATIVE[data_type])
+    dictionary, ids = np.unique(values, return_inverse=True)
+    return create_column_from_dict_ids(name, dictionary, ids.reshape(-1), data_type, inverted,
+                                       run_optimize=run_optimize)
+
+
+def create_segment(name: str, columns: Dict[str, tuple], inverted: Sequence[str] = (),
+                   run_optimize: bool = False) -> SegmentBuffers:
+    """columns: name -> (values, data_type) -- SegmentIndexCreationDriverImpl for dictionary SV columns."""
+    seg = SegmentBuffers(name, 0)
+    n = None
+    for c, (vals, dt) in columns.items():
+        seg.columns[c] = create_column(c, vals, dt, c in inverted, run_optimize)
+        n = len(vals) if n is None else n
+        if n != len(vals):
+            raise ValueError("columns of different lengths")
+    seg.num_docs = n or 0
+    return seg
+
+
+# --------------------------------------------------------------------------- pinning
+class PinnedSegment:
+    """An immutable segment resident in HBM (ph_segment)."""
+
+    def __init__(self, ctx, buffers: SegmentBuffers):
+        self.ctx = ctx
+        self.name = buffers.name
+        self.num_docs = buffers.num_docs
+        self.buffers = buffers
+        cols = (N.ColumnDesc * max(1, len(buffers.columns)))()
+        keep = []
+        for i, cb in enumerate(buffers.columns.values()):
+            d = cols[i]
+            nm = cb.name.encode()
+            keep.append(nm)
+            d.name = nm
+            d.data_type = N.DATA_TYPES[cb.data_type]
+            d.cardinality = cb.cardinality
+            d.bits_per_element = cb.bits
+            d.is_sorted = int(cb.is_sorted)
+            fwd = np.ascontiguousarray(cb.forward_index)
+            dic = np.ascontiguousarray(cb.dictionary)
+            keep += [fwd, dic]
+            d.forward_index = fwd.ctypes.data
+            d.forward_index_size = fwd.nbytes
+            d.dictionary = dic.ctypes.data
+            d.dictionary_size = dic.nbytes
+            d.dictionary_entry_size = cb.entry_size
+            if cb.inverted_index is not None:
+                inv = np.ascontiguousarray(cb.inverted_index)
+                keep.append(inv)
+                d.inverted_index = inv.ctypes.data
+                d.inverted_index_size = inv.nbytes
+        desc = N.SegmentDesc(buffers.name.encode(), buffers.num_docs, len(buffers.columns), cols)
+        h = ctypes.c_void_p()
+        N.check(N.lib().ph_segment_pin(ctx.handle, ctypes.byref(desc), ctypes.byref(h)))
+        self.handle = h
+
+    @property
+    def device_bytes(self) -> int:
+        return N.lib().ph_segment_device_bytes(self.handle)
+
+    def unpin(self):
+        if self.handle:
+            N.check(N.lib().ph_segment_unpin(self.handle))
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.unpin()
+        except Exception:
+            pass

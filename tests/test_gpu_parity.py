@@ -1,0 +1,256 @@
+"""GPU parity: libpinot_hip.so (through the C-ABI) vs the CPU oracle and the reference KATs.
+
+Bar: bit-exact for COUNT, integer SUM, MIN/MAX, HLL registers and group keys; DOUBLE SUM within 1e-9
+relative (BASELINE.json north_star).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from pinot_amd.query import parse_sql
+from pinot_amd.reduce import reduce_groups
+from pinot_amd.segment import create_segment
+from tests import kat_sv
+
+pytestmark = pytest.mark.gpu
+
+DOUBLE_RTOL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from pinot_amd.engine import GpuContext
+    c = GpuContext(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def sv(ctx):
+    cols = kat_sv.load_columns()
+    buf = create_segment("testTable_126164076_167572854", cols, inverted=kat_sv.INVERTED)
+    seg = ctx.pin(buf)
+    return [seg] * 4
+
+
+def rows_equal(got, exp, rtol=0.0):
+    assert len(got) == len(exp), (len(got), len(exp))
+    for g, e in zip(got, exp):
+        assert len(g) == len(e)
+        for a, b in zip(g, e):
+            if isinstance(b, float) and rtol and not (math.isinf(b) or b == 0):
+                assert abs(a - b) <= rtol * abs(b), (a, b)
+            else:
+                assert a == b, (g, e)
+
+
+@pytest.mark.parametrize("sql,rows,stats,src", kat_sv.KATS, ids=[k[3] for k in kat_sv.KATS])
+def test_reference_kat_on_gpu(ctx, sv, sql, rows, stats, src):
+    q = parse_sql(sql)
+    r = ctx.execute(q, sv)
+    table = reduce_groups(q, r.keys, r.aggs)
+    assert table.rows == rows, src
+    docs, post, total = stats
+    assert r.stats.num_total_docs == total
+    assert r.stats.num_docs_scanned == docs
+    assert r.stats.num_entries_scanned_post_filter == post
+
+
+def test_kat_filter_entries_gpu(ctx, sv):
+    r = ctx.execute(parse_sql("SELECT COUNT(*) FROM testTable" + kat_sv.FILTER), sv)
+    assert r.stats.num_entries_scanned_in_filter == 3 * 120000
+
+
+# ------------------------------------------------------------------ randomized parity vs the oracle
+def _random_table(rng, n, int_cards=(7, 300, 5000), with_strings=True, with_double=True):
+    cols = {
+        "a": (rng.integers(0, int_cards[0], n).astype(np.int32), "INT"),
+        "b": (rng.integers(-1000, 1000, n).astype(np.int32) * int(rng.integers(1, 5)), "INT"),
+        "c": (rng.integers(0, int_cards[2], n).astype(np.int64) * 1_000_003 - 7, "LONG"),
+        "m": (rng.integers(0, 1 << 30, n).astype(np.int32), "INT"),
+        "s": (np.sort(rng.integers(0, 40, n)).astype(np.int32), "INT"),  # sorted
+    }
+    if with_strings:
+        words = np.array(["", "P", "gFuH", "o", "t", "zz", "Ünï"])
+        cols["str"] = (words[rng.integers(0, len(words), n)], "STRING")
+    if with_double:
+        cols["d"] = (np.round(rng.normal(0, 1000, n), 3), "DOUBLE")
+    return cols
+
+
+def _both(ctx, cols_list, sql, inverted=(), run_opt=False, rtol=DOUBLE_RTOL):
+    q = parse_sql(sql)
+    gpu_segs = [ctx.pin(create_segment(f"s{i}", c, inverted=inverted, run_optimize=run_opt))
+                for i, c in enumerate(cols_list)]
+    ora_segs = [O.build_segment(f"s{i}", c, inverted=inverted) for i, c in enumerate(cols_list)]
+    r = ctx.execute(q, gpu_segs)
+    e = O.execute(q, ora_segs)
+    got = reduce_groups(q, r.keys, r.aggs)
+    exp = reduce_groups(q, e.keys, e.aggs)
+    rows_equal(got.rows, exp.rows, rtol)
+    # HLL registers are compared raw (bit-exact), not only via the estimate
+    for k, a in enumerate(q.aggregations):
+        if a.function == "DISTINCTCOUNTHLL":
+            gmap = {key: row[k] for key, row in zip(r.keys, r.aggs)}
+            for key, row in zip(e.keys, e.aggs):
+                assert np.array_equal(gmap[key], row[k])
+    assert r.stats.num_docs_scanned == e.stats.num_docs_scanned
+    assert r.stats.num_total_docs == e.stats.num_total_docs
+    assert r.stats.num_entries_scanned_post_filter == e.stats.num_entries_scanned_post_filter
+    return r, got
+
+
+FILTERS = [
+    "",
+    " WHERE a = 3",
+    " WHERE a <> 3",
+    " WHERE a IN (1, 2, 5)",
+    " WHERE a NOT IN (0, 6)",
+    " WHERE b BETWEEN -500 AND 250",
+    " WHERE b > 0 AND m < 536870912",
+    " WHERE (a = 1 OR b >= 900) AND NOT c < 0",
+    " WHERE s BETWEEN 10 AND 20",
+    " WHERE s IN (3, 7, 30) OR a = 2",
+    " WHERE s <> 5 AND a NOT IN (1)",
+    " WHERE str = 'gFuH'",
+    " WHERE str NOT IN ('t', 'P') AND b < 100",
+    " WHERE str > 'o'",
+    " WHERE d > 0.5",
+    " WHERE a = 99",
+    " WHERE a >= 0",
+    " WHERE NOT (a IN (0, 1, 2, 3, 4, 5, 6))",
+]
+
+
+@pytest.mark.parametrize("where", FILTERS)
+def test_random_aggregation_only(ctx, where):
+    rng = np.random.default_rng(abs(hash(where)) % 2**32)
+    tables = [_random_table(rng, n) for n in (20_000, 777, 64 * 300 + 1)]
+    _both(ctx, tables, "SELECT COUNT(*), SUM(m), MIN(b), MAX(c), SUM(d), MIN(d), MAX(d) FROM t" + where,
+          inverted=("a", "str"))
+
+
+@pytest.mark.parametrize("where", FILTERS[:12])
+@pytest.mark.parametrize("group", ["a", "str", "s", "a, str", "s, a, str", "b", "c"])
+def test_random_group_by(ctx, where, group):
+    rng = np.random.default_rng((abs(hash(where + group))) % 2**32)
+    tables = [_random_table(rng, n) for n in (9_999, 30_000)]
+    _both(ctx, tables, f"SET numGroupsLimit=10000000; SELECT {group}, COUNT(*), SUM(m), MIN(d), MAX(b), SUM(d) "
+                       f"FROM t{where} GROUP BY {group} ORDER BY {group} LIMIT 100000", inverted=("a", "str"))
+
+
+@pytest.mark.parametrize("bits", list(range(1, 23)))
+def test_every_bit_width_scan(ctx, bits):
+    rng = np.random.default_rng(bits)
+    n = max(50_000, (1 << (bits - 1)) + 5_000)
+    card = min(1 << bits, n)
+    vals = rng.permutation(np.concatenate([np.arange(card), rng.integers(0, card, n - card)])).astype(np.int32)
+    t = {"v": (vals, "INT"), "m": (rng.integers(0, 100, n).astype(np.int32), "INT")}
+    lo, hi = card // 4, card // 4 + max(1, card // 3)
+    _both(ctx, [t], f"SELECT COUNT(*), SUM(m), MIN(v), MAX(v) FROM t WHERE v BETWEEN {lo} AND {hi}")
+
+
+@pytest.mark.parametrize("bits", list(range(1, 32)))
+def test_device_unpack_every_width(ctx, bits):
+    # the kernel's unpack routine on raw packed streams of every width 1..31 (FixedBitIntReaderTest widths)
+    import ctypes
+    from pinot_amd import native as N
+    rng = np.random.default_rng(1000 + bits)
+    for n in (1, 63, 64, 65, 100_003):
+        ids = rng.integers(0, 1 << bits, n, dtype=np.int64).astype(np.int32)
+        packed = O.fixed_bit_pack(ids, bits)
+        out = np.zeros(n, np.int32)
+        N.check(N.lib().ph_selftest_unpack(ctx.handle, packed.ctypes.data, packed.nbytes, n, bits,
+                                           out.ctypes.data))
+        assert np.array_equal(out, ids), (bits, n)
+
+
+def test_wide_bits_31(ctx):
+    rng = np.random.default_rng(31)
+    n = 4096 + 17
+    vals = rng.integers(-2**31, 2**31 - 1, n, dtype=np.int64).astype(np.int32)
+    vals[:2] = [-2**31, 2**31 - 1]
+    t = {"v": (vals, "INT")}
+    _both(ctx, [t], "SELECT COUNT(*), SUM(v), MIN(v), MAX(v) FROM t WHERE v > -1000000")
+
+
+def test_hll_parity(ctx):
+    rng = np.random.default_rng(3)
+    tables = []
+    for n in (50_000, 12_345):
+        tables.append({"u": (rng.integers(0, 1 << 27, n).astype(np.int32), "INT"),
+                       "l": (rng.integers(0, 1 << 40, n).astype(np.int64), "LONG"),
+                       "st": (np.array([f"k{v}" for v in rng.integers(0, 3000, n)]), "STRING"),
+                       "dd": (rng.normal(size=n), "DOUBLE"),
+                       "c": (rng.integers(0, 100, n).astype(np.int32), "INT")})
+    _both(ctx, tables, "SELECT DISTINCTCOUNTHLL(u), DISTINCTCOUNTHLL(l), DISTINCTCOUNTHLL(st), "
+                       "DISTINCTCOUNTHLL(dd) FROM t WHERE c IN (1, 5, 9, 77)", inverted=("c",))
+    _both(ctx, tables, "SELECT DISTINCTCOUNTHLL(u) FROM t WHERE c IN (1, 5, 9, 77)", inverted=("c",), run_opt=True)
+    _both(ctx, tables, "SELECT c, DISTINCTCOUNTHLL(u, 10) FROM t WHERE c < 20 GROUP BY c ORDER BY c", inverted=("c",))
+    _both(ctx, tables, "SELECT DISTINCTCOUNTHLL(u, 12) FROM t")
+
+
+def test_inverted_index_containers(ctx):
+    # dense values -> bitmap containers; runs -> run containers; sparse -> array containers
+    n = 300_000
+    a = np.zeros(n, np.int32)
+    a[::2] = 1
+    a[100_000:180_000] = 2
+    a[rng_idx(n, 50)] = 3
+    t = {"a": (a, "INT"), "m": (np.arange(n, dtype=np.int32) % 1000, "INT")}
+    for run_opt in (False, True):
+        for where in ("a = 1", "a IN (2, 3)", "a NOT IN (1)", "a <> 0"):
+            _both(ctx, [t], f"SELECT COUNT(*), SUM(m) FROM t WHERE {where}", inverted=("a",), run_opt=run_opt)
+
+
+def rng_idx(n, k):
+    return np.random.default_rng(1).choice(n, k, replace=False)
+
+
+def test_segments_with_different_dictionaries(ctx):
+    rng = np.random.default_rng(8)
+    t1 = {"g": (rng.integers(0, 10, 5000).astype(np.int32) * 2, "INT"), "m": (rng.integers(0, 9, 5000).astype(np.int32), "INT")}
+    t2 = {"g": (rng.integers(5, 30, 7000).astype(np.int32), "INT"), "m": (rng.integers(0, 9, 7000).astype(np.int32) - 4, "INT")}
+    t3 = {"g": (np.full(100, 1000, np.int32), "INT"), "m": (np.full(100, 7, np.int32), "INT")}
+    _both(ctx, [t1, t2, t3], "SELECT g, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t GROUP BY g ORDER BY g LIMIT 1000")
+
+
+def test_empty_and_no_match(ctx):
+    rng = np.random.default_rng(9)
+    t = _random_table(rng, 1000)
+    r, got = _both(ctx, [t], "SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t WHERE a = 12345")
+    assert got.rows == [[0, 0.0, math.inf, -math.inf]]
+    r, got = _both(ctx, [t], "SELECT a, COUNT(*) FROM t WHERE b > 100000 GROUP BY a ORDER BY a")
+    assert got.rows == []
+    _both(ctx, [t], "SELECT COUNT(*) FROM t WHERE a = 1 AND a = 2")
+
+
+def test_large_group_key_space_global_table(ctx):
+    # product of cardinalities beyond the LDS budget -> HBM dense table with device-scope atomics
+    rng = np.random.default_rng(12)
+    n = 400_000
+    t = {"g1": (rng.integers(0, 1000, n).astype(np.int32), "INT"),
+         "g2": (rng.integers(0, 300, n).astype(np.int32), "INT"),
+         "m": (rng.integers(0, 1 << 20, n).astype(np.int32), "INT"),
+         "f": (rng.integers(0, 1000, n).astype(np.int32), "INT")}
+    _both(ctx, [t, t], "SET numGroupsLimit=2000000; SELECT g1, g2, SUM(m), COUNT(*), MIN(m), MAX(m) FROM t "
+                       "WHERE f BETWEEN 0 AND 499 GROUP BY g1, g2 ORDER BY g1, g2 LIMIT 2000000")
+
+
+def test_group_limit_unsupported_is_reported(ctx):
+    from pinot_amd.native import UnsupportedError
+    rng = np.random.default_rng(13)
+    t = {"g": (rng.integers(0, 5000, 10000).astype(np.int32), "INT")}
+    seg = ctx.pin(create_segment("x", t))
+    with pytest.raises(UnsupportedError):
+        ctx.execute(parse_sql("SET numGroupsLimit=100; SELECT g, COUNT(*) FROM t GROUP BY g"), [seg])
+
+
+def test_bad_query_is_reported(ctx, sv):
+    from pinot_amd.native import BadQueryError
+    with pytest.raises(BadQueryError):
+        ctx.execute(parse_sql("SELECT COUNT(*) FROM t WHERE nope = 3"), sv)
+    with pytest.raises(BadQueryError):
+        ctx.execute(parse_sql("SELECT COUNT(*) FROM t WHERE column1 > 'abc'"), sv)
