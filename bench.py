@@ -24,11 +24,30 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-QUERY = ("SET numGroupsLimit=2000000; SET minServerGroupTrimSize=-1; SET minSegmentGroupTrimSize=-1; "
-         "SELECT g1, g2, SUM(m), COUNT(*), MIN(m), MAX(m) FROM t WHERE f BETWEEN 0 AND 499 "
-         "GROUP BY g1, g2 ORDER BY g1, g2 LIMIT 2000000")
-COLS = {"g1": (1000, 10), "g2": (1000, 10), "m": (65536, 16), "f": (1000, 10)}
+# workload -> (query, columns {name: (cardinality, bits)}, description)
+WORKLOADS = {
+    # headline (BASELINE.json configs[2] with the SURVEY 8(d) filter): ~1M groups
+    "config3": ("SET numGroupsLimit=2000000; SET minServerGroupTrimSize=-1; SET minSegmentGroupTrimSize=-1; "
+                "SELECT g1, g2, SUM(m), COUNT(*), MIN(m), MAX(m) FROM t WHERE f BETWEEN 0 AND 499 "
+                "GROUP BY g1, g2 ORDER BY g1, g2 LIMIT 2000000",
+                {"g1": (1000, 10), "g2": (1000, 10), "m": (65536, 16), "f": (1000, 10)},
+                "config3: WHERE f BETWEEN 0 AND 499 GROUP BY g1, g2 (1e6 groups) SUM(m), COUNT(*), MIN(m), MAX(m)"),
+    # BASELINE.json configs[1]: pure unpack + predicate scan, b = 20
+    "config2": ("SELECT COUNT(*) FROM t WHERE v BETWEEN 100000 AND 199999",
+                {"v": (1 << 20, 20)}, "config2: COUNT(*) WHERE v BETWEEN (10% of a 2^20 domain), b = 20"),
+    # SURVEY 8(d) config 3 LDS-regime variant: g1 only with C = 100
+    "config3-lds": ("SELECT g1, SUM(m), COUNT(*), MIN(m), MAX(m) FROM t WHERE f BETWEEN 0 AND 499 "
+                    "GROUP BY g1 ORDER BY g1 LIMIT 1000",
+                    {"g1": (100, 7), "m": (65536, 16), "f": (1000, 10)},
+                    "config3-lds: WHERE f BETWEEN 0 AND 499 GROUP BY g1 (C=100) SUM/COUNT/MIN/MAX(m)"),
+    # aggregation-only over the config-3 metric
+    "config3-agg": ("SELECT SUM(m), COUNT(*), MIN(m), MAX(m) FROM t WHERE f BETWEEN 0 AND 499",
+                    {"m": (65536, 16), "f": (1000, 10)}, "config3-agg: WHERE f BETWEEN 0 AND 499 SUM/COUNT/MIN/MAX(m)"),
+}
+QUERY, COLS, _ = WORKLOADS["config3"]
 HBM_PEAK_GBS = 8000.0
+KERNEL_NAMES = {0: "k_scan<MODE_COUNT>", 1: "k_scan<MODE_AGG>", 2: "k_scan<MODE_GROUP_LDS>",
+                3: "k_scan<MODE_GROUP_GLOBAL>", 4: "k_scan<MODE_PARTITION> + k_part_agg (overlapped)"}
 
 
 def log(*a):
@@ -40,12 +59,13 @@ def m_dictionary():
     return np.sort(rng.choice(1 << 20, 65536, replace=False)).astype(np.int32)
 
 
-def make_segment_buffers(seg_index, rows, seed):
+def make_segment_buffers(seg_index, rows, seed, cols=None):
     from pinot_amd.segment import ColumnBuffers, SegmentBuffers, encode_dictionary, fixed_bit_pack
+    cols = COLS if cols is None else cols
     rng = np.random.default_rng([seed, seg_index])
     seg = SegmentBuffers(f"t_{seed}_{seg_index}", rows)
     mdict = m_dictionary()
-    for name, (card, bits) in COLS.items():
+    for name, (card, bits) in cols.items():
         ids = rng.integers(0, card, rows, dtype=np.int32)
         dictionary = mdict if name == "m" else np.arange(card, dtype=np.int32)
         dbytes, width = encode_dictionary(dictionary, "INT")
@@ -54,8 +74,9 @@ def make_segment_buffers(seg_index, rows, seed):
     return seg
 
 
-def algorithmic_bytes(rows_per_seg, nseg):
-    return nseg * sum((rows_per_seg * b + 7) // 8 for _, b in COLS.values())
+def algorithmic_bytes(rows_per_seg, nseg, cols=None):
+    cols = COLS if cols is None else cols
+    return nseg * sum((rows_per_seg * b + 7) // 8 for _, b in cols.values())
 
 
 def cpu_baseline(bufs, query, threads):
@@ -78,6 +99,7 @@ def main():
     ap.add_argument("--cpu-segments", type=int, default=-1, help="segments in the CPU-baseline sample (-1: auto)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--workload", default="config3", choices=sorted(WORKLOADS))
     args = ap.parse_args()
 
     import torch
@@ -94,24 +116,25 @@ def main():
     from pinot_amd.engine import GpuContext
     from pinot_amd.query import parse_sql
 
-    q = parse_sql(QUERY)
+    query, cols, wdesc = WORKLOADS[args.workload]
+    q = parse_sql(query)
     nseg = max(1, args.rows // args.segment_rows)
     seg_rows = args.rows // nseg
     t0 = time.time()
     ctx = GpuContext(device)
     bufs, pinned = [], []
     for i in range(nseg):
-        b = make_segment_buffers(i, seg_rows, seed=1000 + rank)
+        b = make_segment_buffers(i, seg_rows, seed=1000 + rank, cols=cols)
         pinned.append(ctx.pin(b))
         bufs.append(b)
         if i % 10 == 9:
             log(f"[rank {rank}] pinned {i + 1}/{nseg} segments ({time.time() - t0:.1f}s)")
     # table-level dictionaries: identical on every rank, so group ids align for the RCCL merge
-    ctx.set_table_dictionary("g1", "INT", np.arange(1000, dtype=np.int32))
-    ctx.set_table_dictionary("g2", "INT", np.arange(1000, dtype=np.int32))
+    for g in q.group_by:
+        ctx.set_table_dictionary(g, "INT", np.arange(cols[g][0], dtype=np.int32))
 
     def step():
-        return ctx.execute(q, pinned)
+        return ctx.execute(q, pinned, copy=False)
 
     for _ in range(args.warmup):
         r = step()
@@ -135,11 +158,11 @@ def main():
     total_rows = nseg * seg_rows * world
     value = total_rows / (ms_per_step / 1000.0)
     kernel_ms = float(np.mean(dev_ms))
-    alg = algorithmic_bytes(seg_rows, nseg)
+    alg = algorithmic_bytes(seg_rows, nseg, cols)
     achieved = alg / (kernel_ms / 1000.0) / 1e9
 
     result = {
-        "metric": "filter+group-by rows/s (1B rows/GPU, ~1M groups, SUM/COUNT/MIN/MAX)",
+        "metric": "filter+group-by rows/s and achieved HBM GB/s, 1B rows",
         "value": value,
         "unit": "rows/s",
         "n_gpus": world,
@@ -151,14 +174,13 @@ def main():
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (seeded PCG64 dictIds, 100 x 10M-doc segments per GPU)",
-        "config": {"workload": "config3: WHERE f BETWEEN 0 AND 499 GROUP BY g1, g2 (1e6 groups) "
-                               "SUM(m), COUNT(*), MIN(m), MAX(m)",
+        "config": {"workload": wdesc,
                    "rows_per_gpu": nseg * seg_rows, "segments_per_gpu": nseg, "parallelism": f"segments x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_scan<MODE_GROUP_GLOBAL>", "kernel_ms": kernel_ms,
+                     "kernel": KERNEL_NAMES.get(r.stats.mode, "k_scan"), "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": alg},
-        "groups": len(r.keys),
+        "groups": r.num_groups,
         "docs_scanned": r.stats.num_docs_scanned,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -170,15 +192,19 @@ def main():
                                   "sample": f"{ncpu} segments x {seg_rows} rows, same data and query, oracle "
                                             f"(C restatement of the reference loop nest), {dt:.2f}s"}
         if not args.no_parity:
-            # parity on the sample: GPU over the same segments vs the oracle (count / integer sum / min / max
-            # bit-exact, group keys exact)
+            # parity on the sample: GPU over the same segments vs the oracle -- group keys, COUNT, integer
+            # SUM, MIN, MAX bit-exact (synthetic group dictionaries are 0..C-1, so value == global id)
             r = ctx.execute(q, pinned[:ncpu])
             order = np.argsort(keys)
             k_cpu = keys[order]
             a_cpu = aggs[order]
-            k_gpu = np.array([g1 + 1000 * g2 for (g1, g2) in r.keys], dtype=np.uint64)
+            k_gpu = np.zeros(r.num_groups, np.uint64)
+            stride = 1
+            for gi, g in enumerate(q.group_by):
+                k_gpu += r.key_columns[gi].astype(np.uint64) * np.uint64(stride)
+                stride *= cols[g][0]
             og = np.argsort(k_gpu)
-            a_gpu = np.array(r.aggs, dtype=np.float64)[og]
+            a_gpu = np.stack([c.astype(np.float64) for c in r.agg_columns], axis=1)[og]
             ok = bool(np.array_equal(k_gpu[og], k_cpu) and np.array_equal(a_gpu, a_cpu))
             result["parity_sample"] = {"segments": ncpu, "groups": int(len(k_cpu)), "bit_exact": ok}
     if rank == 0:

@@ -142,6 +142,9 @@ typedef struct {
   int32_t sum_precision_flag;              /* 1 if an integer SUM reached 2^53 (double rounding differs) */
   double device_ms;                        /* kernel time of the query, HIP events */
   double host_ms;                          /* planning + result materialisation */
+  int32_t plan_mode;                       /* physical plan: -1 metadata, 0 count, 1 aggregation, 2 LDS
+                                              group table, 3 HBM atomic group table, 4 partitioned */
+  int32_t reserved;
 } ph_exec_stats;
 
 /* ------------------------------------------------------------------ context */
@@ -175,9 +178,13 @@ int ph_result_key_entry_size(const ph_result* r, int32_t group_by_index);
 /* stored ph_data_type of group-by column i's key values */
 int ph_result_key_type(const ph_result* r, int32_t group_by_index);
 int ph_result_group_keys(const ph_result* r, int32_t group_by_index, void* out);
+/* zero-copy views of the same columns, valid until ph_result_destroy (results must be destroyed before
+ * their context) */
+const void* ph_result_key_data(const ph_result* r, int32_t group_by_index);
 /* intermediate result of aggregation i for every row: COUNT int64, SUM/MIN/MAX double,
  * DISTINCTCOUNTHLL uint8[2^log2m] raw registers (HyperLogLog.addAll = register-wise max) */
 int ph_result_aggregation(const ph_result* r, int32_t aggregation_index, void* out);
+const void* ph_result_aggregation_data(const ph_result* r, int32_t aggregation_index);
 
 /* ------------------------------------------------------------------ segment creation helper */
 /* FixedBitSVForwardIndexWriter: packs n dictIds with `bits` bits, MSB-first big-endian; out_size >=

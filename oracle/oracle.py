@@ -484,6 +484,12 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> Oracl
             vals.append(_py(u[gk % card]))
             gk //= card
         keys.append(tuple(vals))
+    # AggregationPlanNode.java:108-119: no filter, no group-by and only COUNT/MIN/MAX/DISTINCTCOUNTHLL on
+    # dictionary columns -> NonScanBasedAggregationOperator (answered from dictionaries / metadata:
+    # numDocsScanned = totalDocs, numEntriesScannedPostFilter = 0)
+    if q.filter is None and not q.group_by and q.aggregations and all(
+            a.function in ("COUNT", "MIN", "MAX", "DISTINCTCOUNTHLL") for a in q.aggregations):
+        stats[2] = 0
     return OracleResult(keys, merged, OracleStats(*stats))
 
 

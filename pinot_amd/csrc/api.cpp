@@ -60,6 +60,7 @@ int ph_ctx_create(int32_t device_ordinal, ph_ctx** out) {
       PH_HIP_CHECK(hipSetDevice(device_ordinal));
       PH_HIP_CHECK(hipStreamCreateWithFlags(&c.own_stream, hipStreamNonBlocking));
       c.stream = c.own_stream;
+      PH_HIP_CHECK(hipStreamCreateWithFlags(&c.stream_b, hipStreamNonBlocking));
       PH_HIP_CHECK(hipEventCreate(&c.ev_start));
       PH_HIP_CHECK(hipEventCreate(&c.ev_stop));
       hipDeviceProp_t prop;
@@ -82,7 +83,10 @@ int ph_ctx_destroy(ph_ctx* ctx) {
     if (c.ev_start) (void)hipEventDestroy(c.ev_start);
     if (c.ev_stop) (void)hipEventDestroy(c.ev_stop);
     if (c.own_stream) (void)hipStreamDestroy(c.own_stream);
+    if (c.stream_b) (void)hipStreamDestroy(c.stream_b);
+    for (auto e : c.ev_pool) (void)hipEventDestroy(e);
     if (c.pinned) (void)hipHostFree(c.pinned);
+    for (auto& kv : c.pinned_free) (void)hipHostFree(kv.second);
     delete ctx;
   });
 }
@@ -152,8 +156,8 @@ int ph_table_set_dictionary(ph_ctx* ctx, const char* column, int32_t data_type, 
     }
     for (int64_t i = 1; i < count; ++i)
       if (d.compare(i - 1, d, i) >= 0) fail(PH_ERR_INVALID_ARGUMENT, "table dictionary must be sorted and unique");
-    std::lock_guard<std::mutex> lk(ctx->c.mu);
     g->id = ctx->c.next_id++;
+    std::lock_guard<std::mutex> lk(ctx->c.mu);
     ctx->c.table_dicts[column] = g;
   });
 }
@@ -189,6 +193,16 @@ int ph_result_key_entry_size(const ph_result* r, int32_t i) {
 int ph_result_key_type(const ph_result* r, int32_t i) {
   if (!r || i < 0 || i >= (int32_t)r->key_types.size()) return -1;
   return r->key_types[i];
+}
+
+const void* ph_result_key_data(const ph_result* r, int32_t i) {
+  if (!r || i < 0 || i >= (int32_t)r->keys.size()) return nullptr;
+  return r->keys[i].data();
+}
+
+const void* ph_result_aggregation_data(const ph_result* r, int32_t k) {
+  if (!r || k < 0 || k >= (int32_t)r->aggs.size()) return nullptr;
+  return r->aggs[k].data();
 }
 
 int ph_result_group_keys(const ph_result* r, int32_t i, void* out) {

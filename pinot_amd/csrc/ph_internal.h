@@ -13,6 +13,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -43,7 +44,7 @@ constexpr int kMaxAggs = 8;       // aggregation functions per query
 constexpr int kMaxGroupCols = 4;  // group-by columns
 constexpr int kMaxProg = 64;      // filter program length per segment
 constexpr int kMaxStack = 30;     // filter evaluation stack depth (bits of a uint32)
-constexpr int kFwdPadBytes = 64;
+constexpr int kFwdPadBytes = 1024;  // >= one staged span: the scan reads whole 64-doc words
 
 // ------------------------------------------------------------------ device structs
 struct DevColumn {
@@ -75,15 +76,49 @@ struct FilterInsn {
   const uint32_t* ptr;
 };
 
+// Single-leaf filters are specialised (the common shapes); anything else runs the postfix program.
+enum : int32_t { FK_ALL = 0, FK_RANGE = 1, FK_SET = 2, FK_BITMAP = 3, FK_DOCRANGE = 4, FK_GENERIC = 5 };
+
+// How an aggregated numeric column is read:
+//   VK_PACKED   frame-of-reference stream (value - base) in `bits`, built once per column in HBM from the
+//               dictionary-encoded forward index (no per-row dictionary gather on the hot path)
+//   VK_DICT_I64 dictId stream + int64 dictionary table      VK_DICT_F64 dictId stream + float64 table
+enum : int32_t { VK_PACKED = 0, VK_DICT_I64 = 1, VK_DICT_F64 = 2 };
+constexpr int kMaxVals = 4;
+constexpr int kMaxHll = 4;
+
+struct DevValCol {
+  const uint32_t* fwd;
+  const void* table;
+  int64_t base;
+  int32_t bits;
+  int32_t kind;
+};
+
+// A packed bit stream the hot loop reads (dictId or frame-of-reference values).  The first `nstage`
+// streams of a query are staged per wave through LDS: one 16-byte-per-lane coalesced load covers the
+// U consecutive 64-doc words of a wave (U * 8 * bits bytes), then every lane extracts its doc's bits.
+constexpr int kMaxStreams = 8;
+constexpr int kMaxStage = 4;
+constexpr int kStageBytes = 1024;  // per stream per wave: U * 8 * 31 + 8 <= 1000
+struct DevStream {
+  const uint32_t* fwd;
+  int32_t bits;
+  int32_t pad;
+};
+
 struct DevSegment {
   int32_t num_docs;
+  int32_t fkind;       // FK_*
+  int32_t fslot;       // FK_RANGE / FK_SET column slot
+  uint32_t flo, flen;  // FK_RANGE: [flo, flo + flen) ; FK_DOCRANGE: [flo, flo + flen) docs
   int32_t prog_off;
   int32_t prog_len;
-  int32_t fast_range;  // 1: program is a single OP_RANGE on slot fast_col
-  int32_t fast_col;
-  uint32_t fast_lo, fast_len;
   int32_t pad;
+  const uint32_t* fptr;  // FK_SET bitset over dictIds ; FK_BITMAP doc bitmap
   DevColumn cols[kMaxCols];
+  DevValCol vals[kMaxVals];
+  DevStream streams[kMaxStreams];  // packed bit streams read by the scan loop (staged ones first)
 };
 
 struct Chunk {
@@ -95,30 +130,75 @@ struct Chunk {
 
 enum : int32_t { AGG_COUNT = 0, AGG_SUM = 1, AGG_MIN = 2, AGG_MAX = 3, AGG_HLL = 4 };
 
-enum : int32_t { MODE_COUNT = 0, MODE_AGG = 1, MODE_GROUP_LDS = 2, MODE_GROUP_GLOBAL = 3 };
+enum : int32_t { MODE_COUNT = 0, MODE_AGG = 1, MODE_GROUP_LDS = 2, MODE_GROUP_GLOBAL = 3, MODE_PARTITION = 4 };
+
+constexpr int kPartShards = 8;
+constexpr int kPartBlock = 512;  // per-partition write cursors, sharded to spread the reservation atomics
 
 struct KParams {
   const DevSegment* segs;
   const FilterInsn* prog;
   const Chunk* chunks;
-  int32_t num_chunks;
+  int32_t chunk_begin;  // this launch covers chunks [chunk_begin, chunk_end)
+  int32_t chunk_end;
+  int32_t nstage;                 // streams staged through LDS (<= kMaxStage)
+  int32_t f_stream;               // FK_RANGE / FK_SET filter column stream
+  int32_t g_stream[kMaxGroupCols];
+  int32_t v_stream[kMaxVals];
+  int32_t stage_off;              // byte offset of the per-wave staging area in dynamic LDS
+  int32_t lds_cnt_off;            // MODE_GROUP_LDS: byte offset of the count table
   int32_t num_group_cols;
   int32_t group_slot[kMaxGroupCols];
   int64_t group_stride[kMaxGroupCols];
   int64_t num_groups;  // dense key space (1 for aggregation-only)
-  int32_t num_aggs;
-  int32_t num_hll;
+  int32_t num_vals;               // distinct aggregated value columns
+  int32_t num_hll;                // DISTINCTCOUNTHLL register sets
   int32_t log2m;
   int32_t lds_bytes;
-  int32_t agg_type[kMaxAggs];
-  int32_t agg_slot[kMaxAggs];
-  int32_t agg_is_int[kMaxAggs];   // value table is int64 (else double)
-  int32_t agg_hll[kMaxAggs];      // HLL register-set index
-  int32_t lds_off[kMaxAggs];      // MODE_GROUP_LDS: byte offset of the aggregation's table
+  // value-column-centric aggregation state (SUM/MIN/MAX of one column share one decode)
+  int32_t val_ops[kMaxVals];      // bit 0 SUM, bit 1 MIN, bit 2 MAX
+  int32_t val_is_int[kMaxVals];   // int64 arithmetic (else float64 SUM, order-key MIN/MAX)
+  void* out_sum[kMaxVals];        // [num_groups] int64 or double
+  int64_t* out_min[kMaxVals];     // [num_groups] int64 order keys
+  int64_t* out_max[kMaxVals];
+  int32_t lds_sum_off[kMaxVals];  // MODE_GROUP_LDS byte offsets
+  int32_t lds_min_off[kMaxVals];
+  int32_t lds_max_off[kMaxVals];
+  int32_t hll_slot[kMaxHll];      // column slot of each HLL register set
   int32_t lds_hll_off;
   unsigned long long* out_count;  // [num_groups] matched docs per group
-  void* out_agg[kMaxAggs];        // [num_groups]: int64 SUM / ordered MIN/MAX keys, or double SUM
   uint32_t* out_hll;              // [num_groups][num_hll][2^log2m]
+  // MODE_PARTITION (kernel A) -- records to per-partition buffers
+  int32_t part_klo;               // key bits kept in a record (keys per partition = 1 << part_klo)
+  int32_t part_vbits;             // value-offset bits in a record (0: COUNT only)
+  int32_t num_parts;
+  int32_t part_cap;               // records per (shard, partition)
+  int64_t part_vbase;             // record value = value - part_vbase
+  void* part_buf;                 // [kPartShards][num_parts][part_cap] records
+  uint32_t* part_cursor;          // [kPartShards][num_parts]
+  unsigned long long* ovf_count;  // overflow table (same layout as out_*), merged at the end
+  int64_t* ovf_sum;
+  int64_t* ovf_min;
+  int64_t* ovf_max;
+};
+
+// Kernel B of the partitioned group-by: aggregates one batch of records per partition in LDS, then merges
+// the partition's key range into the dense result table (each key range has exactly one owner block).
+struct PartAggParams {
+  const void* part_buf;
+  uint32_t* part_cursor;  // reset to 0 after reading
+  int32_t num_parts;
+  int32_t part_cap;
+  int32_t part_klo;
+  int32_t part_vbits;
+  int32_t rec64;
+  int32_t has_sum, has_min, has_max;
+  int64_t part_vbase;
+  int64_t num_groups;
+  unsigned long long* out_count;
+  int64_t* out_sum;
+  int64_t* out_min;
+  int64_t* out_max;
 };
 
 // order-preserving int64 key of a double (MIN/MAX of FLOAT/DOUBLE columns)
@@ -184,6 +264,10 @@ struct Column {
   DeviceBuffer d_inverted;
   std::mutex cache_mu;
   std::map<int, HllTable> hll_tables;                                // by log2m
+  bool vpacked_ready = false;                                        // VK_PACKED stream built
+  std::unique_ptr<DeviceBuffer> d_vpacked;
+  int64_t vbase = 0;
+  int32_t vbits = 0;
   std::map<uint64_t, std::shared_ptr<DeviceBuffer>> remaps;          // by global dictionary id
   bool has_inverted() const { return !inverted.empty(); }
 };
@@ -206,6 +290,8 @@ namespace ph {
 struct GlobalDict {
   uint64_t id;
   Dictionary dict;
+  std::mutex mu;
+  std::unique_ptr<DeviceBuffer> d_values;  // int64 (INT/LONG) or float64 (FLOAT/DOUBLE) values, on demand
 };
 
 struct Context {
@@ -213,20 +299,43 @@ struct Context {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  hipStream_t stream_b = nullptr;           // partitioned group-by: kernel B overlaps kernel A
+  std::vector<hipEvent_t> ev_pool;          // batch hand-off events
   int num_cus = 256;
   std::mutex mu;  // serialises queries on this context
   std::map<std::string, std::shared_ptr<GlobalDict>> table_dicts;   // ph_table_set_dictionary
   std::map<std::string, std::shared_ptr<GlobalDict>> union_cache;   // column + segment-set -> union
-  uint64_t next_id = 1;
+  std::atomic<uint64_t> next_id{1};
   // scratch
   std::vector<std::unique_ptr<DeviceBuffer>> scratch;
   void* pinned = nullptr;
   size_t pinned_bytes = 0;
   void* host_staging(size_t n);
+  // pinned host blocks for result columns (D2H lands directly in the result; returned on destroy)
+  std::mutex pool_mu;
+  std::multimap<size_t, void*> pinned_free;
+  void* pinned_acquire(size_t n, size_t* cap);
+  void pinned_release(void* p, size_t cap);
 };
 
 // kernels.hip
-void launch_scan(const KParams& p, int mode, int grid, int block, size_t lds, hipStream_t s);
+void launch_scan(const KParams& p, int mode, int ngroup, int rec64, int grid, int block, size_t lds, hipStream_t s);
+void launch_part_agg(const PartAggParams& p, size_t lds, hipStream_t s);
+size_t partition_stage_offset(int rec64);
+struct MergeParams {
+  unsigned long long* out_count;
+  int64_t* out_sum;
+  int64_t* out_min;
+  int64_t* out_max;
+  const unsigned long long* ovf_count;
+  const int64_t* ovf_sum;
+  const int64_t* ovf_min;
+  const int64_t* ovf_max;
+  int64_t n;
+};
+void launch_merge_overflow(const MergeParams& p, hipStream_t s);
+void launch_encode_values(const uint32_t* fwd, int32_t bits, const int64_t* table, int64_t base, int32_t vbits,
+                          int64_t n, uint32_t* out, hipStream_t s);
 void launch_fill_i64(int64_t* p, int64_t v, int64_t n, hipStream_t s);
 void launch_hll_table(const void* values, int32_t is_int, int64_t n, int log2m, uint32_t* out, hipStream_t s);
 struct RoaringContainer {
@@ -240,6 +349,29 @@ void launch_roaring_or(const RoaringContainer* c, int n, const uint8_t* base, ui
                        hipStream_t s);
 void launch_selftest_unpack(const uint32_t* fwd, int64_t n, int bits, int32_t* out, hipStream_t s);
 
+// device-side result compaction of a dense group table (non-empty groups, keys decoded, values converted)
+constexpr int kCompactBlocks = 2048;
+enum : int32_t { CK_COUNT = 0, CK_INT = 1, CK_REAL_SUM = 2, CK_REAL_ORDER = 3 };
+struct CompactParams {
+  int64_t num_groups;
+  int64_t chunk;  // groups per block
+  const unsigned long long* count;
+  int32_t num_aggs;
+  int32_t num_keys;
+  const int64_t* agg_src[kMaxAggs];
+  int32_t agg_kind[kMaxAggs];
+  double* agg_out[kMaxAggs];
+  int64_t key_stride[kMaxGroupCols];
+  int64_t key_size[kMaxGroupCols];
+  const void* key_table[kMaxGroupCols];  // nullptr: emit the int32 global id (STRING keys)
+  int32_t key_type[kMaxGroupCols];
+  void* key_out[kMaxGroupCols];
+  int64_t* count_out;
+  unsigned long long* blk;   // [kCompactBlocks + 1] counts -> offsets, total at [kCompactBlocks]
+  int32_t* flags;            // bit 0: an integer SUM reached 2^53
+};
+void launch_compact(const CompactParams& p, hipStream_t s);
+
 // host helpers
 int32_t murmur_hash_long(int64_t v);
 int32_t murmur_hash_bytes(const uint8_t* data, int32_t len, int32_t seed);
@@ -248,13 +380,36 @@ void fixed_bit_pack_host(const int32_t* ids, int64_t n, int bits, uint8_t* out);
 
 }  // namespace ph
 
+// A result column: small ones live in a host vector, large ones in a pinned block of the context's pool
+// (device-compacted results are copied straight into it).
+struct ResultBuf {
+  std::vector<uint8_t> host;
+  void* pinned = nullptr;
+  size_t cap = 0;
+  size_t n = 0;
+  void assign(size_t bytes, uint8_t v) {
+    host.assign(bytes, v);
+    n = bytes;
+  }
+  uint8_t* data() { return pinned ? static_cast<uint8_t*>(pinned) : host.data(); }
+  const uint8_t* data() const { return pinned ? static_cast<const uint8_t*>(pinned) : host.data(); }
+  size_t size() const { return n; }
+};
+
 struct ph_result {
+  ph::Context* ctx = nullptr;
   std::vector<int32_t> key_types;
   std::vector<int32_t> key_entry_size;
-  std::vector<std::vector<uint8_t>> keys;   // per group-by column, num_groups * entry_size
+  std::vector<ResultBuf> keys;   // per group-by column, num_groups * entry_size
   std::vector<int32_t> agg_types;
   std::vector<int32_t> agg_log2m;
-  std::vector<std::vector<uint8_t>> aggs;   // per aggregation
+  std::vector<ResultBuf> aggs;   // per aggregation
   int64_t num_groups = 0;
+  int32_t mode = 0;
   ph_exec_stats stats{};
+  ~ph_result() {
+    for (auto* v : {&keys, &aggs})
+      for (auto& b : *v)
+        if (b.pinned && ctx) ctx->pinned_release(b.pinned, b.cap);
+  }
 };

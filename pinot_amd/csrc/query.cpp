@@ -435,10 +435,7 @@ std::shared_ptr<GlobalDict> build_union(Context* ctx, const std::string& col, co
   }
   auto g = std::make_shared<GlobalDict>();
   g->dict = std::move(u);
-  {
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    g->id = ctx->next_id++;
-  }
+  g->id = ctx->next_id++;
   return g;
 }
 
@@ -465,6 +462,22 @@ const int32_t* segment_remap(Context* ctx, Column& c, const GlobalDict& g) {
   }
   c.remaps[g.id] = buf;
   return buf ? buf->as<int32_t>() : nullptr;
+}
+
+// table-level dictionary values on the device (group-key decoding in the compaction kernel)
+const void* global_dict_device_values(Context* ctx, GlobalDict& g) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  if (g.dict.type == PH_STRING) return nullptr;
+  if (!g.d_values) {
+    auto b = std::make_unique<DeviceBuffer>();
+    const int64_t n = std::max<int64_t>(1, g.dict.size);
+    b->alloc(8 * n, ctx->device);
+    const void* src = (g.dict.type == PH_INT || g.dict.type == PH_LONG) ? (const void*)g.dict.ints.data()
+                                                                        : (const void*)g.dict.reals.data();
+    PH_HIP_CHECK(hipMemcpy(b->ptr, src, 8 * g.dict.size, hipMemcpyHostToDevice));
+    g.d_values = std::move(b);
+  }
+  return g.d_values->ptr;
 }
 
 const uint32_t* segment_hll_table(Context* ctx, Column& c, int log2m) {
@@ -537,6 +550,44 @@ struct QueryScratch {
   }
 };
 
+namespace {
+
+int bits_for_range(uint64_t range) {
+  int b = 0;
+  while (b < 64 && (range >> b) != 0) ++b;
+  return b;
+}
+
+// Frame-of-reference value stream of an INT/LONG column (VK_PACKED), built once per pinned column.
+bool ensure_value_stream(Context* ctx, ph_segment* seg, Column& c) {
+  std::lock_guard<std::mutex> lk(c.cache_mu);
+  if (c.vpacked_ready) return c.d_vpacked != nullptr;
+  c.vpacked_ready = true;
+  if (c.data_type != PH_INT && c.data_type != PH_LONG) return false;
+  if (c.cardinality <= 0 || seg->num_docs == 0) return false;
+  const int64_t lo = c.dict.ints.front(), hi = c.dict.ints.back();
+  const uint64_t range = (uint64_t)hi - (uint64_t)lo;
+  const int vb = std::max(1, bits_for_range(range));
+  if (vb > 31) return false;
+  // only worth it when it avoids a dictionary gather of meaningful size
+  const int64_t n = seg->num_docs;
+  const size_t bytes = (size_t)((n * vb + 7) / 8);
+  const size_t alloc = ((bytes + kFwdPadBytes + 255) / 256) * 256;
+  auto buf = std::make_unique<DeviceBuffer>();
+  buf->alloc(alloc, ctx->device);
+  PH_HIP_CHECK(hipMemsetAsync(buf->ptr, 0, alloc, ctx->stream));
+  launch_encode_values(c.d_fwd.as<uint32_t>(), c.bits, c.d_values.as<int64_t>(), lo, vb, n, buf->as<uint32_t>(),
+                       ctx->stream);
+  PH_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  c.vbase = lo;
+  c.vbits = vb;
+  seg->device_bytes += (int64_t)alloc;
+  c.d_vpacked = std::move(buf);
+  return true;
+}
+
+}  // namespace
+
 ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const* segs_in, int32_t nseg) {
   using clock = std::chrono::steady_clock;
   const auto t0 = clock::now();
@@ -572,15 +623,19 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     group_cols.push_back(q->group_by[g]);
     add_slot(q->group_by[g]);
   }
-  int log2m = 0, num_hll = 0;
-  std::vector<int> agg_hll(q->num_aggregations, -1);
+  // aggregation -> (value column, op) / HLL register set
+  const int nagg = q->num_aggregations;
+  int log2m = 0;
+  std::vector<std::string> val_cols, hll_cols;
+  std::vector<int> val_ops;
+  std::vector<int> agg_val(nagg, -1), agg_hll(nagg, -1);
   std::set<std::string> projected(group_cols.begin(), group_cols.end());
-  for (int k = 0; k < q->num_aggregations; ++k) {
+  for (int k = 0; k < nagg; ++k) {
     const ph_aggregation& a = q->aggregations[k];
-    res->agg_types.push_back(a.type);
-    int lm = a.type == PH_AGG_DISTINCTCOUNTHLL ? (a.log2m > 0 ? a.log2m : 8) : 0;
-    res->agg_log2m.push_back(lm);
     if (a.type < PH_AGG_COUNT || a.type > PH_AGG_DISTINCTCOUNTHLL) fail(PH_ERR_UNSUPPORTED, "aggregation type");
+    res->agg_types.push_back(a.type);
+    const int lm = a.type == PH_AGG_DISTINCTCOUNTHLL ? (a.log2m > 0 ? a.log2m : 8) : 0;
+    res->agg_log2m.push_back(lm);
     if (a.type == PH_AGG_COUNT) continue;
     if (!a.column) fail(PH_ERR_BAD_QUERY, "aggregation needs a column");
     add_slot(a.column);
@@ -589,27 +644,52 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       if (lm < 4 || lm > 16) fail(PH_ERR_UNSUPPORTED, "log2m out of range");
       if (log2m && lm != log2m) fail(PH_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL with different log2m in one query");
       log2m = lm;
-      agg_hll[k] = num_hll++;
+      auto it = std::find(hll_cols.begin(), hll_cols.end(), std::string(a.column));
+      if (it == hll_cols.end()) {
+        if ((int)hll_cols.size() >= kMaxHll) fail(PH_ERR_UNSUPPORTED, "too many DISTINCTCOUNTHLL columns");
+        hll_cols.push_back(a.column);
+        agg_hll[k] = (int)hll_cols.size() - 1;
+      } else {
+        agg_hll[k] = (int)(it - hll_cols.begin());
+      }
+      continue;
     }
+    auto it = std::find(val_cols.begin(), val_cols.end(), std::string(a.column));
+    int j;
+    if (it == val_cols.end()) {
+      if ((int)val_cols.size() >= kMaxVals) fail(PH_ERR_UNSUPPORTED, "too many aggregated columns");
+      val_cols.push_back(a.column);
+      val_ops.push_back(0);
+      j = (int)val_cols.size() - 1;
+    } else {
+      j = (int)(it - val_cols.begin());
+    }
+    agg_val[k] = j;
+    val_ops[j] |= a.type == PH_AGG_SUM ? 1 : (a.type == PH_AGG_MIN ? 2 : 4);
   }
+  const int nvals = (int)val_cols.size(), num_hll = (int)hll_cols.size();
   if (q->filter_root >= 0)
     for (int i = 0; i < q->num_predicates; ++i) {
       if (!q->predicates[i].column) fail(PH_ERR_BAD_QUERY, "predicate without column");
       add_slot(q->predicates[i].column);
     }
   if ((int)slot_names.size() > kMaxCols) fail(PH_ERR_UNSUPPORTED, "too many columns in one query");
+  std::vector<int> val_is_int(nvals, 1);
   for (auto* s : segs)
     for (auto& c : slot_names) {
       auto it = s->columns.find(c);
       if (it == s->columns.end()) fail(PH_ERR_BAD_QUERY, "Column not found: " + c + " in segment " + s->name);
-      for (int k = 0; k < q->num_aggregations; ++k) {
-        const ph_aggregation& a = q->aggregations[k];
-        if (a.column && c == a.column && (a.type == PH_AGG_SUM || a.type == PH_AGG_MIN || a.type == PH_AGG_MAX) &&
-            it->second->data_type == PH_STRING)
-          fail(PH_ERR_UNSUPPORTED, "numeric aggregation on STRING column " + c);
-      }
     }
-  const int nagg = q->num_aggregations;
+  for (int j = 0; j < nvals; ++j) {
+    for (size_t i = 0; i < segs.size(); ++i) {
+      const int dt = segs[i]->columns.at(val_cols[j])->data_type;
+      if (dt == PH_STRING) fail(PH_ERR_UNSUPPORTED, "numeric aggregation on STRING column " + val_cols[j]);
+      const int is_int = dt == PH_INT || dt == PH_LONG;
+      if (i == 0) val_is_int[j] = is_int;
+      else if (val_is_int[j] != is_int)
+        fail(PH_ERR_UNSUPPORTED, "aggregation column with mixed integer/real types across segments");
+    }
+  }
   const int m = log2m ? (1 << log2m) : 0;
 
   // ---- aggregation-only, no filter, metadata-answerable (NonScanBasedAggregationOperator)
@@ -655,6 +735,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     stats.num_docs_scanned = stats.num_total_docs;
     stats.num_segments_matched = nseg;
+    stats.plan_mode = -1;
     stats.host_ms = std::chrono::duration<double, std::milli>(clock::now() - t0).count();
     return res.release();
   }
@@ -662,33 +743,18 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // ---- per-segment filter plans
   QueryScratch scratch(ctx->device);
   std::vector<SegProgram> progs(nseg);
+  std::vector<PNode> roots(nseg);
   std::vector<char> seg_live(nseg, 1);
-  std::vector<int> seg_fast(nseg, 0);
   for (int i = 0; i < nseg; ++i) {
     PNode root;
     root.kind = L_ALL;
     if (q->filter_root >= 0) root = pl.build(segs[i], q->filter_root, 0);
     stats.num_entries_scanned_in_filter += (int64_t)segs[i]->num_docs * count_scan_leaves(root);
-    if (root.kind == L_NONE || segs[i]->num_docs == 0) {
-      seg_live[i] = 0;
-      continue;
-    }
-    if (root.kind == L_ALL) {
-      seg_fast[i] = 2;
-      continue;
-    }
-    if (root.op == OP_RANGE) seg_fast[i] = 1;
-    emit(root, progs[i]);
-    if (progs[i].max_depth > kMaxStack || (int)progs[i].insns.size() > kMaxProg)
-      fail(PH_ERR_UNSUPPORTED, "filter too large for the GPU program");
-    for (auto& in : progs[i].insns)
-      if ((in.op == OP_AND || in.op == OP_OR) && in.col > kMaxStack) fail(PH_ERR_UNSUPPORTED, "filter too wide");
+    if (root.kind == L_NONE || segs[i]->num_docs == 0) seg_live[i] = 0;
+    roots[i] = std::move(root);
   }
 
   // ---- inverted-index leaves -> device doc bitmaps
-  for (auto& b : pl.bitmaps) {
-    (void)b;
-  }
   std::vector<uint32_t*> bitmap_dev(pl.bitmaps.size(), nullptr);
   for (size_t i = 0; i < pl.bitmaps.size(); ++i) {
     BitmapLeaf& b = pl.bitmaps[i];
@@ -701,9 +767,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       RoaringContainer* dc = scratch.alloc<RoaringContainer>(cs.size());
       PH_HIP_CHECK(hipMemcpyAsync(dc, cs.data(), sizeof(RoaringContainer) * cs.size(), hipMemcpyHostToDevice, st));
       launch_roaring_or(dc, (int)cs.size(), b.col->d_inverted.as<uint8_t>(), bm, b.seg->num_docs, st);
+      PH_HIP_CHECK(hipStreamSynchronize(st));  // `cs` is pageable host memory
     }
     bitmap_dev[i] = bm;
-    PH_HIP_CHECK(hipStreamSynchronize(st));  // `cs` is pageable host memory
   }
 
   // ---- group-by key space over table-level dictionaries
@@ -727,92 +793,130 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
     }
     gdicts.push_back(gd);
-    if (gd->dict.size <= 0) gd->dict.size = 1;
-    if (num_groups > (int64_t(1) << 40) / gd->dict.size) fail(PH_ERR_UNSUPPORTED, "group key space too large");
-    num_groups *= gd->dict.size;
+    const int64_t sz = std::max<int64_t>(1, gd->dict.size);
+    if (num_groups > (int64_t(1) << 40) / sz) fail(PH_ERR_UNSUPPORTED, "group key space too large");
+    num_groups *= sz;
   }
   // numGroupsLimit: segments whose key space exceeds the limit may drop groups in the reference
   // (first-seen order, IntGroupIdMap.getGroupId :992-1017); that emulation is not on the GPU path.
   if (q->num_group_by > 0) {
     const int64_t limit = q->num_groups_limit > 0 ? q->num_groups_limit : 100000;
     for (auto* s : segs) {
-      int64_t p = 1;
-      for (auto& g : group_cols) p = std::min<int64_t>(p * s->columns.at(g)->cardinality, int64_t(1) << 40);
-      if (p > limit)
-        fail(PH_ERR_UNSUPPORTED, "segment " + s->name + ": product of group-by cardinalities " + std::to_string(p) +
+      int64_t pp = 1;
+      for (auto& g : group_cols) pp = std::min<int64_t>(pp * s->columns.at(g)->cardinality, int64_t(1) << 40);
+      if (pp > limit)
+        fail(PH_ERR_UNSUPPORTED, "segment " + s->name + ": product of group-by cardinalities " + std::to_string(pp) +
                                      " exceeds numGroupsLimit " + std::to_string(limit));
     }
   }
+  const int64_t G = num_groups;
 
-  // ---- mode selection
-  int mode;
-  size_t lds = 0;
+  // ---- kernel parameters
   KParams kp{};
-  kp.num_aggs = nagg;
+  kp.num_vals = nvals;
   kp.num_hll = num_hll;
   kp.log2m = log2m ? log2m : 8;
-  kp.num_groups = num_groups;
+  kp.num_groups = G;
   kp.num_group_cols = q->num_group_by;
-  for (int g = 0, stride = 1; g < q->num_group_by; ++g) (void)stride;
   {
     int64_t stride = 1;
     for (int g = 0; g < q->num_group_by; ++g) {
       kp.group_slot[g] = pl.slot.at(group_cols[g]);
       kp.group_stride[g] = stride;
-      stride *= gdicts[g]->dict.size;
+      stride *= std::max<int64_t>(1, gdicts[g]->dict.size);
     }
   }
-  bool only_count = true;
-  for (int k = 0; k < nagg; ++k) {
-    const ph_aggregation& a = q->aggregations[k];
-    kp.agg_type[k] = a.type;
-    kp.agg_hll[k] = agg_hll[k] < 0 ? 0 : agg_hll[k];
-    if (a.type != PH_AGG_COUNT) {
-      only_count = false;
-      kp.agg_slot[k] = pl.slot.at(a.column);
-      const int dt = segs.empty() ? PH_INT : segs[0]->columns.at(a.column)->data_type;
-      kp.agg_is_int[k] = (dt == PH_INT || dt == PH_LONG);
-      for (auto* s : segs)
-        if ((s->columns.at(a.column)->data_type == PH_INT || s->columns.at(a.column)->data_type == PH_LONG) !=
-            (bool)kp.agg_is_int[k])
-          fail(PH_ERR_UNSUPPORTED, "aggregation column with mixed integer/real types across segments");
-    }
+  for (int j = 0; j < nvals; ++j) {
+    kp.val_ops[j] = val_ops[j];
+    kp.val_is_int[j] = val_is_int[j];
   }
+  for (int h = 0; h < num_hll; ++h) kp.hll_slot[h] = pl.slot.at(hll_cols[h]);
+
+  // packed streams of the hot loop: slot 0 = the single-leaf filter column of each segment (if any),
+  // then the group-by columns, then the aggregated value columns; the first kMaxStage are LDS-staged
+  std::vector<std::string> stream_cols;  // "" for the per-segment filter slot
+  if (q->filter_root >= 0) stream_cols.push_back("");
+  kp.f_stream = 0;
+  auto stream_of = [&](const std::string& c, const char* kind) {
+    std::string key = std::string(kind) + ":" + c;
+    for (size_t i = 0; i < stream_cols.size(); ++i)
+      if (stream_cols[i] == key) return (int)i;
+    stream_cols.push_back(key);
+    return (int)stream_cols.size() - 1;
+  };
+  for (int g = 0; g < q->num_group_by; ++g) kp.g_stream[g] = stream_of(group_cols[g], "id");
+  for (int j = 0; j < nvals; ++j) kp.v_stream[j] = stream_of(val_cols[j], "val");
+  if ((int)stream_cols.size() > kMaxStreams) fail(PH_ERR_UNSUPPORTED, "too many column streams in one query");
+  kp.nstage = std::min<int>(kMaxStage, (int)stream_cols.size());
+  const size_t stage_bytes = (size_t)(256 / 64) * kMaxStage * kStageBytes;  // 256-thread blocks
+
+  // value column encodings + the table-wide value range (partitioned records carry value - vmin)
+  int64_t vmin = INT64_MAX, vmax = INT64_MIN;
+  for (int j = 0; j < nvals; ++j)
+    for (auto* s : segs) {
+      Column& c = *s->columns.at(val_cols[j]);
+      if (val_is_int[j] && c.cardinality > 0 && j == 0) {
+        vmin = std::min(vmin, c.dict.ints.front());
+        vmax = std::max(vmax, c.dict.ints.back());
+      }
+    }
+
+  // ---- mode selection
+  int mode;
+  size_t lds = 16;
+  int rec64 = 0;
+  kp.stage_off = 0;
   if (q->num_group_by == 0) {
-    mode = only_count ? MODE_COUNT : MODE_AGG;
-    lds = (size_t)num_hll * (m ? m : 1) * 4 + 16;
-    kp.lds_hll_off = 0;
+    mode = (nvals == 0 && num_hll == 0) ? MODE_COUNT : MODE_AGG;
+    kp.lds_hll_off = (int32_t)stage_bytes;
+    lds = stage_bytes + (size_t)num_hll * (m ? m : 1) * 4 + 16;
   } else {
-    size_t off = ((size_t)num_groups * 4 + 15) / 16 * 16;
-    for (int k = 0; k < nagg; ++k) {
-      if (kp.agg_type[k] == AGG_COUNT || kp.agg_type[k] == AGG_HLL) continue;
-      kp.lds_off[k] = (int32_t)std::min<size_t>(off, INT32_MAX);
-      off += (size_t)num_groups * 8;
-      off = (off + 15) / 16 * 16;
+    kp.lds_cnt_off = (int32_t)stage_bytes;
+    size_t off = stage_bytes + ((size_t)G * 4 + 15) / 16 * 16;
+    for (int j = 0; j < nvals; ++j) {
+      auto place = [&](int32_t& o) {
+        o = (int32_t)std::min<size_t>(off, INT32_MAX);
+        off += (size_t)G * 8;
+        off = (off + 15) / 16 * 16;
+      };
+      if (val_ops[j] & 1) place(kp.lds_sum_off[j]);
+      if (val_ops[j] & 2) place(kp.lds_min_off[j]);
+      if (val_ops[j] & 4) place(kp.lds_max_off[j]);
     }
     kp.lds_hll_off = (int32_t)std::min<size_t>(off, INT32_MAX);
-    off += (size_t)num_groups * num_hll * (m ? m : 1) * 4;
-    if (off <= 64 * 1024) {
+    off += (size_t)G * num_hll * (m ? m : 1) * 4;
+    const bool part_ok = num_hll == 0 && nvals <= 1 && (nvals == 0 || (val_is_int[0] && vmax >= vmin &&
+                                                                       (uint64_t)(vmax - vmin) < (1ull << 32))) &&
+                         G <= (int64_t(1) << 32) && getenv("PH_DISABLE_PARTITION") == nullptr;
+    if (off <= stage_bytes + 64 * 1024) {
       mode = MODE_GROUP_LDS;
       lds = off;
+    } else if (part_ok && G >= 65536) {
+      mode = MODE_PARTITION;
     } else {
       mode = MODE_GROUP_GLOBAL;
-      lds = 16;
-      const double bytes = (double)num_groups * (8 + 8.0 * nagg + 4.0 * num_hll * (m ? m : 1));
+      lds = stage_bytes + 16;
+      const double bytes = (double)G * (8 + 8.0 * 3 * nvals + 4.0 * num_hll * (m ? m : 1));
       if (bytes > 32e9) fail(PH_ERR_UNSUPPORTED, "dense group table too large for HBM budget");
     }
   }
 
   // ---- outputs
-  const int64_t G = num_groups;
   kp.out_count = scratch.alloc<unsigned long long>(G);
   PH_HIP_CHECK(hipMemsetAsync(kp.out_count, 0, sizeof(unsigned long long) * G, st));
-  for (int k = 0; k < nagg; ++k) {
-    const int t = kp.agg_type[k];
-    if (t == AGG_COUNT || t == AGG_HLL) continue;
-    kp.out_agg[k] = scratch.alloc<int64_t>(G);
-    if (t == AGG_SUM) PH_HIP_CHECK(hipMemsetAsync(kp.out_agg[k], 0, 8 * G, st));
-    else launch_fill_i64((int64_t*)kp.out_agg[k], t == AGG_MIN ? INT64_MAX : INT64_MIN, G, st);
+  for (int j = 0; j < nvals; ++j) {
+    if (val_ops[j] & 1) {
+      kp.out_sum[j] = scratch.alloc<int64_t>(G);
+      PH_HIP_CHECK(hipMemsetAsync(kp.out_sum[j], 0, 8 * G, st));
+    }
+    if (val_ops[j] & 2) {
+      kp.out_min[j] = scratch.alloc<int64_t>(G);
+      launch_fill_i64(kp.out_min[j], INT64_MAX, G, st);
+    }
+    if (val_ops[j] & 4) {
+      kp.out_max[j] = scratch.alloc<int64_t>(G);
+      launch_fill_i64(kp.out_max[j], INT64_MIN, G, st);
+    }
   }
   const int64_t hll_words = G * num_hll * (m ? m : 1);
   if (num_hll) {
@@ -826,23 +930,47 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<Chunk> chunks;
   constexpr int kChunkWords = 256;  // 16384 docs per chunk
   std::vector<std::pair<size_t, std::vector<uint32_t>>> payload_fix;  // global insn index -> payload
-  std::vector<std::pair<size_t, int>> bitmap_fix;
+  std::vector<std::pair<size_t, int>> bitmap_fix;                     // global insn index -> bitmap leaf
+  std::vector<std::pair<size_t, std::vector<uint32_t>>> fset_fix;     // segment index -> FK_SET bitset
+  std::vector<std::pair<size_t, int>> fbitmap_fix;                    // segment index -> bitmap leaf
   for (int i = 0; i < nseg; ++i) {
     if (!seg_live[i]) continue;
     ph_segment* s = segs[i];
     DevSegment d{};
     d.num_docs = s->num_docs;
-    d.prog_off = (int32_t)all_insns.size();
-    d.prog_len = (int32_t)progs[i].insns.size();
-    d.fast_range = seg_fast[i];
-    if (seg_fast[i] == 1) {
-      d.fast_col = progs[i].insns[0].col;
-      d.fast_lo = progs[i].insns[0].lo;
-      d.fast_len = progs[i].insns[0].len;
+    const PNode& root = roots[i];
+    const size_t si = dsegs.size();
+    if (root.kind == L_ALL) {
+      d.fkind = FK_ALL;
+    } else if (root.op == OP_RANGE) {
+      d.fkind = FK_RANGE;
+      d.fslot = root.col;
+      d.flo = root.lo;
+      d.flen = root.len;
+    } else if (root.op == OP_SET) {
+      d.fkind = FK_SET;
+      d.fslot = root.col;
+      fset_fix.push_back({si, root.set});
+    } else if (root.op == OP_BITMAP) {
+      d.fkind = FK_BITMAP;
+      fbitmap_fix.push_back({si, root.bitmap_leaf});
+    } else if (root.op == OP_DOCRANGES && root.ranges.size() == 2) {
+      d.fkind = FK_DOCRANGE;
+      d.flo = (uint32_t)root.ranges[0];
+      d.flen = (uint32_t)(root.ranges[1] - root.ranges[0] + 1);
+    } else {
+      d.fkind = FK_GENERIC;
+      emit(root, progs[i]);
+      if (progs[i].max_depth > kMaxStack || (int)progs[i].insns.size() > kMaxProg)
+        fail(PH_ERR_UNSUPPORTED, "filter too large for the GPU program");
+      for (auto& in : progs[i].insns)
+        if ((in.op == OP_AND || in.op == OP_OR) && in.col > kMaxStack) fail(PH_ERR_UNSUPPORTED, "filter too wide");
+      d.prog_off = (int32_t)all_insns.size();
+      d.prog_len = (int32_t)progs[i].insns.size();
+      for (auto& pp : progs[i].payloads) payload_fix.push_back({d.prog_off + pp.first, pp.second});
+      for (auto& bb : progs[i].bitmap_refs) bitmap_fix.push_back({d.prog_off + bb.first, bb.second});
+      all_insns.insert(all_insns.end(), progs[i].insns.begin(), progs[i].insns.end());
     }
-    for (auto& pp : progs[i].payloads) payload_fix.push_back({d.prog_off + pp.first, pp.second});
-    for (auto& bb : progs[i].bitmap_refs) bitmap_fix.push_back({d.prog_off + bb.first, bb.second});
-    all_insns.insert(all_insns.end(), progs[i].insns.begin(), progs[i].insns.end());
     for (size_t sl = 0; sl < slot_names.size(); ++sl) {
       Column& c = *s->columns.at(slot_names[sl]);
       DevColumn& dc = d.cols[sl];
@@ -853,22 +981,55 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     for (int g = 0; g < q->num_group_by; ++g)
       d.cols[kp.group_slot[g]].remap = segment_remap(ctx, *s->columns.at(group_cols[g]), *gdicts[g]);
-    for (int k = 0; k < nagg; ++k)
-      if (q->aggregations[k].type == PH_AGG_DISTINCTCOUNTHLL)
-        d.cols[kp.agg_slot[k]].hll = segment_hll_table(ctx, *s->columns.at(q->aggregations[k].column), log2m);
+    for (int h = 0; h < num_hll; ++h)
+      d.cols[kp.hll_slot[h]].hll = segment_hll_table(ctx, *s->columns.at(hll_cols[h]), log2m);
+    for (int j = 0; j < nvals; ++j) {
+      Column& c = *s->columns.at(val_cols[j]);
+      DevValCol& v = d.vals[j];
+      if (val_is_int[j] && ensure_value_stream(ctx, s, c)) {
+        v.kind = VK_PACKED;
+        v.fwd = c.d_vpacked->as<uint32_t>();
+        v.bits = c.vbits;
+        v.base = c.vbase;
+      } else {
+        v.kind = val_is_int[j] ? VK_DICT_I64 : VK_DICT_F64;
+        v.fwd = c.d_fwd.as<uint32_t>();
+        v.bits = c.bits;
+        v.table = c.d_values.ptr;
+      }
+      d.streams[kp.v_stream[j]] = DevStream{v.fwd, v.bits, 0};
+    }
+    for (int g = 0; g < q->num_group_by; ++g) {
+      Column& c = *s->columns.at(group_cols[g]);
+      d.streams[kp.g_stream[g]] = DevStream{c.d_fwd.as<uint32_t>(), c.bits, 0};
+    }
+    if (q->filter_root >= 0) {
+      // bits = 0: nothing to stage for this segment's filter (FK_ALL / bitmap / doc range / program)
+      d.streams[0] = DevStream{nullptr, 0, 0};
+      if (d.fkind == FK_RANGE || d.fkind == FK_SET) {
+        Column& c = *s->columns.at(slot_names[d.fslot]);
+        d.streams[0] = DevStream{c.d_fwd.as<uint32_t>(), c.bits, 0};
+      }
+    }
     const int32_t words = (s->num_docs + 63) / 64;
-    const int32_t seg_index = (int32_t)dsegs.size();
-    for (int32_t w = 0; w < words; w += kChunkWords) chunks.push_back({seg_index, w, std::min(words, w + kChunkWords), 0});
+    for (int32_t w = 0; w < words; w += kChunkWords)
+      chunks.push_back({(int32_t)si, w, std::min(words, w + kChunkWords), 0});
     dsegs.push_back(d);
     stats.num_segments_matched++;
   }
-  // payload buffers
   for (auto& pf : payload_fix) {
     uint32_t* dp = scratch.alloc<uint32_t>(pf.second.size() + 1);
     PH_HIP_CHECK(hipMemcpyAsync(dp, pf.second.data(), 4 * pf.second.size(), hipMemcpyHostToDevice, st));
     all_insns[pf.first].ptr = dp;
   }
   for (auto& bf : bitmap_fix) all_insns[bf.first].ptr = bitmap_dev[bf.second];
+  for (auto& ff : fset_fix) {
+    uint32_t* dp = scratch.alloc<uint32_t>(ff.second.size() + 1);
+    PH_HIP_CHECK(hipMemcpyAsync(dp, ff.second.data(), 4 * ff.second.size(), hipMemcpyHostToDevice, st));
+    dsegs[ff.first].fptr = dp;
+  }
+  for (auto& fb : fbitmap_fix) dsegs[fb.first].fptr = bitmap_dev[fb.second];
+  PH_HIP_CHECK(hipStreamSynchronize(st));  // pageable payload copies above
 
   float dev_ms = 0.f;
   if (!chunks.empty()) {
@@ -887,59 +1048,277 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     kp.segs = d_segs;
     kp.prog = d_prog;
     kp.chunks = d_chunks;
-    kp.num_chunks = (int32_t)chunks.size();
     kp.lds_bytes = (int32_t)lds;
-    int blocks_per_cu = 8;
-    if (mode == MODE_GROUP_LDS) blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds));
-    const int grid = (int)std::min<int64_t>((int64_t)chunks.size(), (int64_t)ctx->num_cus * blocks_per_cu);
-    PH_HIP_CHECK(hipEventRecord(ctx->ev_start, st));
-    launch_scan(kp, mode, grid, 256, lds, st);
-    PH_HIP_CHECK(hipEventRecord(ctx->ev_stop, st));
+    if (mode != MODE_PARTITION) {
+      kp.chunk_begin = 0;
+      kp.chunk_end = (int32_t)chunks.size();
+      int blocks_per_cu = 8;
+      if (mode == MODE_GROUP_LDS) blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds));
+      const int grid = (int)std::min<int64_t>((int64_t)chunks.size(), (int64_t)ctx->num_cus * blocks_per_cu);
+      PH_HIP_CHECK(hipEventRecord(ctx->ev_start, st));
+      launch_scan(kp, mode, q->num_group_by, 0, grid, 256, lds, st);
+      PH_HIP_CHECK(hipEventRecord(ctx->ev_stop, st));
+    } else {
+      // ---- partitioned group-by: batches of chunks; kernel A (filter + decode + partition) on `st`,
+      // kernel B (per-partition LDS aggregation + owned merge) on stream_b, overlapped across batches
+      const bool has_sum = nvals && (val_ops[0] & 1), has_min = nvals && (val_ops[0] & 2),
+                 has_max = nvals && (val_ops[0] & 4);
+      const int entry = 4 + (has_sum ? 8 : 0) + (has_min ? 4 : 0) + (has_max ? 4 : 0);
+      int klo = 10;
+      while (klo < 16 && ((int64_t)entry << (klo + 1)) <= 96 * 1024) ++klo;
+      int64_t P = (G + (int64_t(1) << klo) - 1) >> klo;
+      while (P > 1024 && klo < 20) {  // keep P within the stage's bucket table
+        ++klo;
+        P = (G + (int64_t(1) << klo) - 1) >> klo;
+      }
+      if (P > 1024 || ((int64_t)entry << klo) > 150 * 1024) fail(PH_ERR_UNSUPPORTED, "partitioned group-by too large");
+      const int vbits = nvals ? std::max(1, bits_for_range((uint64_t)(vmax - vmin))) : 0;
+      rec64 = (klo + vbits > 32) ? 1 : 0;
+      int64_t batch_rows = 16 << 20;
+      if (const char* e = getenv("PH_PART_BATCH_ROWS")) batch_rows = std::max<int64_t>(1 << 16, atoll(e));
+      // batches: contiguous chunk ranges of ~batch_rows docs
+      std::vector<std::pair<int32_t, int32_t>> batches;
+      int64_t max_batch_docs = 0;
+      {
+        int32_t b0 = 0;
+        int64_t acc = 0;
+        for (int32_t c = 0; c < (int32_t)chunks.size(); ++c) {
+          acc += (int64_t)(chunks[c].word_end - chunks[c].word_begin) * 64;
+          if (acc >= batch_rows || c + 1 == (int32_t)chunks.size()) {
+            batches.push_back({b0, c + 1});
+            max_batch_docs = std::max(max_batch_docs, acc);
+            b0 = c + 1;
+            acc = 0;
+          }
+        }
+      }
+      const int64_t cap = (int64_t)((double)max_batch_docs * 1.25 / (double)(P * kPartShards)) + 512;
+      const size_t rec_bytes = rec64 ? 8 : 4;
+      void* bufs[2];
+      uint32_t* curs[2];
+      for (int b = 0; b < 2; ++b) {
+        bufs[b] = scratch.alloc<uint8_t>((size_t)kPartShards * P * cap * rec_bytes);
+        curs[b] = scratch.alloc<uint32_t>((size_t)kPartShards * P);
+        PH_HIP_CHECK(hipMemsetAsync(curs[b], 0, 4 * (size_t)kPartShards * P, st));
+      }
+      kp.ovf_count = scratch.alloc<unsigned long long>(G);
+      PH_HIP_CHECK(hipMemsetAsync(kp.ovf_count, 0, 8 * G, st));
+      if (has_sum) {
+        kp.ovf_sum = scratch.alloc<int64_t>(G);
+        PH_HIP_CHECK(hipMemsetAsync(kp.ovf_sum, 0, 8 * G, st));
+      }
+      if (has_min) {
+        kp.ovf_min = scratch.alloc<int64_t>(G);
+        launch_fill_i64(kp.ovf_min, INT64_MAX, G, st);
+      }
+      if (has_max) {
+        kp.ovf_max = scratch.alloc<int64_t>(G);
+        launch_fill_i64(kp.ovf_max, INT64_MIN, G, st);
+      }
+      kp.stage_off = (int32_t)partition_stage_offset(rec64);
+      kp.part_klo = klo;
+      kp.part_vbits = vbits;
+      kp.num_parts = (int32_t)P;
+      kp.part_cap = (int32_t)cap;
+      kp.part_vbase = nvals ? vmin : 0;
+      PartAggParams bp{};
+      bp.num_parts = (int32_t)P;
+      bp.part_cap = (int32_t)cap;
+      bp.part_klo = klo;
+      bp.part_vbits = vbits;
+      bp.rec64 = rec64;
+      bp.has_sum = has_sum;
+      bp.has_min = has_min;
+      bp.has_max = has_max;
+      bp.part_vbase = kp.part_vbase;
+      bp.num_groups = G;
+      bp.out_count = kp.out_count;
+      bp.out_sum = has_sum ? reinterpret_cast<int64_t*>(kp.out_sum[0]) : nullptr;
+      bp.out_min = has_min ? kp.out_min[0] : nullptr;
+      bp.out_max = has_max ? kp.out_max[0] : nullptr;
+      const size_t lds_b = (size_t)entry << klo;
+      while (ctx->ev_pool.size() < 2 * batches.size() + 2) {
+        hipEvent_t e;
+        PH_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->ev_pool.push_back(e);
+      }
+      hipStream_t sb = ctx->stream_b;
+      PH_HIP_CHECK(hipEventRecord(ctx->ev_start, st));
+      for (size_t b = 0; b < batches.size(); ++b) {
+        const int set = (int)(b & 1);
+        if (b >= 2) PH_HIP_CHECK(hipStreamWaitEvent(st, ctx->ev_pool[2 * (b - 2) + 1], 0));  // set free again
+        kp.chunk_begin = batches[b].first;
+        kp.chunk_end = batches[b].second;
+        kp.part_buf = bufs[set];
+        kp.part_cursor = curs[set];
+        const int nch = kp.chunk_end - kp.chunk_begin;
+        int grid = std::min(nch, ctx->num_cus);
+        grid = std::max(kPartShards, (grid / kPartShards) * kPartShards);
+        launch_scan(kp, MODE_PARTITION, q->num_group_by, rec64, grid, kPartBlock, 0, st);
+        PH_HIP_CHECK(hipEventRecord(ctx->ev_pool[2 * b], st));
+        PH_HIP_CHECK(hipStreamWaitEvent(sb, ctx->ev_pool[2 * b], 0));
+        bp.part_buf = bufs[set];
+        bp.part_cursor = curs[set];
+        launch_part_agg(bp, lds_b, sb);
+        PH_HIP_CHECK(hipEventRecord(ctx->ev_pool[2 * b + 1], sb));
+      }
+      MergeParams mp{kp.out_count, bp.out_sum, bp.out_min, bp.out_max, kp.ovf_count, kp.ovf_sum, kp.ovf_min,
+                     kp.ovf_max, G};
+      PH_HIP_CHECK(hipEventRecord(ctx->ev_pool[2 * batches.size()], st));
+      PH_HIP_CHECK(hipStreamWaitEvent(sb, ctx->ev_pool[2 * batches.size()], 0));
+      launch_merge_overflow(mp, sb);
+      PH_HIP_CHECK(hipEventRecord(ctx->ev_pool[2 * batches.size() + 1], sb));
+      PH_HIP_CHECK(hipStreamWaitEvent(st, ctx->ev_pool[2 * batches.size() + 1], 0));
+      PH_HIP_CHECK(hipEventRecord(ctx->ev_stop, st));
+    }
     PH_HIP_CHECK(hipStreamSynchronize(st));  // staging buffer reuse + results
     PH_HIP_CHECK(hipEventElapsedTime(&dev_ms, ctx->ev_start, ctx->ev_stop));
   } else {
     PH_HIP_CHECK(hipStreamSynchronize(st));
   }
   stats.device_ms = dev_ms;
+  res->mode = mode;
+  stats.plan_mode = mode;
 
   // ---- results
-  int ncols_proj = (int)projected.size();
+  const int ncols_proj = (int)projected.size();
+  auto finish_value = [&](int k, int64_t raw, int64_t cnt_for_default, bool is_sum) -> double {
+    const int j = agg_val[k];
+    const int t = q->aggregations[k].type;
+    double v;
+    if (is_sum) {
+      if (val_is_int[j]) {
+        v = (double)raw;
+        if (raw >= (int64_t(1) << 53) || raw <= -(int64_t(1) << 53)) stats.sum_precision_flag = 1;
+      } else {
+        memcpy(&v, &raw, 8);
+      }
+    } else if (cnt_for_default == 0) {
+      v = t == PH_AGG_MIN ? INFINITY : -INFINITY;  // Min/MaxAggregationFunction defaults
+    } else {
+      v = val_is_int[j] ? (double)raw : double_from_order_key(raw);
+    }
+    return v;
+  };
+  auto src_of = [&](int k) -> void* {
+    const int j = agg_val[k];
+    const int t = q->aggregations[k].type;
+    return t == PH_AGG_SUM ? kp.out_sum[j] : (t == PH_AGG_MIN ? (void*)kp.out_min[j] : (void*)kp.out_max[j]);
+  };
   if (q->num_group_by == 0) {
     init_row_results(1);
     unsigned long long matched = 0;
     PH_HIP_CHECK(hipMemcpy(&matched, kp.out_count, 8, hipMemcpyDeviceToHost));
-    // segments whose filter matched everything (fast_range == 2) are scanned by the kernel as well
     stats.num_docs_scanned = (int64_t)matched;
     for (int k = 0; k < nagg; ++k) {
-      const int t = kp.agg_type[k];
+      const int t = q->aggregations[k].type;
       uint8_t* dst = res->aggs[k].data();
-      if (t == AGG_COUNT) {
+      if (t == PH_AGG_COUNT) {
         int64_t v = (int64_t)matched;
         memcpy(dst, &v, 8);
-      } else if (t == AGG_HLL) {
+      } else if (t == PH_AGG_DISTINCTCOUNTHLL) {
         std::vector<uint32_t> r(m);
         PH_HIP_CHECK(hipMemcpy(r.data(), kp.out_hll + (size_t)agg_hll[k] * m, 4 * m, hipMemcpyDeviceToHost));
         for (int j = 0; j < m; ++j) dst[j] = (uint8_t)r[j];
       } else {
         int64_t raw;
-        PH_HIP_CHECK(hipMemcpy(&raw, kp.out_agg[k], 8, hipMemcpyDeviceToHost));
-        double v;
-        if (t == AGG_SUM) {
-          if (kp.agg_is_int[k]) {
-            v = (double)raw;
-            if (raw >= (int64_t(1) << 53) || raw <= -(int64_t(1) << 53)) stats.sum_precision_flag = 1;
-          } else {
-            memcpy(&v, &raw, 8);
-          }
-        } else if (matched == 0) {
-          v = t == AGG_MIN ? INFINITY : -INFINITY;  // Min/MaxAggregationFunction defaults
-        } else {
-          v = kp.agg_is_int[k] ? (double)raw : double_from_order_key(raw);
-        }
+        PH_HIP_CHECK(hipMemcpy(&raw, src_of(k), 8, hipMemcpyDeviceToHost));
+        double v = finish_value(k, raw, (int64_t)matched, t == PH_AGG_SUM);
         memcpy(dst, &v, 8);
       }
     }
+  } else if (num_hll == 0) {
+    // device-side compaction: non-empty groups in key order, keys decoded, values converted to double,
+    // copied straight into pinned result columns
+    CompactParams cp{};
+    cp.num_groups = G;
+    cp.chunk = std::max<int64_t>(1024, (G + kCompactBlocks - 1) / kCompactBlocks);
+    cp.count = kp.out_count;
+    cp.num_aggs = nagg;
+    cp.num_keys = q->num_group_by;
+    for (int k = 0; k < nagg; ++k) {
+      const int t = q->aggregations[k].type;
+      if (t == PH_AGG_COUNT) {
+        cp.agg_kind[k] = CK_COUNT;
+        continue;
+      }
+      const int j = agg_val[k];
+      cp.agg_kind[k] = val_is_int[j] ? CK_INT : (t == PH_AGG_SUM ? CK_REAL_SUM : CK_REAL_ORDER);
+      cp.agg_src[k] = reinterpret_cast<const int64_t*>(src_of(k));
+      cp.agg_out[k] = scratch.alloc<double>(G);
+    }
+    std::vector<int32_t> key_es(q->num_group_by);
+    for (int g = 0; g < q->num_group_by; ++g) {
+      GlobalDict& gd = *gdicts[g];
+      cp.key_stride[g] = kp.group_stride[g];
+      cp.key_size[g] = std::max<int64_t>(1, gd.dict.size);
+      cp.key_type[g] = gd.dict.type;
+      cp.key_table[g] = global_dict_device_values(ctx, gd);
+      key_es[g] = (gd.dict.type == PH_LONG || gd.dict.type == PH_DOUBLE) ? 8 : 4;
+      cp.key_out[g] = scratch.alloc<uint8_t>((size_t)G * key_es[g]);
+    }
+    cp.count_out = scratch.alloc<int64_t>(G);
+    cp.blk = scratch.alloc<unsigned long long>(kCompactBlocks + 1);
+    launch_compact(cp, st);
+    unsigned long long total = 0;
+    PH_HIP_CHECK(hipMemcpyAsync(&total, cp.blk + kCompactBlocks, 8, hipMemcpyDeviceToHost, st));
+    PH_HIP_CHECK(hipStreamSynchronize(st));
+    const int64_t R = (int64_t)total;
+    res->num_groups = R;
+    res->ctx = ctx;
+    res->aggs.resize(nagg);
+    auto take = [&](ResultBuf& b, const void* dsrc, size_t bytes) {
+      b.pinned = ctx->pinned_acquire(bytes, &b.cap);
+      b.n = bytes;
+      if (bytes) PH_HIP_CHECK(hipMemcpyAsync(b.pinned, dsrc, bytes, hipMemcpyDeviceToHost, st));
+    };
+    for (int k = 0; k < nagg; ++k) {
+      if (cp.agg_kind[k] == CK_COUNT) take(res->aggs[k], cp.count_out, 8 * (size_t)R);
+      else take(res->aggs[k], cp.agg_out[k], 8 * (size_t)R);
+    }
+    ResultBuf counts;
+    take(counts, cp.count_out, 8 * (size_t)R);
+    res->key_types.resize(q->num_group_by);
+    res->key_entry_size.resize(q->num_group_by);
+    res->keys.resize(q->num_group_by);
+    std::vector<ResultBuf> string_ids(q->num_group_by);
+    for (int g = 0; g < q->num_group_by; ++g) {
+      const Dictionary& d = gdicts[g]->dict;
+      res->key_types[g] = d.type;
+      if (d.type == PH_STRING) {
+        take(string_ids[g], cp.key_out[g], 4 * (size_t)R);
+      } else {
+        res->key_entry_size[g] = key_es[g];
+        take(res->keys[g], cp.key_out[g], (size_t)key_es[g] * R);
+      }
+    }
+    PH_HIP_CHECK(hipStreamSynchronize(st));
+    const int64_t* cv = reinterpret_cast<const int64_t*>(counts.data());
+    int64_t docs = 0;
+    for (int64_t r = 0; r < R; ++r) docs += cv[r];
+    stats.num_docs_scanned = docs;
+    ctx->pinned_release(counts.pinned, counts.cap);
+    for (int k = 0; k < nagg; ++k) {
+      if (q->aggregations[k].type != PH_AGG_SUM || !val_is_int[agg_val[k]]) continue;
+      const double* sv = reinterpret_cast<const double*>(res->aggs[k].data());
+      for (int64_t r = 0; r < R; ++r)
+        if (sv[r] >= 9007199254740992.0 || sv[r] <= -9007199254740992.0) {
+          stats.sum_precision_flag = 1;
+          break;
+        }
+    }
+    for (int g = 0; g < q->num_group_by; ++g) {
+      if (res->key_types[g] != PH_STRING) continue;
+      const Dictionary& d = gdicts[g]->dict;
+      const int32_t es = key_entry_size(d);
+      res->key_entry_size[g] = es;
+      res->keys[g].assign((size_t)es * R, 0);
+      const int32_t* ids = reinterpret_cast<const int32_t*>(string_ids[g].data());
+      for (int64_t r = 0; r < R; ++r) put_key_value(d, ids[r], res->keys[g].data() + (size_t)es * r, es);
+      ctx->pinned_release(string_ids[g].pinned, string_ids[g].cap);
+    }
   } else {
+    // group-by with DISTINCTCOUNTHLL registers: host-side materialisation
     std::vector<unsigned long long> cnt(G);
     PH_HIP_CHECK(hipMemcpy(cnt.data(), kp.out_count, 8 * G, hipMemcpyDeviceToHost));
     std::vector<int64_t> live;
@@ -951,41 +1330,37 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     const int64_t R = (int64_t)live.size();
     res->num_groups = R;
     init_row_results(R);
-    std::vector<int64_t> buf;
+    std::map<void*, std::vector<int64_t>> fetched;
+    std::vector<uint32_t> regs;
     for (int k = 0; k < nagg; ++k) {
-      const int t = kp.agg_type[k];
+      const int t = q->aggregations[k].type;
       uint8_t* dst = res->aggs[k].data();
-      if (t == AGG_COUNT) {
+      if (t == PH_AGG_COUNT) {
         for (int64_t r = 0; r < R; ++r) {
           int64_t v = (int64_t)cnt[live[r]];
           memcpy(dst + 8 * r, &v, 8);
         }
-      } else if (t == AGG_HLL) {
-        std::vector<uint32_t> regs(hll_words);
-        PH_HIP_CHECK(hipMemcpy(regs.data(), kp.out_hll, 4 * hll_words, hipMemcpyDeviceToHost));
+      } else if (t == PH_AGG_DISTINCTCOUNTHLL) {
+        if (regs.empty()) {
+          regs.resize(hll_words);
+          PH_HIP_CHECK(hipMemcpy(regs.data(), kp.out_hll, 4 * hll_words, hipMemcpyDeviceToHost));
+        }
         for (int64_t r = 0; r < R; ++r)
-          for (int j = 0; j < m; ++j) dst[(size_t)r * m + j] = (uint8_t)regs[((size_t)live[r] * num_hll + agg_hll[k]) * m + j];
+          for (int j = 0; j < m; ++j)
+            dst[(size_t)r * m + j] = (uint8_t)regs[((size_t)live[r] * num_hll + agg_hll[k]) * m + j];
       } else {
-        buf.resize(G);
-        PH_HIP_CHECK(hipMemcpy(buf.data(), kp.out_agg[k], 8 * G, hipMemcpyDeviceToHost));
+        void* src = src_of(k);
+        auto& buf = fetched[src];
+        if (buf.empty()) {
+          buf.resize(G);
+          PH_HIP_CHECK(hipMemcpy(buf.data(), src, 8 * G, hipMemcpyDeviceToHost));
+        }
         for (int64_t r = 0; r < R; ++r) {
-          const int64_t raw = buf[live[r]];
-          double v;
-          if (t == AGG_SUM) {
-            if (kp.agg_is_int[k]) {
-              v = (double)raw;
-              if (raw >= (int64_t(1) << 53) || raw <= -(int64_t(1) << 53)) stats.sum_precision_flag = 1;
-            } else {
-              memcpy(&v, &raw, 8);
-            }
-          } else {
-            v = kp.agg_is_int[k] ? (double)raw : double_from_order_key(raw);
-          }
+          double v = finish_value(k, buf[live[r]], 1, t == PH_AGG_SUM);
           memcpy(dst + 8 * r, &v, 8);
         }
       }
     }
-    // keys
     res->key_types.resize(q->num_group_by);
     res->key_entry_size.resize(q->num_group_by);
     res->keys.resize(q->num_group_by);
@@ -996,7 +1371,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       res->key_entry_size[g] = es;
       res->keys[g].assign((size_t)es * R, 0);
       for (int64_t r = 0; r < R; ++r) {
-        const int64_t id = (live[r] / kp.group_stride[g]) % d.size;
+        const int64_t id = (live[r] / kp.group_stride[g]) % std::max<int64_t>(1, d.size);
         put_key_value(d, id, res->keys[g].data() + (size_t)es * r, es);
       }
     }

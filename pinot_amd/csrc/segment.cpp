@@ -48,6 +48,37 @@ void* Context::host_staging(size_t n) {
   return pinned;
 }
 
+void* Context::pinned_acquire(size_t n, size_t* cap) {
+  n = std::max<size_t>(n, 4096);
+  {
+    std::lock_guard<std::mutex> lk(pool_mu);
+    auto it = pinned_free.lower_bound(n);
+    if (it != pinned_free.end() && it->first <= 2 * n) {
+      void* p = it->second;
+      *cap = it->first;
+      pinned_free.erase(it);
+      return p;
+    }
+  }
+  void* p = nullptr;
+  PH_HIP_CHECK(hipHostMalloc(&p, n, hipHostMallocDefault));
+  *cap = n;
+  return p;
+}
+
+void Context::pinned_release(void* p, size_t cap) {
+  std::lock_guard<std::mutex> lk(pool_mu);
+  pinned_free.emplace(cap, p);
+  size_t total = 0;
+  for (auto& kv : pinned_free) total += kv.first;
+  while (total > ((size_t)1 << 31) && !pinned_free.empty()) {  // keep at most 2 GiB cached
+    auto it = pinned_free.begin();
+    total -= it->first;
+    (void)hipHostFree(it->second);
+    pinned_free.erase(it);
+  }
+}
+
 // ------------------------------------------------------------------ big-endian readers
 static inline uint32_t be32(const uint8_t* p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
@@ -332,10 +363,7 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
     PH_HIP_CHECK(hipStreamSynchronize(ctx->stream));
     seg->columns[col->name] = std::move(col);
   }
-  {
-    std::lock_guard<std::mutex> g(ctx->mu);
-    seg->id = ctx->next_id++;
-  }
+  seg->id = ctx->next_id++;
   return seg.release();
 }
 

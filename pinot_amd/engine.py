@@ -40,13 +40,39 @@ class ExecutionStats:
     sum_precision_flag: bool
     device_ms: float
     host_ms: float
+    mode: int = 0
 
 
 @dataclass
 class IntermediateResult:
-    keys: List[tuple]
-    aggs: List[list]
+    """Combined server-side result: columnar group keys and intermediate aggregation results."""
+    key_columns: List[object]   # per group-by column: numpy array (numeric) or list of str
+    agg_columns: List[np.ndarray]  # per aggregation: int64 (COUNT), float64 (SUM/MIN/MAX), uint8[n, m] (HLL)
+    num_groups: int
+    functions: List[str]
     stats: ExecutionStats
+
+    @property
+    def keys(self) -> List[tuple]:
+        if not self.key_columns:
+            return [()] * self.num_groups
+        cols = [c.tolist() if isinstance(c, np.ndarray) else c for c in self.key_columns]
+        return list(zip(*cols))
+
+    @property
+    def aggs(self) -> List[list]:
+        out = []
+        conv = []
+        for f, col in zip(self.functions, self.agg_columns):
+            if f == COUNT:
+                conv.append(col.tolist())
+            elif f == DISTINCTCOUNTHLL:
+                conv.append(list(col))
+            else:
+                conv.append(col.tolist())
+        for i in range(self.num_groups):
+            out.append([c[i] for c in conv])
+        return out
 
 
 class _QueryStruct:
@@ -107,6 +133,19 @@ class _QueryStruct:
 _KEY_DTYPE = {N.PH_INT: np.int32, N.PH_LONG: np.int64, N.PH_FLOAT: np.float32, N.PH_DOUBLE: np.float64}
 
 
+class _ResultHandle:
+    """Owns a ph_result; destroyed when the last IntermediateResult referencing it goes away."""
+
+    def __init__(self, r):
+        self.r = r
+
+    def __del__(self):
+        try:
+            N.lib().ph_result_destroy(self.r)
+        except Exception:
+            pass
+
+
 class GpuContext:
     """One context per GPU (ph_ctx)."""
 
@@ -146,75 +185,57 @@ class GpuContext:
             width = buf.dtype.itemsize
         N.check(N.lib().ph_table_set_dictionary(self.handle, column.encode(), dt, buf.ctypes.data, len(values), width))
 
-    def execute(self, q: QueryContext, segments: Sequence[PinnedSegment]) -> IntermediateResult:
+    def execute(self, q: QueryContext, segments: Sequence[PinnedSegment], copy: bool = True) -> IntermediateResult:
+        """copy=False returns zero-copy views of the result's pinned columns; they stay valid while the
+        returned IntermediateResult is alive."""
         qs = _QueryStruct(q)
         segs = (ctypes.c_void_p * max(1, len(segments)))(*[s.handle for s in segments])
         r = ctypes.c_void_p()
         N.check(N.lib().ph_query_execute(self.handle, ctypes.byref(qs.struct), segs, len(segments), ctypes.byref(r)))
-        try:
-            return self._read_result(q, r)
-        finally:
-            N.lib().ph_result_destroy(r)
+        handle = _ResultHandle(r)
+        res = self._read_result(q, r, copy)
+        if not copy:
+            res._handle = handle
+        return res
 
     @staticmethod
-    def _read_result(q: QueryContext, r) -> IntermediateResult:
+    def _read_result(q: QueryContext, r, copy: bool = True) -> IntermediateResult:
         L = N.lib()
         st = N.ExecStats()
         N.check(L.ph_result_stats(r, ctypes.byref(st)))
         n = L.ph_result_num_groups(r)
-        cols = []
+        def view(ptr, nbytes):
+            if not nbytes:
+                return np.zeros(0, np.uint8)
+            a = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint8)), (nbytes,))
+            return a.copy() if copy else a
+
+        key_cols = []
         for g in range(len(q.group_by)):
             es = L.ph_result_key_entry_size(r, g)
-            raw = np.zeros(n * es, np.uint8)
-            if n:
-                N.check(L.ph_result_group_keys(r, g, raw.ctypes.data))
-            cols.append((es, raw))
-        aggs_cols = []
+            raw = view(L.ph_result_key_data(r, g), n * es)
+            t = L.ph_result_key_type(r, g)
+            if t == N.PH_STRING:
+                m = raw[:n * es].reshape(n, es)
+                key_cols.append([bytes(row).rstrip(b"\x00").decode("utf-8") for row in m])
+            else:
+                key_cols.append(raw.view(_KEY_DTYPE[t]))
+        agg_cols = []
         for k, a in enumerate(q.aggregations):
             if a.function == DISTINCTCOUNTHLL:
-                arr = np.zeros((n, 1 << a.log2m), np.uint8)
+                arr = view(L.ph_result_aggregation_data(r, k), n << a.log2m).reshape(n, 1 << a.log2m)
             elif a.function == COUNT:
-                arr = np.zeros(n, np.int64)
+                arr = view(L.ph_result_aggregation_data(r, k), 8 * n).view(np.int64)
             else:
-                arr = np.zeros(n, np.float64)
-            if n:
-                N.check(L.ph_result_aggregation(r, k, arr.ctypes.data))
-            aggs_cols.append(arr)
-        keys = []
-        if q.group_by:
-            decoded = []
-            for g, (es, raw) in enumerate(cols):
-                decoded.append(_decode_keys(raw, es, n, q, g, r))
-            keys = list(zip(*decoded)) if n else []
-        else:
-            keys = [()] * n
-        aggs = []
-        for i in range(n):
-            row = []
-            for k, a in enumerate(q.aggregations):
-                v = aggs_cols[k][i]
-                if a.function == COUNT:
-                    row.append(int(v))
-                elif a.function == DISTINCTCOUNTHLL:
-                    row.append(v)
-                else:
-                    row.append(float(v))
-            aggs.append(row)
+                arr = view(L.ph_result_aggregation_data(r, k), 8 * n).view(np.float64)
+            agg_cols.append(arr)
         stats = ExecutionStats(st.num_docs_scanned, st.num_entries_scanned_in_filter,
                                st.num_entries_scanned_post_filter, st.num_total_docs, st.num_segments_processed,
                                st.num_segments_matched, bool(st.num_groups_limit_reached),
-                               bool(st.sum_precision_flag), st.device_ms, st.host_ms)
-        return IntermediateResult(keys, aggs, stats)
+                               bool(st.sum_precision_flag), st.device_ms, st.host_ms, st.plan_mode)
+        return IntermediateResult(key_cols, agg_cols, n, [a.function for a in q.aggregations], stats)
 
     def query(self, sql_or_q, segments: Sequence[PinnedSegment]) -> ResultTable:
         q = parse_sql(sql_or_q) if isinstance(sql_or_q, str) else sql_or_q
         r = self.execute(q, segments)
         return reduce_groups(q, r.keys, r.aggs)
-
-
-def _decode_keys(raw: np.ndarray, es: int, n: int, q: QueryContext, g: int, r) -> list:
-    t = N.lib().ph_result_key_type(r, g)
-    if t == N.PH_STRING:
-        m = raw.reshape(n, es)
-        return [bytes(row).rstrip(b"\x00").decode("utf-8") for row in m]
-    return np.frombuffer(raw.tobytes(), dtype=_KEY_DTYPE[t]).tolist()

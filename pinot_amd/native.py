@@ -83,7 +83,8 @@ class ExecStats(ctypes.Structure):
                 ("num_entries_scanned_post_filter", ctypes.c_int64), ("num_total_docs", ctypes.c_int64),
                 ("num_segments_processed", ctypes.c_int64), ("num_segments_matched", ctypes.c_int64),
                 ("num_groups_limit_reached", ctypes.c_int32), ("sum_precision_flag", ctypes.c_int32),
-                ("device_ms", ctypes.c_double), ("host_ms", ctypes.c_double)]
+                ("device_ms", ctypes.c_double), ("host_ms", ctypes.c_double), ("plan_mode", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 # every symbol declared in include/pinot_hip.h
@@ -91,7 +92,7 @@ EXPORTED_SYMBOLS = (
     "ph_ctx_create", "ph_ctx_destroy", "ph_ctx_set_stream", "ph_segment_pin", "ph_segment_unpin",
     "ph_segment_device_bytes", "ph_segment_num_docs", "ph_table_set_dictionary", "ph_query_execute",
     "ph_result_destroy", "ph_result_stats", "ph_result_num_groups", "ph_result_key_entry_size", "ph_result_key_type",
-    "ph_result_group_keys", "ph_result_aggregation", "ph_fixed_bit_pack", "ph_selftest_unpack", "ph_last_error", "ph_version",
+    "ph_result_group_keys", "ph_result_aggregation", "ph_result_key_data", "ph_result_aggregation_data", "ph_fixed_bit_pack", "ph_selftest_unpack", "ph_last_error", "ph_version",
 )
 
 _lib = None
@@ -123,6 +124,8 @@ def lib():
         "ph_result_key_type": ([vp, i32], ctypes.c_int),
         "ph_result_group_keys": ([vp, i32, vp], ctypes.c_int),
         "ph_result_aggregation": ([vp, i32, vp], ctypes.c_int),
+        "ph_result_key_data": ([vp, i32], vp),
+        "ph_result_aggregation_data": ([vp, i32], vp),
         "ph_fixed_bit_pack": ([vp, i64, i32, vp, ctypes.c_uint64], ctypes.c_int),
         "ph_selftest_unpack": ([vp, vp, ctypes.c_uint64, i64, i32, vp], ctypes.c_int),
         "ph_last_error": ([], ctypes.c_char_p),

@@ -254,3 +254,78 @@ def test_bad_query_is_reported(ctx, sv):
         ctx.execute(parse_sql("SELECT COUNT(*) FROM t WHERE nope = 3"), sv)
     with pytest.raises(BadQueryError):
         ctx.execute(parse_sql("SELECT COUNT(*) FROM t WHERE column1 > 'abc'"), sv)
+
+
+# ------------------------------------------------------------------ partitioned group-by (MODE_PARTITION)
+def _big_key_table(rng, n, c1=1000, c2=300, mbits=20, skew=0.0):
+    g1 = rng.integers(0, c1, n).astype(np.int32)
+    g2 = rng.integers(0, c2, n).astype(np.int32)
+    if skew:
+        hot = rng.random(n) < skew
+        g1[hot] = 7
+        g2[hot] = 3
+    return {"g1": (g1, "INT"), "g2": (g2, "INT"),
+            "m": (rng.integers(-(1 << (mbits - 1)), 1 << (mbits - 1), n).astype(np.int32), "INT"),
+            "f": (rng.integers(0, 1000, n).astype(np.int32), "INT")}
+
+
+PART_SQL = ("SET numGroupsLimit=2000000; SELECT g1, g2, SUM(m), COUNT(*), MIN(m), MAX(m) FROM t "
+            "WHERE f BETWEEN 0 AND 499 GROUP BY g1, g2 ORDER BY g1, g2 LIMIT 2000000")
+
+
+@pytest.fixture
+def small_batches(monkeypatch):
+    monkeypatch.setenv("PH_PART_BATCH_ROWS", "100000")
+
+
+def test_partition_multi_batch(ctx, small_batches):
+    rng = np.random.default_rng(21)
+    tables = [_big_key_table(rng, n) for n in (300_000, 250_001, 64 * 999)]
+    r, _ = _both(ctx, tables, PART_SQL)
+    assert r.stats.mode == 4
+
+
+def test_partition_overflow_skew(ctx, small_batches):
+    rng = np.random.default_rng(22)
+    tables = [_big_key_table(rng, 400_000, skew=0.6), _big_key_table(rng, 100_000, skew=0.9)]
+    r, _ = _both(ctx, tables, PART_SQL)
+    assert r.stats.mode == 4
+
+
+def test_partition_wide_records(ctx):
+    # value range needs 30 bits: key_lo + value bits > 32 -> 64-bit records
+    rng = np.random.default_rng(23)
+    tables = [_big_key_table(rng, 300_000, mbits=30)]
+    r, _ = _both(ctx, tables, PART_SQL)
+    assert r.stats.mode == 4
+
+
+def test_partition_count_only_and_no_filter(ctx, small_batches):
+    rng = np.random.default_rng(24)
+    tables = [_big_key_table(rng, 200_000), _big_key_table(rng, 150_000)]
+    r, _ = _both(ctx, tables, "SET numGroupsLimit=2000000; SELECT g1, g2, COUNT(*) FROM t GROUP BY g1, g2 "
+                              "ORDER BY g1, g2 LIMIT 2000000")
+    assert r.stats.mode == 4
+    _both(ctx, tables, "SET numGroupsLimit=2000000; SELECT g2, g1, MAX(m) FROM t WHERE f < 100 GROUP BY g2, g1 "
+                       "ORDER BY g2, g1 LIMIT 2000000")
+
+
+def test_global_table_two_value_columns(ctx):
+    rng = np.random.default_rng(25)
+    t = _big_key_table(rng, 200_000)
+    t["d"] = (np.round(rng.normal(size=200_000), 4), "DOUBLE")
+    r, _ = _both(ctx, [t], "SET numGroupsLimit=2000000; SELECT g1, g2, SUM(m), SUM(d), MIN(d) FROM t "
+                           "GROUP BY g1, g2 ORDER BY g1, g2 LIMIT 2000000")
+    assert r.stats.mode == 3
+
+
+def test_value_stream_reencoding_wide_values(ctx):
+    # INT metric spanning the full int32 range: frame-of-reference needs 32 bits -> dictionary gather path
+    rng = np.random.default_rng(26)
+    m = rng.integers(-2**31, 2**31 - 1, 50_000, dtype=np.int64).astype(np.int32)
+    m[:2] = [-2**31, 2**31 - 1]
+    t = {"m": (m, "INT"), "a": (rng.integers(0, 5, 50_000).astype(np.int32), "INT")}
+    _both(ctx, [t], "SELECT a, SUM(m), MIN(m), MAX(m) FROM t GROUP BY a ORDER BY a")
+    t2 = {"m": (rng.integers(-2**40, 2**40, 50_000, dtype=np.int64), "LONG"),
+          "a": (rng.integers(0, 5, 50_000).astype(np.int32), "INT")}
+    _both(ctx, [t2], "SELECT a, SUM(m), MIN(m), MAX(m) FROM t GROUP BY a ORDER BY a")

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_library_exports_every_declared_symbol():
     header = open(os.path.join(ROOT, "include", "pinot_hip.h")).read()
-    declared = set(re.findall(r"^\s*(?:int|int64_t|int32_t|const char\*)\s+(ph_\w+)\(", header, re.M))
+    declared = set(re.findall(r"^\s*(?:int|int64_t|int32_t|const char\*|const void\*)\s+(ph_\w+)\(", header, re.M))
     assert declared == set(N.EXPORTED_SYMBOLS)
     L = N.lib()
     for s in declared:
