@@ -32,6 +32,24 @@ template <class T>
 __device__ __forceinline__ T gld(const T* p) {
   return *(const PH_GLOBAL T*)(p);  // C-style cast = addrspacecast (generic -> global)
 }
+// Read-only per-query descriptors (segments, chunks, filter programs) are read through the constant address
+// space: wave-uniform addresses become scalar loads (s_load, counted by lgkmcnt), so fetching a tile's
+// metadata never waits behind the wave's in-flight vector loads (vmcnt is in-order).
+#define PH_CONST __attribute__((address_space(4)))
+typedef const PH_CONST DevSegment* SegPtr;
+typedef const PH_CONST DevColumn& ColRef;
+typedef const PH_CONST DevValCol& ValRef;
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup-scope fence on every address
+// space and waits for all of the wave's outstanding vector loads (vmcnt(0)) -- including the next tile's
+// prefetch -- before s_barrier; LDS visibility needs only lgkmcnt(0).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// 16-byte load from an 8-byte aligned address (a 64-doc word of a b-bit stream is 8*b bytes)
+typedef uint32_t u32x4a8 __attribute__((ext_vector_type(4), aligned(8)));
+__device__ __forceinline__ u32x4a8 gld16a8(const uint8_t* p) {
+  return *(const PH_GLOBAL u32x4a8*)(p);
+}
 
 __device__ __forceinline__ uint32_t unpack_bits(const uint32_t* __restrict__ fwd, int32_t bits, uint32_t doc) {
   const uint64_t bit = (uint64_t)doc * (uint32_t)bits;
@@ -43,17 +61,17 @@ __device__ __forceinline__ uint32_t unpack_bits(const uint32_t* __restrict__ fwd
   return (uint32_t)((x << sh) >> (64 - bits));
 }
 
-__device__ __forceinline__ uint32_t unpack_col(const DevColumn& c, uint32_t doc) {
+__device__ __forceinline__ uint32_t unpack_col(ColRef c, uint32_t doc) {
   return unpack_bits(c.fwd, c.bits, doc);
 }
 
 // Postfix filter program over a bit stack (bit 0 = top).  Control flow is wave-uniform: every lane of a
 // wave runs the same instruction sequence on its own doc.
-__device__ __forceinline__ bool eval_filter(const FilterInsn* __restrict__ prog, int32_t n, const DevSegment* S,
+__device__ __forceinline__ bool eval_filter(const PH_CONST FilterInsn* prog, int32_t n, SegPtr S,
                                             uint32_t doc) {
   uint32_t st = 0;
   for (int32_t i = 0; i < n; ++i) {
-    const PH_GLOBAL FilterInsn* gi = (const PH_GLOBAL FilterInsn*)(prog + i);
+    const PH_CONST FilterInsn* gi = prog + i;
     FilterInsn in;
     in.op = gi->op;
     in.col = gi->col;
@@ -76,7 +94,7 @@ __device__ __forceinline__ bool eval_filter(const FilterInsn* __restrict__ prog,
       }
       case OP_DOCRANGES: {
         const int32_t* r = reinterpret_cast<const int32_t*>(in.ptr);
-        for (uint32_t k = 0; k < in.lo; ++k) b |= ((int32_t)doc >= gld(r + 2 * k)) & ((int32_t)doc <= gld(r + 2 * k + 1));
+        for (uint32_t k = 0; k < in.lo; ++k) b |= (uint32_t)((int32_t)doc >= gld(r + 2 * k)) & (uint32_t)((int32_t)doc <= gld(r + 2 * k + 1));
         st = (st << 1) | b;
         break;
       }
@@ -141,9 +159,7 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long mask, int lan
   return (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
 }
 
-constexpr int U = 4;  // 64-doc words per wave per iteration (memory-level parallelism)
-
-// compile-time loop: the body sees `u` as a constant expression, so per-word register arrays never spill
+// compile-time loop: the body sees `i` as a constant expression, so register arrays never spill
 template <int I, int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (I < N) {
@@ -152,218 +168,181 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-typedef uint32_t u32x4a8 __attribute__((ext_vector_type(4), aligned(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Stage the first p.nstage streams of this wave's U words into its private LDS area: one coalesced
-// 16-byte-per-lane load per stream (a 64-doc word of a b-bit stream is exactly 8*b bytes, so the span
-// of U words starts 8-byte aligned), all loads issued before any LDS write.
-__device__ __forceinline__ void stage_streams(const KParams& p, const DevSegment* S, int32_t w0, int32_t nvalid,
-                                              uint32_t* wst, int lane) {
-  u32x4 raw[kMaxStage];
-  int nb[kMaxStage];
+// ------------------------------------------------------------------ tile staging
+// A wave tile = p.tile_words consecutive 64-doc words of one chunk.  For each staged stream the tile is one
+// contiguous span (a 64-doc word of a b-bit stream is exactly 8*b bytes, so the span starts 8-byte
+// aligned) read with 16-byte-per-lane coalesced loads (1 KiB per wave-instruction).  The loads of all
+// staged streams share one flat register pool of NL loads per lane, so narrow streams leave room for wide
+// ones; the host sizes the tile so every segment's spans fit.  The loads of tile i+1 are issued before
+// tile i is decoded (software pipelining), so every wave keeps a whole tile of HBM reads in flight.
+template <int NL>
+struct Prefetch {
+  u32x4 r[NL];
+};
+
+template <int NL>
+__device__ __forceinline__ void tile_load(SegPtr S, int32_t w0, int32_t nvalid, int lane, Prefetch<NL>& pf) {
+  if (nvalid <= 0) return;
+  const int np = S->npieces;
 #pragma unroll
-  for (int s = 0; s < kMaxStage; ++s) {
-    nb[s] = 0;
-    if (s >= p.nstage) continue;
-    const int bits = S->streams[s].bits;
-    if (bits == 0) continue;  // nothing to stage for this segment
-    nb[s] = nvalid * 8 * bits + 8;
-    const uint8_t* src = reinterpret_cast<const uint8_t*>(S->streams[s].fwd) + (size_t)w0 * 8 * bits;
-    if (lane * 16 < nb[s]) raw[s] = gld(reinterpret_cast<const u32x4a8*>(src + lane * 16));
+  for (int k = 0; k < NL; ++k) {
+    if (k >= np) break;
+    const uint8_t* fwd = S->pieces[k].fwd;
+    const int32_t stride = S->pieces[k].stride, off = S->pieces[k].off;
+    // bytes of this stream the tile needs (+8: the decode reads the dword after the last value)
+    if (off + lane * 16 < nvalid * stride + 8) pf.r[k] = gld16a8(fwd + (size_t)w0 * stride + lane * 16);
   }
-#pragma unroll
-  for (int s = 0; s < kMaxStage; ++s)
-    if (lane * 16 < nb[s]) *reinterpret_cast<u32x4*>(wst + s * (kStageBytes / 4) + lane * 4) = raw[s];
 }
 
-__device__ __forceinline__ uint32_t staged_bits(const uint32_t* stg, int32_t bits, uint32_t local) {
-  const uint32_t bit = local * (uint32_t)bits;
-  const uint32_t d = bit >> 5, sh = bit & 31u;
-  const uint64_t x = ((uint64_t)__builtin_bswap32(stg[d]) << 32) | __builtin_bswap32(stg[d + 1]);
-  return (uint32_t)((x << sh) >> (64 - bits));
-}
-
-// value of stream s for word u of this wave (LDS-staged or straight from HBM)
-__device__ __forceinline__ uint32_t stream_bits(const KParams& p, const DevSegment* S, const uint32_t* wst, int s,
-                                                int u, int lane, uint32_t doc) {
-  const int32_t bits = S->streams[s].bits;
-  if (s < p.nstage) return staged_bits(wst + s * (kStageBytes / 4), bits, (uint32_t)(u * 64 + lane));
-  return unpack_bits(S->streams[s].fwd, bits, doc);
-}
-
-// Applies the segment's filter to U words of one wave (control flow uniform per segment).
-__device__ __forceinline__ void filter_words(const KParams& p, const DevSegment* S, const uint32_t* wst, int lane,
-                                             const uint32_t (&doc)[U], bool (&hit)[U]) {
-  switch (S->fkind) {
-    case FK_ALL:
-      break;
-    case FK_RANGE: {
-      const uint32_t lo = S->flo, len = S->flen;
-      uint32_t v[U];
+template <int NL>
+__device__ __forceinline__ void tile_store(SegPtr S, int32_t nvalid, uint8_t* wst, int lane, const Prefetch<NL>& pf) {
+  if (nvalid > 0) {
+    const int np = S->npieces;
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = hit[u] ? stream_bits(p, S, wst, p.f_stream, u, lane, doc[u]) : 0u;
-#pragma unroll
-      for (int u = 0; u < U; ++u) hit[u] = hit[u] && (v[u] - lo) < len;
-      break;
-    }
-    case FK_SET: {
-      const uint32_t* bs = S->fptr;
-      uint32_t v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = hit[u] ? stream_bits(p, S, wst, p.f_stream, u, lane, doc[u]) : 0u;
-#pragma unroll
-      for (int u = 0; u < U; ++u) hit[u] = hit[u] && ((gld(bs + (v[u] >> 5)) >> (v[u] & 31u)) & 1u);
-      break;
-    }
-    case FK_BITMAP: {
-      const uint32_t* bm = S->fptr;
-#pragma unroll
-      for (int u = 0; u < U; ++u) hit[u] = hit[u] && ((gld(bm + (doc[u] >> 5)) >> (doc[u] & 31u)) & 1u);
-      break;
-    }
-    case FK_DOCRANGE: {
-#pragma unroll
-      for (int u = 0; u < U; ++u) hit[u] = hit[u] && (doc[u] - S->flo) < S->flen;
-      break;
-    }
-    default: {
-#pragma unroll
-      for (int u = 0; u < U; ++u) hit[u] = hit[u] && eval_filter(p.prog + S->prog_off, S->prog_len, S, doc[u]);
+    for (int k = 0; k < NL; ++k) {
+      if (k >= np) break;
+      const int32_t stride = S->pieces[k].stride, off = S->pieces[k].off, lds = S->pieces[k].lds;
+      if (off + lane * 16 < nvalid * stride + 8) {
+        // byte-swap once here (the stream is big-endian) so the decode is one funnel shift per value
+        u32x4 v = pf.r[k];
+        v.x = __builtin_bswap32(v.x);
+        v.y = __builtin_bswap32(v.y);
+        v.z = __builtin_bswap32(v.z);
+        v.w = __builtin_bswap32(v.w);
+        *reinterpret_cast<u32x4*>(wst + lds + lane * 16) = v;
+      }
     }
   }
+  // every load of this tile has been consumed; saying so explicitly keeps the waitcnt pass from
+  // assuming a predicated-off load into the pool is still pending (it would then put vmcnt(0) before
+  // each load of the next prefetch, serialising it)
+  __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+}
+
+// Per-lane decode cursor over a staged (byte-swapped) stream.  Doc `lane` of 64-doc word u ends at bit
+// e = (64u + lane + 1) * b - 1 of the span; word u+1 starts exactly 2b dwords later, so the dword index
+// advances by 2b per word and the in-dword position of the value's last bit never changes: the value is
+// alignbit(dw[j-1], dw[j], 31 - (e & 31)) & mask, one funnel shift and one AND.
+struct BitCursor {
+  const uint32_t* dw;  // dword j of word 0 (dw[-1] is inside the 16-byte front pad for the first doc)
+  uint32_t rsh;
+  uint32_t mask;
+  int32_t step;        // dwords per 64-doc word = 2b
+};
+
+__device__ __forceinline__ BitCursor bit_cursor(const uint8_t* stg, int32_t bits, int lane) {
+  BitCursor c;
+  const uint32_t e1 = (uint32_t)lane * (uint32_t)bits + (uint32_t)bits - 1u;
+  c.dw = reinterpret_cast<const uint32_t*>(stg + 16) + (e1 >> 5);
+  c.rsh = 31u - (e1 & 31u);
+  c.mask = bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
+  c.step = 2 * bits;
+  return c;
+}
+
+__device__ __forceinline__ uint32_t cursor_value(const BitCursor& c, int u) {
+  const uint32_t* w = c.dw + u * c.step;
+  return __builtin_amdgcn_alignbit(w[-1], w[0], c.rsh) & c.mask;
 }
 
 // value of value-column j for a doc: int64 (integer columns) or float64 (real columns)
-__device__ __forceinline__ void read_value(const DevValCol& c, uint32_t x, int64_t& iv, double& dv) {
-  if (c.kind == VK_PACKED) {
-    iv = c.base + (int64_t)x;
+__device__ __forceinline__ void read_value(int kind, int64_t base, const void* table, uint32_t x, int64_t& iv,
+                                           double& dv) {
+  if (kind == VK_PACKED) {
+    iv = base + (int64_t)x;
     dv = 0.0;
-  } else if (c.kind == VK_DICT_I64) {
-    iv = gld(reinterpret_cast<const int64_t*>(c.table) + x);
+  } else if (kind == VK_DICT_I64) {
+    iv = gld(reinterpret_cast<const int64_t*>(table) + x);
     dv = 0.0;
   } else {
-    dv = gld(reinterpret_cast<const double*>(c.table) + x);
+    dv = gld(reinterpret_cast<const double*>(table) + x);
     iv = double_order_key(dv);
   }
 }
 
-template <class T>
-__device__ __forceinline__ T pick(const T (&a)[kMaxVals], int j) {
-  T x = a[0];
-#pragma unroll
-  for (int i = 1; i < kMaxVals; ++i)
-    if (j == i) x = a[i];
-  return x;
-}
-
-template <int NG>
-__device__ __forceinline__ int64_t group_key(const KParams& p, const DevSegment* S, const uint32_t* wst, int u,
-                                             int lane, uint32_t doc) {
-  int64_t key = 0;
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    const int32_t* remap = S->cols[p.group_slot[g]].remap;
-    uint32_t v = stream_bits(p, S, wst, p.g_stream[g], u, lane, doc);
-    if (remap) v = (uint32_t)gld(remap + v);
-    key += (int64_t)v * p.group_stride[g];
-  }
-  return key;
-}
-
-// ------------------------------------------------------------------ partition staging (MODE_PARTITION)
-constexpr int kMaxParts = 1024;
-
+// ------------------------------------------------------------------ partition flush (MODE_PARTITION)
+// The workgroup's staged records (record word + partition) are counting-sorted by partition in LDS and
+// appended, in coalesced runs, to the workgroup's own region of each partition buffer: region
+// (partition, blockIdx) is written by exactly one workgroup, so no global atomics or cross-workgroup
+// reservations are needed; the per-region fill level lives in LDS (bcnt) and is published at exit.
 template <int REC64>
-struct PartLds {  // with the 8-wave staging area: <= 160 KiB, one 512-thread block per CU
-  static constexpr int kStage = REC64 ? 5120 : 8192;  // staged records per flush
-  uint32_t st_key[kStage];
-  uint32_t st_val[kStage];
-  typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type sorted[kStage];
-  uint16_t sbucket[kStage];
-  uint32_t cnt[kMaxParts];
-  uint32_t off[kMaxParts];
-  uint32_t gpos[kMaxParts];
-  uint32_t wsum[32];
-  uint32_t stage_n;
-};
-constexpr size_t part_stage_off(int rec64) {
-  return ((rec64 ? sizeof(PartLds<1>) : sizeof(PartLds<0>)) + 15) / 16 * 16;
-}
-static_assert(part_stage_off(0) + (kPartBlock / 64) * kMaxStage * kStageBytes <= 160 * 1024, "partition LDS");
-static_assert(part_stage_off(1) + (kPartBlock / 64) * kMaxStage * kStageBytes <= 160 * 1024, "partition LDS");
-
-template <int REC64>
-__device__ void part_flush(const KParams& p, PartLds<REC64>& L, int shard) {
-  __syncthreads();
+__device__ void part_flush(const KParams& p, uint8_t* smem, uint32_t n) {
+  using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
   const int tid = threadIdx.x;
-  const uint32_t n = L.stage_n;
   const int P = p.num_parts;
-  for (int i = tid; i < P; i += blockDim.x) L.cnt[i] = 0;
-  __syncthreads();
-  constexpr int K = PartLds<REC64>::kStage / kPartBlock;
-  uint32_t rk[K], pb[K];
+  const Rec* rec = reinterpret_cast<const Rec*>(smem + p.pl_rec_off);
+  const uint16_t* bkt = reinterpret_cast<const uint16_t*>(smem + p.pl_bkt_off);
+  Rec* sorted = reinterpret_cast<Rec*>(smem + p.pl_sorted_off);
+  uint16_t* sbkt = reinterpret_cast<uint16_t*>(smem + p.pl_sbkt_off);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + p.pl_cnt_off);
+  uint32_t* off = cnt + P;
+  uint32_t* bcnt = off + P;
+  uint32_t* wsum = reinterpret_cast<uint32_t*>(smem + p.pl_misc_off) + 4;
+
+  for (int i = tid; i < P; i += kBlock) cnt[i] = 0;
+  lds_barrier();
+  constexpr int K = kPartS / kBlock;
+  uint32_t br[K];  // (partition << 16) | rank within the partition
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const uint32_t i = tid + k * kPartBlock;
+    const uint32_t i = tid + k * kBlock;
     if (i < n) {
-      pb[k] = L.st_key[i] >> p.part_klo;
-      rk[k] = atomicAdd(&L.cnt[pb[k]], 1u);
+      const uint32_t b = bkt[i];
+      br[k] = (b << 16) | atomicAdd(&cnt[b], 1u);
     }
   }
-  __syncthreads();
-  // exclusive scan of the bucket counts (P <= blockDim.x) + one reservation per non-empty bucket
-  {
-    const int lane = tid & 63, w = tid >> 6;
-    const uint32_t v = tid < P ? L.cnt[tid] : 0u;
+  lds_barrier();
+  // exclusive scan of the partition counts
+  const int lane = tid & 63, w = tid >> 6;
+  for (int base = 0; base < P; base += kBlock) {
+    const int i = base + tid;
+    const uint32_t v = i < P ? cnt[i] : 0u;
     uint32_t inc = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t t = __shfl_up(inc, o, 64);
       if (lane >= o) inc += t;
     }
-    if (lane == 63) L.wsum[w] = inc;
-    __syncthreads();
+    if (lane == 63) wsum[w] = inc;
+    lds_barrier();
     if (tid == 0) {
-      uint32_t acc = 0;
-      for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
-        const uint32_t t = L.wsum[i];
-        L.wsum[i] = acc;
+      uint32_t acc = base ? wsum[kWaves] : 0u;  // running total of the previous slices
+      for (int j = 0; j < kWaves; ++j) {
+        const uint32_t t = wsum[j];
+        wsum[j] = acc;
         acc += t;
       }
+      wsum[kWaves] = acc;
     }
-    __syncthreads();
-    if (tid < P) {
-      L.off[tid] = L.wsum[w] + inc - v;
-      L.gpos[tid] = v ? atomicAdd(&p.part_cursor[shard * P + tid], v) : 0u;
-    }
+    lds_barrier();
+    if (i < P) off[i] = wsum[w] + inc - v;
+    lds_barrier();
   }
-  __syncthreads();
-  const uint32_t kmask = (1u << p.part_klo) - 1u;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const uint32_t i = tid + k * kPartBlock;
+    const uint32_t i = tid + k * kBlock;
     if (i < n) {
-      const uint32_t pos = L.off[pb[k]] + rk[k];
-      const uint32_t klo = L.st_key[i] & kmask;
-      if (REC64) L.sorted[pos] = (((unsigned long long)klo << 32) | L.st_val[i]);
-      else L.sorted[pos] = (klo << p.part_vbits) | L.st_val[i];
-      L.sbucket[pos] = (uint16_t)pb[k];
+      const uint32_t b = br[k] >> 16;
+      const uint32_t pos = off[b] + (br[k] & 0xffffu);
+      sorted[pos] = rec[i];
+      sbkt[pos] = (uint16_t)b;
     }
   }
-  __syncthreads();
-  for (uint32_t j = tid; j < n; j += blockDim.x) {
-    const uint32_t b = L.sbucket[j];
-    const uint32_t dst = L.gpos[b] + (j - L.off[b]);
-    const unsigned long long rec = (unsigned long long)L.sorted[j];
-    const size_t slot = ((size_t)shard * P + b) * (size_t)p.part_cap + dst;
+  lds_barrier();
+  const size_t regions = gridDim.x;
+  for (uint32_t j = tid; j < n; j += kBlock) {
+    const uint32_t b = sbkt[j];
+    const uint32_t dst = bcnt[b] + (j - off[b]);
+    const Rec r = sorted[j];
     if (dst < (uint32_t)p.part_cap) {
-      if (REC64) reinterpret_cast<unsigned long long*>(p.part_buf)[slot] = rec;
-      else reinterpret_cast<uint32_t*>(p.part_buf)[slot] = (uint32_t)rec;
+      reinterpret_cast<Rec*>(p.part_buf)[((size_t)b * regions + blockIdx.x) * (size_t)p.part_cap + dst] = r;
     } else {
-      // partition overflow (skewed keys): aggregate directly into the overflow table
-      const uint32_t klo = REC64 ? (uint32_t)(rec >> 32) : (uint32_t)rec >> p.part_vbits;
-      const uint32_t vo = REC64 ? (uint32_t)rec : ((uint32_t)rec & ((p.part_vbits ? (1u << p.part_vbits) : 1u) - 1u));
+      // region overflow (skewed keys): aggregate straight into the overflow table
+      const uint32_t klo = REC64 ? (uint32_t)((unsigned long long)r >> 32) : (uint32_t)r >> p.part_vbits;
+      const uint32_t vo = REC64 ? (uint32_t)r
+                                : ((uint32_t)r & (p.part_vbits ? ((1u << p.part_vbits) - 1u) : 0u));
       const int64_t g = ((int64_t)b << p.part_klo) | klo;
       const int64_t v = p.part_vbase + (int64_t)vo;
       atomicAdd(&p.ovf_count[g], 1ull);
@@ -372,197 +351,430 @@ __device__ void part_flush(const KParams& p, PartLds<REC64>& L, int shard) {
       if (p.ovf_max) atomicMax(reinterpret_cast<long long*>(p.ovf_max) + g, (long long)v);
     }
   }
-  __syncthreads();
-  if (tid == 0) L.stage_n = 0;
-  __syncthreads();
+  lds_barrier();
+  for (int i = tid; i < P; i += kBlock) bcnt[i] += cnt[i];
+  lds_barrier();
 }
 
+size_t partition_lds_bytes(KParams& p) {
+  const size_t rec = p.part_vbits + p.part_klo > 32 ? 8 : 4;
+  size_t o = 0;
+  auto place = [&](int32_t& dst, size_t bytes) {
+    dst = (int32_t)o;
+    o = (o + bytes + 15) / 16 * 16;
+  };
+  // the flush's sorted copy reuses the tile staging area (every wave has consumed its tile by then)
+  const size_t stage = (size_t)kWaves * p.stage_stride;
+  const size_t sorted = kPartS * rec, sbkt = kPartS * 2;
+  p.stage_off = 0;
+  p.pl_sorted_off = 0;
+  p.pl_sbkt_off = (int32_t)((sorted + 15) / 16 * 16);
+  o = std::max(stage, (size_t)p.pl_sbkt_off + sbkt);
+  o = (o + 15) / 16 * 16;
+  place(p.pl_rec_off, kPartS * rec);
+  place(p.pl_bkt_off, kPartS * 2);
+  place(p.pl_cnt_off, 3 * 4 * (size_t)p.num_parts);  // cnt | off | bcnt
+  place(p.pl_misc_off, 64);
+  return o;
+}
 
 // ------------------------------------------------------------------ the scan kernel
 enum : int32_t { OPS_SUM = 1, OPS_MIN = 2, OPS_MAX = 4 };
 
-template <int MODE, int NG, int REC64>
-__global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : 256) k_scan(const KParams p) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int nwaves = blockDim.x >> 6;
+template <int MODE>
+struct NumLoads {
+  static constexpr int value = MODE == MODE_COUNT ? kPrefetchCount : kPrefetchOther;
+};
+
+// Per-wave accumulation state of the scan (registers).
+struct ScanAcc {
+  unsigned long long matched;  // wave-uniform
+  int64_t isum[kMaxVals], vmin[kMaxVals], vmax[kMaxVals];
+  double dsum[kMaxVals];
+};
+
+// One staged tile of one segment: every parameter the inner loop needs is hoisted into (scalar) registers
+// once per tile, and the filter kind is a template parameter, so the per-64-doc body is LDS reads + ALU.
+template <int MODE, int NG, int REC64, int FK>
+__device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t* smem, const uint8_t* wst, int lane,
+                                             int32_t w0, int32_t nvalid, ScanAcc& acc) {
+  const uint32_t ndocs = (uint32_t)S->num_docs;
   const int m = 1 << p.log2m;
+  // filter leaf
+  const int fbits = (FK == FK_RANGE || FK == FK_SET) ? S->streams[p.f_stream].bits : 1;
+  const BitCursor fcur = bit_cursor(wst + p.stage_soff[p.f_stream], fbits, lane);
+  const uint32_t flo = S->flo, flen = S->flen;
+  const uint32_t* fptr = S->fptr;
+  // group-by key streams
+  BitCursor gcur[NG > 0 ? NG : 1];
+  const int32_t* gremap[NG > 0 ? NG : 1];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    gcur[g] = bit_cursor(wst + p.stage_soff[p.g_stream[g]], S->streams[p.g_stream[g]].bits, lane);
+    gremap[g] = S->cols[p.group_slot[g]].remap;
+  }
+  // aggregated value streams
+  int vkind[kMaxVals];
+  int64_t vbase[kMaxVals];
+  const void* vtab[kMaxVals];
+  BitCursor vcur[kMaxVals];
+#pragma unroll
+  for (int j = 0; j < kMaxVals; ++j) {
+    if (MODE == MODE_COUNT || j >= p.num_vals || (MODE == MODE_PARTITION && j > 0)) continue;
+    vcur[j] = bit_cursor(wst + p.stage_soff[p.v_stream[j]], S->streams[p.v_stream[j]].bits, lane);
+    vkind[j] = S->vals[j].kind;
+    vbase[j] = S->vals[j].base;
+    vtab[j] = S->vals[j].table;
+  }
+  uint32_t* lds_cnt = reinterpret_cast<uint32_t*>(smem + p.lds_cnt_off);
+  uint32_t* lds_hll = reinterpret_cast<uint32_t*>(smem + p.lds_hll_off);
+  uint32_t* pl_n = reinterpret_cast<uint32_t*>(smem + p.pl_misc_off);
+
+  // filter of one 64-doc word, branch-free (bitwise AND, no short-circuit: no exec-mask branches)
+  auto filter_word = [&](int u) -> bool {
+    const uint32_t doc = (uint32_t)(w0 + u) * 64u + (uint32_t)lane;
+    bool hit = doc < ndocs;
+    if constexpr (FK == FK_RANGE) {
+      hit &= (cursor_value(fcur, u) - flo) < flen;
+    } else if constexpr (FK == FK_SET) {
+      const uint32_t v = cursor_value(fcur, u);
+      hit &= (bool)((gld(fptr + (v >> 5)) >> (v & 31u)) & 1u);
+    } else if constexpr (FK == FK_BITMAP) {
+      hit &= (bool)((gld(fptr + (min(doc, ndocs - 1) >> 5)) >> (doc & 31u)) & 1u);
+    } else if constexpr (FK == FK_DOCRANGE) {
+      hit &= (doc - flo) < flen;
+    } else if constexpr (FK == FK_GENERIC) {
+      if (hit) hit = eval_filter((const PH_CONST FilterInsn*)p.prog + S->prog_off, S->prog_len, S, doc);
+    }
+    return hit;
+  };
+
+  // per-word aggregation of the matched docs
+  auto aggregate_word = [&](int u, bool hit, unsigned long long bal) {
+    const uint32_t doc = (uint32_t)(w0 + u) * 64u + (uint32_t)lane;
+    int64_t vi[kMaxVals];
+    double vd[kMaxVals];
+    int64_t key = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxVals; ++j) {
+      vi[j] = 0;
+      vd[j] = 0.0;
+    }
+    if (hit) {
+#pragma unroll
+      for (int j = 0; j < kMaxVals; ++j)
+        if (j < p.num_vals) read_value(vkind[j], vbase[j], vtab[j], cursor_value(vcur[j], u), vi[j], vd[j]);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        uint32_t id = cursor_value(gcur[g], u);
+        if (gremap[g]) id = (uint32_t)gld(gremap[g] + id);
+        key += (int64_t)id * p.group_stride[g];
+      }
+    }
+
+    if constexpr (MODE == MODE_PARTITION) {
+      // append matched records to the workgroup's LDS stage (one LDS atomic per wave)
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(pl_n, (uint32_t)__popcll(bal));
+      base = __shfl(base, 0, 64);
+      if (hit) {
+        const uint32_t idx = base + lanes_below(bal, lane);
+        const uint32_t k32 = (uint32_t)key;
+        const uint32_t klo = k32 & ((1u << p.part_klo) - 1u);
+        const uint32_t vo = p.num_vals ? (uint32_t)(vi[0] - p.part_vbase) : 0u;
+        if (REC64)
+          reinterpret_cast<unsigned long long*>(smem + p.pl_rec_off)[idx] = ((unsigned long long)klo << 32) | vo;
+        else
+          reinterpret_cast<uint32_t*>(smem + p.pl_rec_off)[idx] = (klo << p.part_vbits) | vo;
+        reinterpret_cast<uint16_t*>(smem + p.pl_bkt_off)[idx] = (uint16_t)(k32 >> p.part_klo);
+      }
+      return;
+    } else {
+      if (!hit) return;
+      const int64_t g = key;
+      if (MODE == MODE_GROUP_LDS) atomicAdd(&lds_cnt[g], 1u);
+      else if (MODE == MODE_GROUP_GLOBAL) atomicAdd(&p.out_count[g], 1ull);
+#pragma unroll
+      for (int j = 0; j < kMaxVals; ++j) {
+        if (j >= p.num_vals) continue;
+        const int ops = p.val_ops[j];
+        const int64_t iv = vi[j];
+        if (MODE == MODE_AGG) {
+          if (ops & OPS_SUM) {
+            if (p.val_is_int[j]) acc.isum[j] += iv; else acc.dsum[j] += vd[j];
+          }
+          if (ops & OPS_MIN) acc.vmin[j] = iv < acc.vmin[j] ? iv : acc.vmin[j];
+          if (ops & OPS_MAX) acc.vmax[j] = iv > acc.vmax[j] ? iv : acc.vmax[j];
+        } else {
+          void* sb = MODE == MODE_GROUP_LDS ? (void*)(smem + p.lds_sum_off[j]) : p.out_sum[j];
+          long long* mnb = MODE == MODE_GROUP_LDS ? reinterpret_cast<long long*>(smem + p.lds_min_off[j])
+                                                  : reinterpret_cast<long long*>(p.out_min[j]);
+          long long* mxb = MODE == MODE_GROUP_LDS ? reinterpret_cast<long long*>(smem + p.lds_max_off[j])
+                                                  : reinterpret_cast<long long*>(p.out_max[j]);
+          if (ops & OPS_SUM) {
+            if (p.val_is_int[j]) atomicAdd(reinterpret_cast<unsigned long long*>(sb) + g, (unsigned long long)iv);
+            else atomicAdd(reinterpret_cast<double*>(sb) + g, vd[j]);
+          }
+          if (ops & OPS_MIN) atomicMin(mnb + g, (long long)iv);
+          if (ops & OPS_MAX) atomicMax(mxb + g, (long long)iv);
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < kMaxHll; ++h) {
+        if (h >= p.num_hll) continue;
+        ColRef col = S->cols[p.hll_slot[h]];
+        const uint32_t e = gld(col.hll + unpack_col(col, doc));
+        const int64_t ri = (g * p.num_hll + h) * m + (e >> 8);
+        if (MODE == MODE_GROUP_GLOBAL) atomicMax(&p.out_hll[ri], e & 0xffu);
+        else atomicMax(&lds_hll[ri], e & 0xffu);
+      }
+    }
+  };
+
+  // 4 words per step: their filter decodes are independent, so their LDS reads (and bitmap gathers) overlap
+  constexpr int UB = 4;
+  if constexpr (MODE == MODE_PARTITION) {
+    // lean path: <= 1 value column (the host only plans MODE_PARTITION for that shape); one LDS reservation
+    // per 4 words; records are (key low bits << vbits | value - vbase) with the partition id beside them
+    const uint32_t kmask = (1u << p.part_klo) - 1u;
+    uint32_t* recs = reinterpret_cast<uint32_t*>(smem + p.pl_rec_off);
+    unsigned long long* recs64 = reinterpret_cast<unsigned long long*>(smem + p.pl_rec_off);
+    uint16_t* bkts = reinterpret_cast<uint16_t*>(smem + p.pl_bkt_off);
+    for (int u = 0; u < nvalid; u += UB) {
+      bool hit[UB];
+      unsigned long long bal[UB];
+      uint32_t tot = 0;
+#pragma unroll
+      for (int q = 0; q < UB; ++q) hit[q] = (u + q < nvalid) ? filter_word(u + q) : false;
+#pragma unroll
+      for (int q = 0; q < UB; ++q) {
+        bal[q] = __ballot(hit[q]);
+        tot += (uint32_t)__popcll(bal[q]);
+      }
+      acc.matched += tot;
+      if (tot == 0) continue;
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(pl_n, tot);
+      base = __shfl(base, 0, 64);
+#pragma unroll
+      for (int q = 0; q < UB; ++q) {
+        if (hit[q]) {
+          uint32_t key = 0;
+#pragma unroll
+          for (int g = 0; g < NG; ++g) {
+            uint32_t id = cursor_value(gcur[g], u + q);
+            if (gremap[g]) id = (uint32_t)gld(gremap[g] + id);
+            key += id * (uint32_t)p.group_stride[g];
+          }
+          uint32_t vo = 0;
+          if (p.num_vals) {
+            int64_t iv;
+            double dv;
+            read_value(vkind[0], vbase[0], vtab[0], cursor_value(vcur[0], u + q), iv, dv);
+            vo = (uint32_t)(iv - p.part_vbase);
+          }
+          const uint32_t idx = base + lanes_below(bal[q], lane);
+          if (REC64) recs64[idx] = ((unsigned long long)(key & kmask) << 32) | vo;
+          else recs[idx] = ((key & kmask) << p.part_vbits) | vo;
+          bkts[idx] = (uint16_t)(key >> p.part_klo);
+        }
+        base += (uint32_t)__popcll(bal[q]);
+      }
+    }
+    return;
+  }
+  int u = 0;
+  for (; u + UB <= nvalid; u += UB) {
+    bool hit[UB];
+    unsigned long long bal[UB];
+#pragma unroll
+    for (int q = 0; q < UB; ++q) hit[q] = filter_word(u + q);
+#pragma unroll
+    for (int q = 0; q < UB; ++q) {
+      bal[q] = __ballot(hit[q]);
+      acc.matched += __popcll(bal[q]);
+    }
+    if constexpr (MODE != MODE_COUNT) {
+#pragma unroll
+      for (int q = 0; q < UB; ++q)
+        if (bal[q]) aggregate_word(u + q, hit[q], bal[q]);
+    }
+  }
+  for (; u < nvalid; ++u) {
+    const bool hit = filter_word(u);
+    const unsigned long long bal = __ballot(hit);
+    acc.matched += __popcll(bal);
+    if constexpr (MODE != MODE_COUNT) {
+      if (bal) aggregate_word(u, hit, bal);
+    }
+  }
+}
+
+// Persistent grid over the chunk list.  A chunk (<= 256 words of one segment) is processed in rounds: in
+// round r wave w takes tile r * kWaves + w.  Rounds are workgroup-uniform (MODE_PARTITION flushes at round
+// boundaries with workgroup barriers); the other modes never synchronise inside the loop.
+template <int MODE, int NG, int REC64, int LATE>
+__global__ void __launch_bounds__(kBlock) k_scan(const KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NL = NumLoads<MODE>::value;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably wave-uniform
+  const int m = 1 << p.log2m;
+  SegPtr segs = (SegPtr)p.segs;
+  const PH_CONST Chunk* chunks = (const PH_CONST Chunk*)p.chunks;
 
   uint32_t* lds_cnt = reinterpret_cast<uint32_t*>(smem + p.lds_cnt_off);
   uint32_t* lds_hll = reinterpret_cast<uint32_t*>(smem + p.lds_hll_off);
-  PartLds<REC64>& PL = *reinterpret_cast<PartLds<REC64>*>(smem);
-  uint32_t* wst = reinterpret_cast<uint32_t*>(smem + p.stage_off + (size_t)wave * kMaxStage * kStageBytes);
+  uint8_t* wst = smem + p.stage_off + (size_t)wave * p.stage_stride;
+  uint32_t* pl_n = reinterpret_cast<uint32_t*>(smem + p.pl_misc_off);
   if (MODE == MODE_GROUP_LDS) {
-    for (int64_t g = threadIdx.x; g < p.num_groups; g += blockDim.x) lds_cnt[g] = 0;
+    for (int64_t g = threadIdx.x; g < p.num_groups; g += kBlock) lds_cnt[g] = 0;
 #pragma unroll
     for (int j = 0; j < kMaxVals; ++j) {
       if (j >= p.num_vals) continue;
       const int ops = p.val_ops[j];
-      for (int64_t g = threadIdx.x; g < p.num_groups; g += blockDim.x) {
+      for (int64_t g = threadIdx.x; g < p.num_groups; g += kBlock) {
         if (ops & OPS_SUM) reinterpret_cast<int64_t*>(smem + p.lds_sum_off[j])[g] = 0;  // 0 == +0.0
         if (ops & OPS_MIN) reinterpret_cast<int64_t*>(smem + p.lds_min_off[j])[g] = INT64_MAX;
         if (ops & OPS_MAX) reinterpret_cast<int64_t*>(smem + p.lds_max_off[j])[g] = INT64_MIN;
       }
     }
     const int64_t nh = p.num_groups * p.num_hll * m;
-    for (int64_t i = threadIdx.x; i < nh; i += blockDim.x) lds_hll[i] = 0;
+    for (int64_t i = threadIdx.x; i < nh; i += kBlock) lds_hll[i] = 0;
   } else if (MODE == MODE_AGG) {
-    for (int i = threadIdx.x; i < p.num_hll * m; i += blockDim.x) lds_hll[i] = 0;
+    for (int i = threadIdx.x; i < p.num_hll * m; i += kBlock) lds_hll[i] = 0;
   } else if (MODE == MODE_PARTITION) {
-    if (threadIdx.x == 0) PL.stage_n = 0;
+    if (threadIdx.x == 0) *pl_n = 0;
+    uint32_t* bcnt = reinterpret_cast<uint32_t*>(smem + p.pl_cnt_off) + 2 * p.num_parts;
+    for (int i = threadIdx.x; i < p.num_parts; i += kBlock) bcnt[i] = 0;
   }
   __syncthreads();
-  const int shard = blockIdx.x & (kPartShards - 1);
 
-  unsigned long long matched = 0;  // wave-uniform
-  // MODE_AGG per-lane accumulators, one set per value column
-  int64_t a_isum[kMaxVals], a_min[kMaxVals], a_max[kMaxVals];
-  double a_dsum[kMaxVals];
+  ScanAcc acc;
+  acc.matched = 0;
 #pragma unroll
   for (int j = 0; j < kMaxVals; ++j) {
-    a_isum[j] = 0;
-    a_dsum[j] = 0.0;
-    a_min[j] = INT64_MAX;
-    a_max[j] = INT64_MIN;
+    acc.isum[j] = 0;
+    acc.dsum[j] = 0.0;
+    acc.vmin[j] = INT64_MAX;
+    acc.vmax[j] = INT64_MIN;
   }
 
-  for (int32_t c = p.chunk_begin + blockIdx.x; c < p.chunk_end; c += gridDim.x) {
-    const Chunk ch = p.chunks[c];
-    const DevSegment* S = p.segs + ch.seg;
-    const uint32_t ndocs = (uint32_t)S->num_docs;
-    const int32_t iters = (ch.word_end - ch.word_begin + nwaves * U - 1) / (nwaves * U);
-    for (int32_t it = 0; it < iters; ++it) {
-      const int32_t w0 = ch.word_begin + (it * nwaves + wave) * U;
-      uint32_t doc[U];
-      bool hit[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        doc[u] = (uint32_t)(w0 + u) * 64u + (uint32_t)lane;
-        hit[u] = (w0 + u) < ch.word_end && doc[u] < ndocs;
-      }
-      const int32_t nvalid = min(U, ch.word_end - w0);
-      if (nvalid > 0) stage_streams(p, S, w0, nvalid, wst, lane);
-      filter_words(p, S, wst, lane, doc, hit);
-      unsigned long long bal[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        bal[u] = __ballot(hit[u]);
-        matched += __popcll(bal[u]);
-      }
-      if (MODE == MODE_COUNT) continue;
+  // ---- round iterator: (chunk c, round r); the tile of this wave starts at word w0 and has nvalid words
+  const int32_t tw = p.tile_words;
+  const int32_t round_words = kWaves * tw;
+  // each workgroup takes a contiguous run of chunks (mostly one segment: its descriptor stays in the
+  // scalar cache, and neighbouring tiles are neighbours in HBM)
+  const int64_t nch = p.chunk_end - p.chunk_begin;
+  int32_t c = p.chunk_begin + (int32_t)(nch * blockIdx.x / gridDim.x), r = 0;
+  const int32_t c_end = p.chunk_begin + (int32_t)(nch * (blockIdx.x + 1) / gridDim.x);
+  int32_t cseg = 0, cbeg = 0, cend = 0;
+  SegPtr S = nullptr;
+  int32_t w0 = 0, nvalid = 0;
+  auto locate = [&]() {
+    if (c < c_end) {
+      cseg = chunks[c].seg;
+      cbeg = chunks[c].word_begin;
+      cend = chunks[c].word_end;
+      S = segs + cseg;
+      w0 = cbeg + r * round_words + wave * tw;
+      nvalid = min(tw, cend - w0);
+    }
+  };
+  auto advance = [&]() {
+    if (cbeg + (r + 1) * round_words < cend) {
+      ++r;
+    } else {
+      ++c;
+      r = 0;
+    }
+  };
+  Prefetch<NL> pf;
+  locate();
+  if (c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
 
-      // decode-once: group key and every value column of the U docs (independent loads in flight)
-      int64_t vi[U][kMaxVals];
-      double vd[U][kMaxVals];
-      int64_t key[U];
-      static_for<0, U>([&](auto uc) {
-        constexpr int u = decltype(uc)::value;
-        key[u] = 0;
-#pragma unroll
-        for (int j = 0; j < kMaxVals; ++j) {
-          vi[u][j] = 0;
-          vd[u][j] = 0.0;
-        }
-        if (!hit[u]) return;
-#pragma unroll
-        for (int j = 0; j < kMaxVals; ++j)
-          if (j < p.num_vals)
-            read_value(S->vals[j], stream_bits(p, S, wst, p.v_stream[j], u, lane, doc[u]), vi[u][j], vd[u][j]);
-        if (NG > 0) key[u] = group_key<NG>(p, S, wst, u, lane, doc[u]);
-      });
+  unsigned long long t_stage = 0, t_proc = 0, t_sync = 0, t0 = 0, t1 = 0;
+  const bool stamps = p.dbg != nullptr;
+  while (c < c_end) {
+    if (stamps) t0 = __builtin_readcyclecounter();
+    // stage the prefetched tile, then prefetch the next one of this wave
+    tile_store<NL>(S, nvalid, wst, lane, pf);
+    SegPtr cs = S;
+    const int32_t cw0 = w0, cnvalid = nvalid;
+    advance();
+    locate();
+    // early prefetch overlaps the next tile's loads with this tile's decode; a tile whose decode gathers
+    // from HBM (bitsets, remaps, dictionaries) would wait behind them (vmcnt is in-order): prefetch late
+    if (!LATE && c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (stamps) {
+      t1 = __builtin_readcyclecounter();
+      t_stage += t1 - t0;
+      t0 = t1;
+    }
 
-      if (MODE == MODE_PARTITION) {
-        // append matched records to the block's LDS stage (one LDS atomic per wave)
-        uint32_t tot = 0, pre[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          pre[u] = tot;
-          tot += (uint32_t)__popcll(bal[u]);
-        }
-        uint32_t base = 0;
-        if (tot) {
-          if (lane == 0) base = atomicAdd(&PL.stage_n, tot);
-          base = __shfl(base, 0, 64);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (hit[u]) {
-            const uint32_t idx = base + pre[u] + lanes_below(bal[u], lane);
-            PL.st_key[idx] = (uint32_t)key[u];
-            PL.st_val[idx] = p.num_vals ? (uint32_t)(vi[u][0] - p.part_vbase) : 0u;
-          }
-        }
-        __syncthreads();
-        if (PL.stage_n > (uint32_t)(PartLds<REC64>::kStage - kPartBlock * U)) part_flush<REC64>(p, PL, shard);
-        continue;
+    if (cnvalid > 0) {
+      switch (cs->fkind) {
+        case FK_ALL: process_tile<MODE, NG, REC64, FK_ALL>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
+        case FK_RANGE: process_tile<MODE, NG, REC64, FK_RANGE>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
+        case FK_SET: process_tile<MODE, NG, REC64, FK_SET>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
+        case FK_BITMAP: process_tile<MODE, NG, REC64, FK_BITMAP>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
+        case FK_DOCRANGE:
+          process_tile<MODE, NG, REC64, FK_DOCRANGE>(p, cs, smem, wst, lane, cw0, cnvalid, acc);
+          break;
+        default: process_tile<MODE, NG, REC64, FK_GENERIC>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
       }
-
-      static_for<0, U>([&](auto uc) {
-        constexpr int u = decltype(uc)::value;
-        if (!hit[u]) return;
-        const int64_t g = key[u];
-        if (MODE == MODE_GROUP_LDS) atomicAdd(&lds_cnt[g], 1u);
-        else if (MODE == MODE_GROUP_GLOBAL) atomicAdd(&p.out_count[g], 1ull);
-#pragma unroll
-        for (int j = 0; j < kMaxVals; ++j) {
-          if (j >= p.num_vals) continue;
-          const int ops = p.val_ops[j];
-          const int64_t iv = vi[u][j];
-          if (MODE == MODE_AGG) {
-            if (ops & OPS_SUM) {
-              if (p.val_is_int[j]) a_isum[j] += iv; else a_dsum[j] += vd[u][j];
-            }
-            if (ops & OPS_MIN) a_min[j] = iv < a_min[j] ? iv : a_min[j];
-            if (ops & OPS_MAX) a_max[j] = iv > a_max[j] ? iv : a_max[j];
-          } else {
-            void* sb = MODE == MODE_GROUP_LDS ? (void*)(smem + p.lds_sum_off[j]) : p.out_sum[j];
-            long long* mnb = MODE == MODE_GROUP_LDS ? reinterpret_cast<long long*>(smem + p.lds_min_off[j])
-                                                    : reinterpret_cast<long long*>(p.out_min[j]);
-            long long* mxb = MODE == MODE_GROUP_LDS ? reinterpret_cast<long long*>(smem + p.lds_max_off[j])
-                                                    : reinterpret_cast<long long*>(p.out_max[j]);
-            if (ops & OPS_SUM) {
-              if (p.val_is_int[j]) atomicAdd(reinterpret_cast<unsigned long long*>(sb) + g, (unsigned long long)iv);
-              else atomicAdd(reinterpret_cast<double*>(sb) + g, vd[u][j]);
-            }
-            if (ops & OPS_MIN) atomicMin(mnb + g, (long long)iv);
-            if (ops & OPS_MAX) atomicMax(mxb + g, (long long)iv);
-          }
-        }
-#pragma unroll
-        for (int h = 0; h < kMaxHll; ++h) {
-          if (h >= p.num_hll) continue;
-          const DevColumn& col = S->cols[p.hll_slot[h]];
-          const uint32_t e = gld(col.hll + unpack_col(col, doc[u]));
-          const int64_t r = (g * p.num_hll + h) * m + (e >> 8);
-          if (MODE == MODE_GROUP_GLOBAL) atomicMax(&p.out_hll[r], e & 0xffu);
-          else atomicMax(&lds_hll[r], e & 0xffu);
-        }
-      });
+    }
+    if (LATE && c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
+    if (stamps) {
+      t1 = __builtin_readcyclecounter();
+      t_proc += t1 - t0;
+      t0 = t1;
+    }
+    if (MODE == MODE_PARTITION) {
+      lds_barrier();
+      const uint32_t n = *pl_n;
+      // flush when the next round (<= kWaves * tile_words * 64 records) might not fit
+      if (n > (uint32_t)(kPartS - round_words * 64)) {
+        part_flush<REC64>(p, smem, n);
+        if (threadIdx.x == 0) *pl_n = 0;
+      }
+      lds_barrier();
+      if (stamps) t_sync += __builtin_readcyclecounter() - t0;
     }
   }
+  if (stamps && threadIdx.x == 0) {
+    p.dbg[4 * blockIdx.x + 0] = t_stage;
+    p.dbg[4 * blockIdx.x + 1] = t_proc;
+    p.dbg[4 * blockIdx.x + 2] = t_sync;
+    p.dbg[4 * blockIdx.x + 3] = 1;
+  }
 
-  // ---- block epilogue
+  // ---- workgroup epilogue
   if (MODE == MODE_PARTITION) {
-    __syncthreads();
-    if (PL.stage_n) part_flush<REC64>(p, PL, shard);
+    const uint32_t n = *pl_n;
+    if (n) part_flush<REC64>(p, smem, n);
+    const uint32_t* bcnt = reinterpret_cast<const uint32_t*>(smem + p.pl_cnt_off) + 2 * p.num_parts;
+    for (int i = threadIdx.x; i < p.num_parts; i += kBlock) p.part_count[(size_t)i * gridDim.x + blockIdx.x] = bcnt[i];
     return;
   }
+  const unsigned long long matched = acc.matched;
   __shared__ unsigned long long s_matched;
   if (threadIdx.x == 0) s_matched = 0;
   __syncthreads();
   if (lane == 0 && matched) atomicAdd(&s_matched, matched);
   if (MODE == MODE_AGG) {
-    __shared__ int64_t s_isum[4][kMaxVals], s_min[4][kMaxVals], s_max[4][kMaxVals];
-    __shared__ double s_dsum[4][kMaxVals];
+    __shared__ int64_t s_isum[kWaves][kMaxVals], s_min[kWaves][kMaxVals], s_max[kWaves][kMaxVals];
+    __shared__ double s_dsum[kWaves][kMaxVals];
 #pragma unroll
     for (int j = 0; j < kMaxVals; ++j) {
       if (j >= p.num_vals) continue;
-      const int64_t si = wave_sum_i64(a_isum[j]);
-      const double sd = wave_sum_f64(a_dsum[j]);
-      const int64_t mn = wave_min_i64(a_min[j]);
-      const int64_t mx = wave_max_i64(a_max[j]);
-      if (lane == 0 && wave < 4) {
+      const int64_t si = wave_sum_i64(acc.isum[j]);
+      const double sd = wave_sum_f64(acc.dsum[j]);
+      const int64_t mn = wave_min_i64(acc.vmin[j]);
+      const int64_t mx = wave_max_i64(acc.vmax[j]);
+      if (lane == 0) {
         s_isum[wave][j] = si;
         s_dsum[wave][j] = sd;
         s_min[wave][j] = mn;
@@ -574,7 +786,7 @@ __global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : 256) k_s
       const int j = threadIdx.x;
       int64_t si = s_isum[0][j], mn = s_min[0][j], mx = s_max[0][j];
       double sd = s_dsum[0][j];
-      for (int wv = 1; wv < nwaves && wv < 4; ++wv) {
+      for (int wv = 1; wv < kWaves; ++wv) {
         si += s_isum[wv][j];
         sd += s_dsum[wv][j];
         mn = s_min[wv][j] < mn ? s_min[wv][j] : mn;
@@ -588,12 +800,12 @@ __global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : 256) k_s
       if (ops & OPS_MIN) atomicMin(reinterpret_cast<long long*>(p.out_min[j]), (long long)mn);
       if (ops & OPS_MAX) atomicMax(reinterpret_cast<long long*>(p.out_max[j]), (long long)mx);
     }
-    for (int i = threadIdx.x; i < p.num_hll * m; i += blockDim.x)
+    for (int i = threadIdx.x; i < p.num_hll * m; i += kBlock)
       if (lds_hll[i]) atomicMax(&p.out_hll[i], lds_hll[i]);
   }
   if (MODE == MODE_GROUP_LDS) {
     __syncthreads();
-    for (int64_t g = threadIdx.x; g < p.num_groups; g += blockDim.x) {
+    for (int64_t g = threadIdx.x; g < p.num_groups; g += kBlock) {
       const uint32_t cnt = lds_cnt[g];
       if (!cnt) continue;
       atomicAdd(&p.out_count[g], (unsigned long long)cnt);
@@ -618,7 +830,7 @@ __global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : 256) k_s
       }
     }
     const int64_t nh = p.num_groups * p.num_hll * m;
-    for (int64_t i = threadIdx.x; i < nh; i += blockDim.x)
+    for (int64_t i = threadIdx.x; i < nh; i += kBlock)
       if (lds_hll[i]) atomicMax(&p.out_hll[i], lds_hll[i]);
   }
   __syncthreads();
@@ -634,100 +846,158 @@ static void allow_lds(K kernel, size_t lds) {
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
 }
 
-template <int MODE, int NG>
-static void launch_ng(const KParams& p, int rec64, int grid, int block, size_t lds, hipStream_t s) {
-  if (rec64) {
-    allow_lds(k_scan<MODE, NG, 1>, lds);
-    hipLaunchKernelGGL((k_scan<MODE, NG, 1>), dim3(grid), dim3(block), lds, s, p);
+template <int MODE, int NG, int REC64>
+static void launch_late(const KParams& p, int grid, size_t lds, hipStream_t s) {
+  if (p.late_prefetch) {
+    allow_lds(k_scan<MODE, NG, REC64, 1>, lds);
+    hipLaunchKernelGGL((k_scan<MODE, NG, REC64, 1>), dim3(grid), dim3(kBlock), lds, s, p);
   } else {
-    allow_lds(k_scan<MODE, NG, 0>, lds);
-    hipLaunchKernelGGL((k_scan<MODE, NG, 0>), dim3(grid), dim3(block), lds, s, p);
+    allow_lds(k_scan<MODE, NG, REC64, 0>, lds);
+    hipLaunchKernelGGL((k_scan<MODE, NG, REC64, 0>), dim3(grid), dim3(kBlock), lds, s, p);
   }
+}
+
+template <int MODE, int NG>
+static void launch_ng(const KParams& p, int rec64, int grid, size_t lds, hipStream_t s) {
+  if (rec64) launch_late<MODE, NG, 1>(p, grid, lds, s);
+  else launch_late<MODE, NG, 0>(p, grid, lds, s);
 }
 
 template <int MODE>
-static void launch_mode(const KParams& p, int ng, int rec64, int grid, int block, size_t lds, hipStream_t s) {
+static void launch_mode(const KParams& p, int ng, int rec64, int grid, size_t lds, hipStream_t s) {
   switch (ng) {
-    case 0: launch_ng<MODE, 0>(p, rec64, grid, block, lds, s); break;
-    case 1: launch_ng<MODE, 1>(p, rec64, grid, block, lds, s); break;
-    case 2: launch_ng<MODE, 2>(p, rec64, grid, block, lds, s); break;
-    case 3: launch_ng<MODE, 3>(p, rec64, grid, block, lds, s); break;
-    default: launch_ng<MODE, 4>(p, rec64, grid, block, lds, s); break;
+    case 1: launch_ng<MODE, 1>(p, rec64, grid, lds, s); break;
+    case 2: launch_ng<MODE, 2>(p, rec64, grid, lds, s); break;
+    case 3: launch_ng<MODE, 3>(p, rec64, grid, lds, s); break;
+    default: launch_ng<MODE, 4>(p, rec64, grid, lds, s); break;
   }
 }
 
-size_t partition_stage_offset(int rec64) { return part_stage_off(rec64); }
-
-void launch_scan(const KParams& p, int mode, int ng, int rec64, int grid, int block, size_t lds, hipStream_t s) {
+void launch_scan(const KParams& p, int mode, int ng, int rec64, int grid, size_t lds, hipStream_t s) {
   switch (mode) {
-    case MODE_COUNT: hipLaunchKernelGGL((k_scan<MODE_COUNT, 0, 0>), dim3(grid), dim3(block), lds, s, p); break;
-    case MODE_AGG: hipLaunchKernelGGL((k_scan<MODE_AGG, 0, 0>), dim3(grid), dim3(block), lds, s, p); break;
-    case MODE_GROUP_LDS: launch_mode<MODE_GROUP_LDS>(p, ng, 0, grid, block, lds, s); break;
-    case MODE_GROUP_GLOBAL: launch_mode<MODE_GROUP_GLOBAL>(p, ng, 0, grid, block, lds, s); break;
-    default:
-      launch_mode<MODE_PARTITION>(p, ng, rec64, grid, kPartBlock,
-                                  part_stage_off(rec64) + (kPartBlock / 64) * kMaxStage * kStageBytes, s);
-      break;
+    case MODE_COUNT: launch_late<MODE_COUNT, 0, 0>(p, grid, lds, s); break;
+    case MODE_AGG: launch_late<MODE_AGG, 0, 0>(p, grid, lds, s); break;
+    case MODE_GROUP_LDS: launch_mode<MODE_GROUP_LDS>(p, ng, 0, grid, lds, s); break;
+    case MODE_GROUP_GLOBAL: launch_mode<MODE_GROUP_GLOBAL>(p, ng, 0, grid, lds, s); break;
+    default: launch_mode<MODE_PARTITION>(p, ng, rec64, grid, lds, s); break;
   }
   PH_HIP_CHECK(hipGetLastError());
 }
 
 // ------------------------------------------------------------------ kernel B: partition aggregation
+// One workgroup per partition: every record of the partition (every region kernel A wrote) goes through an
+// LDS table of the partition's keys, then the workgroup merges its key range into the dense result table
+// (each key range has exactly one owner, so the merge needs no atomics).  Region fill levels are read
+// once into LDS; each wave then keeps 4 regions' 16-byte-per-lane record loads in flight.  With pack_cs,
+// COUNT and the value-offset SUM share one 64-bit LDS add (count << 40 | sum): 3 LDS atomics per record.
+template <int REC64>
+__device__ __forceinline__ void part_agg_record(const PartAggParams& p, unsigned long long r, uint32_t vmask,
+                                                uint32_t* cnt, unsigned long long* cs, unsigned long long* sum,
+                                                uint32_t* mn, uint32_t* mx) {
+  uint32_t k, v;
+  if (REC64) {
+    k = (uint32_t)(r >> 32);
+    v = (uint32_t)r;
+  } else {
+    k = (uint32_t)r >> p.part_vbits;
+    v = (uint32_t)r & vmask;
+  }
+  if (p.pack_cs) {
+    atomicAdd(&cs[k], (1ull << 40) | (unsigned long long)v);
+  } else {
+    atomicAdd(&cnt[k], 1u);
+    if (p.has_sum) atomicAdd(&sum[k], (unsigned long long)v);
+  }
+  if (p.has_min) atomicMin(&mn[k], v);
+  if (p.has_max) atomicMax(&mx[k], v);
+}
+
+template <int REC64>
 __global__ void __launch_bounds__(1024) k_part_agg(const PartAggParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int P = p.num_parts;
   const int part = blockIdx.x;
   const uint32_t KP = 1u << p.part_klo;
-  // compact LDS layout: count | sum (8 B) | min | max, only the tables the query needs
+  const int R = p.regions;
+  // LDS layout: [count u32 | count<<40|sum u64] [sum u64] [min u32] [max u32] [region fill u32 x R]
+  size_t off = 0;
   uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);
-  size_t off = 4 * (size_t)KP;
+  unsigned long long* cs = reinterpret_cast<unsigned long long*>(smem);
+  off += p.pack_cs ? 8 * (size_t)KP : 4 * (size_t)KP;
   unsigned long long* sum = reinterpret_cast<unsigned long long*>(smem + off);
-  off += p.has_sum ? 8 * (size_t)KP : 0;
+  off += (p.has_sum && !p.pack_cs) ? 8 * (size_t)KP : 0;
   uint32_t* mn = reinterpret_cast<uint32_t*>(smem + off);
   off += p.has_min ? 4 * (size_t)KP : 0;
   uint32_t* mx = reinterpret_cast<uint32_t*>(smem + off);
+  off += p.has_max ? 4 * (size_t)KP : 0;
+  uint32_t* fill = reinterpret_cast<uint32_t*>(smem + off);
   for (uint32_t k = threadIdx.x; k < KP; k += blockDim.x) {
-    cnt[k] = 0;
-    if (p.has_sum) sum[k] = 0;
+    if (p.pack_cs) cs[k] = 0; else cnt[k] = 0;
+    if (p.has_sum && !p.pack_cs) sum[k] = 0;
     if (p.has_min) mn[k] = 0xffffffffu;
     if (p.has_max) mx[k] = 0u;
   }
-  __shared__ uint32_t s_n[kPartShards];
-  if (threadIdx.x < kPartShards) {
-    const uint32_t c = p.part_cursor[threadIdx.x * P + part];
-    s_n[threadIdx.x] = c < (uint32_t)p.part_cap ? c : (uint32_t)p.part_cap;
+  for (int i = threadIdx.x; i < R; i += blockDim.x) {
+    const uint32_t c = p.part_count[(size_t)part * R + i];
+    fill[i] = c < (uint32_t)p.part_cap ? c : (uint32_t)p.part_cap;
   }
   __syncthreads();
   const uint32_t vmask = p.part_vbits ? ((p.part_vbits >= 32) ? 0xffffffffu : ((1u << p.part_vbits) - 1u)) : 0u;
-  for (int sh = 0; sh < kPartShards; ++sh) {
-    const uint32_t n = s_n[sh];
-    const size_t base = ((size_t)sh * P + part) * (size_t)p.part_cap;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-      uint32_t k, v;
-      if (p.rec64) {
-        const unsigned long long r = reinterpret_cast<const unsigned long long*>(p.part_buf)[base + i];
-        k = (uint32_t)(r >> 32);
-        v = (uint32_t)r;
-      } else {
-        const uint32_t r = reinterpret_cast<const uint32_t*>(p.part_buf)[base + i];
-        k = r >> p.part_vbits;
-        v = r & vmask;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwaves = blockDim.x >> 6;
+  constexpr int RPW = 4;                          // regions per wave per step
+  constexpr int PER = REC64 ? 2 : 4;              // records per 16-byte lane load
+  constexpr uint32_t SPAN = 64 * PER;             // records per wave-load
+  using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
+  const Rec* buf = reinterpret_cast<const Rec*>(p.part_buf);
+  for (int b0 = wave * RPW; b0 < R; b0 += nwaves * RPW) {
+    uint32_t nn[RPW];
+    uint32_t maxn = 0;
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      nn[q] = (b0 + q < R) ? fill[b0 + q] : 0u;
+      maxn = nn[q] > maxn ? nn[q] : maxn;
+    }
+    for (uint32_t base = 0; base < maxn; base += SPAN) {
+      u32x4 v[RPW];
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const uint32_t i0 = base + lane * PER;
+        if (i0 < nn[q]) {
+          const Rec* src = buf + ((size_t)part * R + b0 + q) * (size_t)p.part_cap + i0;
+          v[q] = *reinterpret_cast<const u32x4*>(src);
+        }
       }
-      atomicAdd(&cnt[k], 1u);
-      if (p.has_sum) atomicAdd(&sum[k], (unsigned long long)v);
-      if (p.has_min) atomicMin(&mn[k], v);
-      if (p.has_max) atomicMax(&mx[k], v);
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const uint32_t i0 = base + lane * PER;
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+          if (i0 + e >= nn[q]) continue;
+          const unsigned long long r = REC64 ? ((unsigned long long)v[q][2 * e + 1] << 32) | v[q][2 * e]
+                                             : (unsigned long long)v[q][e];
+          part_agg_record<REC64>(p, r, vmask, cnt, cs, sum, mn, mx);
+        }
+      }
     }
   }
   __syncthreads();
-  if (threadIdx.x < kPartShards) p.part_cursor[threadIdx.x * P + part] = 0;  // ready for the next batch
   for (uint32_t k = threadIdx.x; k < KP; k += blockDim.x) {
-    const uint32_t c = cnt[k];
+    uint32_t c;
+    int64_t s = 0;
+    if (p.pack_cs) {
+      const unsigned long long x = cs[k];
+      c = (uint32_t)(x >> 40);
+      s = (int64_t)(x & ((1ull << 40) - 1ull));
+    } else {
+      c = cnt[k];
+      if (p.has_sum) s = (int64_t)sum[k];
+    }
     if (!c) continue;
     const int64_t g = ((int64_t)part << p.part_klo) | k;
     if (g >= p.num_groups) continue;
     p.out_count[g] += c;  // this block owns keys [part << klo, (part + 1) << klo)
-    if (p.has_sum) p.out_sum[g] += (int64_t)sum[k] + (int64_t)c * p.part_vbase;
+    if (p.has_sum) p.out_sum[g] += s + (int64_t)c * p.part_vbase;
     if (p.has_min) {
       const int64_t v = p.part_vbase + (int64_t)mn[k];
       if (v < p.out_min[g]) p.out_min[g] = v;
@@ -740,8 +1010,13 @@ __global__ void __launch_bounds__(1024) k_part_agg(const PartAggParams p) {
 }
 
 void launch_part_agg(const PartAggParams& p, size_t lds, hipStream_t s) {
-  allow_lds(k_part_agg, lds);
-  hipLaunchKernelGGL(k_part_agg, dim3(p.num_parts), dim3(1024), lds, s, p);
+  if (p.rec64) {
+    allow_lds(k_part_agg<1>, lds);
+    hipLaunchKernelGGL(k_part_agg<1>, dim3(p.num_parts), dim3(1024), lds, s, p);
+  } else {
+    allow_lds(k_part_agg<0>, lds);
+    hipLaunchKernelGGL(k_part_agg<0>, dim3(p.num_parts), dim3(1024), lds, s, p);
+  }
   PH_HIP_CHECK(hipGetLastError());
 }
 

@@ -96,19 +96,41 @@ struct DevValCol {
 };
 
 // A packed bit stream the hot loop reads (dictId or frame-of-reference values).  The first `nstage`
-// streams of a query are staged per wave through LDS: one 16-byte-per-lane coalesced load covers the
-// U consecutive 64-doc words of a wave (U * 8 * bits bytes), then every lane extracts its doc's bits.
+// streams of a query are staged per wave through LDS: each wave works on tiles of kTileWords consecutive
+// 64-doc words; a tile of a b-bit stream is one contiguous span of kTileWords * 8 * b bytes, moved with
+// 16-byte-per-lane coalesced loads (prefetched into registers one tile ahead) and decoded from LDS.
 constexpr int kMaxStreams = 8;
-constexpr int kMaxStage = 4;
-constexpr int kStageBytes = 1024;  // per stream per wave: U * 8 * 31 + 8 <= 1000
+constexpr int kMaxStage = kMaxStreams;  // every stream of the hot loop is LDS-staged
+constexpr int kMaxTileWords = 32;                    // <= 2048 docs per wave tile (host picks 4..32)
+constexpr int kBlock = 256;                          // threads per scan workgroup (4 waves)
+constexpr int kWaves = kBlock / 64;
+constexpr int kChunkWords = 256;                     // 16384 docs per chunk (a multiple of every round)
+// 16-byte-per-lane loads (1 KiB per wave-instruction) a wave keeps in flight per tile, over all streams
+constexpr int kPrefetchCount = 8;                    // MODE_COUNT: one stream
+constexpr int kPrefetchOther = 12;
+constexpr int stage_loads(int tile_words, int bits) { return (tile_words * 8 * bits + 8 + 1023) / 1024; }
+// staged span of one stream: 16-byte front pad (the decode reads dword j-1 and j) + the tile's bytes
+constexpr int stage_stream_bytes(int tile_words, int bits) { return 16 + (tile_words * 8 * bits + 8 + 15) / 16 * 16; }
 struct DevStream {
   const uint32_t* fwd;
   int32_t bits;
   int32_t pad;
 };
 
+// One 1 KiB wave-load of a full tile's staged data (precomputed per segment on the host): the piece
+// covers bytes [off, off + 1024) of stream `stream`'s span; the span of word w0 starts at fwd + w0 * stride.
+struct DevPiece {
+  const uint8_t* fwd;  // stream base + off
+  int32_t stride;      // bytes per 64-doc word (8 * bits)
+  int32_t off;         // byte offset of the piece inside the span
+  int32_t lds;         // LDS destination inside the wave's staging area (stage_soff + 16 + off)
+  int32_t pad;
+};
+constexpr int kMaxPieces = 12;  // == kPrefetchOther >= kPrefetchCount
+
 struct DevSegment {
   int32_t num_docs;
+  int32_t npieces;
   int32_t fkind;       // FK_*
   int32_t fslot;       // FK_RANGE / FK_SET column slot
   uint32_t flo, flen;  // FK_RANGE: [flo, flo + flen) ; FK_DOCRANGE: [flo, flo + flen) docs
@@ -119,6 +141,7 @@ struct DevSegment {
   DevColumn cols[kMaxCols];
   DevValCol vals[kMaxVals];
   DevStream streams[kMaxStreams];  // packed bit streams read by the scan loop (staged ones first)
+  DevPiece pieces[kMaxPieces];     // the tile's 1 KiB loads, all streams
 };
 
 struct Chunk {
@@ -132,8 +155,9 @@ enum : int32_t { AGG_COUNT = 0, AGG_SUM = 1, AGG_MIN = 2, AGG_MAX = 3, AGG_HLL =
 
 enum : int32_t { MODE_COUNT = 0, MODE_AGG = 1, MODE_GROUP_LDS = 2, MODE_GROUP_GLOBAL = 3, MODE_PARTITION = 4 };
 
-constexpr int kPartShards = 8;
-constexpr int kPartBlock = 512;  // per-partition write cursors, sharded to spread the reservation atomics
+constexpr int kPartS = 4096;        // records staged per workgroup before a flush (16 per thread)
+constexpr int kPartMaxParts = 1024;
+constexpr int kPartKeysLog2 = 12;   // keys per partition = 4096: kernel B's LDS table <= 80 KiB
 
 struct KParams {
   const DevSegment* segs;
@@ -145,7 +169,12 @@ struct KParams {
   int32_t f_stream;               // FK_RANGE / FK_SET filter column stream
   int32_t g_stream[kMaxGroupCols];
   int32_t v_stream[kMaxVals];
-  int32_t stage_off;              // byte offset of the per-wave staging area in dynamic LDS
+  int32_t stage_off;              // byte offset of the per-wave staging areas in dynamic LDS
+  int32_t stage_stride;           // bytes of one wave's staging area
+  int32_t tile_words;             // 64-doc words per wave tile
+  int32_t late_prefetch;          // decode gathers from HBM: issue the next tile's loads after it
+  unsigned long long* dbg;        // PH_DEBUG_STAMPS: per-workgroup cycle totals [grid][4] (wave 0)
+  int32_t stage_soff[kMaxStage];  // byte offset of staged stream s inside a wave's area
   int32_t lds_cnt_off;            // MODE_GROUP_LDS: byte offset of the count table
   int32_t num_group_cols;
   int32_t group_slot[kMaxGroupCols];
@@ -172,10 +201,11 @@ struct KParams {
   int32_t part_klo;               // key bits kept in a record (keys per partition = 1 << part_klo)
   int32_t part_vbits;             // value-offset bits in a record (0: COUNT only)
   int32_t num_parts;
-  int32_t part_cap;               // records per (shard, partition)
+  int32_t part_cap;               // records per (partition, workgroup) region
   int64_t part_vbase;             // record value = value - part_vbase
-  void* part_buf;                 // [kPartShards][num_parts][part_cap] records
-  uint32_t* part_cursor;          // [kPartShards][num_parts]
+  void* part_buf;                 // [num_parts][gridDim.x][part_cap] records: one region per workgroup
+  uint32_t* part_count;           // [num_parts][gridDim.x] records written per region (may exceed part_cap)
+  int32_t pl_rec_off, pl_bkt_off, pl_sorted_off, pl_sbkt_off, pl_cnt_off, pl_misc_off;  // LDS layout
   unsigned long long* ovf_count;  // overflow table (same layout as out_*), merged at the end
   int64_t* ovf_sum;
   int64_t* ovf_min;
@@ -186,13 +216,15 @@ struct KParams {
 // the partition's key range into the dense result table (each key range has exactly one owner block).
 struct PartAggParams {
   const void* part_buf;
-  uint32_t* part_cursor;  // reset to 0 after reading
+  const uint32_t* part_count;  // [num_parts][regions]
+  int32_t regions;             // kernel A's grid size
   int32_t num_parts;
   int32_t part_cap;
   int32_t part_klo;
   int32_t part_vbits;
   int32_t rec64;
   int32_t has_sum, has_min, has_max;
+  int32_t pack_cs;        // count and value-offset sum share one 64-bit LDS word (count << 40 | sum)
   int64_t part_vbase;
   int64_t num_groups;
   unsigned long long* out_count;
@@ -316,12 +348,18 @@ struct Context {
   std::multimap<size_t, void*> pinned_free;
   void* pinned_acquire(size_t n, size_t* cap);
   void pinned_release(void* p, size_t cap);
+  // device scratch pool: per-query work buffers (dense group tables, partition buffers, descriptors) are
+  // recycled across queries instead of hipMalloc/hipFree per query (queries on a context are serialised)
+  std::multimap<size_t, std::unique_ptr<DeviceBuffer>> scratch_free;
+  size_t scratch_free_bytes = 0;
+  std::unique_ptr<DeviceBuffer> scratch_acquire(size_t n);
+  void scratch_release(std::unique_ptr<DeviceBuffer> b);
 };
 
 // kernels.hip
-void launch_scan(const KParams& p, int mode, int ngroup, int rec64, int grid, int block, size_t lds, hipStream_t s);
+void launch_scan(const KParams& p, int mode, int ngroup, int rec64, int grid, size_t lds, hipStream_t s);
 void launch_part_agg(const PartAggParams& p, size_t lds, hipStream_t s);
-size_t partition_stage_offset(int rec64);
+size_t partition_lds_bytes(KParams& p);  // fills the pl_* offsets, returns the dynamic LDS size
 struct MergeParams {
   unsigned long long* out_count;
   int64_t* out_sum;

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <numeric>
 #include <set>
@@ -536,14 +537,20 @@ double value_as_double(const Dictionary& d, int64_t i) {
 }  // namespace
 
 // scratch device allocation living for one query
+// Per-query device buffers drawn from the context's scratch pool and returned to it when the query ends
+// (every query synchronises its stream before returning, so nothing is in flight by then).
 struct QueryScratch {
   std::vector<std::unique_ptr<DeviceBuffer>> bufs;
-  int device;
-  explicit QueryScratch(int d) : device(d) {}
+  Context* ctx;
+  explicit QueryScratch(Context* c) : ctx(c) {}
+  ~QueryScratch() {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamSynchronize(ctx->stream_b);
+    for (auto& b : bufs) ctx->scratch_release(std::move(b));
+  }
   template <class T>
   T* alloc(size_t count) {
-    auto b = std::make_unique<DeviceBuffer>();
-    b->alloc(std::max<size_t>(16, sizeof(T) * count), device);
+    auto b = ctx->scratch_acquire(std::max<size_t>(16, sizeof(T) * count));
     T* p = b->as<T>();
     bufs.push_back(std::move(b));
     return p;
@@ -741,7 +748,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   }
 
   // ---- per-segment filter plans
-  QueryScratch scratch(ctx->device);
+  QueryScratch scratch(ctx);
   std::vector<SegProgram> progs(nseg);
   std::vector<PNode> roots(nseg);
   std::vector<char> seg_live(nseg, 1);
@@ -833,7 +840,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   for (int h = 0; h < num_hll; ++h) kp.hll_slot[h] = pl.slot.at(hll_cols[h]);
 
   // packed streams of the hot loop: slot 0 = the single-leaf filter column of each segment (if any),
-  // then the group-by columns, then the aggregated value columns; the first kMaxStage are LDS-staged
+  // then the group-by columns, then the aggregated value columns; all of them are LDS-staged
   std::vector<std::string> stream_cols;  // "" for the per-segment filter slot
   if (q->filter_root >= 0) stream_cols.push_back("");
   kp.f_stream = 0;
@@ -847,8 +854,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   for (int g = 0; g < q->num_group_by; ++g) kp.g_stream[g] = stream_of(group_cols[g], "id");
   for (int j = 0; j < nvals; ++j) kp.v_stream[j] = stream_of(val_cols[j], "val");
   if ((int)stream_cols.size() > kMaxStreams) fail(PH_ERR_UNSUPPORTED, "too many column streams in one query");
-  kp.nstage = std::min<int>(kMaxStage, (int)stream_cols.size());
-  const size_t stage_bytes = (size_t)(256 / 64) * kMaxStage * kStageBytes;  // 256-thread blocks
+  kp.nstage = (int)stream_cols.size();  // <= kMaxStreams == kMaxStage: every stream is staged
 
   // value column encodings + the table-wide value range (partitioned records carry value - vmin)
   int64_t vmin = INT64_MAX, vmax = INT64_MIN;
@@ -861,18 +867,18 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
     }
 
-  // ---- mode selection
+  // ---- mode selection (LDS table offsets are relative to the end of the staging areas, fixed below)
   int mode;
-  size_t lds = 16;
+  size_t lds_tables = 16;
   int rec64 = 0;
   kp.stage_off = 0;
   if (q->num_group_by == 0) {
     mode = (nvals == 0 && num_hll == 0) ? MODE_COUNT : MODE_AGG;
-    kp.lds_hll_off = (int32_t)stage_bytes;
-    lds = stage_bytes + (size_t)num_hll * (m ? m : 1) * 4 + 16;
+    kp.lds_hll_off = 0;
+    lds_tables = (size_t)num_hll * (m ? m : 1) * 4 + 16;
   } else {
-    kp.lds_cnt_off = (int32_t)stage_bytes;
-    size_t off = stage_bytes + ((size_t)G * 4 + 15) / 16 * 16;
+    kp.lds_cnt_off = 0;
+    size_t off = ((size_t)G * 4 + 15) / 16 * 16;
     for (int j = 0; j < nvals; ++j) {
       auto place = [&](int32_t& o) {
         o = (int32_t)std::min<size_t>(off, INT32_MAX);
@@ -887,15 +893,14 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     off += (size_t)G * num_hll * (m ? m : 1) * 4;
     const bool part_ok = num_hll == 0 && nvals <= 1 && (nvals == 0 || (val_is_int[0] && vmax >= vmin &&
                                                                        (uint64_t)(vmax - vmin) < (1ull << 32))) &&
-                         G <= (int64_t(1) << 32) && getenv("PH_DISABLE_PARTITION") == nullptr;
-    if (off <= stage_bytes + 64 * 1024) {
+                         G <= ((int64_t)kPartMaxParts << kPartKeysLog2) && getenv("PH_DISABLE_PARTITION") == nullptr;
+    if (off <= 64 * 1024) {
       mode = MODE_GROUP_LDS;
-      lds = off;
+      lds_tables = off;
     } else if (part_ok && G >= 65536) {
       mode = MODE_PARTITION;
     } else {
       mode = MODE_GROUP_GLOBAL;
-      lds = stage_bytes + 16;
       const double bytes = (double)G * (8 + 8.0 * 3 * nvals + 4.0 * num_hll * (m ? m : 1));
       if (bytes > 32e9) fail(PH_ERR_UNSUPPORTED, "dense group table too large for HBM budget");
     }
@@ -928,7 +933,6 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<DevSegment> dsegs;
   std::vector<FilterInsn> all_insns;
   std::vector<Chunk> chunks;
-  constexpr int kChunkWords = 256;  // 16384 docs per chunk
   std::vector<std::pair<size_t, std::vector<uint32_t>>> payload_fix;  // global insn index -> payload
   std::vector<std::pair<size_t, int>> bitmap_fix;                     // global insn index -> bitmap leaf
   std::vector<std::pair<size_t, std::vector<uint32_t>>> fset_fix;     // segment index -> FK_SET bitset
@@ -1017,6 +1021,76 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     dsegs.push_back(d);
     stats.num_segments_matched++;
   }
+  // ---- per-wave staging layout: one span per staged stream, sized by its widest segment; the tile is the
+  // largest (<= 32 words) whose spans fit the kernel's prefetch register pool
+  {
+    int maxbits[kMaxStage] = {};
+    for (int s = 0; s < kp.nstage; ++s)
+      for (auto& d : dsegs) maxbits[s] = std::max(maxbits[s], (int)d.streams[s].bits);
+    const int pool = mode == MODE_COUNT ? kPrefetchCount : kPrefetchOther;
+    int tw = mode == MODE_PARTITION ? 16 : kMaxTileWords;
+    auto loads = [&](int t) {
+      int n = 0;
+      for (int s = 0; s < kp.nstage; ++s) n += maxbits[s] ? stage_loads(t, maxbits[s]) : 0;
+      return n;
+    };
+    while (tw > 4 && loads(tw) > pool) tw /= 2;
+    if (loads(tw) > pool) fail(PH_ERR_UNSUPPORTED, "staged streams too wide for the prefetch pool");
+    kp.tile_words = tw;
+    int32_t soff = 0;
+    for (int s = 0; s < kp.nstage; ++s) {
+      kp.stage_soff[s] = soff;
+      soff += maxbits[s] ? stage_stream_bytes(tw, maxbits[s]) : 0;
+    }
+    kp.stage_stride = std::max<int32_t>(16, soff);
+  }
+  // a decode that gathers (bitset / bitmap / program filters, key remaps, dictionary values, HLL tables)
+  // would wait behind an early prefetch
+  for (auto& d : dsegs) {
+    bool g = d.fkind == FK_SET || d.fkind == FK_BITMAP || d.fkind == FK_GENERIC || num_hll > 0;
+    for (int gi = 0; gi < q->num_group_by; ++gi) g |= d.cols[kp.group_slot[gi]].remap != nullptr;
+    for (int j = 0; j < nvals; ++j) g |= d.vals[j].kind != VK_PACKED;
+    if (g && mode != MODE_COUNT) kp.late_prefetch = 1;
+    if (g && mode == MODE_COUNT && d.fkind != FK_RANGE && d.fkind != FK_ALL && d.fkind != FK_DOCRANGE) kp.late_prefetch = 1;
+  }
+  // per-segment tile pieces: the 1 KiB wave-loads of a full tile, stream by stream
+  for (auto& d : dsegs) {
+    int np = 0;
+    for (int s = 0; s < kp.nstage; ++s) {
+      const int bits = d.streams[s].bits;
+      if (!bits) continue;
+      const int n = stage_loads(kp.tile_words, bits);
+      for (int i = 0; i < n; ++i) {
+        if (np >= kMaxPieces) fail(PH_ERR_UNSUPPORTED, "tile pieces exceed the prefetch pool");
+        DevPiece& pc = d.pieces[np++];
+        pc.fwd = reinterpret_cast<const uint8_t*>(d.streams[s].fwd) + 1024 * i;
+        pc.stride = 8 * bits;
+        pc.off = 1024 * i;
+        pc.lds = kp.stage_soff[s] + 16 + 1024 * i;
+      }
+    }
+    d.npieces = np;
+  }
+  if (getenv("PH_DEBUG_STAMPS")) {
+    kp.dbg = scratch.alloc<unsigned long long>(4 * (size_t)ctx->num_cus * 8);
+    PH_HIP_CHECK(hipMemsetAsync(kp.dbg, 0, 32 * (size_t)ctx->num_cus * 8, st));
+  }
+  const size_t stage_bytes = (size_t)kWaves * kp.stage_stride;
+  size_t lds = 0;
+  if (mode == MODE_PARTITION) {
+    lds = 0;  // laid out with the partition parameters below
+  } else {
+    kp.stage_off = 0;
+    kp.lds_cnt_off += (int32_t)stage_bytes;
+    kp.lds_hll_off += (int32_t)stage_bytes;
+    for (int j = 0; j < nvals; ++j) {
+      kp.lds_sum_off[j] += (int32_t)stage_bytes;
+      kp.lds_min_off[j] += (int32_t)stage_bytes;
+      kp.lds_max_off[j] += (int32_t)stage_bytes;
+    }
+    lds = stage_bytes + lds_tables;
+    kp.pl_misc_off = 0;
+  }
   for (auto& pf : payload_fix) {
     uint32_t* dp = scratch.alloc<uint32_t>(pf.second.size() + 1);
     PH_HIP_CHECK(hipMemcpyAsync(dp, pf.second.data(), 4 * pf.second.size(), hipMemcpyHostToDevice, st));
@@ -1052,29 +1126,26 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if (mode != MODE_PARTITION) {
       kp.chunk_begin = 0;
       kp.chunk_end = (int32_t)chunks.size();
-      int blocks_per_cu = 8;
-      if (mode == MODE_GROUP_LDS) blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds));
+      int blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1)));
+      if (mode == MODE_GROUP_LDS) blocks_per_cu = std::min(blocks_per_cu, 4);
       const int grid = (int)std::min<int64_t>((int64_t)chunks.size(), (int64_t)ctx->num_cus * blocks_per_cu);
       PH_HIP_CHECK(hipEventRecord(ctx->ev_start, st));
-      launch_scan(kp, mode, q->num_group_by, 0, grid, 256, lds, st);
+      launch_scan(kp, mode, q->num_group_by, 0, grid, lds, st);
       PH_HIP_CHECK(hipEventRecord(ctx->ev_stop, st));
     } else {
       // ---- partitioned group-by: batches of chunks; kernel A (filter + decode + partition) on `st`,
-      // kernel B (per-partition LDS aggregation + owned merge) on stream_b, overlapped across batches
+      // kernel B (per-partition LDS aggregation + owned merge) on stream_b, overlapped across batches.
+      // A batch's records (~batch_rows x selectivity x 4 B, double-buffered) stay resident in the 256 MiB
+      // Infinity Cache between kernel A's writes and kernel B's reads.
       const bool has_sum = nvals && (val_ops[0] & 1), has_min = nvals && (val_ops[0] & 2),
                  has_max = nvals && (val_ops[0] & 4);
-      const int entry = 4 + (has_sum ? 8 : 0) + (has_min ? 4 : 0) + (has_max ? 4 : 0);
-      int klo = 10;
-      while (klo < 16 && ((int64_t)entry << (klo + 1)) <= 96 * 1024) ++klo;
-      int64_t P = (G + (int64_t(1) << klo) - 1) >> klo;
-      while (P > 1024 && klo < 20) {  // keep P within the stage's bucket table
-        ++klo;
-        P = (G + (int64_t(1) << klo) - 1) >> klo;
-      }
-      if (P > 1024 || ((int64_t)entry << klo) > 150 * 1024) fail(PH_ERR_UNSUPPORTED, "partitioned group-by too large");
+      int klo = kPartKeysLog2;
+      while (klo > 8 && (G >> (klo - 1)) < 256) --klo;  // small key spaces: more partitions, more workgroups
+      const int64_t P = (G + (int64_t(1) << klo) - 1) >> klo;
+      if (P > kPartMaxParts) fail(PH_ERR_UNSUPPORTED, "partitioned group-by too large");
       const int vbits = nvals ? std::max(1, bits_for_range((uint64_t)(vmax - vmin))) : 0;
       rec64 = (klo + vbits > 32) ? 1 : 0;
-      int64_t batch_rows = 16 << 20;
+      int64_t batch_rows = 32 << 20;
       if (const char* e = getenv("PH_PART_BATCH_ROWS")) batch_rows = std::max<int64_t>(1 << 16, atoll(e));
       // batches: contiguous chunk ranges of ~batch_rows docs
       std::vector<std::pair<int32_t, int32_t>> batches;
@@ -1092,14 +1163,31 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           }
         }
       }
-      const int64_t cap = (int64_t)((double)max_batch_docs * 1.25 / (double)(P * kPartShards)) + 512;
+      kp.part_klo = klo;
+      kp.part_vbits = vbits;
+      kp.num_parts = (int32_t)P;
+      const size_t lds_a = partition_lds_bytes(kp);
+      const int a_per_cu = (int)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / lds_a));
+      const int grid_a = ctx->num_cus * a_per_cu;
+      int max_batch_chunks = 0;
+      for (auto& bt : batches) max_batch_chunks = std::max(max_batch_chunks, bt.second - bt.first);
+      // region (partition, workgroup) capacity: a workgroup scans <= ceil(chunks / grid) chunks; uniform keys
+      // put 1/P of its docs in each partition; 25 % headroom + 64, rounded to 64 records (16-byte aligned
+      // regions).  Skew beyond that spills to the overflow table.
+      const int64_t wg_docs = (int64_t)((max_batch_chunks + grid_a - 1) / grid_a) * kChunkWords * 64;
+      int64_t cap = (int64_t)((double)wg_docs * 1.25 / (double)P) + 64;
+      cap = (cap + 63) / 64 * 64;
+      const int64_t max_part_records = cap * grid_a;
+      // COUNT and the value-offset SUM share one 64-bit LDS word in kernel B when both fit
+      const bool pack_cs = !rec64 && max_part_records < (int64_t(1) << 24) &&
+                           (vbits == 0 || (double)max_part_records * (double)((int64_t(1) << vbits) - 1) <
+                                              (double)(int64_t(1) << 40));
       const size_t rec_bytes = rec64 ? 8 : 4;
       void* bufs[2];
-      uint32_t* curs[2];
+      uint32_t* counts[2];
       for (int b = 0; b < 2; ++b) {
-        bufs[b] = scratch.alloc<uint8_t>((size_t)kPartShards * P * cap * rec_bytes);
-        curs[b] = scratch.alloc<uint32_t>((size_t)kPartShards * P);
-        PH_HIP_CHECK(hipMemsetAsync(curs[b], 0, 4 * (size_t)kPartShards * P, st));
+        bufs[b] = scratch.alloc<uint8_t>((size_t)P * grid_a * cap * rec_bytes);
+        counts[b] = scratch.alloc<uint32_t>((size_t)P * grid_a);
       }
       kp.ovf_count = scratch.alloc<unsigned long long>(G);
       PH_HIP_CHECK(hipMemsetAsync(kp.ovf_count, 0, 8 * G, st));
@@ -1115,12 +1203,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         kp.ovf_max = scratch.alloc<int64_t>(G);
         launch_fill_i64(kp.ovf_max, INT64_MIN, G, st);
       }
-      kp.stage_off = (int32_t)partition_stage_offset(rec64);
-      kp.part_klo = klo;
-      kp.part_vbits = vbits;
-      kp.num_parts = (int32_t)P;
       kp.part_cap = (int32_t)cap;
       kp.part_vbase = nvals ? vmin : 0;
+      kp.lds_bytes = (int32_t)lds_a;
       PartAggParams bp{};
       bp.num_parts = (int32_t)P;
       bp.part_cap = (int32_t)cap;
@@ -1130,19 +1215,24 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       bp.has_sum = has_sum;
       bp.has_min = has_min;
       bp.has_max = has_max;
+      bp.pack_cs = pack_cs;
       bp.part_vbase = kp.part_vbase;
       bp.num_groups = G;
       bp.out_count = kp.out_count;
       bp.out_sum = has_sum ? reinterpret_cast<int64_t*>(kp.out_sum[0]) : nullptr;
       bp.out_min = has_min ? kp.out_min[0] : nullptr;
       bp.out_max = has_max ? kp.out_max[0] : nullptr;
-      const size_t lds_b = (size_t)entry << klo;
+      const size_t lds_b = (((size_t)(pack_cs ? 8 : 4) + (has_sum && !pack_cs ? 8 : 0) + (has_min ? 4 : 0) +
+                            (has_max ? 4 : 0))
+                               << klo) +
+                           4 * (size_t)grid_a;  // + region fill levels
       while (ctx->ev_pool.size() < 2 * batches.size() + 2) {
         hipEvent_t e;
         PH_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         ctx->ev_pool.push_back(e);
       }
-      hipStream_t sb = ctx->stream_b;
+      // PH_PART_SERIAL=1 runs kernel B on the scan stream (profiling each kernel without overlap)
+      hipStream_t sb = getenv("PH_PART_SERIAL") ? st : ctx->stream_b;
       PH_HIP_CHECK(hipEventRecord(ctx->ev_start, st));
       for (size_t b = 0; b < batches.size(); ++b) {
         const int set = (int)(b & 1);
@@ -1150,15 +1240,15 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         kp.chunk_begin = batches[b].first;
         kp.chunk_end = batches[b].second;
         kp.part_buf = bufs[set];
-        kp.part_cursor = curs[set];
+        kp.part_count = counts[set];
         const int nch = kp.chunk_end - kp.chunk_begin;
-        int grid = std::min(nch, ctx->num_cus);
-        grid = std::max(kPartShards, (grid / kPartShards) * kPartShards);
-        launch_scan(kp, MODE_PARTITION, q->num_group_by, rec64, grid, kPartBlock, 0, st);
+        const int grid = std::min(nch, grid_a);
+        launch_scan(kp, MODE_PARTITION, q->num_group_by, rec64, grid, lds_a, st);
         PH_HIP_CHECK(hipEventRecord(ctx->ev_pool[2 * b], st));
         PH_HIP_CHECK(hipStreamWaitEvent(sb, ctx->ev_pool[2 * b], 0));
         bp.part_buf = bufs[set];
-        bp.part_cursor = curs[set];
+        bp.part_count = counts[set];
+        bp.regions = grid;
         launch_part_agg(bp, lds_b, sb);
         PH_HIP_CHECK(hipEventRecord(ctx->ev_pool[2 * b + 1], sb));
       }
@@ -1173,6 +1263,15 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     PH_HIP_CHECK(hipStreamSynchronize(st));  // staging buffer reuse + results
     PH_HIP_CHECK(hipEventElapsedTime(&dev_ms, ctx->ev_start, ctx->ev_stop));
+    if (kp.dbg) {  // PH_DEBUG_STAMPS: where wave 0 of each workgroup spent its cycles (last launch)
+      std::vector<unsigned long long> h(4 * (size_t)ctx->num_cus * 8);
+      PH_HIP_CHECK(hipMemcpy(h.data(), kp.dbg, 8 * h.size(), hipMemcpyDeviceToHost));
+      double a = 0, b = 0, c = 0, n = 0;
+      for (size_t i = 0; i < h.size(); i += 4)
+        if (h[i + 3]) { a += h[i]; b += h[i + 1]; c += h[i + 2]; n += 1; }
+      if (n) fprintf(stderr, "[ph stamps] mode %d workgroups %.0f: stage %.0f  decode %.0f  sync/flush %.0f cycles avg\n",
+                     mode, n, a / n, b / n, c / n);
+    }
   } else {
     PH_HIP_CHECK(hipStreamSynchronize(st));
   }

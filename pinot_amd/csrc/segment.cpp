@@ -37,6 +37,40 @@ void DeviceBuffer::alloc(size_t n, int dev) {
   }
 }
 
+std::unique_ptr<DeviceBuffer> Context::scratch_acquire(size_t n) {
+  n = std::max<size_t>(256, (n + 255) / 256 * 256);
+  auto it = scratch_free.lower_bound(n);
+  if (it != scratch_free.end() && it->first <= n + n / 2 + (1 << 20)) {
+    auto b = std::move(it->second);
+    scratch_free_bytes -= it->first;
+    scratch_free.erase(it);
+    return b;
+  }
+  auto b = std::make_unique<DeviceBuffer>();
+  try {
+    b->alloc(n, device);
+  } catch (const Error&) {
+    scratch_free.clear();  // give cached scratch back to the allocator and retry once
+    scratch_free_bytes = 0;
+    b->alloc(n, device);
+  }
+  return b;
+}
+
+void Context::scratch_release(std::unique_ptr<DeviceBuffer> b) {
+  if (!b || !b->ptr) return;
+  constexpr size_t kMaxCached = size_t(8) << 30;  // keep at most 8 GiB of idle scratch per context
+  if (b->bytes > kMaxCached) return;
+  while (scratch_free_bytes + b->bytes > kMaxCached && !scratch_free.empty()) {
+    auto it = scratch_free.begin();
+    scratch_free_bytes -= it->first;
+    scratch_free.erase(it);
+  }
+  scratch_free_bytes += b->bytes;
+  const size_t k = b->bytes;
+  scratch_free.emplace(k, std::move(b));
+}
+
 void* Context::host_staging(size_t n) {
   if (n > pinned_bytes) {
     if (pinned) PH_HIP_CHECK(hipHostFree(pinned));

@@ -1,15 +1,16 @@
 #!/bin/bash
 # rocprofv3 kernel-trace summary of one bench workload (no PMC counters in this pass).
 W=${1:-config3}
+TAG=${2:-}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$ROOT/gpurun_out/prof_$W
+OUT=$ROOT/gpurun_out/prof_$W$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o run -- \
   python3 $ROOT/bench.py --workload $W --steps 3 --warmup 1 --no-cpu > $OUT/bench.json 2> $OUT/bench.err
 rc=$?
-echo "rocprof $W rc=$rc"
-cat $OUT/bench.json
-find $OUT -name "*kernel_stats.csv" | head -3 | while read f; do echo "== $f"; head -20 "$f"; done
+echo "rocprof $W$TAG rc=$rc"
+python3 -c "import json,sys; d=json.load(open('$OUT/bench.json')); r=d['roofline']; print('ms/step %.3f kernel_ms %.3f frac %.3f GB/s %.0f' % (d['ms_per_step'], r['kernel_ms'], r['frac'], r['achieved']))" || tail -5 $OUT/bench.err
+find $OUT -name "*kernel_stats.csv" | head -1 | while read f; do head -6 "$f" | cut -d, -f1-4 | cut -c1-120; done
 exit $rc
