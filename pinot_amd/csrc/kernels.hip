@@ -19,6 +19,7 @@
 //   DefaultGroupByExecutor.process + aggregateGroupBySV      pinot-core/.../groupby/DefaultGroupByExecutor.java:131-148
 //   Sum/Count/Min/Max/DistinctCountHLL aggregate*            pinot-core/.../aggregation/function/*.java
 //   BitmapInvertedIndexReader.getDocIds + roaring OR         pinot-segment-local/.../readers/BitmapInvertedIndexReader.java:45-62
+#include <cstdlib>
 #include <type_traits>
 
 #include "ph_internal.h"
@@ -186,13 +187,15 @@ template <int NL>
 __device__ __forceinline__ void tile_load(SegPtr S, int32_t w0, int32_t nvalid, int lane, Prefetch<NL>& pf) {
   if (nvalid <= 0) return;
   const int np = S->npieces;
+  // fixed trip count (no early exit), so the pool is fully unrolled and stays in VGPRs
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
-    if (k >= np) break;
-    const uint8_t* fwd = S->pieces[k].fwd;
-    const int32_t stride = S->pieces[k].stride, off = S->pieces[k].off;
-    // bytes of this stream the tile needs (+8: the decode reads the dword after the last value)
-    if (off + lane * 16 < nvalid * stride + 8) pf.r[k] = gld16a8(fwd + (size_t)w0 * stride + lane * 16);
+    if (k < np) {
+      const uint8_t* fwd = S->pieces[k].fwd;
+      const int32_t stride = S->pieces[k].stride, off = S->pieces[k].off;
+      // bytes of this stream the tile needs (+8: the decode reads the dword after the last value)
+      if (off + lane * 16 < nvalid * stride + 8) pf.r[k] = gld16a8(fwd + (size_t)w0 * stride + lane * 16);
+    }
   }
 }
 
@@ -202,9 +205,8 @@ __device__ __forceinline__ void tile_store(SegPtr S, int32_t nvalid, uint8_t* ws
     const int np = S->npieces;
 #pragma unroll
     for (int k = 0; k < NL; ++k) {
-      if (k >= np) break;
       const int32_t stride = S->pieces[k].stride, off = S->pieces[k].off, lds = S->pieces[k].lds;
-      if (off + lane * 16 < nvalid * stride + 8) {
+      if (k < np && off + lane * 16 < nvalid * stride + 8) {
         // byte-swap once here (the stream is big-endian) so the decode is one funnel shift per value
         u32x4 v = pf.r[k];
         v.x = __builtin_bswap32(v.x);
@@ -262,97 +264,56 @@ __device__ __forceinline__ void read_value(int kind, int64_t base, const void* t
   }
 }
 
-// ------------------------------------------------------------------ partition flush (MODE_PARTITION)
-// The workgroup's staged records (record word + partition) are counting-sorted by partition in LDS and
-// appended, in coalesced runs, to the workgroup's own region of each partition buffer: region
-// (partition, blockIdx) is written by exactly one workgroup, so no global atomics or cross-workgroup
-// reservations are needed; the per-region fill level lives in LDS (bcnt) and is published at exit.
-template <int REC64>
-__device__ void part_flush(const KParams& p, uint8_t* smem, uint32_t n) {
-  using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
-  const int tid = threadIdx.x;
-  const int P = p.num_parts;
-  const Rec* rec = reinterpret_cast<const Rec*>(smem + p.pl_rec_off);
-  const uint16_t* bkt = reinterpret_cast<const uint16_t*>(smem + p.pl_bkt_off);
-  Rec* sorted = reinterpret_cast<Rec*>(smem + p.pl_sorted_off);
-  uint16_t* sbkt = reinterpret_cast<uint16_t*>(smem + p.pl_sbkt_off);
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + p.pl_cnt_off);
-  uint32_t* off = cnt + P;
-  uint32_t* bcnt = off + P;
-  uint32_t* wsum = reinterpret_cast<uint32_t*>(smem + p.pl_misc_off) + 4;
+// ------------------------------------------------------------------ partition slots (MODE_PARTITION)
+// Each workgroup owns one region of every partition's buffer (region (partition, blockIdx) is written by
+// exactly one workgroup: no global atomics, no cross-workgroup reservations).  Matched records are appended
+// straight into per-partition LDS slots (C per partition; one returning LDS atomic per record); a flush
+// copies every partition's slots to the end of its region in coalesced runs.  A record that finds its
+// partition's slots full goes straight to its final region position (bcnt + rank), so the order of the
+// region is exactly the LDS rank order either way; beyond the region capacity it spills to the overflow
+// table.
 
-  for (int i = tid; i < P; i += kBlock) cnt[i] = 0;
-  lds_barrier();
-  constexpr int K = kPartS / kBlock;
-  uint32_t br[K];  // (partition << 16) | rank within the partition
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const uint32_t i = tid + k * kBlock;
-    if (i < n) {
-      const uint32_t b = bkt[i];
-      br[k] = (b << 16) | atomicAdd(&cnt[b], 1u);
-    }
+template <int REC64>
+__device__ __forceinline__ void part_store(const KParams& p, uint32_t b, uint32_t dst,
+                                           typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type r) {
+  using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
+  if (dst < (uint32_t)p.part_cap) {
+    reinterpret_cast<Rec*>(p.part_buf)[((size_t)b * gridDim.x + blockIdx.x) * (size_t)p.part_cap + dst] = r;
+  } else {
+    // region overflow (skewed keys): aggregate straight into the overflow table
+    const uint32_t klo = REC64 ? (uint32_t)((unsigned long long)r >> 32) : (uint32_t)r >> p.part_vbits;
+    const uint32_t vo = REC64 ? (uint32_t)r : ((uint32_t)r & (p.part_vbits ? ((1u << p.part_vbits) - 1u) : 0u));
+    const int64_t g = ((int64_t)b << p.part_klo) | klo;
+    const int64_t v = p.part_vbase + (int64_t)vo;
+    atomicAdd(&p.ovf_count[g], 1ull);
+    if (p.ovf_sum) atomicAdd(reinterpret_cast<unsigned long long*>(p.ovf_sum) + g, (unsigned long long)v);
+    if (p.ovf_min) atomicMin(reinterpret_cast<long long*>(p.ovf_min) + g, (long long)v);
+    if (p.ovf_max) atomicMax(reinterpret_cast<long long*>(p.ovf_max) + g, (long long)v);
+  }
+}
+
+template <int REC64>
+__device__ void part_flush(const KParams& p, uint8_t* smem) {
+  using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
+  const Rec* slots = reinterpret_cast<const Rec*>(smem + p.pl_slot_off);
+  uint32_t* lcnt = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
+  uint32_t* bcnt = reinterpret_cast<uint32_t*>(smem + p.pl_bcnt_off);
+  const int P = p.num_parts;
+  const int cl = p.part_slot_log2;
+  const uint32_t C = 1u << cl;
+  const int total = P << cl;
+#pragma unroll 4
+  for (int s = threadIdx.x; s < total; s += kBlock) {
+    const uint32_t b = (uint32_t)s >> cl, i = (uint32_t)s & (C - 1u);
+    const uint32_t n = lcnt[b];
+    if (i < n && i < C) part_store<REC64>(p, b, bcnt[b] + i, slots[s]);
   }
   lds_barrier();
-  // exclusive scan of the partition counts
-  const int lane = tid & 63, w = tid >> 6;
-  for (int base = 0; base < P; base += kBlock) {
-    const int i = base + tid;
-    const uint32_t v = i < P ? cnt[i] : 0u;
-    uint32_t inc = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += t;
-    }
-    if (lane == 63) wsum[w] = inc;
-    lds_barrier();
-    if (tid == 0) {
-      uint32_t acc = base ? wsum[kWaves] : 0u;  // running total of the previous slices
-      for (int j = 0; j < kWaves; ++j) {
-        const uint32_t t = wsum[j];
-        wsum[j] = acc;
-        acc += t;
-      }
-      wsum[kWaves] = acc;
-    }
-    lds_barrier();
-    if (i < P) off[i] = wsum[w] + inc - v;
-    lds_barrier();
+  for (int b = threadIdx.x; b < P; b += kBlock) {
+    bcnt[b] += lcnt[b];
+    lcnt[b] = 0;
   }
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const uint32_t i = tid + k * kBlock;
-    if (i < n) {
-      const uint32_t b = br[k] >> 16;
-      const uint32_t pos = off[b] + (br[k] & 0xffffu);
-      sorted[pos] = rec[i];
-      sbkt[pos] = (uint16_t)b;
-    }
-  }
-  lds_barrier();
-  const size_t regions = gridDim.x;
-  for (uint32_t j = tid; j < n; j += kBlock) {
-    const uint32_t b = sbkt[j];
-    const uint32_t dst = bcnt[b] + (j - off[b]);
-    const Rec r = sorted[j];
-    if (dst < (uint32_t)p.part_cap) {
-      reinterpret_cast<Rec*>(p.part_buf)[((size_t)b * regions + blockIdx.x) * (size_t)p.part_cap + dst] = r;
-    } else {
-      // region overflow (skewed keys): aggregate straight into the overflow table
-      const uint32_t klo = REC64 ? (uint32_t)((unsigned long long)r >> 32) : (uint32_t)r >> p.part_vbits;
-      const uint32_t vo = REC64 ? (uint32_t)r
-                                : ((uint32_t)r & (p.part_vbits ? ((1u << p.part_vbits) - 1u) : 0u));
-      const int64_t g = ((int64_t)b << p.part_klo) | klo;
-      const int64_t v = p.part_vbase + (int64_t)vo;
-      atomicAdd(&p.ovf_count[g], 1ull);
-      if (p.ovf_sum) atomicAdd(reinterpret_cast<unsigned long long*>(p.ovf_sum) + g, (unsigned long long)v);
-      if (p.ovf_min) atomicMin(reinterpret_cast<long long*>(p.ovf_min) + g, (long long)v);
-      if (p.ovf_max) atomicMax(reinterpret_cast<long long*>(p.ovf_max) + g, (long long)v);
-    }
-  }
-  lds_barrier();
-  for (int i = tid; i < P; i += kBlock) bcnt[i] += cnt[i];
+  if (threadIdx.x == 0) *reinterpret_cast<uint32_t*>(smem + p.pl_misc_off) = 0;
   lds_barrier();
 }
 
@@ -363,17 +324,19 @@ size_t partition_lds_bytes(KParams& p) {
     dst = (int32_t)o;
     o = (o + bytes + 15) / 16 * 16;
   };
-  // the flush's sorted copy reuses the tile staging area (every wave has consumed its tile by then)
-  const size_t stage = (size_t)kWaves * p.stage_stride;
-  const size_t sorted = kPartS * rec, sbkt = kPartS * 2;
-  p.stage_off = 0;
-  p.pl_sorted_off = 0;
-  p.pl_sbkt_off = (int32_t)((sorted + 15) / 16 * 16);
-  o = std::max(stage, (size_t)p.pl_sbkt_off + sbkt);
-  o = (o + 15) / 16 * 16;
-  place(p.pl_rec_off, kPartS * rec);
-  place(p.pl_bkt_off, kPartS * 2);
-  place(p.pl_cnt_off, 3 * 4 * (size_t)p.num_parts);  // cnt | off | bcnt
+  int32_t stage_off = 0;
+  place(stage_off, (size_t)kWaves * p.stage_stride);
+  p.stage_off = stage_off;
+  int slots = kPartSlots;
+  if (const char* e = getenv("PH_PART_SLOTS")) slots = std::max(256, atoi(e));  // tuning knob
+  int cl = 0;
+  while ((p.num_parts << (cl + 1)) <= slots) ++cl;
+  p.part_slot_log2 = cl;
+  // flush before the next round (<= kWaves * tile_words * 64 records) could overrun the slots on average
+  p.part_flush_at = std::max(1, (p.num_parts << cl) - kWaves * p.tile_words * 64);
+  place(p.pl_slot_off, (size_t)(p.num_parts << cl) * rec);
+  place(p.pl_lcnt_off, 4 * (size_t)p.num_parts);
+  place(p.pl_bcnt_off, 4 * (size_t)p.num_parts);
   place(p.pl_misc_off, 64);
   return o;
 }
@@ -395,7 +358,7 @@ struct ScanAcc {
 
 // One staged tile of one segment: every parameter the inner loop needs is hoisted into (scalar) registers
 // once per tile, and the filter kind is a template parameter, so the per-64-doc body is LDS reads + ALU.
-template <int MODE, int NG, int REC64, int FK>
+template <int MODE, int NG, int REC64, int FK, int LATE>
 __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t* smem, const uint8_t* wst, int lane,
                                              int32_t w0, int32_t nvalid, ScanAcc& acc) {
   const uint32_t ndocs = (uint32_t)S->num_docs;
@@ -436,14 +399,14 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
     bool hit = doc < ndocs;
     if constexpr (FK == FK_RANGE) {
       hit &= (cursor_value(fcur, u) - flo) < flen;
-    } else if constexpr (FK == FK_SET) {
+    } else if constexpr (FK == FK_SET && LATE) {
       const uint32_t v = cursor_value(fcur, u);
       hit &= (bool)((gld(fptr + (v >> 5)) >> (v & 31u)) & 1u);
-    } else if constexpr (FK == FK_BITMAP) {
+    } else if constexpr (FK == FK_BITMAP && LATE) {
       hit &= (bool)((gld(fptr + (min(doc, ndocs - 1) >> 5)) >> (doc & 31u)) & 1u);
     } else if constexpr (FK == FK_DOCRANGE) {
       hit &= (doc - flo) < flen;
-    } else if constexpr (FK == FK_GENERIC) {
+    } else if constexpr (FK == FK_GENERIC && LATE) {
       if (hit) hit = eval_filter((const PH_CONST FilterInsn*)p.prog + S->prog_off, S->prog_len, S, doc);
     }
     return hit;
@@ -463,31 +426,19 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
     if (hit) {
 #pragma unroll
       for (int j = 0; j < kMaxVals; ++j)
-        if (j < p.num_vals) read_value(vkind[j], vbase[j], vtab[j], cursor_value(vcur[j], u), vi[j], vd[j]);
+        if (j < p.num_vals) {
+          if (LATE) read_value(vkind[j], vbase[j], vtab[j], cursor_value(vcur[j], u), vi[j], vd[j]);
+          else vi[j] = vbase[j] + (int64_t)cursor_value(vcur[j], u);  // VK_PACKED: no gather
+        }
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
         uint32_t id = cursor_value(gcur[g], u);
-        if (gremap[g]) id = (uint32_t)gld(gremap[g] + id);
+        if (LATE && gremap[g]) id = (uint32_t)gld(gremap[g] + id);
         key += (int64_t)id * p.group_stride[g];
       }
     }
 
     if constexpr (MODE == MODE_PARTITION) {
-      // append matched records to the workgroup's LDS stage (one LDS atomic per wave)
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(pl_n, (uint32_t)__popcll(bal));
-      base = __shfl(base, 0, 64);
-      if (hit) {
-        const uint32_t idx = base + lanes_below(bal, lane);
-        const uint32_t k32 = (uint32_t)key;
-        const uint32_t klo = k32 & ((1u << p.part_klo) - 1u);
-        const uint32_t vo = p.num_vals ? (uint32_t)(vi[0] - p.part_vbase) : 0u;
-        if (REC64)
-          reinterpret_cast<unsigned long long*>(smem + p.pl_rec_off)[idx] = ((unsigned long long)klo << 32) | vo;
-        else
-          reinterpret_cast<uint32_t*>(smem + p.pl_rec_off)[idx] = (klo << p.part_vbits) | vo;
-        reinterpret_cast<uint16_t*>(smem + p.pl_bkt_off)[idx] = (uint16_t)(k32 >> p.part_klo);
-      }
       return;
     } else {
       if (!hit) return;
@@ -521,7 +472,7 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
       }
 #pragma unroll
       for (int h = 0; h < kMaxHll; ++h) {
-        if (h >= p.num_hll) continue;
+        if (!LATE || h >= p.num_hll) continue;
         ColRef col = S->cols[p.hll_slot[h]];
         const uint32_t e = gld(col.hll + unpack_col(col, doc));
         const int64_t ri = (g * p.num_hll + h) * m + (e >> 8);
@@ -534,51 +485,54 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
   // 4 words per step: their filter decodes are independent, so their LDS reads (and bitmap gathers) overlap
   constexpr int UB = 4;
   if constexpr (MODE == MODE_PARTITION) {
-    // lean path: <= 1 value column (the host only plans MODE_PARTITION for that shape); one LDS reservation
-    // per 4 words; records are (key low bits << vbits | value - vbase) with the partition id beside them
+    // lean path: <= 1 value column (the host only plans MODE_PARTITION for that shape).  Records are
+    // (key low bits << vbits | value - vbase); the partition (key high bits) picks the LDS slot run.
+    using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
     const uint32_t kmask = (1u << p.part_klo) - 1u;
-    uint32_t* recs = reinterpret_cast<uint32_t*>(smem + p.pl_rec_off);
-    unsigned long long* recs64 = reinterpret_cast<unsigned long long*>(smem + p.pl_rec_off);
-    uint16_t* bkts = reinterpret_cast<uint16_t*>(smem + p.pl_bkt_off);
+    Rec* slots = reinterpret_cast<Rec*>(smem + p.pl_slot_off);
+    uint32_t* lcnt = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
+    const uint32_t* bcnt = reinterpret_cast<const uint32_t*>(smem + p.pl_bcnt_off);
+    const int cl = p.part_slot_log2;
+    const uint32_t C = 1u << cl;
     for (int u = 0; u < nvalid; u += UB) {
       bool hit[UB];
-      unsigned long long bal[UB];
       uint32_t tot = 0;
 #pragma unroll
       for (int q = 0; q < UB; ++q) hit[q] = (u + q < nvalid) ? filter_word(u + q) : false;
 #pragma unroll
-      for (int q = 0; q < UB; ++q) {
-        bal[q] = __ballot(hit[q]);
-        tot += (uint32_t)__popcll(bal[q]);
-      }
+      for (int q = 0; q < UB; ++q) tot += (uint32_t)__popcll(__ballot(hit[q]));
       acc.matched += tot;
-      if (tot == 0) continue;
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(pl_n, tot);
-      base = __shfl(base, 0, 64);
+      if (tot == 0 || (p.dbg_flags & 4)) continue;
+      if (lane == 0) atomicAdd(pl_n, tot);
+      uint32_t bk[UB], rk[UB];
+      Rec rec[UB];
 #pragma unroll
       for (int q = 0; q < UB; ++q) {
-        if (hit[q]) {
-          uint32_t key = 0;
+        if (!hit[q]) continue;
+        uint32_t key = 0;
 #pragma unroll
-          for (int g = 0; g < NG; ++g) {
-            uint32_t id = cursor_value(gcur[g], u + q);
-            if (gremap[g]) id = (uint32_t)gld(gremap[g] + id);
-            key += id * (uint32_t)p.group_stride[g];
-          }
-          uint32_t vo = 0;
-          if (p.num_vals) {
-            int64_t iv;
-            double dv;
-            read_value(vkind[0], vbase[0], vtab[0], cursor_value(vcur[0], u + q), iv, dv);
-            vo = (uint32_t)(iv - p.part_vbase);
-          }
-          const uint32_t idx = base + lanes_below(bal[q], lane);
-          if (REC64) recs64[idx] = ((unsigned long long)(key & kmask) << 32) | vo;
-          else recs[idx] = ((key & kmask) << p.part_vbits) | vo;
-          bkts[idx] = (uint16_t)(key >> p.part_klo);
+        for (int g = 0; g < NG; ++g) {
+          uint32_t id = cursor_value(gcur[g], u + q);
+          if (LATE && gremap[g]) id = (uint32_t)gld(gremap[g] + id);
+          key += id * (uint32_t)p.group_stride[g];
         }
-        base += (uint32_t)__popcll(bal[q]);
+        uint32_t vo = 0;
+        if (p.num_vals) {
+          int64_t iv;
+          double dv;
+          if (LATE) read_value(vkind[0], vbase[0], vtab[0], cursor_value(vcur[0], u + q), iv, dv);
+          else iv = vbase[0] + (int64_t)cursor_value(vcur[0], u + q);  // VK_PACKED: no gather
+          vo = (uint32_t)(iv - p.part_vbase);
+        }
+        bk[q] = key >> p.part_klo;
+        rec[q] = REC64 ? (Rec)(((unsigned long long)(key & kmask) << 32) | vo) : (Rec)(((key & kmask) << p.part_vbits) | vo);
+        rk[q] = atomicAdd(&lcnt[bk[q]], 1u);
+      }
+#pragma unroll
+      for (int q = 0; q < UB; ++q) {
+        if (!hit[q]) continue;
+        if (rk[q] < C) slots[(bk[q] << cl) + rk[q]] = rec[q];
+        else part_store<REC64>(p, bk[q], bcnt[bk[q]] + rk[q], rec[q]);  // slots full: straight to HBM
       }
     }
     return;
@@ -645,8 +599,9 @@ __global__ void __launch_bounds__(kBlock) k_scan(const KParams p) {
     for (int i = threadIdx.x; i < p.num_hll * m; i += kBlock) lds_hll[i] = 0;
   } else if (MODE == MODE_PARTITION) {
     if (threadIdx.x == 0) *pl_n = 0;
-    uint32_t* bcnt = reinterpret_cast<uint32_t*>(smem + p.pl_cnt_off) + 2 * p.num_parts;
-    for (int i = threadIdx.x; i < p.num_parts; i += kBlock) bcnt[i] = 0;
+    uint32_t* lcnt = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
+    uint32_t* bcnt = reinterpret_cast<uint32_t*>(smem + p.pl_bcnt_off);
+    for (int i = threadIdx.x; i < p.num_parts; i += kBlock) lcnt[i] = bcnt[i] = 0;
   }
   __syncthreads();
 
@@ -699,6 +654,13 @@ __global__ void __launch_bounds__(kBlock) k_scan(const KParams p) {
     if (stamps) t0 = __builtin_readcyclecounter();
     // stage the prefetched tile, then prefetch the next one of this wave
     tile_store<NL>(S, nvalid, wst, lane, pf);
+    if (MODE == MODE_PARTITION) {
+      // flush the slots filled in the previous round here, before this round's prefetch: the stores then
+      // complete under the decode instead of stalling the next tile_store (stores count in vmcnt too)
+      const uint32_t n = *pl_n;
+      lds_barrier();  // every wave has read n before anyone appends again
+      if (n >= (uint32_t)p.part_flush_at && !(p.dbg_flags & 2)) part_flush<REC64>(p, smem);
+    }
     SegPtr cs = S;
     const int32_t cw0 = w0, cnvalid = nvalid;
     advance();
@@ -716,14 +678,14 @@ __global__ void __launch_bounds__(kBlock) k_scan(const KParams p) {
 
     if (cnvalid > 0) {
       switch (cs->fkind) {
-        case FK_ALL: process_tile<MODE, NG, REC64, FK_ALL>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
-        case FK_RANGE: process_tile<MODE, NG, REC64, FK_RANGE>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
-        case FK_SET: process_tile<MODE, NG, REC64, FK_SET>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
-        case FK_BITMAP: process_tile<MODE, NG, REC64, FK_BITMAP>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
+        case FK_ALL: process_tile<MODE, NG, REC64, FK_ALL, LATE>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
+        case FK_RANGE: process_tile<MODE, NG, REC64, FK_RANGE, LATE>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
+        case FK_SET: process_tile<MODE, NG, REC64, FK_SET, LATE>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
+        case FK_BITMAP: process_tile<MODE, NG, REC64, FK_BITMAP, LATE>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
         case FK_DOCRANGE:
-          process_tile<MODE, NG, REC64, FK_DOCRANGE>(p, cs, smem, wst, lane, cw0, cnvalid, acc);
+          process_tile<MODE, NG, REC64, FK_DOCRANGE, LATE>(p, cs, smem, wst, lane, cw0, cnvalid, acc);
           break;
-        default: process_tile<MODE, NG, REC64, FK_GENERIC>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
+        default: process_tile<MODE, NG, REC64, FK_GENERIC, LATE>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
       }
     }
     if (LATE && c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
@@ -733,14 +695,7 @@ __global__ void __launch_bounds__(kBlock) k_scan(const KParams p) {
       t0 = t1;
     }
     if (MODE == MODE_PARTITION) {
-      lds_barrier();
-      const uint32_t n = *pl_n;
-      // flush when the next round (<= kWaves * tile_words * 64 records) might not fit
-      if (n > (uint32_t)(kPartS - round_words * 64)) {
-        part_flush<REC64>(p, smem, n);
-        if (threadIdx.x == 0) *pl_n = 0;
-      }
-      lds_barrier();
+      lds_barrier();  // this round's appends are complete before the next round's flush check
       if (stamps) t_sync += __builtin_readcyclecounter() - t0;
     }
   }
@@ -753,9 +708,9 @@ __global__ void __launch_bounds__(kBlock) k_scan(const KParams p) {
 
   // ---- workgroup epilogue
   if (MODE == MODE_PARTITION) {
-    const uint32_t n = *pl_n;
-    if (n) part_flush<REC64>(p, smem, n);
-    const uint32_t* bcnt = reinterpret_cast<const uint32_t*>(smem + p.pl_cnt_off) + 2 * p.num_parts;
+    lds_barrier();
+    if (*pl_n) part_flush<REC64>(p, smem);
+    const uint32_t* bcnt = reinterpret_cast<const uint32_t*>(smem + p.pl_bcnt_off);
     for (int i = threadIdx.x; i < p.num_parts; i += kBlock) p.part_count[(size_t)i * gridDim.x + blockIdx.x] = bcnt[i];
     return;
   }

@@ -155,7 +155,7 @@ enum : int32_t { AGG_COUNT = 0, AGG_SUM = 1, AGG_MIN = 2, AGG_MAX = 3, AGG_HLL =
 
 enum : int32_t { MODE_COUNT = 0, MODE_AGG = 1, MODE_GROUP_LDS = 2, MODE_GROUP_GLOBAL = 3, MODE_PARTITION = 4 };
 
-constexpr int kPartS = 4096;        // records staged per workgroup before a flush (16 per thread)
+constexpr int kPartSlots = 8192;    // LDS record slots per workgroup (partition p owns slots [p*C, (p+1)*C))
 constexpr int kPartMaxParts = 1024;
 constexpr int kPartKeysLog2 = 12;   // keys per partition = 4096: kernel B's LDS table <= 80 KiB
 
@@ -173,6 +173,8 @@ struct KParams {
   int32_t stage_stride;           // bytes of one wave's staging area
   int32_t tile_words;             // 64-doc words per wave tile
   int32_t late_prefetch;          // decode gathers from HBM: issue the next tile's loads after it
+  int32_t dbg_flags;              // PH_DEBUG_FLAGS (timing experiments only; results are wrong when set):
+                                  // 1 no record stores, 2 no flush, 4 no record append
   unsigned long long* dbg;        // PH_DEBUG_STAMPS: per-workgroup cycle totals [grid][4] (wave 0)
   int32_t stage_soff[kMaxStage];  // byte offset of staged stream s inside a wave's area
   int32_t lds_cnt_off;            // MODE_GROUP_LDS: byte offset of the count table
@@ -205,7 +207,9 @@ struct KParams {
   int64_t part_vbase;             // record value = value - part_vbase
   void* part_buf;                 // [num_parts][gridDim.x][part_cap] records: one region per workgroup
   uint32_t* part_count;           // [num_parts][gridDim.x] records written per region (may exceed part_cap)
-  int32_t pl_rec_off, pl_bkt_off, pl_sorted_off, pl_sbkt_off, pl_cnt_off, pl_misc_off;  // LDS layout
+  int32_t pl_slot_off, pl_lcnt_off, pl_bcnt_off, pl_misc_off;  // LDS layout
+  int32_t part_slot_log2;         // C = 1 << part_slot_log2 LDS slots per partition
+  int32_t part_flush_at;          // flush the slots once this many records were appended
   unsigned long long* ovf_count;  // overflow table (same layout as out_*), merged at the end
   int64_t* ovf_sum;
   int64_t* ovf_min;

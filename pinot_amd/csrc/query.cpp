@@ -1028,7 +1028,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     for (int s = 0; s < kp.nstage; ++s)
       for (auto& d : dsegs) maxbits[s] = std::max(maxbits[s], (int)d.streams[s].bits);
     const int pool = mode == MODE_COUNT ? kPrefetchCount : kPrefetchOther;
-    int tw = mode == MODE_PARTITION ? 16 : kMaxTileWords;
+    int tw = mode == MODE_PARTITION ? 8 : kMaxTileWords;
+    if (const char* e = getenv("PH_TILE_WORDS")) tw = std::max(4, std::min(kMaxTileWords, atoi(e)));  // tuning knob
     auto loads = [&](int t) {
       int n = 0;
       for (int s = 0; s < kp.nstage; ++s) n += maxbits[s] ? stage_loads(t, maxbits[s]) : 0;
@@ -1071,6 +1072,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     d.npieces = np;
   }
+  if (const char* e = getenv("PH_DEBUG_FLAGS")) kp.dbg_flags = atoi(e);
   if (getenv("PH_DEBUG_STAMPS")) {
     kp.dbg = scratch.alloc<unsigned long long>(4 * (size_t)ctx->num_cus * 8);
     PH_HIP_CHECK(hipMemsetAsync(kp.dbg, 0, 32 * (size_t)ctx->num_cus * 8, st));
@@ -1145,7 +1147,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       if (P > kPartMaxParts) fail(PH_ERR_UNSUPPORTED, "partitioned group-by too large");
       const int vbits = nvals ? std::max(1, bits_for_range((uint64_t)(vmax - vmin))) : 0;
       rec64 = (klo + vbits > 32) ? 1 : 0;
-      int64_t batch_rows = 32 << 20;
+      int64_t batch_rows = int64_t(1) << 31;  // one batch: launch tails of many short batches cost more than MALL reuse saves
       if (const char* e = getenv("PH_PART_BATCH_ROWS")) batch_rows = std::max<int64_t>(1 << 16, atoll(e));
       // batches: contiguous chunk ranges of ~batch_rows docs
       std::vector<std::pair<int32_t, int32_t>> batches;
@@ -1186,6 +1188,11 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       void* bufs[2];
       uint32_t* counts[2];
       for (int b = 0; b < 2; ++b) {
+        if (b == 1 && batches.size() == 1) {  // one batch: no double buffering
+          bufs[1] = bufs[0];
+          counts[1] = counts[0];
+          break;
+        }
         bufs[b] = scratch.alloc<uint8_t>((size_t)P * grid_a * cap * rec_bytes);
         counts[b] = scratch.alloc<uint32_t>((size_t)P * grid_a);
       }

@@ -59,7 +59,7 @@ std::unique_ptr<DeviceBuffer> Context::scratch_acquire(size_t n) {
 
 void Context::scratch_release(std::unique_ptr<DeviceBuffer> b) {
   if (!b || !b->ptr) return;
-  constexpr size_t kMaxCached = size_t(8) << 30;  // keep at most 8 GiB of idle scratch per context
+  constexpr size_t kMaxCached = size_t(32) << 30;  // keep at most 32 GiB of idle scratch per context (of 288)
   if (b->bytes > kMaxCached) return;
   while (scratch_free_bytes + b->bytes > kMaxCached && !scratch_free.empty()) {
     auto it = scratch_free.begin();

@@ -88,6 +88,43 @@ __global__ void __launch_bounds__(256) k_tiles_pf(const uint8_t* __restrict__ p,
   if (acc == 0x12345678u) out[0] = acc;
 }
 
+// 4 separate streams (b = 10, 10, 10, 20 bits): each wave reads the same 16-word tile span of every stream
+// (1280, 1280, 1280, 2560 bytes), like the partitioned group-by scan; optional workgroup barrier per round.
+template <int BAR>
+__global__ void __launch_bounds__(256) k_4streams(const uint8_t* __restrict__ s0, const uint8_t* __restrict__ s1,
+                                                  const uint8_t* __restrict__ s2, const uint8_t* __restrict__ s3,
+                                                  size_t words, uint32_t* out) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const size_t tiles = words / 16;
+  const size_t t0 = tiles * blockIdx.x / gridDim.x, t1 = tiles * (blockIdx.x + 1) / gridDim.x;
+  uint32_t acc = 0;
+  for (size_t t = t0 + wave; t < t1 + 4; t += 4) {
+    u32x4 v[9];
+    const bool ok = t < t1;
+    if (ok) {
+      const size_t w0 = t * 16;
+      const uint8_t* srcs[3] = {s0 + w0 * 80, s1 + w0 * 80, s2 + w0 * 80};
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        v[2 * s] = *reinterpret_cast<const u32x4*>(srcs[s] + lane * 16);
+        if (1024 + lane * 16 < 1288) v[2 * s + 1] = *reinterpret_cast<const u32x4*>(srcs[s] + 1024 + lane * 16);
+        else v[2 * s + 1] = u32x4{0, 0, 0, 0};
+      }
+      const uint8_t* d = s3 + w0 * 160;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        if (k * 1024 + lane * 16 < 2568) v[6 + k] = *reinterpret_cast<const u32x4*>(d + k * 1024 + lane * 16);
+        else v[6 + k] = u32x4{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    if (BAR) __syncthreads();
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main(int argc, char** argv) {
   const size_t bytes = (size_t)2560 << 20;  // 2.5 GiB
   uint8_t* d;
@@ -95,9 +132,10 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&d, bytes + 65536));
   CK(hipMalloc(&out, 64));
   CK(hipMemset(d, 1, bytes));
-  hipEvent_t a, b;
+  hipEvent_t a, b, b_ev;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
+  b_ev = b;
   auto run = [&](const char* name, auto launch) {
     for (int i = 0; i < 3; ++i) launch();
     CK(hipDeviceSynchronize());
@@ -131,6 +169,35 @@ int main(int argc, char** argv) {
     run(nm, [&] {
       hipLaunchKernelGGL(k_tiles_pf<5>, dim3(256 * bpc), dim3(256), 4 * 5 * 1024, 0, d, bytes, chunk, out);
     });
+  }
+  {
+    // 1e9 docs: streams of 1.25, 1.25, 1.25, 2.5 GB in 4 allocations
+    const size_t words = 1000000000 / 64;
+    uint8_t* b[4];
+    for (int i = 0; i < 4; ++i) {
+      const size_t n = words * (i == 3 ? 160 : 80) + 65536;
+      CK(hipMalloc(&b[i], n));
+      CK(hipMemset(b[i], 1, n));
+    }
+    const double tot = words * 400.0;
+    for (int bpc : {3, 4, 8}) {
+      for (int bar : {0, 1}) {
+        auto launch = [&] {
+          if (bar) hipLaunchKernelGGL(k_4streams<1>, dim3(256 * bpc), dim3(256), 0, 0, b[0], b[1], b[2], b[3], words, out);
+          else hipLaunchKernelGGL(k_4streams<0>, dim3(256 * bpc), dim3(256), 0, 0, b[0], b[1], b[2], b[3], words, out);
+        };
+        for (int i = 0; i < 2; ++i) launch();
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(a));
+        for (int i = 0; i < 5; ++i) launch();
+        CK(hipEventRecord(b_ev));
+        CK(hipEventSynchronize(b_ev));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b_ev));
+        ms /= 5;
+        printf("4 streams %d/CU barrier=%d                   %8.3f ms  %7.0f GB/s\n", bpc, bar, ms, tot / ms / 1e6);
+      }
+    }
   }
   return 0;
 }
