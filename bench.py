@@ -1,17 +1,22 @@
-"""Benchmark of the segment filter -> group-by hot path (BASELINE.json configs[2], the headline
-"filter+group-by SUM query"):
+"""Benchmark of the segment filter -> group-by hot path (BASELINE.json metric "filter+group-by rows/s and achieved
+HBM GB/s, 1B rows"; headline = configs[2] with SURVEY.md 8(d)'s filter, "filter+group-by SUM query"):
 
     SET numGroupsLimit=2000000; SET minServerGroupTrimSize=-1; SET minSegmentGroupTrimSize=-1;
     SELECT g1, g2, SUM(m), COUNT(*), MIN(m), MAX(m) FROM t WHERE f BETWEEN 0 AND 499
     GROUP BY g1, g2 ORDER BY g1, g2 LIMIT 2000000
 
-over 1e9 synthetic rows per GPU in 100 segments x 10M docs: g1, g2 INT uniform
-over 1000 values (b = 10), m INT through a 65 536-entry dictionary over [0, 2^20) (b = 16), f INT uniform
-over 1000 values (b = 10).  Algorithmic bytes = sum over the 4 referenced columns of ceil(N*b/8) = 5.75 GB.
+over 1e9 synthetic rows per GPU in 100 segments x 10M docs: g1, g2 INT uniform over 1000 values (b = 10),
+m INT through a 65 536-entry dictionary over [0, 2^20) (b = 16), f INT uniform over 1000 values (b = 10).
+Algorithmic bytes = sum over the 4 referenced columns of ceil(N*b/8) = 5.75 GB per GPU.
 
-A step = one full ph_query_execute (plan + one batched kernel over all segments + result materialisation
-of ~1M groups to the host).  Segments are pinned in HBM before timing.  Multi-GPU: one process per GPU,
-each rank holds its own 1e9 rows (weak scaling); the dense partial tables are merged with RCCL.
+A step = one full query: plan + the batched scan kernels over every segment of this GPU + (N > 1) the RCCL
+reduce-scatter of the dense partial tables by key range + finalising this rank's key shard into host result
+columns (~1M groups at N = 1).  Segments are pinned in HBM before timing.  Multi-GPU: one process per GPU,
+each rank holds its own 1e9 rows (weak scaling).
+
+`roofline.kernel_ms` is the device time of the scan kernels of one step, taken with HIP events recorded on the
+stream the kernels run on (ph_exec_stats.device_ms); `traffic` is read from the PMC summary under profiles/
+(tools/gpu_pmc.sh) when one exists for the workload.
 """
 import argparse
 import json
@@ -44,10 +49,9 @@ WORKLOADS = {
     "config3-agg": ("SELECT SUM(m), COUNT(*), MIN(m), MAX(m) FROM t WHERE f BETWEEN 0 AND 499",
                     {"m": (65536, 16), "f": (1000, 10)}, "config3-agg: WHERE f BETWEEN 0 AND 499 SUM/COUNT/MIN/MAX(m)"),
 }
-QUERY, COLS, _ = WORKLOADS["config3"]
-HBM_PEAK_GBS = 8000.0
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 KERNEL_NAMES = {0: "k_scan<MODE_COUNT>", 1: "k_scan<MODE_AGG>", 2: "k_scan<MODE_GROUP_LDS>",
-                3: "k_scan<MODE_GROUP_GLOBAL>", 4: "k_scan<MODE_PARTITION> + k_part_agg (overlapped)"}
+                3: "k_scan<MODE_GROUP_GLOBAL>", 4: "k_scan<MODE_PARTITION> + k_part_agg"}
 
 
 def log(*a):
@@ -59,9 +63,8 @@ def m_dictionary():
     return np.sort(rng.choice(1 << 20, 65536, replace=False)).astype(np.int32)
 
 
-def make_segment_buffers(seg_index, rows, seed, cols=None):
+def make_segment_buffers(seg_index, rows, seed, cols):
     from pinot_amd.segment import ColumnBuffers, SegmentBuffers, encode_dictionary, fixed_bit_pack
-    cols = COLS if cols is None else cols
     rng = np.random.default_rng([seed, seg_index])
     seg = SegmentBuffers(f"t_{seed}_{seg_index}", rows)
     mdict = m_dictionary()
@@ -74,19 +77,41 @@ def make_segment_buffers(seg_index, rows, seed, cols=None):
     return seg
 
 
-def algorithmic_bytes(rows_per_seg, nseg, cols=None):
-    cols = COLS if cols is None else cols
+def algorithmic_bytes(rows_per_seg, nseg, cols):
     return nseg * sum((rows_per_seg * b + 7) // 8 for _, b in cols.values())
 
 
-def cpu_baseline(bufs, query, threads):
-    """The oracle (C restatement of the reference loop nest) over the same segments on host cores."""
+def oracle_segments(bufs):
     from oracle import oracle as O
-    segs = [O.segment_from_dict_ids(b.name, {c: dict(dictionary=cb.dictionary_values, fwd=cb.forward_index,
-                                                       bits=cb.bits, data_type="INT", num_docs=b.num_docs)
-                                             for c, cb in b.columns.items()}) for b in bufs]
-    dt, keys, aggs = O.execute_timed(query, segs, threads)
-    return dt, keys, aggs
+    return [O.segment_from_dict_ids(b.name, {c: dict(dictionary=cb.dictionary_values, fwd=cb.forward_index,
+                                                     bits=cb.bits, data_type="INT", num_docs=b.num_docs)
+                                           for c, cb in b.columns.items()}) for b in bufs]
+
+
+def cpu_baseline(bufs, q, threads, target_s=10.0):
+    """The oracle (C restatement of the reference loop nest, one worker per segment on `threads` host threads,
+    as GroupByCombineOperator) over a bounded sample of the same segments: calibrated on one segment, then
+    as many segments as make ~target_s seconds of CPU work."""
+    from oracle import oracle as O
+    dt1, _, _ = O.execute_timed(q, oracle_segments(bufs[:1]), 1)  # one segment on one thread
+    waves = max(1, int(target_s / max(dt1, 1e-3)))                 # segments per thread in ~target_s
+    n = int(max(1, min(len(bufs), waves * threads)))
+    segs = oracle_segments(bufs[:n])
+    dt, keys, aggs = O.execute_timed(q, segs, threads)
+    return n, dt, keys, aggs
+
+
+def load_traffic(workload, kernel_count):
+    """HBM bytes per launch from profiles/<round>_pmc_<workload>.json (tools/gpu_pmc.sh), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*pmc_{workload}.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+        return float(d["hbm_bytes_per_query"])
+    except Exception:
+        return None
 
 
 def main():
@@ -96,7 +121,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--rows", type=int, default=1_000_000_000, help="rows per GPU")
     ap.add_argument("--segment-rows", type=int, default=10_000_000)
-    ap.add_argument("--cpu-segments", type=int, default=-1, help="segments in the CPU-baseline sample (-1: auto)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample size in seconds of work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--workload", default="config3", choices=sorted(WORKLOADS))
@@ -113,6 +138,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = local_rank
 
+    from pinot_amd.distributed import DistributedQuery
     from pinot_amd.engine import GpuContext
     from pinot_amd.query import parse_sql
 
@@ -127,17 +153,26 @@ def main():
         b = make_segment_buffers(i, seg_rows, seed=1000 + rank, cols=cols)
         pinned.append(ctx.pin(b))
         bufs.append(b)
-        if i % 10 == 9:
+        if i % 20 == 19:
             log(f"[rank {rank}] pinned {i + 1}/{nseg} segments ({time.time() - t0:.1f}s)")
-    # table-level dictionaries: identical on every rank, so group ids align for the RCCL merge
+    # table-level dictionaries: identical on every rank, so dense group ids line up for the RCCL merge
     for g in q.group_by:
         ctx.set_table_dictionary(g, "INT", np.arange(cols[g][0], dtype=np.int32))
 
+    runner = DistributedQuery(ctx)
+    last = {}
+
     def step():
-        return ctx.execute(q, pinned, copy=False)
+        if world > 1:
+            res, shard = runner.execute(q, pinned, copy=False)
+            last["res"], last["shard"] = res, shard
+            return res
+        r = ctx.execute(q, pinned, copy=False)
+        last["res"] = r
+        return r
 
     for _ in range(args.warmup):
-        r = step()
+        step()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -145,7 +180,8 @@ def main():
     ts = time.perf_counter()
     for _ in range(args.steps):
         r = step()
-        dev_ms.append(r.stats.device_ms)
+        if r is not None:
+            dev_ms.append(r.stats.device_ms)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -157,9 +193,14 @@ def main():
     ms_per_step = elapsed * 1000.0 / args.steps
     total_rows = nseg * seg_rows * world
     value = total_rows / (ms_per_step / 1000.0)
-    kernel_ms = float(np.mean(dev_ms))
+    if world > 1:  # device time of the scan is measured inside execute_dense; report rank 0's
+        kernel_ms = float(np.mean(dev_ms)) if dev_ms else float("nan")
+    else:
+        kernel_ms = float(np.mean(dev_ms))
     alg = algorithmic_bytes(seg_rows, nseg, cols)
     achieved = alg / (kernel_ms / 1000.0) / 1e9
+    mode = last["res"].stats.mode if last.get("res") is not None else -1
+    traffic = load_traffic(args.workload, 1)
 
     result = {
         "metric": "filter+group-by rows/s and achieved HBM GB/s, 1B rows",
@@ -174,27 +215,28 @@ def main():
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (seeded PCG64 dictIds, 100 x 10M-doc segments per GPU)",
-        "config": {"workload": wdesc,
-                   "rows_per_gpu": nseg * seg_rows, "segments_per_gpu": nseg, "parallelism": f"segments x{world}"},
+        "config": {"workload": wdesc, "rows_per_gpu": nseg * seg_rows, "segments_per_gpu": nseg,
+                   "parallelism": f"segments sharded x{world}" + (", RCCL reduce-scatter by key range" if world > 1
+                                                                  else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": KERNEL_NAMES.get(r.stats.mode, "k_scan"), "kernel_ms": kernel_ms,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": KERNEL_NAMES.get(mode, "k_scan"), "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": alg},
-        "groups": r.num_groups,
-        "docs_scanned": r.stats.num_docs_scanned,
     }
+    if last.get("res") is not None:
+        result["groups"] = last["res"].num_groups
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = min(16, os.cpu_count() or 1)
-        ncpu = min(nseg, 8) if args.cpu_segments < 0 else min(nseg, args.cpu_segments)
-        dt, keys, aggs = cpu_baseline(bufs[:ncpu], q, threads)
-        rows = ncpu * seg_rows
+        n, dt, keys, aggs = cpu_baseline(bufs, q, threads, args.cpu_seconds)
+        rows = n * seg_rows
         result["cpu_baseline"] = {"value": rows / dt, "unit": "rows/s", "cores": threads, "kind": "port",
-                                  "sample": f"{ncpu} segments x {seg_rows} rows, same data and query, oracle "
-                                            f"(C restatement of the reference loop nest), {dt:.2f}s"}
+                                  "sample": f"{n} of {nseg} segments x {seg_rows} rows (same data and query), oracle "
+                                            f"C restatement of the reference loop nest on {threads} host threads, "
+                                            f"{dt:.2f}s"}
         if not args.no_parity:
-            # parity on the sample: GPU over the same segments vs the oracle -- group keys, COUNT, integer
-            # SUM, MIN, MAX bit-exact (synthetic group dictionaries are 0..C-1, so value == global id)
-            r = ctx.execute(q, pinned[:ncpu])
+            # parity on the sample: GPU over the same segments vs the oracle -- group keys, COUNT, integer SUM,
+            # MIN, MAX bit-exact (synthetic group dictionaries are 0..C-1, so value == global id)
+            r = ctx.execute(q, pinned[:n])
             order = np.argsort(keys)
             k_cpu = keys[order]
             a_cpu = aggs[order]
@@ -206,7 +248,7 @@ def main():
             og = np.argsort(k_gpu)
             a_gpu = np.stack([c.astype(np.float64) for c in r.agg_columns], axis=1)[og]
             ok = bool(np.array_equal(k_gpu[og], k_cpu) and np.array_equal(a_gpu, a_cpu))
-            result["parity_sample"] = {"segments": ncpu, "groups": int(len(k_cpu)), "bit_exact": ok}
+            result["parity_sample"] = {"segments": n, "groups": int(len(k_cpu)), "bit_exact": ok}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

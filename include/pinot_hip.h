@@ -186,6 +186,43 @@ const void* ph_result_key_data(const ph_result* r, int32_t group_by_index);
 int ph_result_aggregation(const ph_result* r, int32_t aggregation_index, void* out);
 const void* ph_result_aggregation_data(const ph_result* r, int32_t aggregation_index);
 
+/* ------------------------------------------------------------------ multi-GPU combine: dense partials */
+/* GroupByCombineOperator.mergeResults (GroupByCombineOperator.java:169-181) and
+ * AggregationResultsBlockMerger (:33-45) merge per-segment results keyed by group VALUES.  Over table-level
+ * dictionaries (ph_table_set_dictionary, identical on every GPU) a group is a dense id in
+ * [0, num_groups), so the partial results of one GPU are a few dense device tables and the cross-GPU
+ * merge is a plain reduction of those tables (RCCL reduce-scatter / all-reduce over xGMI, one op per
+ * table: COUNT/SUM add, MIN/MAX min/max, HLL registers max = HyperLogLog.addAll).
+ *
+ *   ph_query_dense_layout   the tables of a query: count, per element type and reduce op
+ *   ph_query_execute_dense  scans this GPU's segments into caller-allocated device tables (initialised
+ *                           here), launching on the context's stream; nothing is copied to the host
+ *   ph_dense_finalize       turns key shard [group_begin, group_end) of reduced tables (device pointers to
+ *                           the shard's first group) into a ph_result, exactly like ph_query_execute's */
+typedef enum {
+  PH_REDUCE_SUM_I64 = 0, /* int64 add (COUNT, integer SUM) */
+  PH_REDUCE_SUM_F64 = 1, /* float64 add (FLOAT/DOUBLE SUM; order-dependent within 1e-9 relative) */
+  PH_REDUCE_MIN_I64 = 2, /* int64 min (MIN: integer values, or order keys of doubles) */
+  PH_REDUCE_MAX_I64 = 3, /* int64 max (MAX) */
+  PH_REDUCE_MAX_U32 = 4  /* uint32 max (DISTINCTCOUNTHLL registers) */
+} ph_reduce_op;
+
+#define PH_MAX_DENSE_TABLES 16
+typedef struct {
+  int64_t num_groups;                            /* dense key space (1 for aggregation-only queries) */
+  int32_t num_tables;
+  int32_t elems_per_group[PH_MAX_DENSE_TABLES];  /* table t: num_groups * elems_per_group[t] elements */
+  int32_t reduce_op[PH_MAX_DENSE_TABLES];        /* ph_reduce_op */
+  int32_t elem_bytes[PH_MAX_DENSE_TABLES];       /* 8 or 4 */
+} ph_dense_layout;
+
+int ph_query_dense_layout(ph_ctx* ctx, const ph_query* query, ph_segment* const* segments, int32_t num_segments,
+                          ph_dense_layout* out);
+int ph_query_execute_dense(ph_ctx* ctx, const ph_query* query, ph_segment* const* segments, int32_t num_segments,
+                           void* const* device_tables, ph_exec_stats* stats);
+int ph_dense_finalize(ph_ctx* ctx, const ph_query* query, ph_segment* const* segments, int32_t num_segments,
+                      const void* const* device_tables, int64_t group_begin, int64_t group_end, ph_result** out);
+
 /* ------------------------------------------------------------------ segment creation helper */
 /* FixedBitSVForwardIndexWriter: packs n dictIds with `bits` bits, MSB-first big-endian; out_size >=
  * (n*bits+7)/8 */

@@ -11,7 +11,8 @@ thread_local std::string g_last_error;
 void fail(int code, const std::string& msg) { throw Error{code, msg}; }
 
 ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc);
-ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const* segs, int32_t nseg);
+ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const* segs, int32_t nseg,
+                              const DenseArgs* dense);
 }  // namespace ph
 
 using namespace ph;
@@ -167,7 +168,36 @@ int ph_query_execute(ph_ctx* ctx, const ph_query* query, ph_segment* const* segm
   return guarded([&] {
     if (!ctx || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
     *out = nullptr;
-    *out = query_execute_impl(&ctx->c, query, segments, num_segments);
+    *out = query_execute_impl(&ctx->c, query, segments, num_segments, nullptr);
+  });
+}
+
+int ph_query_dense_layout(ph_ctx* ctx, const ph_query* query, ph_segment* const* segments, int32_t num_segments,
+                          ph_dense_layout* out) {
+  return guarded([&] {
+    if (!ctx || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
+    DenseArgs d{DENSE_LAYOUT, nullptr, 0, 0, out};
+    query_execute_impl(&ctx->c, query, segments, num_segments, &d);
+  });
+}
+
+int ph_query_execute_dense(ph_ctx* ctx, const ph_query* query, ph_segment* const* segments, int32_t num_segments,
+                           void* const* device_tables, ph_exec_stats* stats) {
+  return guarded([&] {
+    if (!ctx || !device_tables) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
+    DenseArgs d{DENSE_EXECUTE, device_tables, 0, 0, nullptr};
+    std::unique_ptr<ph_result> r(query_execute_impl(&ctx->c, query, segments, num_segments, &d));
+    if (stats && r) *stats = r->stats;
+  });
+}
+
+int ph_dense_finalize(ph_ctx* ctx, const ph_query* query, ph_segment* const* segments, int32_t num_segments,
+                      const void* const* device_tables, int64_t group_begin, int64_t group_end, ph_result** out) {
+  return guarded([&] {
+    if (!ctx || !device_tables || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    DenseArgs d{DENSE_FINALIZE, const_cast<void* const*>(device_tables), group_begin, group_end, nullptr};
+    *out = query_execute_impl(&ctx->c, query, segments, num_segments, &d);
   });
 }
 

@@ -1099,7 +1099,7 @@ __global__ void __launch_bounds__(256) k_compact_write(const CompactParams p) {
       }
       for (int j = 0; j < kMaxGroupCols; ++j) {
         if (j >= p.num_keys) continue;
-        const int64_t id = (g / p.key_stride[j]) % p.key_size[j];
+        const int64_t id = ((g + p.key_base) / p.key_stride[j]) % p.key_size[j];
         switch (p.key_type[j]) {
           case PH_INT:
             reinterpret_cast<int32_t*>(p.key_out[j])[r] = (int32_t)reinterpret_cast<const int64_t*>(p.key_table[j])[id];

@@ -264,6 +264,15 @@ struct DeviceBuffer {
   T* as() const { return reinterpret_cast<T*>(ptr); }
 };
 
+// ------------------------------------------------------------------ dense partial tables (multi-GPU combine)
+enum : int32_t { DENSE_LAYOUT = 1, DENSE_EXECUTE = 2, DENSE_FINALIZE = 3 };
+struct DenseArgs {
+  int32_t op;
+  void* const* tables;     // DENSE_EXECUTE / DENSE_FINALIZE: caller-owned device tables (layout order)
+  int64_t g0, g1;          // DENSE_FINALIZE: the key shard [g0, g1) the tables hold
+  ph_dense_layout* layout; // DENSE_LAYOUT output
+};
+
 // ------------------------------------------------------------------ host-side segment model
 struct Dictionary {
   int32_t type = PH_INT;
@@ -409,6 +418,7 @@ struct CompactParams {
   int32_t key_type[kMaxGroupCols];
   void* key_out[kMaxGroupCols];
   int64_t* count_out;
+  int64_t key_base;          // group id of element 0 (finalizing one key shard of a dense table)
   unsigned long long* blk;   // [kCompactBlocks + 1] counts -> offsets, total at [kCompactBlocks]
   int32_t* flags;            // bit 0: an integer SUM reached 2^53
 };

@@ -595,7 +595,10 @@ bool ensure_value_stream(Context* ctx, ph_segment* seg, Column& c) {
 
 }  // namespace
 
-ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const* segs_in, int32_t nseg) {
+ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const* segs_in, int32_t nseg,
+                              const DenseArgs* dn) {
+  const int dop = dn ? dn->op : 0;
+  const bool fin = dop == DENSE_FINALIZE;
   using clock = std::chrono::steady_clock;
   const auto t0 = clock::now();
   if (!q) fail(PH_ERR_INVALID_ARGUMENT, "null query");
@@ -702,6 +705,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // ---- aggregation-only, no filter, metadata-answerable (NonScanBasedAggregationOperator)
   bool non_scan = q->filter_root < 0 && q->num_group_by == 0 && nagg > 0;
   for (int k = 0; k < nagg && non_scan; ++k) non_scan = q->aggregations[k].type != PH_AGG_SUM;
+  if (dop) non_scan = false;  // dense partials always come from the scan
   res->num_groups = 1;
   auto init_row_results = [&](int64_t rows) {
     res->aggs.resize(nagg);
@@ -752,7 +756,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<SegProgram> progs(nseg);
   std::vector<PNode> roots(nseg);
   std::vector<char> seg_live(nseg, 1);
-  for (int i = 0; i < nseg; ++i) {
+  for (int i = 0; i < nseg && dop != DENSE_LAYOUT && !fin; ++i) {
     PNode root;
     root.kind = L_ALL;
     if (q->filter_root >= 0) root = pl.build(segs[i], q->filter_root, 0);
@@ -763,7 +767,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
 
   // ---- inverted-index leaves -> device doc bitmaps
   std::vector<uint32_t*> bitmap_dev(pl.bitmaps.size(), nullptr);
-  for (size_t i = 0; i < pl.bitmaps.size(); ++i) {
+  for (size_t i = 0; i < pl.bitmaps.size() && dop != DENSE_LAYOUT && !fin; ++i) {
     BitmapLeaf& b = pl.bitmaps[i];
     const size_t words = ((size_t)b.seg->num_docs + 31) / 32 + 1;
     uint32_t* bm = scratch.alloc<uint32_t>(words);
@@ -817,6 +821,32 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
   }
   const int64_t G = num_groups;
+  if (dop) {
+    // partial tables of different GPUs line up only over table-level dictionaries
+    for (auto& g : group_cols)
+      if (!ctx->table_dicts.count(g))
+        fail(PH_ERR_INVALID_ARGUMENT, "dense partials need ph_table_set_dictionary for group-by column " + g);
+    if (fin && (dn->g0 < 0 || dn->g1 < dn->g0 || dn->g1 > G)) fail(PH_ERR_INVALID_ARGUMENT, "bad key shard");
+  }
+  if (dop == DENSE_LAYOUT) {
+    ph_dense_layout& L = *dn->layout;
+    L = ph_dense_layout{};
+    L.num_groups = G;
+    auto add = [&](int32_t per_group, int32_t op, int32_t bytes) {
+      L.elems_per_group[L.num_tables] = per_group;
+      L.reduce_op[L.num_tables] = op;
+      L.elem_bytes[L.num_tables] = bytes;
+      L.num_tables++;
+    };
+    add(1, PH_REDUCE_SUM_I64, 8);  // matched docs per group
+    for (int j = 0; j < nvals; ++j) {
+      if (val_ops[j] & 1) add(1, val_is_int[j] ? PH_REDUCE_SUM_I64 : PH_REDUCE_SUM_F64, 8);
+      if (val_ops[j] & 2) add(1, PH_REDUCE_MIN_I64, 8);  // int64 values / order keys of doubles
+      if (val_ops[j] & 4) add(1, PH_REDUCE_MAX_I64, 8);
+    }
+    if (num_hll) add(num_hll * m, PH_REDUCE_MAX_U32, 4);
+    return nullptr;
+  }
 
   // ---- kernel parameters
   KParams kp{};
@@ -867,8 +897,23 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
     }
 
+  int mode = -3;  // DENSE_FINALIZE: no scan
+  float dev_ms = 0.f;
+  const int64_t hll_words = G * num_hll * (m ? m : 1);
+  if (fin) {
+    // the tables hold the (already reduced) key shard [g0, g1): layout order of ph_query_dense_layout
+    int t = 0;
+    kp.out_count = reinterpret_cast<unsigned long long*>(dn->tables[t++]);
+    for (int j = 0; j < nvals; ++j) {
+      if (val_ops[j] & 1) kp.out_sum[j] = dn->tables[t++];
+      if (val_ops[j] & 2) kp.out_min[j] = reinterpret_cast<int64_t*>(dn->tables[t++]);
+      if (val_ops[j] & 4) kp.out_max[j] = reinterpret_cast<int64_t*>(dn->tables[t++]);
+    }
+    if (num_hll) kp.out_hll = reinterpret_cast<uint32_t*>(dn->tables[t++]);
+    stats.plan_mode = mode;
+    res->mode = mode;
+  } else {
   // ---- mode selection (LDS table offsets are relative to the end of the staging areas, fixed below)
-  int mode;
   size_t lds_tables = 16;
   int rec64 = 0;
   kp.stage_off = 0;
@@ -906,26 +951,30 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
   }
 
-  // ---- outputs
-  kp.out_count = scratch.alloc<unsigned long long>(G);
+  // ---- outputs (dense execute: the caller's tables, initialised here)
+  auto out_table = [&](int& t, size_t bytes) -> void* {
+    if (dop == DENSE_EXECUTE) return dn->tables[t++];
+    return scratch.alloc<uint8_t>(bytes);
+  };
+  int tix = 0;
+  kp.out_count = reinterpret_cast<unsigned long long*>(out_table(tix, 8 * (size_t)G));
   PH_HIP_CHECK(hipMemsetAsync(kp.out_count, 0, sizeof(unsigned long long) * G, st));
   for (int j = 0; j < nvals; ++j) {
     if (val_ops[j] & 1) {
-      kp.out_sum[j] = scratch.alloc<int64_t>(G);
+      kp.out_sum[j] = out_table(tix, 8 * (size_t)G);
       PH_HIP_CHECK(hipMemsetAsync(kp.out_sum[j], 0, 8 * G, st));
     }
     if (val_ops[j] & 2) {
-      kp.out_min[j] = scratch.alloc<int64_t>(G);
+      kp.out_min[j] = reinterpret_cast<int64_t*>(out_table(tix, 8 * (size_t)G));
       launch_fill_i64(kp.out_min[j], INT64_MAX, G, st);
     }
     if (val_ops[j] & 4) {
-      kp.out_max[j] = scratch.alloc<int64_t>(G);
+      kp.out_max[j] = reinterpret_cast<int64_t*>(out_table(tix, 8 * (size_t)G));
       launch_fill_i64(kp.out_max[j], INT64_MIN, G, st);
     }
   }
-  const int64_t hll_words = G * num_hll * (m ? m : 1);
   if (num_hll) {
-    kp.out_hll = scratch.alloc<uint32_t>(hll_words);
+    kp.out_hll = reinterpret_cast<uint32_t*>(out_table(tix, 4 * (size_t)hll_words));
     PH_HIP_CHECK(hipMemsetAsync(kp.out_hll, 0, 4 * hll_words, st));
   }
 
@@ -1107,7 +1156,6 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   for (auto& fb : fbitmap_fix) dsegs[fb.first].fptr = bitmap_dev[fb.second];
   PH_HIP_CHECK(hipStreamSynchronize(st));  // pageable payload copies above
 
-  float dev_ms = 0.f;
   if (!chunks.empty()) {
     DevSegment* d_segs = scratch.alloc<DevSegment>(dsegs.size());
     FilterInsn* d_prog = scratch.alloc<FilterInsn>(std::max<size_t>(1, all_insns.size()));
@@ -1285,8 +1333,19 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   stats.device_ms = dev_ms;
   res->mode = mode;
   stats.plan_mode = mode;
+  if (dop == DENSE_EXECUTE) {
+    // partial tables stay on the device for the cross-GPU reduction; matched docs are counted when a key
+    // shard is finalised
+    stats.num_docs_scanned = -1;
+    stats.host_ms = std::chrono::duration<double, std::milli>(clock::now() - t0).count() - dev_ms;
+    return res.release();
+  }
+  }  // !fin
 
-  // ---- results
+  // ---- results (DENSE_FINALIZE: only the key shard [RB, RB + RG) of the tables)
+  const int64_t RB = fin ? dn->g0 : 0;
+  const int64_t RG = fin ? dn->g1 - dn->g0 : G;
+  const int64_t rhll_words = RG * num_hll * (m ? m : 1);
   const int ncols_proj = (int)projected.size();
   auto finish_value = [&](int k, int64_t raw, int64_t cnt_for_default, bool is_sum) -> double {
     const int j = agg_val[k];
@@ -1337,8 +1396,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     // device-side compaction: non-empty groups in key order, keys decoded, values converted to double,
     // copied straight into pinned result columns
     CompactParams cp{};
-    cp.num_groups = G;
-    cp.chunk = std::max<int64_t>(1024, (G + kCompactBlocks - 1) / kCompactBlocks);
+    cp.num_groups = RG;
+    cp.chunk = std::max<int64_t>(1024, (RG + kCompactBlocks - 1) / kCompactBlocks);
     cp.count = kp.out_count;
     cp.num_aggs = nagg;
     cp.num_keys = q->num_group_by;
@@ -1351,7 +1410,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       const int j = agg_val[k];
       cp.agg_kind[k] = val_is_int[j] ? CK_INT : (t == PH_AGG_SUM ? CK_REAL_SUM : CK_REAL_ORDER);
       cp.agg_src[k] = reinterpret_cast<const int64_t*>(src_of(k));
-      cp.agg_out[k] = scratch.alloc<double>(G);
+      cp.agg_out[k] = scratch.alloc<double>(RG);
     }
     std::vector<int32_t> key_es(q->num_group_by);
     for (int g = 0; g < q->num_group_by; ++g) {
@@ -1361,9 +1420,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       cp.key_type[g] = gd.dict.type;
       cp.key_table[g] = global_dict_device_values(ctx, gd);
       key_es[g] = (gd.dict.type == PH_LONG || gd.dict.type == PH_DOUBLE) ? 8 : 4;
-      cp.key_out[g] = scratch.alloc<uint8_t>((size_t)G * key_es[g]);
+      cp.key_out[g] = scratch.alloc<uint8_t>((size_t)RG * key_es[g]);
     }
-    cp.count_out = scratch.alloc<int64_t>(G);
+    cp.count_out = scratch.alloc<int64_t>(RG);
+    cp.key_base = RB;
     cp.blk = scratch.alloc<unsigned long long>(kCompactBlocks + 1);
     launch_compact(cp, st);
     unsigned long long total = 0;
@@ -1425,10 +1485,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
   } else {
     // group-by with DISTINCTCOUNTHLL registers: host-side materialisation
-    std::vector<unsigned long long> cnt(G);
-    PH_HIP_CHECK(hipMemcpy(cnt.data(), kp.out_count, 8 * G, hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> cnt(RG);
+    PH_HIP_CHECK(hipMemcpy(cnt.data(), kp.out_count, 8 * RG, hipMemcpyDeviceToHost));
     std::vector<int64_t> live;
-    for (int64_t g = 0; g < G; ++g)
+    for (int64_t g = 0; g < RG; ++g)
       if (cnt[g]) {
         live.push_back(g);
         stats.num_docs_scanned += (int64_t)cnt[g];
@@ -1448,8 +1508,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         }
       } else if (t == PH_AGG_DISTINCTCOUNTHLL) {
         if (regs.empty()) {
-          regs.resize(hll_words);
-          PH_HIP_CHECK(hipMemcpy(regs.data(), kp.out_hll, 4 * hll_words, hipMemcpyDeviceToHost));
+          regs.resize(rhll_words);
+          PH_HIP_CHECK(hipMemcpy(regs.data(), kp.out_hll, 4 * rhll_words, hipMemcpyDeviceToHost));
         }
         for (int64_t r = 0; r < R; ++r)
           for (int j = 0; j < m; ++j)
@@ -1458,8 +1518,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         void* src = src_of(k);
         auto& buf = fetched[src];
         if (buf.empty()) {
-          buf.resize(G);
-          PH_HIP_CHECK(hipMemcpy(buf.data(), src, 8 * G, hipMemcpyDeviceToHost));
+          buf.resize(RG);
+          PH_HIP_CHECK(hipMemcpy(buf.data(), src, 8 * RG, hipMemcpyDeviceToHost));
         }
         for (int64_t r = 0; r < R; ++r) {
           double v = finish_value(k, buf[live[r]], 1, t == PH_AGG_SUM);
@@ -1477,7 +1537,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       res->key_entry_size[g] = es;
       res->keys[g].assign((size_t)es * R, 0);
       for (int64_t r = 0; r < R; ++r) {
-        const int64_t id = (live[r] / kp.group_stride[g]) % std::max<int64_t>(1, d.size);
+        const int64_t id = ((RB + live[r]) / kp.group_stride[g]) % std::max<int64_t>(1, d.size);
         put_key_value(d, id, res->keys[g].data() + (size_t)es * r, es);
       }
     }

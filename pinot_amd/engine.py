@@ -235,6 +235,41 @@ class GpuContext:
                                bool(st.sum_precision_flag), st.device_ms, st.host_ms, st.plan_mode)
         return IntermediateResult(key_cols, agg_cols, n, [a.function for a in q.aggregations], stats)
 
+    # ---------------------------------------------------------------- dense partials (multi-GPU combine)
+    def dense_layout(self, q: QueryContext, segments: Sequence[PinnedSegment]) -> N.DenseLayout:
+        """ph_query_dense_layout: the dense partial tables of ``q`` (count, element type, reduce op)."""
+        qs = _QueryStruct(q)
+        segs = (ctypes.c_void_p * max(1, len(segments)))(*[s.handle for s in segments])
+        lay = N.DenseLayout()
+        N.check(N.lib().ph_query_dense_layout(self.handle, ctypes.byref(qs.struct), segs, len(segments),
+                                              ctypes.byref(lay)))
+        return lay
+
+    def execute_dense(self, q: QueryContext, segments: Sequence[PinnedSegment], table_ptrs: Sequence[int]):
+        """ph_query_execute_dense into caller-owned device tables (device pointers, layout order)."""
+        qs = _QueryStruct(q)
+        segs = (ctypes.c_void_p * max(1, len(segments)))(*[s.handle for s in segments])
+        tabs = (ctypes.c_void_p * max(1, len(table_ptrs)))(*table_ptrs)
+        st = N.ExecStats()
+        N.check(N.lib().ph_query_execute_dense(self.handle, ctypes.byref(qs.struct), segs, len(segments), tabs,
+                                               ctypes.byref(st)))
+        return st
+
+    def dense_finalize(self, q: QueryContext, segments: Sequence[PinnedSegment], table_ptrs: Sequence[int],
+                       group_begin: int, group_end: int, copy: bool = True) -> IntermediateResult:
+        """ph_dense_finalize of key shard [group_begin, group_end) (pointers to the shard's first group)."""
+        qs = _QueryStruct(q)
+        segs = (ctypes.c_void_p * max(1, len(segments)))(*[s.handle for s in segments])
+        tabs = (ctypes.c_void_p * max(1, len(table_ptrs)))(*table_ptrs)
+        r = ctypes.c_void_p()
+        N.check(N.lib().ph_dense_finalize(self.handle, ctypes.byref(qs.struct), segs, len(segments), tabs,
+                                          group_begin, group_end, ctypes.byref(r)))
+        handle = _ResultHandle(r)
+        res = self._read_result(q, r, copy)
+        if not copy:
+            res._handle = handle
+        return res
+
     def query(self, sql_or_q, segments: Sequence[PinnedSegment]) -> ResultTable:
         q = parse_sql(sql_or_q) if isinstance(sql_or_q, str) else sql_or_q
         r = self.execute(q, segments)

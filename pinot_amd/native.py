@@ -78,6 +78,17 @@ class Query(ctypes.Structure):
                 ("aggregations", ctypes.POINTER(Aggregation)), ("num_groups_limit", ctypes.c_int64)]
 
 
+PH_MAX_DENSE_TABLES = 16
+PH_REDUCE_SUM_I64, PH_REDUCE_SUM_F64, PH_REDUCE_MIN_I64, PH_REDUCE_MAX_I64, PH_REDUCE_MAX_U32 = range(5)
+
+
+class DenseLayout(ctypes.Structure):
+    _fields_ = [("num_groups", ctypes.c_int64), ("num_tables", ctypes.c_int32),
+                ("elems_per_group", ctypes.c_int32 * PH_MAX_DENSE_TABLES),
+                ("reduce_op", ctypes.c_int32 * PH_MAX_DENSE_TABLES),
+                ("elem_bytes", ctypes.c_int32 * PH_MAX_DENSE_TABLES)]
+
+
 class ExecStats(ctypes.Structure):
     _fields_ = [("num_docs_scanned", ctypes.c_int64), ("num_entries_scanned_in_filter", ctypes.c_int64),
                 ("num_entries_scanned_post_filter", ctypes.c_int64), ("num_total_docs", ctypes.c_int64),
@@ -92,10 +103,29 @@ EXPORTED_SYMBOLS = (
     "ph_ctx_create", "ph_ctx_destroy", "ph_ctx_set_stream", "ph_segment_pin", "ph_segment_unpin",
     "ph_segment_device_bytes", "ph_segment_num_docs", "ph_table_set_dictionary", "ph_query_execute",
     "ph_result_destroy", "ph_result_stats", "ph_result_num_groups", "ph_result_key_entry_size", "ph_result_key_type",
-    "ph_result_group_keys", "ph_result_aggregation", "ph_result_key_data", "ph_result_aggregation_data", "ph_fixed_bit_pack", "ph_selftest_unpack", "ph_last_error", "ph_version",
+    "ph_result_group_keys", "ph_result_aggregation", "ph_result_key_data", "ph_result_aggregation_data",
+    "ph_query_dense_layout", "ph_query_execute_dense", "ph_dense_finalize", "ph_fixed_bit_pack", "ph_selftest_unpack",
+    "ph_last_error", "ph_version",
 )
 
 _lib = None
+
+
+def _share_torch_hip_runtime():
+    """One HIP runtime per process.  The PyTorch-ROCm wheel bundles its own libamdhip64 (same SONAME
+    libamdhip64.so.7 as /opt/rocm's).  Loaded first, /opt/rocm's copy would make torch load a second runtime
+    (with its own HSA runtime) that then finds no GPU; so when torch is installed its copy is loaded first, by
+    path and RTLD_GLOBAL, and libpinot_hip.so's NEEDED entry binds to it by SONAME.  Device pointers, streams
+    and events are then shared with torch (the multi-GPU combine passes torch tensors to the C-ABI)."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        p = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(p):
+            ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+            return
 
 
 def lib():
@@ -105,6 +135,7 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise FileNotFoundError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    _share_torch_hip_runtime()
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     sig = {
@@ -126,6 +157,12 @@ def lib():
         "ph_result_aggregation": ([vp, i32, vp], ctypes.c_int),
         "ph_result_key_data": ([vp, i32], vp),
         "ph_result_aggregation_data": ([vp, i32], vp),
+        "ph_query_dense_layout": ([vp, ctypes.POINTER(Query), ctypes.POINTER(vp), i32, ctypes.POINTER(DenseLayout)],
+                                  ctypes.c_int),
+        "ph_query_execute_dense": ([vp, ctypes.POINTER(Query), ctypes.POINTER(vp), i32, ctypes.POINTER(vp),
+                                    ctypes.POINTER(ExecStats)], ctypes.c_int),
+        "ph_dense_finalize": ([vp, ctypes.POINTER(Query), ctypes.POINTER(vp), i32, ctypes.POINTER(vp), i64, i64,
+                               ctypes.POINTER(vp)], ctypes.c_int),
         "ph_fixed_bit_pack": ([vp, i64, i32, vp, ctypes.c_uint64], ctypes.c_int),
         "ph_selftest_unpack": ([vp, vp, ctypes.c_uint64, i64, i32, vp], ctypes.c_int),
         "ph_last_error": ([], ctypes.c_char_p),

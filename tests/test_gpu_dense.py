@@ -1,0 +1,97 @@
+"""GPU: the dense-partials C-ABI (ph_query_dense_layout / ph_query_execute_dense / ph_dense_finalize) that the
+multi-GPU combine is built on.  Finalising the dense tables whole, or as key shards concatenated, must give
+exactly ph_query_execute's result -- for every plan mode (aggregation-only, LDS table, HBM table,
+partitioned) -- and DistributedQuery at world size 1 must match too.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from pinot_amd.query import parse_sql
+from pinot_amd.segment import create_segment
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from pinot_amd.engine import GpuContext
+    c = GpuContext(0)
+    yield c
+    c.close()
+
+
+def _segs(ctx, seed, n=200_000, nseg=3, ca=50, cb=2000):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(nseg):
+        cols = {
+            "a": (rng.integers(0, ca, n).astype(np.int32), "INT"),
+            "b": (rng.integers(0, cb, n).astype(np.int32), "INT"),
+            "f": (rng.integers(0, 100, n).astype(np.int32), "INT"),
+            "m": (rng.integers(0, 1 << 20, n).astype(np.int32), "INT"),
+            "d": (np.round(rng.normal(0, 10, n), 3), "DOUBLE"),
+        }
+        out.append(ctx.pin(create_segment(f"dense_{seed}_{i}", cols)))
+    ctx.set_table_dictionary("a", "INT", np.arange(ca, dtype=np.int32))
+    ctx.set_table_dictionary("b", "INT", np.arange(cb, dtype=np.int32))
+    return out
+
+
+def _rows(r):
+    return sorted(zip(r.keys, [tuple(a) for a in r.aggs]))
+
+
+QUERIES = [
+    ("SELECT COUNT(*), SUM(m), MIN(m), MAX(m), SUM(d) FROM t WHERE f BETWEEN 10 AND 70", 1),
+    ("SELECT a, COUNT(*), SUM(m), MIN(d), MAX(m) FROM t WHERE f < 50 GROUP BY a", 2),
+    ("SET numGroupsLimit=200000; SELECT a, b, COUNT(*), SUM(m), MAX(d) FROM t GROUP BY a, b", 3),
+    ("SET numGroupsLimit=200000; SELECT a, b, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t WHERE f < 60 "
+     "GROUP BY a, b", 4),
+]
+
+
+@pytest.mark.parametrize("sql,mode", QUERIES, ids=["agg", "lds", "global", "partition"])
+def test_dense_matches_execute(ctx, sql, mode):
+    import torch
+
+    from pinot_amd.distributed import Layout, alloc_tables, shard_bounds
+    segs = _segs(ctx, 5)
+    q = parse_sql(sql)
+    ref = ctx.execute(q, segs)
+    assert ref.stats.mode == mode
+    lay = Layout.from_native(ctx.dense_layout(q, segs))
+    assert lay.num_groups == (1 if mode == 1 else (50 if mode == 2 else 100_000))
+    for world in (1, 3):
+        tabs = alloc_tables(lay, world, torch.device("cuda", 0))
+        ctx.execute_dense(q, segs, [t.data_ptr() for t in tabs])
+        torch.cuda.synchronize()
+        rows = []
+        for r in range(world):
+            s, g0, g1 = shard_bounds(lay.num_groups, world, r)
+            if g1 <= g0:
+                continue
+            shard = [t[g0 * per:g1 * per] for t, per in zip(tabs, lay.elems_per_group)]
+            res = ctx.dense_finalize(q, segs, [t.data_ptr() for t in shard], g0, g1)
+            rows += _rows(res)
+        assert sorted(rows) == _rows(ref), world
+
+
+def test_distributed_query_world1(ctx):
+    import torch.distributed as dist
+
+    from pinot_amd.distributed import DistributedQuery
+    segs = _segs(ctx, 9)
+    q = parse_sql("SET numGroupsLimit=200000; SELECT a, b, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t "
+                  "WHERE f < 60 GROUP BY a, b")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29517")
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        res, (g0, g1) = DistributedQuery(ctx).execute(q, segs)
+        assert (g0, g1) == (0, 100_000)
+        assert _rows(res) == _rows(ctx.execute(q, segs))
+    finally:
+        dist.destroy_process_group()
+        ctx.set_stream(0)
