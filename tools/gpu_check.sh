@@ -8,7 +8,7 @@ echo "pytest rc=$rc"
 grep -E "FAILED|ERROR|passed|failed" gpurun_out/pytest_gpu.log | tail -30
 if [ $rc -gt 1 ]; then exit $rc; fi
 for w in ${WORKLOADS:-config2 config3-agg config3-lds config3}; do
-  timeout -k 10 400 python -u bench.py --workload $w --steps ${STEPS:-5} --warmup 2 --cpu-segments ${CPU_SEGS:-2} \
+  timeout -k 10 400 python -u bench.py --workload $w --steps ${STEPS:-5} --warmup 2 --cpu-seconds ${CPU_SECS:-5} \
     > gpurun_out/bench_$w.json 2> gpurun_out/bench_$w.err
   rc=$?
   echo "bench $w rc=$rc"
