@@ -346,7 +346,7 @@ enum : int32_t { OPS_SUM = 1, OPS_MIN = 2, OPS_MAX = 4 };
 
 template <int MODE>
 struct NumLoads {
-  static constexpr int value = MODE == MODE_COUNT ? kPrefetchCount : kPrefetchOther;
+  static constexpr int value = MODE == MODE_COUNT ? kPrefetchCount : (MODE == MODE_PARTITION ? kPrefetchPartition : kPrefetchOther);
 };
 
 // Per-wave accumulation state of the scan (registers).
@@ -485,6 +485,7 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
   // 4 words per step: their filter decodes are independent, so their LDS reads (and bitmap gathers) overlap
   constexpr int UB = 4;
   if constexpr (MODE == MODE_PARTITION) {
+    constexpr int UB = kPartUnroll;
     // lean path: <= 1 value column (the host only plans MODE_PARTITION for that shape).  Records are
     // (key low bits << vbits | value - vbase); the partition (key high bits) picks the LDS slot run.
     using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
@@ -508,7 +509,10 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
       Rec rec[UB];
 #pragma unroll
       for (int q = 0; q < UB; ++q) {
-        if (!hit[q]) continue;
+        // without gathers, keys and values are decoded for every lane (branch-free; a miss reads in-tile LDS
+        // bytes and discards them): only the rank atomic and the slot store are predicated.  Gathers (LATE:
+        // remaps, dictionaries) stay predicated so a miss never indexes a table with a stale id.
+        if (LATE && !hit[q]) continue;
         uint32_t key = 0;
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
@@ -516,8 +520,9 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
           if (LATE && gremap[g]) id = (uint32_t)gld(gremap[g] + id);
           key += id * (uint32_t)p.group_stride[g];
         }
+        if (p.dbg_flags & 16) key = ((uint32_t)lane * 16411u + (uint32_t)(u + q) * 977u) % (uint32_t)p.num_groups;  // timing only: no key decode
         uint32_t vo = 0;
-        if (p.num_vals) {
+        if (p.num_vals && !(p.dbg_flags & 16)) {
           int64_t iv;
           double dv;
           if (LATE) read_value(vkind[0], vbase[0], vtab[0], cursor_value(vcur[0], u + q), iv, dv);
@@ -526,7 +531,7 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
         }
         bk[q] = key >> p.part_klo;
         rec[q] = REC64 ? (Rec)(((unsigned long long)(key & kmask) << 32) | vo) : (Rec)(((key & kmask) << p.part_vbits) | vo);
-        rk[q] = atomicAdd(&lcnt[bk[q]], 1u);
+        if (hit[q]) rk[q] = (p.dbg_flags & 8) ? 0u : atomicAdd(&lcnt[bk[q]], 1u);  // flag 8 (timing only): no rank atomic
       }
 #pragma unroll
       for (int q = 0; q < UB; ++q) {

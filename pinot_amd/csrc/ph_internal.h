@@ -108,6 +108,7 @@ constexpr int kChunkWords = 256;                     // 16384 docs per chunk (a 
 // 16-byte-per-lane loads (1 KiB per wave-instruction) a wave keeps in flight per tile, over all streams
 constexpr int kPrefetchCount = 8;                    // MODE_COUNT: one stream
 constexpr int kPrefetchOther = 12;
+constexpr int kPrefetchPartition = 12;               // MODE_PARTITION prefetch pool (tile_words 16 needs 9 loads at 10+10+10+16 bits)
 constexpr int stage_loads(int tile_words, int bits) { return (tile_words * 8 * bits + 8 + 1023) / 1024; }
 // staged span of one stream: 16-byte front pad (the decode reads dword j-1 and j) + the tile's bytes
 constexpr int stage_stream_bytes(int tile_words, int bits) { return 16 + (tile_words * 8 * bits + 8 + 15) / 16 * 16; }
@@ -155,7 +156,9 @@ enum : int32_t { AGG_COUNT = 0, AGG_SUM = 1, AGG_MIN = 2, AGG_MAX = 3, AGG_HLL =
 
 enum : int32_t { MODE_COUNT = 0, MODE_AGG = 1, MODE_GROUP_LDS = 2, MODE_GROUP_GLOBAL = 3, MODE_PARTITION = 4 };
 
-constexpr int kPartSlots = 8192;    // LDS record slots per workgroup (partition p owns slots [p*C, (p+1)*C))
+constexpr int kPartUnroll = 4;     // 64-doc words per step of the partition append loop (independent LDS chains)
+constexpr int kPartSlots = 2048;    // LDS record slots per workgroup (partition p owns slots [p*C, (p+1)*C)); swept r1: small
+                                     // slot sets + more resident workgroups beat 8192 slots at 3 WG/CU
 constexpr int kPartMaxParts = 1024;
 constexpr int kPartKeysLog2 = 12;   // keys per partition = 4096: kernel B's LDS table <= 80 KiB
 

@@ -897,6 +897,21 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
     }
 
+  // |integer SUM| < 2^53 whenever max |value| x total docs is: then no group's double can be inexact and the
+  // per-group precision check is skipped (only for a local execute; a finalised shard also holds other ranks)
+  bool sum_bounded[kMaxVals] = {};
+  for (int j = 0; j < nvals; ++j) {
+    if (!val_is_int[j]) continue;
+    double amax = 0.0;
+    for (auto* s : segs) {
+      Column& c = *s->columns.at(val_cols[j]);
+      if (c.cardinality <= 0) continue;
+      amax = std::max(amax, std::fabs((double)c.dict.ints.front()));
+      amax = std::max(amax, std::fabs((double)c.dict.ints.back()));
+    }
+    sum_bounded[j] = amax * (double)stats.num_total_docs < 4503599627370496.0;  // 2^52: margin for rounding
+  }
+
   int mode = -3;  // DENSE_FINALIZE: no scan
   float dev_ms = 0.f;
   const int64_t hll_words = G * num_hll * (m ? m : 1);
@@ -1076,8 +1091,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     int maxbits[kMaxStage] = {};
     for (int s = 0; s < kp.nstage; ++s)
       for (auto& d : dsegs) maxbits[s] = std::max(maxbits[s], (int)d.streams[s].bits);
-    const int pool = mode == MODE_COUNT ? kPrefetchCount : kPrefetchOther;
-    int tw = mode == MODE_PARTITION ? 8 : kMaxTileWords;
+    const int pool = mode == MODE_COUNT ? kPrefetchCount : (mode == MODE_PARTITION ? kPrefetchPartition : kPrefetchOther);
+    int tw = mode == MODE_PARTITION ? 16 : kMaxTileWords;
     if (const char* e = getenv("PH_TILE_WORDS")) tw = std::max(4, std::min(kMaxTileWords, atoi(e)));  // tuning knob
     auto loads = [&](int t) {
       int n = 0;
@@ -1217,7 +1232,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       kp.part_vbits = vbits;
       kp.num_parts = (int32_t)P;
       const size_t lds_a = partition_lds_bytes(kp);
-      const int a_per_cu = (int)std::max<size_t>(1, std::min<size_t>(4, (160 * 1024) / lds_a));
+      int a_cap = 6;  // swept r1 (tile 16, 2048 slots): 6 resident workgroups per CU
+      if (const char* e = getenv("PH_PART_WG_PER_CU")) a_cap = std::max(1, std::min(8, atoi(e)));  // tuning knob
+      const int a_per_cu = (int)std::max<size_t>(1, std::min<size_t>(a_cap, (160 * 1024) / lds_a));
       const int grid_a = ctx->num_cus * a_per_cu;
       int max_batch_chunks = 0;
       for (auto& bt : batches) max_batch_chunks = std::max(max_batch_chunks, bt.second - bt.first);
@@ -1442,8 +1459,12 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       if (cp.agg_kind[k] == CK_COUNT) take(res->aggs[k], cp.count_out, 8 * (size_t)R);
       else take(res->aggs[k], cp.agg_out[k], 8 * (size_t)R);
     }
+    // num_docs_scanned = sum of the per-group counts: read from the COUNT column when the query has one
+    int count_k = -1;
+    for (int k = 0; k < nagg; ++k)
+      if (cp.agg_kind[k] == CK_COUNT) count_k = k;
     ResultBuf counts;
-    take(counts, cp.count_out, 8 * (size_t)R);
+    if (count_k < 0) take(counts, cp.count_out, 8 * (size_t)R);
     res->key_types.resize(q->num_group_by);
     res->key_entry_size.resize(q->num_group_by);
     res->keys.resize(q->num_group_by);
@@ -1459,13 +1480,14 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
     }
     PH_HIP_CHECK(hipStreamSynchronize(st));
-    const int64_t* cv = reinterpret_cast<const int64_t*>(counts.data());
+    const int64_t* cv = reinterpret_cast<const int64_t*>(count_k >= 0 ? res->aggs[count_k].data() : counts.data());
     int64_t docs = 0;
     for (int64_t r = 0; r < R; ++r) docs += cv[r];
     stats.num_docs_scanned = docs;
-    ctx->pinned_release(counts.pinned, counts.cap);
+    if (count_k < 0) ctx->pinned_release(counts.pinned, counts.cap);
     for (int k = 0; k < nagg; ++k) {
       if (q->aggregations[k].type != PH_AGG_SUM || !val_is_int[agg_val[k]]) continue;
+      if (!fin && sum_bounded[agg_val[k]]) continue;
       const double* sv = reinterpret_cast<const double*>(res->aggs[k].data());
       for (int64_t r = 0; r < R; ++r)
         if (sv[r] >= 9007199254740992.0 || sv[r] <= -9007199254740992.0) {
