@@ -1033,12 +1033,28 @@ void launch_encode_values(const uint32_t* fwd, int32_t bits, const int64_t* tabl
 __global__ void __launch_bounds__(256) k_compact_count(const CompactParams p) {
   const int64_t g0 = blockIdx.x * p.chunk, g1 = min(p.num_groups, g0 + p.chunk);
   uint32_t c = 0;
-  for (int64_t g = g0 + threadIdx.x; g < g1; g += blockDim.x) c += p.count[g] != 0;
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  unsigned long long d = 0;
+  for (int64_t g = g0 + threadIdx.x; g < g1; g += blockDim.x) {
+    const unsigned long long n = p.count[g];
+    c += n != 0;
+    d += n;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    c += __shfl_xor(c, o, 64);
+    d += __shfl_xor(d, o, 64);
+  }
   __shared__ uint32_t ws[4];
-  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __shared__ unsigned long long wd[4];
+  if ((threadIdx.x & 63) == 0) {
+    ws[threadIdx.x >> 6] = c;
+    wd[threadIdx.x >> 6] = d;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) p.blk[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+  if (threadIdx.x == 0) {
+    p.blk[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+    const unsigned long long bd = wd[0] + wd[1] + wd[2] + wd[3];
+    if (bd) atomicAdd(&p.blk[kCompactBlocks + 1], bd);  // numDocsScanned without a host pass over the counts
+  }
 }
 
 __global__ void __launch_bounds__(1024) k_compact_scan(const CompactParams p, int nblk) {

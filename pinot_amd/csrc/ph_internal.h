@@ -422,7 +422,8 @@ struct CompactParams {
   void* key_out[kMaxGroupCols];
   int64_t* count_out;
   int64_t key_base;          // group id of element 0 (finalizing one key shard of a dense table)
-  unsigned long long* blk;   // [kCompactBlocks + 1] counts -> offsets, total at [kCompactBlocks]
+  unsigned long long* blk;   // [kCompactBlocks + 2] counts -> offsets, total at [kCompactBlocks], matched docs
+                             // (sum of the group counts = numDocsScanned) at [kCompactBlocks + 1], zeroed by the host
   int32_t* flags;            // bit 0: an integer SUM reached 2^53
 };
 void launch_compact(const CompactParams& p, hipStream_t s);

@@ -1441,12 +1441,16 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     cp.count_out = scratch.alloc<int64_t>(RG);
     cp.key_base = RB;
-    cp.blk = scratch.alloc<unsigned long long>(kCompactBlocks + 1);
+    cp.blk = scratch.alloc<unsigned long long>(kCompactBlocks + 2);
+    PH_HIP_CHECK(hipMemsetAsync(cp.blk + kCompactBlocks + 1, 0, 8, st));
     launch_compact(cp, st);
-    unsigned long long total = 0;
-    PH_HIP_CHECK(hipMemcpyAsync(&total, cp.blk + kCompactBlocks, 8, hipMemcpyDeviceToHost, st));
+    size_t tot_cap = 0;
+    unsigned long long* tot = static_cast<unsigned long long*>(ctx->pinned_acquire(16, &tot_cap));
+    PH_HIP_CHECK(hipMemcpyAsync(tot, cp.blk + kCompactBlocks, 16, hipMemcpyDeviceToHost, st));
     PH_HIP_CHECK(hipStreamSynchronize(st));
-    const int64_t R = (int64_t)total;
+    const int64_t R = (int64_t)tot[0];
+    const int64_t docs = (int64_t)tot[1];
+    ctx->pinned_release(tot, tot_cap);
     res->num_groups = R;
     res->ctx = ctx;
     res->aggs.resize(nagg);
@@ -1459,12 +1463,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       if (cp.agg_kind[k] == CK_COUNT) take(res->aggs[k], cp.count_out, 8 * (size_t)R);
       else take(res->aggs[k], cp.agg_out[k], 8 * (size_t)R);
     }
-    // num_docs_scanned = sum of the per-group counts: read from the COUNT column when the query has one
-    int count_k = -1;
-    for (int k = 0; k < nagg; ++k)
-      if (cp.agg_kind[k] == CK_COUNT) count_k = k;
-    ResultBuf counts;
-    if (count_k < 0) take(counts, cp.count_out, 8 * (size_t)R);
+
     res->key_types.resize(q->num_group_by);
     res->key_entry_size.resize(q->num_group_by);
     res->keys.resize(q->num_group_by);
@@ -1480,11 +1479,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
     }
     PH_HIP_CHECK(hipStreamSynchronize(st));
-    const int64_t* cv = reinterpret_cast<const int64_t*>(count_k >= 0 ? res->aggs[count_k].data() : counts.data());
-    int64_t docs = 0;
-    for (int64_t r = 0; r < R; ++r) docs += cv[r];
-    stats.num_docs_scanned = docs;
-    if (count_k < 0) ctx->pinned_release(counts.pinned, counts.cap);
+    stats.num_docs_scanned = docs;  // sum of the group counts, reduced on the device by k_compact_count
     for (int k = 0; k < nagg; ++k) {
       if (q->aggregations[k].type != PH_AGG_SUM || !val_is_int[agg_val[k]]) continue;
       if (!fin && sum_bounded[agg_val[k]]) continue;
