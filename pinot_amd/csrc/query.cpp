@@ -1205,6 +1205,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       const bool has_sum = nvals && (val_ops[0] & 1), has_min = nvals && (val_ops[0] & 2),
                  has_max = nvals && (val_ops[0] & 4);
       int klo = kPartKeysLog2;
+      if (const char* e = getenv("PH_PART_KLO")) klo = std::max(8, std::min(13, atoi(e)));  // tuning knob (13: kernel B table 128 KiB)
       while (klo > 8 && (G >> (klo - 1)) < 256) --klo;  // small key spaces: more partitions, more workgroups
       const int64_t P = (G + (int64_t(1) << klo) - 1) >> klo;
       if (P > kPartMaxParts) fail(PH_ERR_UNSUPPORTED, "partitioned group-by too large");
