@@ -1092,7 +1092,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     for (int s = 0; s < kp.nstage; ++s)
       for (auto& d : dsegs) maxbits[s] = std::max(maxbits[s], (int)d.streams[s].bits);
     const int pool = mode == MODE_COUNT ? kPrefetchCount : (mode == MODE_PARTITION ? kPrefetchPartition : kPrefetchOther);
-    int tw = mode == MODE_PARTITION ? 16 : kMaxTileWords;
+    int tw = (mode == MODE_PARTITION || mode == MODE_GROUP_LDS) ? 16 : kMaxTileWords;  // r1 sweeps
     if (const char* e = getenv("PH_TILE_WORDS")) tw = std::max(4, std::min(kMaxTileWords, atoi(e)));  // tuning knob
     auto loads = [&](int t) {
       int n = 0;
