@@ -349,6 +349,14 @@ struct NumLoads {
   static constexpr int value = MODE == MODE_COUNT ? kPrefetchCount : (MODE == MODE_PARTITION ? kPrefetchPartition : kPrefetchOther);
 };
 
+// Value columns the register state is sized for.  REC64 means 64-bit partition records in MODE_PARTITION; in
+// every other mode it selects the single-value-column variant, so a one-column query does not carry the
+// accumulators and cursors of kMaxVals columns (r1: 158 VGPRs / 3 waves per SIMD in MODE_AGG otherwise).
+template <int MODE, int REC64>
+struct ValCap {
+  static constexpr int value = (MODE != MODE_PARTITION && REC64) ? 1 : kMaxVals;
+};
+
 // Per-wave accumulation state of the scan (registers).
 struct ScanAcc {
   unsigned long long matched;  // wave-uniform
@@ -361,6 +369,7 @@ struct ScanAcc {
 template <int MODE, int NG, int REC64, int FK, int LATE>
 __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t* smem, const uint8_t* wst, int lane,
                                              int32_t w0, int32_t nvalid, ScanAcc& acc) {
+  constexpr int VC = ValCap<MODE, REC64>::value;
   const uint32_t ndocs = (uint32_t)S->num_docs;
   const int m = 1 << p.log2m;
   // filter leaf
@@ -382,7 +391,7 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
   const void* vtab[kMaxVals];
   BitCursor vcur[kMaxVals];
 #pragma unroll
-  for (int j = 0; j < kMaxVals; ++j) {
+  for (int j = 0; j < VC; ++j) {
     if (MODE == MODE_COUNT || j >= p.num_vals || (MODE == MODE_PARTITION && j > 0)) continue;
     vcur[j] = bit_cursor(wst + p.stage_soff[p.v_stream[j]], S->streams[p.v_stream[j]].bits, lane);
     vkind[j] = S->vals[j].kind;
@@ -415,17 +424,17 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
   // per-word aggregation of the matched docs
   auto aggregate_word = [&](int u, bool hit, unsigned long long bal) {
     const uint32_t doc = (uint32_t)(w0 + u) * 64u + (uint32_t)lane;
-    int64_t vi[kMaxVals];
-    double vd[kMaxVals];
+    int64_t vi[VC];
+    double vd[VC];
     int64_t key = 0;
 #pragma unroll
-    for (int j = 0; j < kMaxVals; ++j) {
+    for (int j = 0; j < VC; ++j) {
       vi[j] = 0;
       vd[j] = 0.0;
     }
     if (hit) {
 #pragma unroll
-      for (int j = 0; j < kMaxVals; ++j)
+      for (int j = 0; j < VC; ++j)
         if (j < p.num_vals) {
           if (LATE) read_value(vkind[j], vbase[j], vtab[j], cursor_value(vcur[j], u), vi[j], vd[j]);
           else vi[j] = vbase[j] + (int64_t)cursor_value(vcur[j], u);  // VK_PACKED: no gather
@@ -446,7 +455,7 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
       if (MODE == MODE_GROUP_LDS) atomicAdd(&lds_cnt[g], 1u);
       else if (MODE == MODE_GROUP_GLOBAL) atomicAdd(&p.out_count[g], 1ull);
 #pragma unroll
-      for (int j = 0; j < kMaxVals; ++j) {
+      for (int j = 0; j < VC; ++j) {
         if (j >= p.num_vals) continue;
         const int ops = p.val_ops[j];
         const int64_t iv = vi[j];
@@ -576,6 +585,7 @@ template <int MODE, int NG, int REC64, int LATE>
 __global__ void __launch_bounds__(kBlock) k_scan(const KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NL = NumLoads<MODE>::value;
+  constexpr int VC = ValCap<MODE, REC64>::value;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably wave-uniform
   const int m = 1 << p.log2m;
@@ -589,7 +599,7 @@ __global__ void __launch_bounds__(kBlock) k_scan(const KParams p) {
   if (MODE == MODE_GROUP_LDS) {
     for (int64_t g = threadIdx.x; g < p.num_groups; g += kBlock) lds_cnt[g] = 0;
 #pragma unroll
-    for (int j = 0; j < kMaxVals; ++j) {
+    for (int j = 0; j < VC; ++j) {
       if (j >= p.num_vals) continue;
       const int ops = p.val_ops[j];
       for (int64_t g = threadIdx.x; g < p.num_groups; g += kBlock) {
@@ -613,7 +623,7 @@ __global__ void __launch_bounds__(kBlock) k_scan(const KParams p) {
   ScanAcc acc;
   acc.matched = 0;
 #pragma unroll
-  for (int j = 0; j < kMaxVals; ++j) {
+  for (int j = 0; j < VC; ++j) {
     acc.isum[j] = 0;
     acc.dsum[j] = 0.0;
     acc.vmin[j] = INT64_MAX;
@@ -728,7 +738,7 @@ __global__ void __launch_bounds__(kBlock) k_scan(const KParams p) {
     __shared__ int64_t s_isum[kWaves][kMaxVals], s_min[kWaves][kMaxVals], s_max[kWaves][kMaxVals];
     __shared__ double s_dsum[kWaves][kMaxVals];
 #pragma unroll
-    for (int j = 0; j < kMaxVals; ++j) {
+    for (int j = 0; j < VC; ++j) {
       if (j >= p.num_vals) continue;
       const int64_t si = wave_sum_i64(acc.isum[j]);
       const double sd = wave_sum_f64(acc.dsum[j]);
@@ -770,7 +780,7 @@ __global__ void __launch_bounds__(kBlock) k_scan(const KParams p) {
       if (!cnt) continue;
       atomicAdd(&p.out_count[g], (unsigned long long)cnt);
 #pragma unroll
-      for (int j = 0; j < kMaxVals; ++j) {
+      for (int j = 0; j < VC; ++j) {
         if (j >= p.num_vals) continue;
         const int ops = p.val_ops[j];
         if (ops & OPS_SUM) {
@@ -836,8 +846,11 @@ static void launch_mode(const KParams& p, int ng, int rec64, int grid, size_t ld
 void launch_scan(const KParams& p, int mode, int ng, int rec64, int grid, size_t lds, hipStream_t s) {
   switch (mode) {
     case MODE_COUNT: launch_late<MODE_COUNT, 0, 0>(p, grid, lds, s); break;
-    case MODE_AGG: launch_late<MODE_AGG, 0, 0>(p, grid, lds, s); break;
-    case MODE_GROUP_LDS: launch_mode<MODE_GROUP_LDS>(p, ng, 0, grid, lds, s); break;
+    case MODE_AGG:
+      if (p.num_vals <= 1) launch_late<MODE_AGG, 0, 1>(p, grid, lds, s);  // ValCap 1
+      else launch_late<MODE_AGG, 0, 0>(p, grid, lds, s);
+      break;
+    case MODE_GROUP_LDS: launch_mode<MODE_GROUP_LDS>(p, ng, p.num_vals <= 1 ? 1 : 0, grid, lds, s); break;
     case MODE_GROUP_GLOBAL: launch_mode<MODE_GROUP_GLOBAL>(p, ng, 0, grid, lds, s); break;
     default: launch_mode<MODE_PARTITION>(p, ng, rec64, grid, lds, s); break;
   }
