@@ -354,7 +354,8 @@ struct NumLoads {
 // accumulators and cursors of kMaxVals columns (r1: 158 VGPRs / 3 waves per SIMD in MODE_AGG otherwise).
 template <int MODE, int REC64>
 struct ValCap {
-  static constexpr int value = (MODE != MODE_PARTITION && REC64) ? 1 : kMaxVals;
+  // MODE_PARTITION is only planned for <= 1 value column (query.cpp part_ok)
+  static constexpr int value = (MODE == MODE_PARTITION || REC64) ? 1 : kMaxVals;
 };
 
 // Per-wave accumulation state of the scan (registers).
