@@ -852,7 +852,7 @@ void launch_scan(const KParams& p, int mode, int ng, int rec64, int grid, size_t
       else launch_late<MODE_AGG, 0, 0>(p, grid, lds, s);
       break;
     case MODE_GROUP_LDS: launch_mode<MODE_GROUP_LDS>(p, ng, p.num_vals <= 1 ? 1 : 0, grid, lds, s); break;
-    case MODE_GROUP_GLOBAL: launch_mode<MODE_GROUP_GLOBAL>(p, ng, 0, grid, lds, s); break;
+    case MODE_GROUP_GLOBAL: launch_mode<MODE_GROUP_GLOBAL>(p, ng, p.num_vals <= 1 ? 1 : 0, grid, lds, s); break;
     default: launch_mode<MODE_PARTITION>(p, ng, rec64, grid, lds, s); break;
   }
   PH_HIP_CHECK(hipGetLastError());
