@@ -11,8 +11,10 @@ Algorithmic bytes = sum over the 4 referenced columns of ceil(N*b/8) = 5.75 GB p
 
 A step = one full query: plan + the batched scan kernels over every segment of this GPU + (N > 1) the RCCL
 reduce-scatter of the dense partial tables by key range + finalising this rank's key shard into host result
-columns (~1M groups at N = 1).  Segments are pinned in HBM before timing.  Multi-GPU: one process per GPU,
-each rank holds its own 1e9 rows (weak scaling).
+columns (~1M groups at N = 1).  Segments are pinned in HBM before timing.  Multi-GPU: one process per GPU and
+ONE 1e9-row table of 100 segments sharded across the ranks (segment i on rank i mod N: equal rows per
+segment, so this is the greedy-by-rows assignment), i.e. strong scaling -- the N = 1 line is the same query
+over the same data as every other N.
 
 `roofline.kernel_ms` is the device time of the scan kernels of one step, taken with HIP events recorded on the
 stream the kernels run on (ph_exec_stats.device_ms); `traffic` is read from the PMC summary under profiles/
@@ -88,17 +90,37 @@ def oracle_segments(bufs):
                                            for c, cb in b.columns.items()}) for b in bufs]
 
 
+def host_threads():
+    """Host cores this process may use: the affinity mask, capped by OMP_NUM_THREADS (the GPU box sets it to
+    the job's CPU share; nproc there reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS")
+    if cap and cap.isdigit() and int(cap) > 0:
+        n = min(n, int(cap))
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(bufs, q, threads, target_s=10.0):
     """The oracle (C restatement of the reference loop nest, one worker per segment on `threads` host threads,
-    as GroupByCombineOperator) over a bounded sample of the same segments: calibrated on one segment, then
-    as many segments as make ~target_s seconds of CPU work."""
+    as GroupByCombineOperator) over a bounded sample of the same segments: calibrated on one segment on one
+    thread (the T = 1 leg), then as many segments as make ~target_s seconds of CPU work on `threads`."""
     from oracle import oracle as O
     dt1, _, _ = O.execute_timed(q, oracle_segments(bufs[:1]), 1)  # one segment on one thread
     waves = max(1, int(target_s / max(dt1, 1e-3)))                 # segments per thread in ~target_s
     n = int(max(1, min(len(bufs), waves * threads)))
     segs = oracle_segments(bufs[:n])
     dt, keys, aggs = O.execute_timed(q, segs, threads)
-    return n, dt, keys, aggs
+    return n, dt, dt1, keys, aggs
 
 
 def load_traffic(workload, kernel_count):
@@ -119,7 +141,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rows", type=int, default=1_000_000_000, help="rows per GPU")
+    ap.add_argument("--rows", type=int, default=1_000_000_000, help="table rows (sharded across the GPUs)")
     ap.add_argument("--segment-rows", type=int, default=10_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample size in seconds of work")
     ap.add_argument("--no-cpu", action="store_true")
@@ -146,15 +168,16 @@ def main():
     q = parse_sql(query)
     nseg = max(1, args.rows // args.segment_rows)
     seg_rows = args.rows // nseg
+    mine = [i for i in range(nseg) if i % world == rank]  # this rank's shard of the table
     t0 = time.time()
     ctx = GpuContext(device)
     bufs, pinned = [], []
-    for i in range(nseg):
-        b = make_segment_buffers(i, seg_rows, seed=1000 + rank, cols=cols)
+    for k, i in enumerate(mine):
+        b = make_segment_buffers(i, seg_rows, seed=1000, cols=cols)
         pinned.append(ctx.pin(b))
         bufs.append(b)
-        if i % 20 == 19:
-            log(f"[rank {rank}] pinned {i + 1}/{nseg} segments ({time.time() - t0:.1f}s)")
+        if k % 20 == 19:
+            log(f"[rank {rank}] pinned {k + 1}/{len(mine)} segments ({time.time() - t0:.1f}s)")
     # table-level dictionaries: identical on every rank, so dense group ids line up for the RCCL merge
     for g in q.group_by:
         ctx.set_table_dictionary(g, "INT", np.arange(cols[g][0], dtype=np.int32))
@@ -164,24 +187,26 @@ def main():
 
     def step():
         if world > 1:
-            res, shard = runner.execute(q, pinned, copy=False)
+            res, shard, scan = runner.execute(q, pinned, copy=False)
             last["res"], last["shard"] = res, shard
-            return res
+            return scan.device_ms, scan.plan_mode
         r = ctx.execute(q, pinned, copy=False)
         last["res"] = r
-        return r
+        return r.stats.device_ms, r.stats.mode
 
     for _ in range(args.warmup):
         step()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    dev_ms = []
+    dev_ms, phases = [], []
+    mode = -1
     ts = time.perf_counter()
     for _ in range(args.steps):
-        r = step()
-        if r is not None:
-            dev_ms.append(r.stats.device_ms)
+        ms, mode = step()
+        dev_ms.append(ms)
+        if world > 1:
+            phases.append(dict(runner.last_times))
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -191,16 +216,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1000.0 / args.steps
-    total_rows = nseg * seg_rows * world
+    total_rows = nseg * seg_rows
     value = total_rows / (ms_per_step / 1000.0)
-    if world > 1:  # device time of the scan is measured inside execute_dense; report rank 0's
-        kernel_ms = float(np.mean(dev_ms)) if dev_ms else float("nan")
-    else:
-        kernel_ms = float(np.mean(dev_ms))
-    alg = algorithmic_bytes(seg_rows, nseg, cols)
-    achieved = alg / (kernel_ms / 1000.0) / 1e9
-    mode = last["res"].stats.mode if last.get("res") is not None else -1
-    traffic = load_traffic(args.workload, 1)
+    # roofline of the dominant kernel: this rank's scan kernels (HIP events on their stream) over this rank's
+    # algorithmic bytes
+    kernel_ms = float(np.mean(dev_ms)) if dev_ms else 0.0
+    alg = algorithmic_bytes(seg_rows, len(mine), cols)
+    achieved = alg / (kernel_ms / 1000.0) / 1e9 if kernel_ms > 0 else None
+    traffic = load_traffic(args.workload, 1) if world == 1 else None
 
     result = {
         "metric": "filter+group-by rows/s and achieved HBM GB/s, 1B rows",
@@ -211,28 +234,34 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "int64",
-        "data": "synthetic (seeded PCG64 dictIds, 100 x 10M-doc segments per GPU)",
-        "config": {"workload": wdesc, "rows_per_gpu": nseg * seg_rows, "segments_per_gpu": nseg,
+        "data": f"synthetic (seeded PCG64 dictIds, one {total_rows}-row table of {nseg} x {seg_rows}-doc segments, "
+                f"sharded over {world} GPU(s))",
+        "config": {"workload": wdesc, "table_rows": total_rows, "segments": nseg, "segments_per_gpu": len(mine),
                    "parallelism": f"segments sharded x{world}" + (", RCCL reduce-scatter by key range" if world > 1
                                                                   else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                      "kernel": KERNEL_NAMES.get(mode, "k_scan"), "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": alg},
     }
+    if phases:
+        result["phases_ms"] = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
     if last.get("res") is not None:
         result["groups"] = last["res"].num_groups
     if rank == 0 and world == 1 and not args.no_cpu:
-        threads = min(16, os.cpu_count() or 1)
-        n, dt, keys, aggs = cpu_baseline(bufs, q, threads, args.cpu_seconds)
+        threads = host_threads()
+        n, dt, dt1, keys, aggs = cpu_baseline(bufs, q, threads, args.cpu_seconds)
         rows = n * seg_rows
         result["cpu_baseline"] = {"value": rows / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+                                  "value_t1": seg_rows / dt1, "host_cores": os.cpu_count(),
+                                  "cpu_model": cpu_model(),
                                   "sample": f"{n} of {nseg} segments x {seg_rows} rows (same data and query), oracle "
-                                            f"C restatement of the reference loop nest on {threads} host threads, "
-                                            f"{dt:.2f}s"}
+                                            f"C restatement of the reference loop nest (one worker per segment, as "
+                                            f"GroupByCombineOperator) on {threads} host threads, {dt:.2f}s; "
+                                            f"value_t1 = one segment on one thread, {dt1:.2f}s"}
         if not args.no_parity:
             # parity on the sample: GPU over the same segments vs the oracle -- group keys, COUNT, integer SUM,
             # MIN, MAX bit-exact (synthetic group dictionaries are 0..C-1, so value == global id)

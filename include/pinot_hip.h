@@ -46,6 +46,9 @@ extern "C" {
 #define PH_ERR_UNSUPPORTED 3      /* shape not on the GPU path: caller falls back to the CPU plan */
 #define PH_ERR_DEVICE 4           /* HIP runtime / kernel error */
 #define PH_ERR_OUT_OF_MEMORY 5    /* HBM budget exhausted */
+#define PH_ERR_CANCELLED 6        /* ph_query.interrupt set or ph_query.end_time_ms passed: the caller raises the
+                                     reference's timeout / cancellation (QueryException EXECUTION_TIMEOUT,
+                                     QUERY_CANCELLATION; BaseOperator.java:39, GroupByCombineOperator.java:225-234) */
 
 /* ------------------------------------------------------------------ handles */
 typedef struct ph_ctx ph_ctx;         /* one per GPU; owns streams, scratch, pinned-segment registry */
@@ -112,10 +115,18 @@ typedef struct {
 typedef enum { PH_AGG_COUNT = 0, PH_AGG_SUM = 1, PH_AGG_MIN = 2, PH_AGG_MAX = 3, PH_AGG_DISTINCTCOUNTHLL = 4 }
     ph_aggregation_type;
 
+/* 2-operand expression argument of SUM / MIN / MAX: `column <op> column2`, evaluated per row like the reference's
+ * TransformOperator (ProjectPlanNode.java:82, AggregationFunctionUtils.java:86): MultiplicationTransformFunction
+ * ("mult"), SubtractionTransformFunction ("sub"), AdditionTransformFunction ("add"), DOUBLE results.  Integer
+ * operands whose results fit int64 are computed exactly in int64 (== the double result while |value| < 2^53). */
+typedef enum { PH_EXPR_NONE = 0, PH_EXPR_MULT = 1, PH_EXPR_SUB = 2, PH_EXPR_ADD = 3 } ph_expr_op;
+
 typedef struct {
   int32_t type;                 /* ph_aggregation_type */
-  const char* column;           /* NULL for COUNT(*) */
+  const char* column;           /* NULL for COUNT(*); first operand of an expression */
   int32_t log2m;                /* DISTINCTCOUNTHLL; 0 = default 8 (CommonConstants.java:96-97) */
+  const char* column2;          /* second operand (expr_op != PH_EXPR_NONE), else NULL */
+  int32_t expr_op;              /* ph_expr_op */
 } ph_aggregation;
 
 typedef struct {
@@ -129,6 +140,12 @@ typedef struct {
   int32_t num_aggregations;
   const ph_aggregation* aggregations;
   int64_t num_groups_limit;     /* per-segment numGroupsLimit (InstancePlanMakerImplV2.java:72-73) */
+  /* Interruption (BaseOperator.nextBlock checks Tracing.ThreadAccountantOps.isInterrupted, BaseOperator.java:39;
+   * the combine waits until QueryContext.getEndTimeMs, GroupByCombineOperator.java:225-234).  A call checks both
+   * before its launches and between scan batches (with either set, a scan is cut into batches of ~128M docs and
+   * the stream is drained between them), and returns PH_ERR_CANCELLED. */
+  int64_t end_time_ms;                /* wall-clock deadline, ms since the Unix epoch; 0 = none */
+  const volatile int32_t* interrupt;  /* the caller sets *interrupt != 0 to cancel; NULL = none */
 } ph_query;
 
 typedef struct {
@@ -228,10 +245,15 @@ int ph_dense_finalize(ph_ctx* ctx, const ph_query* query, ph_segment* const* seg
  * (n*bits+7)/8 */
 int ph_fixed_bit_pack(const int32_t* dict_ids, int64_t n, int32_t bits, uint8_t* out, uint64_t out_size);
 
-/* Self-test hook: unpack n values of a packed fixed-bit stream on the device with the same routine the
- * scan kernels use, writing dictIds to host memory `out` (FixedBitIntReaderTest-style parity checks). */
+/* Self-test hooks (FixedBitIntReaderTest-style parity checks, FixedBitIntReaderTest.java:43-81): unpack n values
+ * of a packed fixed-bit stream on the device, writing dictIds to host memory `out`.
+ *   ph_selftest_unpack         the per-doc gather routine (generic filter programs, value re-encoding, HLL)
+ *   ph_selftest_unpack_staged  the scan kernels' staged tile decode (coalesced 16-byte loads -> LDS ->
+ *                              one funnel shift per value) with `tile_words` 64-doc words per wave tile */
 int ph_selftest_unpack(ph_ctx* ctx, const uint8_t* packed, uint64_t packed_size, int64_t n, int32_t bits,
                        int32_t* out);
+int ph_selftest_unpack_staged(ph_ctx* ctx, const uint8_t* packed, uint64_t packed_size, int64_t n, int32_t bits,
+                              int32_t tile_words, int32_t* out);
 
 /* thread-local message of the last error on this thread */
 const char* ph_last_error(void);

@@ -87,7 +87,28 @@ class _Query(ctypes.Structure):
                 ("num_group_by", ctypes.c_int32), ("group_cols", ctypes.c_void_p),
                 ("group_global_card", ctypes.c_void_p), ("num_aggs", ctypes.c_int32),
                 ("agg_fn", ctypes.c_void_p), ("agg_col", ctypes.c_void_p), ("log2m", ctypes.c_int32),
-                ("num_groups_limit", ctypes.c_int64)]
+                ("num_groups_limit", ctypes.c_int64), ("agg_col2", ctypes.c_void_p), ("agg_op", ctypes.c_void_p)]
+
+
+OP_CODES = {None: 0, "*": 1, "-": 2, "+": 3}
+
+
+def _agg_arrays(q, col_index):
+    fn = np.array([AGG_CODES[a.function] for a in q.aggregations], dtype=np.int32)
+    col = np.array([col_index[a.column] if a.column else -1 for a in q.aggregations], dtype=np.int32)
+    col2 = np.array([col_index[a.column2] if getattr(a, "column2", None) else -1 for a in q.aggregations],
+                    dtype=np.int32)
+    op = np.array([OP_CODES[getattr(a, "op", None)] for a in q.aggregations], dtype=np.int32)
+    return fn, col, col2, op
+
+
+def _used_columns(q):
+    cols = list(q.group_by)
+    for a in q.aggregations:
+        cols += [c for c in (a.column, getattr(a, "column2", None)) if c]
+    if q.filter is not None:
+        cols += q.filter.columns()
+    return list(dict.fromkeys(cols))
 
 
 class _Result(ctypes.Structure):
@@ -389,9 +410,7 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> Oracl
     """Run a QueryContext over oracle segments; returns groups (value tuples) and intermediate
     aggregation results, plus execution statistics."""
     keep = []  # keep numpy buffers alive
-    used = list(dict.fromkeys(
-        list(q.group_by) + [a.column for a in q.aggregations if a.column] +
-        (q.filter.columns() if q.filter is not None else [])))
+    used = _used_columns(q)
     col_index = {c: i for i, c in enumerate(used)}
 
     # table-level value unions for group-by columns
@@ -446,8 +465,7 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> Oracl
     stats = [0, 0, 0, 0, False]
     group_cols = np.array([col_index[g] for g in q.group_by], dtype=np.int32)
     gcard = np.array([len(u) for u in unions], dtype=np.int64)
-    agg_fn = np.array([AGG_CODES[a.function] for a in q.aggregations], dtype=np.int32)
-    agg_col = np.array([col_index[a.column] if a.column else -1 for a in q.aggregations], dtype=np.int32)
+    agg_fn, agg_col, agg_col2, agg_op = _agg_arrays(q, col_index)
     nagg = len(q.aggregations)
     m = 1 << log2m
     hll_idx = [k for k, a in enumerate(q.aggregations) if a.function == "DISTINCTCOUNTHLL"]
@@ -462,7 +480,8 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> Oracl
             for i, (op, arg, ptr, scan) in enumerate(prog):
                 ops[i].op, ops[i].arg, ops[i].match, ops[i].is_scan = op, arg, ptr, scan
             qs = _Query(len(prog), ops, len(q.group_by), group_cols.ctypes.data, gcard.ctypes.data, nagg,
-                        agg_fn.ctypes.data, agg_col.ctypes.data, log2m, q.num_groups_limit)
+                        agg_fn.ctypes.data, agg_col.ctypes.data, log2m, q.num_groups_limit,
+                        agg_col2.ctypes.data, agg_op.ctypes.data)
             one = (_Segment * 1)(seg_structs[si])
             res = _Result()
             LIB.or_execute(ctypes.byref(qs), one, 1, 1, ctypes.byref(res))
@@ -498,9 +517,7 @@ def execute_timed(q, segments: Sequence[OracleSegment], num_threads: int):
     baseline).  All segments must share one filter plan shape (true for the bench workloads)."""
     import time
     keep = []
-    used = list(dict.fromkeys(
-        list(q.group_by) + [a.column for a in q.aggregations if a.column] +
-        (q.filter.columns() if q.filter is not None else [])))
+    used = _used_columns(q)
     col_index = {c: i for i, c in enumerate(used)}
     unions = [np.unique(np.concatenate([s.columns[g].dictionary for s in segments])) for g in q.group_by]
     seg_structs = (_Segment * len(segments))()
@@ -533,10 +550,10 @@ def execute_timed(q, segments: Sequence[OracleSegment], num_threads: int):
         ops[i].op, ops[i].arg, ops[i].match, ops[i].is_scan = op, arg, ptr, scan
     group_cols = np.array([col_index[g] for g in q.group_by], dtype=np.int32)
     gcard = np.array([len(u) for u in unions], dtype=np.int64)
-    agg_fn = np.array([AGG_CODES[a.function] for a in q.aggregations], dtype=np.int32)
-    agg_col = np.array([col_index[a.column] if a.column else -1 for a in q.aggregations], dtype=np.int32)
+    agg_fn, agg_col, agg_col2, agg_op = _agg_arrays(q, col_index)
     qs = _Query(len(prog), ops, len(q.group_by), group_cols.ctypes.data, gcard.ctypes.data,
-                len(q.aggregations), agg_fn.ctypes.data, agg_col.ctypes.data, 8, q.num_groups_limit)
+                len(q.aggregations), agg_fn.ctypes.data, agg_col.ctypes.data, 8, q.num_groups_limit,
+                agg_col2.ctypes.data, agg_op.ctypes.data)
     res = _Result()
     t0 = time.perf_counter()
     LIB.or_execute(ctypes.byref(qs), seg_structs, len(segments), num_threads, ctypes.byref(res))

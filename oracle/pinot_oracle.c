@@ -367,6 +367,18 @@ static int32_t hll_hash(const or_column* c, int32_t dict_id) {
   return c->hash_ints[dict_id];
 }
 
+/* DataFetcher.readDoubleValues (DataFetcher.java:529-539) of the aggregated argument; a 2-operand expression is
+ * evaluated in double like the reference's TransformFunction.transformToDoubleValuesSV */
+static double agg_value(const or_query* q, const or_segment* s, int k, int32_t doc) {
+  const or_column* ca = &s->columns[q->agg_col[k]];
+  const double a = ca->values[read_dict_id(ca, doc)];
+  const int op = q->agg_op ? q->agg_op[k] : 0;
+  if (!op) return a;
+  const or_column* cb = &s->columns[q->agg_col2[k]];
+  const double b = cb->values[read_dict_id(cb, doc)];
+  return op == 1 ? (1.0 * a) * b : (op == 2 ? a - b : a + b);
+}
+
 static void run_segment(const or_query* q, const or_segment* s, seg_result* r) {
   const int nagg = q->num_aggs;
   const int m = 1 << q->log2m;
@@ -460,14 +472,14 @@ static void run_segment(const or_query* q, const or_segment* s, seg_result* r) {
         int32_t col = q->agg_col[k];
         switch (q->agg_fn[k]) {
           case OR_AGG_COUNT: a[k] += 1.0; break;
-          case OR_AGG_SUM: a[k] += s->columns[col].values[read_dict_id(&s->columns[col], doc)]; break;
+          case OR_AGG_SUM: a[k] += agg_value(q, s, k, doc); break;
           case OR_AGG_MIN: {
-            double v = s->columns[col].values[read_dict_id(&s->columns[col], doc)];
+            double v = agg_value(q, s, k, doc);
             if (v < a[k]) a[k] = v;
             break;
           }
           case OR_AGG_MAX: {
-            double v = s->columns[col].values[read_dict_id(&s->columns[col], doc)];
+            double v = agg_value(q, s, k, doc);
             if (v > a[k]) a[k] = v;
             break;
           }
@@ -488,8 +500,10 @@ static void run_segment(const or_query* q, const or_segment* s, seg_result* r) {
     int seen[256] = {0};
     for (int g = 0; g < q->num_group_by; g++)
       if (!seen[q->group_cols[g]]) { seen[q->group_cols[g]] = 1; ncols_proj++; }
-    for (int k = 0; k < nagg; k++)
+    for (int k = 0; k < nagg; k++) {
       if (q->agg_col[k] >= 0 && !seen[q->agg_col[k]]) { seen[q->agg_col[k]] = 1; ncols_proj++; }
+      if (q->agg_op && q->agg_op[k] && !seen[q->agg_col2[k]]) { seen[q->agg_col2[k]] = 1; ncols_proj++; }
+    }
   }
   r->post_filter = r->docs_scanned * ncols_proj;
   (void)card_product;

@@ -78,6 +78,11 @@ typedef struct {
   const int32_t* agg_col;     /* -1 for COUNT(*) */
   int32_t log2m;
   int64_t num_groups_limit;   /* per segment (InstancePlanMakerImplV2 numGroupsLimit) */
+  /* 2-operand expression arguments (TransformOperator, ProjectPlanNode.java:82): agg_op[k] = 0 plain column,
+   * 1 mult, 2 sub, 3 add over agg_col[k] and agg_col2[k], evaluated per row in double
+   * (MultiplicationTransformFunction.java:89-104, SubtractionTransformFunction.java:99-124); NULL = none */
+  const int32_t* agg_col2;
+  const int32_t* agg_op;
 } or_query;
 
 typedef struct {

@@ -59,11 +59,7 @@ int ph_ctx_create(int32_t device_ordinal, ph_ctx** out) {
       Context& c = ctx->c;
       c.device = device_ordinal;
       PH_HIP_CHECK(hipSetDevice(device_ordinal));
-      PH_HIP_CHECK(hipStreamCreateWithFlags(&c.own_stream, hipStreamNonBlocking));
-      c.stream = c.own_stream;
-      PH_HIP_CHECK(hipStreamCreateWithFlags(&c.stream_b, hipStreamNonBlocking));
-      PH_HIP_CHECK(hipEventCreate(&c.ev_start));
-      PH_HIP_CHECK(hipEventCreate(&c.ev_stop));
+      c.lane_release(c.lane_acquire());  // one execution lane up front (fails here, not in a query, on a bad device)
       hipDeviceProp_t prop;
       PH_HIP_CHECK(hipGetDeviceProperties(&prop, device_ordinal));
       c.num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
@@ -78,25 +74,15 @@ int ph_ctx_create(int32_t device_ordinal, ph_ctx** out) {
 int ph_ctx_destroy(ph_ctx* ctx) {
   return guarded([&] {
     if (!ctx) return;
-    Context& c = ctx->c;
-    (void)hipSetDevice(c.device);
-    if (c.own_stream) (void)hipStreamSynchronize(c.own_stream);
-    if (c.ev_start) (void)hipEventDestroy(c.ev_start);
-    if (c.ev_stop) (void)hipEventDestroy(c.ev_stop);
-    if (c.own_stream) (void)hipStreamDestroy(c.own_stream);
-    if (c.stream_b) (void)hipStreamDestroy(c.stream_b);
-    for (auto e : c.ev_pool) (void)hipEventDestroy(e);
-    if (c.pinned) (void)hipHostFree(c.pinned);
-    for (auto& kv : c.pinned_free) (void)hipHostFree(kv.second);
-    delete ctx;
+    (void)hipSetDevice(ctx->c.device);
+    delete ctx;  // Context::~Context drains and frees the lanes and the pinned pool
   });
 }
 
 int ph_ctx_set_stream(ph_ctx* ctx, void* hip_stream) {
   return guarded([&] {
     if (!ctx) fail(PH_ERR_INVALID_ARGUMENT, "ctx is null");
-    std::lock_guard<std::mutex> g(ctx->c.mu);
-    ctx->c.stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->c.own_stream;
+    ctx->c.ext_stream.store(static_cast<hipStream_t>(hip_stream));
   });
 }
 
@@ -111,8 +97,7 @@ int ph_segment_unpin(ph_segment* seg) {
   return guarded([&] {
     if (!seg) return;
     (void)hipSetDevice(seg->ctx->device);
-    (void)hipStreamSynchronize(seg->ctx->stream);
-    delete seg;
+    delete seg;  // hipFree waits for work in flight on the buffers
   });
 }
 
@@ -254,16 +239,47 @@ int ph_selftest_unpack(ph_ctx* ctx, const uint8_t* packed, uint64_t packed_size,
   return guarded([&] {
     if (!ctx || !packed || !out || n < 0 || bits < 1 || bits > 31) fail(PH_ERR_INVALID_ARGUMENT, "bad arguments");
     if (packed_size < (uint64_t)((n * bits + 7) / 8)) fail(PH_ERR_INVALID_ARGUMENT, "packed buffer too small");
-    std::lock_guard<std::mutex> lk(ctx->c.mu);
     PH_HIP_CHECK(hipSetDevice(ctx->c.device));
+    LaneGuard lg(&ctx->c);
+    const hipStream_t st = lg.lane->stream;
     DeviceBuffer in, o;
     in.alloc(packed_size + kFwdPadBytes, ctx->c.device);
     o.alloc(sizeof(int32_t) * std::max<int64_t>(1, n), ctx->c.device);
-    PH_HIP_CHECK(hipMemsetAsync(in.ptr, 0, packed_size + kFwdPadBytes, ctx->c.stream));
-    PH_HIP_CHECK(hipMemcpyAsync(in.ptr, packed, packed_size, hipMemcpyHostToDevice, ctx->c.stream));
-    launch_selftest_unpack(in.as<uint32_t>(), n, bits, o.as<int32_t>(), ctx->c.stream);
-    PH_HIP_CHECK(hipMemcpyAsync(out, o.ptr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, ctx->c.stream));
-    PH_HIP_CHECK(hipStreamSynchronize(ctx->c.stream));
+    PH_HIP_CHECK(hipMemsetAsync(in.ptr, 0, packed_size + kFwdPadBytes, st));
+    PH_HIP_CHECK(hipMemcpyAsync(in.ptr, packed, packed_size, hipMemcpyHostToDevice, st));
+    launch_selftest_unpack(in.as<uint32_t>(), n, bits, o.as<int32_t>(), st);
+    PH_HIP_CHECK(hipMemcpyAsync(out, o.ptr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+    PH_HIP_CHECK(hipStreamSynchronize(st));
+  });
+}
+
+int ph_selftest_unpack_staged(ph_ctx* ctx, const uint8_t* packed, uint64_t packed_size, int64_t n, int32_t bits,
+                              int32_t tile_words, int32_t* out) {
+  return guarded([&] {
+    if (!ctx || !packed || !out || n < 0 || n > INT32_MAX || bits < 1 || bits > 31)
+      fail(PH_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (tile_words < 1 || tile_words > kMaxTileWords) fail(PH_ERR_INVALID_ARGUMENT, "tile_words out of range");
+    if (packed_size < (uint64_t)((n * bits + 7) / 8)) fail(PH_ERR_INVALID_ARGUMENT, "packed buffer too small");
+    if (stage_loads(tile_words, bits) > kPrefetchOther) fail(PH_ERR_UNSUPPORTED, "tile too wide for the prefetch pool");
+    PH_HIP_CHECK(hipSetDevice(ctx->c.device));
+    LaneGuard lg(&ctx->c);
+    const hipStream_t st = lg.lane->stream;
+    DeviceBuffer in, o, dseg;
+    in.alloc(packed_size + kFwdPadBytes, ctx->c.device);
+    o.alloc(sizeof(int32_t) * std::max<int64_t>(1, n), ctx->c.device);
+    dseg.alloc(sizeof(DevSegment), ctx->c.device);
+    PH_HIP_CHECK(hipMemsetAsync(in.ptr, 0, packed_size + kFwdPadBytes, st));
+    PH_HIP_CHECK(hipMemcpyAsync(in.ptr, packed, packed_size, hipMemcpyHostToDevice, st));
+    DevSegment d{};
+    d.num_docs = (int32_t)n;
+    d.streams[0] = DevStream{in.as<uint32_t>(), bits, 0};
+    const int32_t soff[1] = {0};
+    fill_tile_pieces(d, 1, soff, tile_words);
+    PH_HIP_CHECK(hipMemcpyAsync(dseg.ptr, &d, sizeof(d), hipMemcpyHostToDevice, st));
+    const int32_t stride = stage_stream_bytes(tile_words, bits);
+    launch_selftest_staged(dseg.as<DevSegment>(), tile_words, stride, n, o.as<int32_t>(), st);
+    PH_HIP_CHECK(hipMemcpyAsync(out, o.ptr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+    PH_HIP_CHECK(hipStreamSynchronize(st));
   });
 }
 

@@ -104,14 +104,20 @@ constexpr int kMaxStage = kMaxStreams;  // every stream of the hot loop is LDS-s
 constexpr int kMaxTileWords = 32;                    // <= 2048 docs per wave tile (host picks 4..32)
 constexpr int kBlock = 256;                          // threads per scan workgroup (4 waves)
 constexpr int kWaves = kBlock / 64;
+// MODE_PARTITION workgroups are 8 waves sharing ONE set of partition rings (the rings, not the staging, are
+// the big LDS item: 8 waves per ring set doubles the resident waves per CU at the same ring footprint)
+constexpr int kPartBlock = 512;
+constexpr int kPartWaves = kPartBlock / 64;
 constexpr int kChunkWords = 256;                     // 16384 docs per chunk (a multiple of every round)
+constexpr int kInterruptChunks = 8192;               // an interruptible scan checks every 8192 chunks (~134M docs)
 // 16-byte-per-lane loads (1 KiB per wave-instruction) a wave keeps in flight per tile, over all streams
 constexpr int kPrefetchCount = 8;                    // MODE_COUNT: one stream
 constexpr int kPrefetchOther = 12;
 constexpr int kPrefetchPartition = 12;               // MODE_PARTITION prefetch pool (tile_words 16 needs 9 loads at 10+10+10+16 bits)
 constexpr int stage_loads(int tile_words, int bits) { return (tile_words * 8 * bits + 8 + 1023) / 1024; }
-// staged span of one stream: 16-byte front pad (the decode reads dword j-1 and j) + the tile's bytes
-constexpr int stage_stream_bytes(int tile_words, int bits) { return 16 + (tile_words * 8 * bits + 8 + 15) / 16 * 16; }
+// staged span of one stream: 16-byte front pad (the decode reads dword j-1 and j) + whole 1 KiB pieces (every
+// lane of a piece stores its 16 bytes, those past the tile's bytes included, so the staging has no exec branches)
+constexpr int stage_stream_bytes(int tile_words, int bits) { return 16 + 1024 * stage_loads(tile_words, bits); }
 struct DevStream {
   const uint32_t* fwd;
   int32_t bits;
@@ -141,6 +147,7 @@ struct DevSegment {
   const uint32_t* fptr;  // FK_SET bitset over dictIds ; FK_BITMAP doc bitmap
   DevColumn cols[kMaxCols];
   DevValCol vals[kMaxVals];
+  DevValCol vals2[kMaxVals];       // second operand of a 2-operand expression term (KParams::val_op)
   DevStream streams[kMaxStreams];  // packed bit streams read by the scan loop (staged ones first)
   DevPiece pieces[kMaxPieces];     // the tile's 1 KiB loads, all streams
 };
@@ -172,6 +179,8 @@ struct KParams {
   int32_t f_stream;               // FK_RANGE / FK_SET filter column stream
   int32_t g_stream[kMaxGroupCols];
   int32_t v_stream[kMaxVals];
+  int32_t v2_stream[kMaxVals];    // stream of an expression term's second operand
+  int32_t val_op[kMaxVals];       // ph_expr_op of value term j (0: plain column)
   int32_t stage_off;              // byte offset of the per-wave staging areas in dynamic LDS
   int32_t stage_stride;           // bytes of one wave's staging area
   int32_t tile_words;             // 64-doc words per wave tile
@@ -211,8 +220,8 @@ struct KParams {
   void* part_buf;                 // [num_parts][gridDim.x][part_cap] records: one region per workgroup
   uint32_t* part_count;           // [num_parts][gridDim.x] records written per region (may exceed part_cap)
   int32_t pl_slot_off, pl_lcnt_off, pl_bcnt_off, pl_misc_off;  // LDS layout
-  int32_t part_slot_log2;         // C = 1 << part_slot_log2 LDS slots per partition
-  int32_t part_flush_at;          // flush the slots once this many records were appended
+  int32_t part_slot_log2;         // C = 1 << part_slot_log2 LDS ring slots per partition
+  int32_t part_fast;              // kernel A may run the lean k_part_scan (no gathers; ALL / RANGE / DOCRANGE leaves)
   unsigned long long* ovf_count;  // overflow table (same layout as out_*), merged at the end
   int64_t* ovf_sum;
   int64_t* ovf_min;
@@ -232,6 +241,7 @@ struct PartAggParams {
   int32_t rec64;
   int32_t has_sum, has_min, has_max;
   int32_t pack_cs;        // count and value-offset sum share one 64-bit LDS word (count << 40 | sum)
+  int32_t slices;         // workgroups per partition (each aggregates a contiguous range of the regions)
   int64_t part_vbase;
   int64_t num_groups;
   unsigned long long* out_count;
@@ -342,39 +352,70 @@ struct GlobalDict {
   std::unique_ptr<DeviceBuffer> d_values;  // int64 (INT/LONG) or float64 (FLOAT/DOUBLE) values, on demand
 };
 
+// One execution lane = what a single call needs exclusively: a stream (and a second one for the partitioned
+// plan's kernel B), timing events, hand-off events and a pinned host staging block.  Every call takes a lane
+// from the context's pool and returns it, so concurrent queries on one context run on their own streams
+// (SURVEY.md 8(b) Threading: per-call stream and scratch; operators run on many worker threads).
+struct Lane {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t stream_b = nullptr;
+  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  std::vector<hipEvent_t> ev_pool;
+  void* staging = nullptr;
+  size_t staging_bytes = 0;
+  explicit Lane(int dev);
+  ~Lane();
+  void* host_staging(size_t n);
+  hipEvent_t event(size_t i);  // hand-off event i (created on demand)
+};
+
 struct Context {
   int device = 0;
-  hipStream_t own_stream = nullptr;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
-  hipStream_t stream_b = nullptr;           // partitioned group-by: kernel B overlaps kernel A
-  std::vector<hipEvent_t> ev_pool;          // batch hand-off events
   int num_cus = 256;
-  std::mutex mu;  // serialises queries on this context
+  std::atomic<hipStream_t> ext_stream{nullptr};  // ph_ctx_set_stream: run calls on the caller's stream
+  std::mutex mu;  // guards table_dicts and union_cache (held only around their lookups / inserts)
   std::map<std::string, std::shared_ptr<GlobalDict>> table_dicts;   // ph_table_set_dictionary
   std::map<std::string, std::shared_ptr<GlobalDict>> union_cache;   // column + segment-set -> union
   std::atomic<uint64_t> next_id{1};
-  // scratch
-  std::vector<std::unique_ptr<DeviceBuffer>> scratch;
-  void* pinned = nullptr;
-  size_t pinned_bytes = 0;
-  void* host_staging(size_t n);
+  // execution lanes
+  std::mutex lane_mu;
+  std::vector<std::unique_ptr<Lane>> lanes_free;
+  std::unique_ptr<Lane> lane_acquire();
+  void lane_release(std::unique_ptr<Lane> l);
   // pinned host blocks for result columns (D2H lands directly in the result; returned on destroy)
   std::mutex pool_mu;
   std::multimap<size_t, void*> pinned_free;
   void* pinned_acquire(size_t n, size_t* cap);
   void pinned_release(void* p, size_t cap);
   // device scratch pool: per-query work buffers (dense group tables, partition buffers, descriptors) are
-  // recycled across queries instead of hipMalloc/hipFree per query (queries on a context are serialised)
+  // recycled across queries instead of hipMalloc/hipFree per query
+  std::mutex scratch_mu;
   std::multimap<size_t, std::unique_ptr<DeviceBuffer>> scratch_free;
   size_t scratch_free_bytes = 0;
   std::unique_ptr<DeviceBuffer> scratch_acquire(size_t n);
   void scratch_release(std::unique_ptr<DeviceBuffer> b);
+  ~Context();
+};
+
+// RAII lane of one call; stream() is the caller's external stream when one is set (ph_ctx_set_stream)
+struct LaneGuard {
+  Context* ctx;
+  std::unique_ptr<Lane> lane;
+  explicit LaneGuard(Context* c) : ctx(c), lane(c->lane_acquire()) {}
+  ~LaneGuard() { ctx->lane_release(std::move(lane)); }
+  hipStream_t stream() const {
+    hipStream_t e = ctx->ext_stream.load();
+    return e ? e : lane->stream;
+  }
+  LaneGuard(const LaneGuard&) = delete;
+  LaneGuard& operator=(const LaneGuard&) = delete;
 };
 
 // kernels.hip
 void launch_scan(const KParams& p, int mode, int ngroup, int rec64, int grid, size_t lds, hipStream_t s);
 void launch_part_agg(const PartAggParams& p, size_t lds, hipStream_t s);
+size_t part_agg_lds_bytes(const PartAggParams& p);
 size_t partition_lds_bytes(KParams& p);  // fills the pl_* offsets, returns the dynamic LDS size
 struct MergeParams {
   unsigned long long* out_count;
@@ -402,6 +443,10 @@ struct RoaringContainer {
 void launch_roaring_or(const RoaringContainer* c, int n, const uint8_t* base, uint32_t* bitmap, int32_t num_docs,
                        hipStream_t s);
 void launch_selftest_unpack(const uint32_t* fwd, int64_t n, int bits, int32_t* out, hipStream_t s);
+void launch_selftest_staged(const DevSegment* seg, int32_t tile_words, int32_t stage_stride, int64_t n, int32_t* out,
+                            hipStream_t s);
+// the 1 KiB wave-loads of a full tile of every staged stream of `d` (stage offsets per stream)
+void fill_tile_pieces(DevSegment& d, int nstage, const int32_t* stage_soff, int tile_words);
 
 // device-side result compaction of a dense group table (non-empty groups, keys decoded, values converted)
 constexpr int kCompactBlocks = 2048;

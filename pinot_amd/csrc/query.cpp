@@ -481,7 +481,7 @@ const void* global_dict_device_values(Context* ctx, GlobalDict& g) {
   return g.d_values->ptr;
 }
 
-const uint32_t* segment_hll_table(Context* ctx, Column& c, int log2m) {
+const uint32_t* segment_hll_table(Context* ctx, Column& c, int log2m, hipStream_t st) {
   std::lock_guard<std::mutex> lk(c.cache_mu);
   auto it = c.hll_tables.find(log2m);
   if (it != c.hll_tables.end()) return it->second.buf->as<uint32_t>();
@@ -500,9 +500,8 @@ const uint32_t* segment_hll_table(Context* ctx, Column& c, int log2m) {
     fail(PH_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL on FLOAT columns is not on the GPU path");
   } else {
     // INT / LONG -> hashLong((long) value); DOUBLE -> hashLong(doubleToRawLongBits)
-    launch_hll_table(c.d_values.ptr, c.data_type != PH_DOUBLE, c.cardinality, log2m, t.buf->as<uint32_t>(),
-                     ctx->stream);
-    PH_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    launch_hll_table(c.d_values.ptr, c.data_type != PH_DOUBLE, c.cardinality, log2m, t.buf->as<uint32_t>(), st);
+    PH_HIP_CHECK(hipStreamSynchronize(st));
   }
   const uint32_t* p = t.buf->as<uint32_t>();
   c.hll_tables[log2m] = std::move(t);
@@ -542,10 +541,11 @@ double value_as_double(const Dictionary& d, int64_t i) {
 struct QueryScratch {
   std::vector<std::unique_ptr<DeviceBuffer>> bufs;
   Context* ctx;
-  explicit QueryScratch(Context* c) : ctx(c) {}
+  hipStream_t st, sb;  // the call's streams: drained before the buffers go back to the pool
+  QueryScratch(Context* c, hipStream_t s1, hipStream_t s2) : ctx(c), st(s1), sb(s2) {}
   ~QueryScratch() {
-    (void)hipStreamSynchronize(ctx->stream);
-    (void)hipStreamSynchronize(ctx->stream_b);
+    (void)hipStreamSynchronize(st);
+    (void)hipStreamSynchronize(sb);
     for (auto& b : bufs) ctx->scratch_release(std::move(b));
   }
   template <class T>
@@ -566,7 +566,7 @@ int bits_for_range(uint64_t range) {
 }
 
 // Frame-of-reference value stream of an INT/LONG column (VK_PACKED), built once per pinned column.
-bool ensure_value_stream(Context* ctx, ph_segment* seg, Column& c) {
+bool ensure_value_stream(Context* ctx, ph_segment* seg, Column& c, hipStream_t st) {
   std::lock_guard<std::mutex> lk(c.cache_mu);
   if (c.vpacked_ready) return c.d_vpacked != nullptr;
   c.vpacked_ready = true;
@@ -582,10 +582,9 @@ bool ensure_value_stream(Context* ctx, ph_segment* seg, Column& c) {
   const size_t alloc = ((bytes + kFwdPadBytes + 255) / 256) * 256;
   auto buf = std::make_unique<DeviceBuffer>();
   buf->alloc(alloc, ctx->device);
-  PH_HIP_CHECK(hipMemsetAsync(buf->ptr, 0, alloc, ctx->stream));
-  launch_encode_values(c.d_fwd.as<uint32_t>(), c.bits, c.d_values.as<int64_t>(), lo, vb, n, buf->as<uint32_t>(),
-                       ctx->stream);
-  PH_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+  PH_HIP_CHECK(hipMemsetAsync(buf->ptr, 0, alloc, st));
+  launch_encode_values(c.d_fwd.as<uint32_t>(), c.bits, c.d_values.as<int64_t>(), lo, vb, n, buf->as<uint32_t>(), st);
+  PH_HIP_CHECK(hipStreamSynchronize(st));
   c.vbase = lo;
   c.vbits = vb;
   seg->device_bytes += (int64_t)alloc;
@@ -594,6 +593,24 @@ bool ensure_value_stream(Context* ctx, ph_segment* seg, Column& c) {
 }
 
 }  // namespace
+
+void fill_tile_pieces(DevSegment& d, int nstage, const int32_t* stage_soff, int tile_words) {
+  int np = 0;
+  for (int s = 0; s < nstage; ++s) {
+    const int bits = d.streams[s].bits;
+    if (!bits) continue;
+    const int n = stage_loads(tile_words, bits);
+    for (int i = 0; i < n; ++i) {
+      if (np >= kMaxPieces) fail(PH_ERR_UNSUPPORTED, "tile pieces exceed the prefetch pool");
+      DevPiece& pc = d.pieces[np++];
+      pc.fwd = reinterpret_cast<const uint8_t*>(d.streams[s].fwd) + 1024 * i;
+      pc.stride = 8 * bits;
+      pc.off = 1024 * i;
+      pc.lds = stage_soff[s] + 16 + 1024 * i;
+    }
+  }
+  d.npieces = np;
+}
 
 ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const* segs_in, int32_t nseg,
                               const DenseArgs* dn) {
@@ -605,13 +622,25 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   if (nseg < 0 || (nseg > 0 && !segs_in)) fail(PH_ERR_INVALID_ARGUMENT, "bad segment list");
   if (q->num_aggregations > kMaxAggs) fail(PH_ERR_UNSUPPORTED, "too many aggregations");
   if (q->num_group_by > kMaxGroupCols) fail(PH_ERR_UNSUPPORTED, "too many group-by columns");
-  std::lock_guard<std::mutex> qlock(ctx->mu);
   PH_HIP_CHECK(hipSetDevice(ctx->device));
-  hipStream_t st = ctx->stream;
+  LaneGuard lane(ctx);  // this call's streams, events and staging (concurrent calls use their own)
+  const hipStream_t st = lane.stream();
   std::vector<ph_segment*> segs(segs_in, segs_in + nseg);
   for (auto* s : segs)
     if (!s || s->ctx != ctx) fail(PH_ERR_INVALID_ARGUMENT, "segment is null or pinned on another context");
 
+  // BaseOperator.nextBlock's interruption check (BaseOperator.java:39) and the combine's end time
+  // (GroupByCombineOperator.java:225-234), at the points where a call can stop without work in flight
+  const bool interruptible = q->interrupt != nullptr || q->end_time_ms > 0;
+  auto check_interrupt = [&]() {
+    if (q->interrupt && *q->interrupt) fail(PH_ERR_CANCELLED, "query interrupted");
+    if (q->end_time_ms > 0) {
+      const int64_t now = std::chrono::duration_cast<std::chrono::milliseconds>(
+                              std::chrono::system_clock::now().time_since_epoch()).count();
+      if (now > q->end_time_ms) fail(PH_ERR_CANCELLED, "query timed out (end time passed)");
+    }
+  };
+  check_interrupt();
   auto res = std::make_unique<ph_result>();
   ph_exec_stats& stats = res->stats;
   stats.num_segments_processed = nseg;
@@ -636,8 +665,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // aggregation -> (value column, op) / HLL register set
   const int nagg = q->num_aggregations;
   int log2m = 0;
-  std::vector<std::string> val_cols, hll_cols;
-  std::vector<int> val_ops;
+  // value terms: a column, or a 2-operand expression `val_cols[j] <op> val_cols2[j]`
+  std::vector<std::string> val_cols, val_cols2, hll_cols;
+  std::vector<int> val_ops, val_exprs;
   std::vector<int> agg_val(nagg, -1), agg_hll(nagg, -1);
   std::set<std::string> projected(group_cols.begin(), group_cols.end());
   for (int k = 0; k < nagg; ++k) {
@@ -664,15 +694,24 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
       continue;
     }
-    auto it = std::find(val_cols.begin(), val_cols.end(), std::string(a.column));
-    int j;
-    if (it == val_cols.end()) {
+    const int eop = a.expr_op;
+    if (eop < PH_EXPR_NONE || eop > PH_EXPR_ADD) fail(PH_ERR_UNSUPPORTED, "expression operator");
+    const std::string col2 = eop ? lit(a.column2) : std::string();
+    if (eop) {
+      if (!a.column2) fail(PH_ERR_BAD_QUERY, "expression needs a second operand");
+      add_slot(col2);
+      projected.insert(col2);
+    }
+    int j = -1;
+    for (size_t t = 0; t < val_cols.size(); ++t)
+      if (val_cols[t] == a.column && val_exprs[t] == eop && val_cols2[t] == col2) j = (int)t;
+    if (j < 0) {
       if ((int)val_cols.size() >= kMaxVals) fail(PH_ERR_UNSUPPORTED, "too many aggregated columns");
       val_cols.push_back(a.column);
+      val_cols2.push_back(col2);
+      val_exprs.push_back(eop);
       val_ops.push_back(0);
       j = (int)val_cols.size() - 1;
-    } else {
-      j = (int)(it - val_cols.begin());
     }
     agg_val[k] = j;
     val_ops[j] |= a.type == PH_AGG_SUM ? 1 : (a.type == PH_AGG_MIN ? 2 : 4);
@@ -690,15 +729,37 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       auto it = s->columns.find(c);
       if (it == s->columns.end()) fail(PH_ERR_BAD_QUERY, "Column not found: " + c + " in segment " + s->name);
     }
+  // |value| bound of term j over the queried segments (integer terms only; 0 when unknown)
+  std::vector<double> term_amax(nvals, 0.0);
   for (int j = 0; j < nvals; ++j) {
-    for (size_t i = 0; i < segs.size(); ++i) {
-      const int dt = segs[i]->columns.at(val_cols[j])->data_type;
-      if (dt == PH_STRING) fail(PH_ERR_UNSUPPORTED, "numeric aggregation on STRING column " + val_cols[j]);
-      const int is_int = dt == PH_INT || dt == PH_LONG;
-      if (i == 0) val_is_int[j] = is_int;
-      else if (val_is_int[j] != is_int)
-        fail(PH_ERR_UNSUPPORTED, "aggregation column with mixed integer/real types across segments");
+    int is_int = 1;
+    double amax[2] = {0.0, 0.0};
+    for (int o = 0; o < (val_exprs[j] ? 2 : 1); ++o) {
+      const std::string& cn = o ? val_cols2[j] : val_cols[j];
+      int col_int = -1;
+      for (size_t i = 0; i < segs.size(); ++i) {
+        const Column& c = *segs[i]->columns.at(cn);
+        const int dt = c.data_type;
+        if (dt == PH_STRING) fail(PH_ERR_UNSUPPORTED, "numeric aggregation on STRING column " + cn);
+        const int ci = dt == PH_INT || dt == PH_LONG;
+        if (col_int < 0) col_int = ci;
+        else if (col_int != ci)
+          fail(PH_ERR_UNSUPPORTED, "aggregation column with mixed integer/real types across segments");
+        if (ci && c.cardinality > 0) {
+          amax[o] = std::max(amax[o], std::fabs((double)c.dict.ints.front()));
+          amax[o] = std::max(amax[o], std::fabs((double)c.dict.ints.back()));
+        }
+      }
+      is_int &= col_int != 0;
     }
+    double bound = amax[0];
+    if (val_exprs[j] == PH_EXPR_MULT) bound = amax[0] * amax[1];
+    else if (val_exprs[j]) bound = amax[0] + amax[1];
+    // an integer expression is exact in int64 only while it cannot overflow; else double arithmetic, as the
+    // reference computes it
+    if (val_exprs[j] && bound >= 4.0e18) is_int = 0;
+    val_is_int[j] = is_int;
+    term_amax[j] = is_int ? bound : 0.0;
   }
   const int m = log2m ? (1 << log2m) : 0;
 
@@ -737,7 +798,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         for (auto* s : segs) {
           Column& c = *s->columns.at(a.column);
           if (s->num_docs == 0) continue;
-          const uint32_t* dt = segment_hll_table(ctx, c, lm);
+          const uint32_t* dt = segment_hll_table(ctx, c, lm, st);
           std::vector<uint32_t> h(c.cardinality);
           PH_HIP_CHECK(hipMemcpy(h.data(), dt, sizeof(uint32_t) * h.size(), hipMemcpyDeviceToHost));
           for (uint32_t e : h) regs[e >> 8] = std::max<uint8_t>(regs[e >> 8], (uint8_t)(e & 0xff));
@@ -752,7 +813,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   }
 
   // ---- per-segment filter plans
-  QueryScratch scratch(ctx);
+  QueryScratch scratch(ctx, st, lane.lane->stream_b);
   std::vector<SegProgram> progs(nseg);
   std::vector<PNode> roots(nseg);
   std::vector<char> seg_live(nseg, 1);
@@ -788,6 +849,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   int64_t num_groups = 1;
   for (auto& g : group_cols) {
     std::shared_ptr<GlobalDict> gd;
+    std::lock_guard<std::mutex> dlk(ctx->mu);  // table dictionaries / union cache
     auto it = ctx->table_dicts.find(g);
     if (it != ctx->table_dicts.end()) {
       gd = it->second;
@@ -823,6 +885,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   const int64_t G = num_groups;
   if (dop) {
     // partial tables of different GPUs line up only over table-level dictionaries
+    std::lock_guard<std::mutex> dlk(ctx->mu);
     for (auto& g : group_cols)
       if (!ctx->table_dicts.count(g))
         fail(PH_ERR_INVALID_ARGUMENT, "dense partials need ph_table_set_dictionary for group-by column " + g);
@@ -866,6 +929,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   for (int j = 0; j < nvals; ++j) {
     kp.val_ops[j] = val_ops[j];
     kp.val_is_int[j] = val_is_int[j];
+    kp.val_op[j] = val_exprs[j];
   }
   for (int h = 0; h < num_hll; ++h) kp.hll_slot[h] = pl.slot.at(hll_cols[h]);
 
@@ -882,7 +946,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     return (int)stream_cols.size() - 1;
   };
   for (int g = 0; g < q->num_group_by; ++g) kp.g_stream[g] = stream_of(group_cols[g], "id");
-  for (int j = 0; j < nvals; ++j) kp.v_stream[j] = stream_of(val_cols[j], "val");
+  for (int j = 0; j < nvals; ++j) {
+    kp.v_stream[j] = stream_of(val_cols[j], "val");
+    kp.v2_stream[j] = val_exprs[j] ? stream_of(val_cols2[j], "val") : kp.v_stream[j];
+  }
   if ((int)stream_cols.size() > kMaxStreams) fail(PH_ERR_UNSUPPORTED, "too many column streams in one query");
   kp.nstage = (int)stream_cols.size();  // <= kMaxStreams == kMaxStage: every stream is staged
 
@@ -891,7 +958,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   for (int j = 0; j < nvals; ++j)
     for (auto* s : segs) {
       Column& c = *s->columns.at(val_cols[j]);
-      if (val_is_int[j] && c.cardinality > 0 && j == 0) {
+      if (val_is_int[j] && !val_exprs[j] && c.cardinality > 0 && j == 0) {
         vmin = std::min(vmin, c.dict.ints.front());
         vmax = std::max(vmax, c.dict.ints.back());
       }
@@ -900,17 +967,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // |integer SUM| < 2^53 whenever max |value| x total docs is: then no group's double can be inexact and the
   // per-group precision check is skipped (only for a local execute; a finalised shard also holds other ranks)
   bool sum_bounded[kMaxVals] = {};
-  for (int j = 0; j < nvals; ++j) {
-    if (!val_is_int[j]) continue;
-    double amax = 0.0;
-    for (auto* s : segs) {
-      Column& c = *s->columns.at(val_cols[j]);
-      if (c.cardinality <= 0) continue;
-      amax = std::max(amax, std::fabs((double)c.dict.ints.front()));
-      amax = std::max(amax, std::fabs((double)c.dict.ints.back()));
-    }
-    sum_bounded[j] = amax * (double)stats.num_total_docs < 4503599627370496.0;  // 2^52: margin for rounding
-  }
+  for (int j = 0; j < nvals; ++j)
+    if (val_is_int[j]) sum_bounded[j] = term_amax[j] * (double)stats.num_total_docs < 4503599627370496.0;  // 2^52
 
   int mode = -3;  // DENSE_FINALIZE: no scan
   float dev_ms = 0.f;
@@ -951,7 +1009,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     kp.lds_hll_off = (int32_t)std::min<size_t>(off, INT32_MAX);
     off += (size_t)G * num_hll * (m ? m : 1) * 4;
-    const bool part_ok = num_hll == 0 && nvals <= 1 && (nvals == 0 || (val_is_int[0] && vmax >= vmin &&
+    const bool part_ok = num_hll == 0 && nvals <= 1 && (nvals == 0 || (val_is_int[0] && !val_exprs[0] && vmax >= vmin &&
                                                                        (uint64_t)(vmax - vmin) < (1ull << 32))) &&
                          G <= ((int64_t)kPartMaxParts << kPartKeysLog2) && getenv("PH_DISABLE_PARTITION") == nullptr;
     if (off <= 64 * 1024) {
@@ -1050,22 +1108,25 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     for (int g = 0; g < q->num_group_by; ++g)
       d.cols[kp.group_slot[g]].remap = segment_remap(ctx, *s->columns.at(group_cols[g]), *gdicts[g]);
     for (int h = 0; h < num_hll; ++h)
-      d.cols[kp.hll_slot[h]].hll = segment_hll_table(ctx, *s->columns.at(hll_cols[h]), log2m);
+      d.cols[kp.hll_slot[h]].hll = segment_hll_table(ctx, *s->columns.at(hll_cols[h]), log2m, st);
     for (int j = 0; j < nvals; ++j) {
-      Column& c = *s->columns.at(val_cols[j]);
-      DevValCol& v = d.vals[j];
-      if (val_is_int[j] && ensure_value_stream(ctx, s, c)) {
-        v.kind = VK_PACKED;
-        v.fwd = c.d_vpacked->as<uint32_t>();
-        v.bits = c.vbits;
-        v.base = c.vbase;
-      } else {
-        v.kind = val_is_int[j] ? VK_DICT_I64 : VK_DICT_F64;
-        v.fwd = c.d_fwd.as<uint32_t>();
-        v.bits = c.bits;
-        v.table = c.d_values.ptr;
+      for (int o = 0; o < (val_exprs[j] ? 2 : 1); ++o) {
+        Column& c = *s->columns.at(o ? val_cols2[j] : val_cols[j]);
+        DevValCol& v = o ? d.vals2[j] : d.vals[j];
+        const bool col_int = c.data_type == PH_INT || c.data_type == PH_LONG;
+        if (col_int && ensure_value_stream(ctx, s, c, st)) {
+          v.kind = VK_PACKED;
+          v.fwd = c.d_vpacked->as<uint32_t>();
+          v.bits = c.vbits;
+          v.base = c.vbase;
+        } else {
+          v.kind = col_int ? VK_DICT_I64 : VK_DICT_F64;
+          v.fwd = c.d_fwd.as<uint32_t>();
+          v.bits = c.bits;
+          v.table = c.d_values.ptr;
+        }
+        d.streams[o ? kp.v2_stream[j] : kp.v_stream[j]] = DevStream{v.fwd, v.bits, 0};
       }
-      d.streams[kp.v_stream[j]] = DevStream{v.fwd, v.bits, 0};
     }
     for (int g = 0; g < q->num_group_by; ++g) {
       Column& c = *s->columns.at(group_cols[g]);
@@ -1092,7 +1153,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     for (int s = 0; s < kp.nstage; ++s)
       for (auto& d : dsegs) maxbits[s] = std::max(maxbits[s], (int)d.streams[s].bits);
     const int pool = mode == MODE_COUNT ? kPrefetchCount : (mode == MODE_PARTITION ? kPrefetchPartition : kPrefetchOther);
-    int tw = (mode == MODE_PARTITION || mode == MODE_GROUP_LDS) ? 16 : kMaxTileWords;  // r1 sweeps
+    // r1/r2 sweeps: MODE_PARTITION rounds (8 waves x 8 words) append ~2048 records, which keeps a
+    // partition's ring (32 slots) from overflowing
+    int tw = mode == MODE_PARTITION ? 8 : (mode == MODE_GROUP_LDS ? 16 : kMaxTileWords);
     if (const char* e = getenv("PH_TILE_WORDS")) tw = std::max(4, std::min(kMaxTileWords, atoi(e)));  // tuning knob
     auto loads = [&](int t) {
       int n = 0;
@@ -1114,34 +1177,23 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   for (auto& d : dsegs) {
     bool g = d.fkind == FK_SET || d.fkind == FK_BITMAP || d.fkind == FK_GENERIC || num_hll > 0;
     for (int gi = 0; gi < q->num_group_by; ++gi) g |= d.cols[kp.group_slot[gi]].remap != nullptr;
-    for (int j = 0; j < nvals; ++j) g |= d.vals[j].kind != VK_PACKED;
+    for (int j = 0; j < nvals; ++j) g |= d.vals[j].kind != VK_PACKED || (val_exprs[j] && d.vals2[j].kind != VK_PACKED);
     if (g && mode != MODE_COUNT) kp.late_prefetch = 1;
     if (g && mode == MODE_COUNT && d.fkind != FK_RANGE && d.fkind != FK_ALL && d.fkind != FK_DOCRANGE) kp.late_prefetch = 1;
   }
   // per-segment tile pieces: the 1 KiB wave-loads of a full tile, stream by stream
-  for (auto& d : dsegs) {
-    int np = 0;
-    for (int s = 0; s < kp.nstage; ++s) {
-      const int bits = d.streams[s].bits;
-      if (!bits) continue;
-      const int n = stage_loads(kp.tile_words, bits);
-      for (int i = 0; i < n; ++i) {
-        if (np >= kMaxPieces) fail(PH_ERR_UNSUPPORTED, "tile pieces exceed the prefetch pool");
-        DevPiece& pc = d.pieces[np++];
-        pc.fwd = reinterpret_cast<const uint8_t*>(d.streams[s].fwd) + 1024 * i;
-        pc.stride = 8 * bits;
-        pc.off = 1024 * i;
-        pc.lds = kp.stage_soff[s] + 16 + 1024 * i;
-      }
-    }
-    d.npieces = np;
-  }
+  for (auto& d : dsegs) fill_tile_pieces(d, kp.nstage, kp.stage_soff, kp.tile_words);
+  // the lean kernel A (k_part_scan) covers gather-free tiles with ALL / RANGE / DOCRANGE filter leaves
+  kp.part_fast = !kp.late_prefetch && getenv("PH_PART_GENERIC") == nullptr;
+  for (auto& d : dsegs)
+    if (d.fkind != FK_ALL && d.fkind != FK_RANGE && d.fkind != FK_DOCRANGE) kp.part_fast = 0;
   if (const char* e = getenv("PH_DEBUG_FLAGS")) kp.dbg_flags = atoi(e);
+  if (kp.dbg_flags) kp.part_fast = 0;  // timing experiments run on the generic form
   if (getenv("PH_DEBUG_STAMPS")) {
     kp.dbg = scratch.alloc<unsigned long long>(4 * (size_t)ctx->num_cus * 8);
     PH_HIP_CHECK(hipMemsetAsync(kp.dbg, 0, 32 * (size_t)ctx->num_cus * 8, st));
   }
-  const size_t stage_bytes = (size_t)kWaves * kp.stage_stride;
+  const size_t stage_bytes = (size_t)(mode == MODE_PARTITION ? kPartWaves : kWaves) * kp.stage_stride;
   size_t lds = 0;
   if (mode == MODE_PARTITION) {
     lds = 0;  // laid out with the partition parameters below
@@ -1171,13 +1223,14 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   for (auto& fb : fbitmap_fix) dsegs[fb.first].fptr = bitmap_dev[fb.second];
   PH_HIP_CHECK(hipStreamSynchronize(st));  // pageable payload copies above
 
+  check_interrupt();
   if (!chunks.empty()) {
     DevSegment* d_segs = scratch.alloc<DevSegment>(dsegs.size());
     FilterInsn* d_prog = scratch.alloc<FilterInsn>(std::max<size_t>(1, all_insns.size()));
     Chunk* d_chunks = scratch.alloc<Chunk>(chunks.size());
     const size_t b1 = sizeof(DevSegment) * dsegs.size(), b2 = sizeof(FilterInsn) * all_insns.size(),
                  b3 = sizeof(Chunk) * chunks.size();
-    uint8_t* stage = static_cast<uint8_t*>(ctx->host_staging(b1 + b2 + b3));
+    uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(b1 + b2 + b3));
     memcpy(stage, dsegs.data(), b1);
     memcpy(stage + b1, all_insns.data(), b2);
     memcpy(stage + b1 + b2, chunks.data(), b3);
@@ -1194,9 +1247,20 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       int blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1)));
       if (mode == MODE_GROUP_LDS) blocks_per_cu = std::min(blocks_per_cu, 4);
       const int grid = (int)std::min<int64_t>((int64_t)chunks.size(), (int64_t)ctx->num_cus * blocks_per_cu);
-      PH_HIP_CHECK(hipEventRecord(ctx->ev_start, st));
-      launch_scan(kp, mode, q->num_group_by, 0, grid, lds, st);
-      PH_HIP_CHECK(hipEventRecord(ctx->ev_stop, st));
+      // an interruptible call scans in batches of kInterruptChunks chunks and checks between them
+      const int32_t nchunks = (int32_t)chunks.size();
+      const int32_t step = interruptible ? kInterruptChunks : nchunks;
+      PH_HIP_CHECK(hipEventRecord(lane.lane->ev_start, st));
+      for (int32_t cb = 0; cb < nchunks; cb += step) {
+        kp.chunk_begin = cb;
+        kp.chunk_end = std::min(nchunks, cb + step);
+        launch_scan(kp, mode, q->num_group_by, 0, std::min(grid, kp.chunk_end - cb), lds, st);
+        if (interruptible && kp.chunk_end < nchunks) {
+          PH_HIP_CHECK(hipStreamSynchronize(st));
+          check_interrupt();
+        }
+      }
+      PH_HIP_CHECK(hipEventRecord(lane.lane->ev_stop, st));
     } else {
       // ---- partitioned group-by: batches of chunks; kernel A (filter + decode + partition) on `st`,
       // kernel B (per-partition LDS aggregation + owned merge) on stream_b, overlapped across batches.
@@ -1213,6 +1277,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       rec64 = (klo + vbits > 32) ? 1 : 0;
       int64_t batch_rows = int64_t(1) << 31;  // one batch: launch tails of many short batches cost more than MALL reuse saves
       if (const char* e = getenv("PH_PART_BATCH_ROWS")) batch_rows = std::max<int64_t>(1 << 16, atoll(e));
+      if (interruptible) batch_rows = std::min<int64_t>(batch_rows, (int64_t)kInterruptChunks * kChunkWords * 64);
       // batches: contiguous chunk ranges of ~batch_rows docs
       std::vector<std::pair<int32_t, int32_t>> batches;
       int64_t max_batch_docs = 0;
@@ -1233,8 +1298,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       kp.part_vbits = vbits;
       kp.num_parts = (int32_t)P;
       const size_t lds_a = partition_lds_bytes(kp);
-      int a_cap = 6;  // swept r1 (tile 16, 2048 slots): 6 resident workgroups per CU
-      if (const char* e = getenv("PH_PART_WG_PER_CU")) a_cap = std::max(1, std::min(8, atoi(e)));  // tuning knob
+      int a_cap = 4;  // 8-wave workgroups: <= 4 per CU (32 waves)
+      if (const char* e = getenv("PH_PART_WG_PER_CU")) a_cap = std::max(1, std::min(4, atoi(e)));  // tuning knob
       const int a_per_cu = (int)std::max<size_t>(1, std::min<size_t>(a_cap, (160 * 1024) / lds_a));
       const int grid_a = ctx->num_cus * a_per_cu;
       int max_batch_chunks = 0;
@@ -1245,6 +1310,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       const int64_t wg_docs = (int64_t)((max_batch_chunks + grid_a - 1) / grid_a) * kChunkWords * 64;
       int64_t cap = (int64_t)((double)wg_docs * 1.25 / (double)P) + 64;
       cap = (cap + 63) / 64 * 64;
+      // the ring word keeps flushed / chunk in 16 bits; ranks beyond the capacity go to the overflow table
+      cap = std::min<int64_t>(cap, 65535 * (rec64 ? 8 : 16));
       const int64_t max_part_records = cap * grid_a;
       // COUNT and the value-offset SUM share one 64-bit LDS word in kernel B when both fit
       const bool pack_cs = !rec64 && max_part_records < (int64_t(1) << 24) &&
@@ -1295,21 +1362,24 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       bp.out_sum = has_sum ? reinterpret_cast<int64_t*>(kp.out_sum[0]) : nullptr;
       bp.out_min = has_min ? kp.out_min[0] : nullptr;
       bp.out_max = has_max ? kp.out_max[0] : nullptr;
-      const size_t lds_b = (((size_t)(pack_cs ? 8 : 4) + (has_sum && !pack_cs ? 8 : 0) + (has_min ? 4 : 0) +
-                            (has_max ? 4 : 0))
-                               << klo) +
-                           4 * (size_t)grid_a;  // + region fill levels
-      while (ctx->ev_pool.size() < 2 * batches.size() + 2) {
-        hipEvent_t e;
-        PH_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        ctx->ev_pool.push_back(e);
-      }
+      // kernel B slices: enough (partition, slice) workgroups to give every CU two
+      int slices = (int)std::max<int64_t>(1, std::min<int64_t>(8, (2 * (int64_t)ctx->num_cus + P - 1) / P));
+      if (const char* e = getenv("PH_PART_SLICES")) slices = std::max(1, std::min(16, atoi(e)));  // tuning knob
+      bp.slices = slices;
+      bp.regions = grid_a;
+      const size_t lds_b = part_agg_lds_bytes(bp);
+      Lane& L = *lane.lane;
       // PH_PART_SERIAL=1 runs kernel B on the scan stream (profiling each kernel without overlap)
-      hipStream_t sb = getenv("PH_PART_SERIAL") ? st : ctx->stream_b;
-      PH_HIP_CHECK(hipEventRecord(ctx->ev_start, st));
+      hipStream_t sb = getenv("PH_PART_SERIAL") ? st : L.stream_b;
+      PH_HIP_CHECK(hipEventRecord(L.ev_start, st));
       for (size_t b = 0; b < batches.size(); ++b) {
+        if (interruptible && b > 0) {
+          PH_HIP_CHECK(hipStreamSynchronize(st));
+          PH_HIP_CHECK(hipStreamSynchronize(sb));
+          check_interrupt();
+        }
         const int set = (int)(b & 1);
-        if (b >= 2) PH_HIP_CHECK(hipStreamWaitEvent(st, ctx->ev_pool[2 * (b - 2) + 1], 0));  // set free again
+        if (b >= 2) PH_HIP_CHECK(hipStreamWaitEvent(st, L.event(2 * (b - 2) + 1), 0));  // set free again
         kp.chunk_begin = batches[b].first;
         kp.chunk_end = batches[b].second;
         kp.part_buf = bufs[set];
@@ -1317,25 +1387,25 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         const int nch = kp.chunk_end - kp.chunk_begin;
         const int grid = std::min(nch, grid_a);
         launch_scan(kp, MODE_PARTITION, q->num_group_by, rec64, grid, lds_a, st);
-        PH_HIP_CHECK(hipEventRecord(ctx->ev_pool[2 * b], st));
-        PH_HIP_CHECK(hipStreamWaitEvent(sb, ctx->ev_pool[2 * b], 0));
+        PH_HIP_CHECK(hipEventRecord(L.event(2 * b), st));
+        PH_HIP_CHECK(hipStreamWaitEvent(sb, L.event(2 * b), 0));
         bp.part_buf = bufs[set];
         bp.part_count = counts[set];
         bp.regions = grid;
         launch_part_agg(bp, lds_b, sb);
-        PH_HIP_CHECK(hipEventRecord(ctx->ev_pool[2 * b + 1], sb));
+        PH_HIP_CHECK(hipEventRecord(L.event(2 * b + 1), sb));
       }
       MergeParams mp{kp.out_count, bp.out_sum, bp.out_min, bp.out_max, kp.ovf_count, kp.ovf_sum, kp.ovf_min,
                      kp.ovf_max, G};
-      PH_HIP_CHECK(hipEventRecord(ctx->ev_pool[2 * batches.size()], st));
-      PH_HIP_CHECK(hipStreamWaitEvent(sb, ctx->ev_pool[2 * batches.size()], 0));
+      PH_HIP_CHECK(hipEventRecord(L.event(2 * batches.size()), st));
+      PH_HIP_CHECK(hipStreamWaitEvent(sb, L.event(2 * batches.size()), 0));
       launch_merge_overflow(mp, sb);
-      PH_HIP_CHECK(hipEventRecord(ctx->ev_pool[2 * batches.size() + 1], sb));
-      PH_HIP_CHECK(hipStreamWaitEvent(st, ctx->ev_pool[2 * batches.size() + 1], 0));
-      PH_HIP_CHECK(hipEventRecord(ctx->ev_stop, st));
+      PH_HIP_CHECK(hipEventRecord(L.event(2 * batches.size() + 1), sb));
+      PH_HIP_CHECK(hipStreamWaitEvent(st, L.event(2 * batches.size() + 1), 0));
+      PH_HIP_CHECK(hipEventRecord(L.ev_stop, st));
     }
     PH_HIP_CHECK(hipStreamSynchronize(st));  // staging buffer reuse + results
-    PH_HIP_CHECK(hipEventElapsedTime(&dev_ms, ctx->ev_start, ctx->ev_stop));
+    PH_HIP_CHECK(hipEventElapsedTime(&dev_ms, lane.lane->ev_start, lane.lane->ev_stop));
     if (kp.dbg) {  // PH_DEBUG_STAMPS: where wave 0 of each workgroup spent its cycles (last launch)
       std::vector<unsigned long long> h(4 * (size_t)ctx->num_cus * 8);
       PH_HIP_CHECK(hipMemcpy(h.data(), kp.dbg, 8 * h.size(), hipMemcpyDeviceToHost));

@@ -1,0 +1,411 @@
+// scan_partition.hip -- the partitioned group-by (MODE_PARTITION): kernel A (k_scan instantiations that append records
+// to per-(partition, workgroup) regions) and kernel B (k_part_agg), plus the overflow-table merge.
+#include "scan_kernel.h"
+
+namespace ph {
+
+size_t partition_lds_bytes(KParams& p) {
+  const size_t rec = p.part_vbits + p.part_klo > 32 ? 8 : 4;
+  size_t o = 0;
+  auto place = [&](int32_t& dst, size_t bytes) {
+    dst = (int32_t)o;
+    o = (o + bytes + 15) / 16 * 16;
+  };
+  int32_t stage_off = 0;
+  place(stage_off, (size_t)kPartWaves * p.stage_stride);
+  p.stage_off = stage_off;
+  // ring slots per partition: a whole 64-byte chunk of leftovers (< 16 records) plus one round's appends
+  // (~ round records / P, Poisson) must fit or records take the overflow-table path
+  int cl = 5;
+  if (const char* e = getenv("PH_PART_RING_LOG2")) cl = std::max(3, std::min(7, atoi(e)));  // tuning knob (<= 7: a partition's flush lanes stay in one wave)
+  while (cl > 4 && (size_t)(p.num_parts << cl) * rec > 48 * 1024) --cl;
+  p.part_slot_log2 = cl;
+  // + one scratch slot and one scratch word per lane: k_part_scan appends misses there (branch-free)
+  place(p.pl_slot_off, ((size_t)(p.num_parts << cl) + 64) * rec);
+  place(p.pl_lcnt_off, 4 * ((size_t)p.num_parts + 64));  // (flushed / CH << 16 | pending) per partition
+  p.pl_bcnt_off = p.pl_lcnt_off;
+  place(p.pl_misc_off, 64);
+  return o;
+}
+
+// ------------------------------------------------------------------ kernel A, lean form
+// k_part_scan is k_scan<MODE_PARTITION> for the common shapes (no gathers: identity key remaps, a packed value
+// stream; filter leaf ALL / RANGE / DOCRANGE) written for issue efficiency: per group of 4 words the filter,
+// key and value decodes of every lane are straight-line, keys are 24-bit multiply-adds, the 4 rank atomics
+// issue back to back (a miss increments its lane's scratch word instead of branching) and the ring stores
+// likewise (a miss stores to its lane's scratch slot).  r2 SQ counters on the generic form: 61 VALU + 44 SALU
+// per 64-doc word and 51 % of wave cycles waiting.
+template <int NG, int REC64, int HASV, int FK>
+__device__ __forceinline__ void part_tile(const KParams& p, SegPtr S, uint8_t* smem, const uint8_t* wst, int lane,
+                                          int32_t w0, int32_t nvalid, unsigned long long& matched) {
+  using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
+  constexpr uint32_t CH = 64 / sizeof(Rec);
+  const uint32_t ndocs = (uint32_t)S->num_docs;
+  const int fbits = FK == FK_RANGE ? S->streams[p.f_stream].bits : 1;
+  const BitCursor fcur = bit_cursor(wst + p.stage_soff[p.f_stream], fbits, lane);
+  const uint32_t flo = S->flo, flen = S->flen;
+  BitCursor gcur[NG];
+  uint32_t gstr[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    gcur[g] = bit_cursor(wst + p.stage_soff[p.g_stream[g]], S->streams[p.g_stream[g]].bits, lane);
+    gstr[g] = (uint32_t)p.group_stride[g];
+  }
+  BitCursor vcur = fcur;
+  uint32_t vadd = 0;
+  if (HASV) {
+    vcur = bit_cursor(wst + p.stage_soff[p.v_stream[0]], S->streams[p.v_stream[0]].bits, lane);
+    vadd = (uint32_t)(S->vals[0].base - p.part_vbase);  // record value = packed offset + (base - vmin)
+  }
+  const uint32_t klo = (uint32_t)p.part_klo, kmask = (1u << klo) - 1u, vbits = (uint32_t)p.part_vbits;
+  const int cl = p.part_slot_log2;
+  const uint32_t C = 1u << cl;
+  uint32_t* words = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
+  Rec* slots = reinterpret_cast<Rec*>(smem + p.pl_slot_off);
+  const uint32_t dummy_word = (uint32_t)p.num_parts + (uint32_t)lane;
+  const uint32_t dummy_slot = ((uint32_t)p.num_parts << cl) + (uint32_t)lane;
+  const uint32_t docbase = (uint32_t)w0 * 64u + (uint32_t)lane;
+  for (int u = 0; u < nvalid; u += 4) {
+    bool h[4];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t doc = docbase + (uint32_t)(u + q) * 64u;
+      bool hh = (u + q < nvalid) & (doc < ndocs);
+      if constexpr (FK == FK_RANGE) hh &= (cursor_value(fcur, u + q) - flo) < flen;
+      if constexpr (FK == FK_DOCRANGE) hh &= (doc - flo) < flen;
+      h[q] = hh;
+      tot += (uint32_t)__popcll(__ballot(hh));
+    }
+    matched += tot;
+    if (tot == 0) continue;
+    uint32_t bk[4], widx[4];
+    Rec rec[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t key = 0;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) key += __umul24(cursor_value(gcur[g], u + q), gstr[g]);  // keys < 2^22
+      const uint32_t vo = HASV ? cursor_value(vcur, u + q) + vadd : 0u;
+      bk[q] = key >> klo;
+      rec[q] = REC64 ? (Rec)(((unsigned long long)(key & kmask) << 32) | vo) : (Rec)(((key & kmask) << vbits) | vo);
+      widx[q] = h[q] ? bk[q] : dummy_word;
+    }
+    uint32_t w[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w[q] = atomicAdd(&words[widx[q]], 1u);
+    bool ovf = false;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t pend = w[q] & 0xffffu, F = (w[q] >> 16) * CH;
+      const bool ok = h[q] & (pend < C);
+      ovf |= h[q] & (pend >= C);
+      slots[ok ? (bk[q] << cl) + ((F + pend) & (C - 1u)) : dummy_slot] = rec[q];
+    }
+    if (__ballot(ovf)) {  // a skewed round filled a ring: those records aggregate into the overflow table
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (h[q] && (w[q] & 0xffffu) >= C) part_overflow<REC64>(p, bk[q], rec[q]);
+    }
+  }
+}
+
+template <int NG, int REC64, int HASV>
+__global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NL = kPrefetchPartition;
+  constexpr int WAVES = kPartWaves;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  SegPtr segs = (SegPtr)p.segs;
+  const PH_CONST Chunk* chunks = (const PH_CONST Chunk*)p.chunks;
+  uint8_t* wst = smem + p.stage_off + (size_t)wave * p.stage_stride;
+  uint32_t* words = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
+  for (int i = threadIdx.x; i < p.num_parts + 64; i += kPartBlock) words[i] = 0;
+  __syncthreads();
+
+  unsigned long long matched = 0;
+  const int32_t tw = p.tile_words;
+  const int32_t round_words = WAVES * tw;
+  const int64_t nch = p.chunk_end - p.chunk_begin;
+  int32_t c = p.chunk_begin + (int32_t)(nch * blockIdx.x / gridDim.x), r = 0;
+  const int32_t c_end = p.chunk_begin + (int32_t)(nch * (blockIdx.x + 1) / gridDim.x);
+  int32_t cbeg = 0, cend = 0;
+  SegPtr S = nullptr;
+  int32_t w0 = 0, nvalid = 0;
+  auto locate = [&]() {
+    if (c < c_end) {
+      cbeg = chunks[c].word_begin;
+      cend = chunks[c].word_end;
+      S = segs + chunks[c].seg;
+      w0 = cbeg + r * round_words + wave * tw;
+      nvalid = min(tw, cend - w0);
+    }
+  };
+  auto advance = [&]() {
+    if (cbeg + (r + 1) * round_words < cend) {
+      ++r;
+    } else {
+      ++c;
+      r = 0;
+    }
+  };
+  Prefetch<NL> pf;
+  locate();
+  if (c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
+  unsigned long long t_stage = 0, t_proc = 0, t_sync = 0, t0 = 0, t1 = 0;
+  const bool stamps = p.dbg != nullptr;
+  while (c < c_end) {
+    if (stamps) t0 = __builtin_readcyclecounter();
+    tile_store<NL>(S, nvalid, wst, lane, pf);
+    // flush the chunks completed in the previous round before this round's prefetch: the stores complete
+    // under the decode instead of stalling the next tile_store (stores count in vmcnt too)
+    part_flush<REC64, kPartBlock>(p, smem, false);
+    lds_barrier();  // ring words are final before anyone appends again
+    SegPtr cs = S;
+    const int32_t cw0 = w0, cnvalid = nvalid;
+    advance();
+    locate();
+    if (c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (stamps) {
+      t1 = __builtin_readcyclecounter();
+      t_stage += t1 - t0;
+      t0 = t1;
+    }
+    if (cnvalid > 0) {
+      const int fk = cs->fkind;
+      if (fk == FK_RANGE) part_tile<NG, REC64, HASV, FK_RANGE>(p, cs, smem, wst, lane, cw0, cnvalid, matched);
+      else if (fk == FK_DOCRANGE) part_tile<NG, REC64, HASV, FK_DOCRANGE>(p, cs, smem, wst, lane, cw0, cnvalid, matched);
+      else part_tile<NG, REC64, HASV, FK_ALL>(p, cs, smem, wst, lane, cw0, cnvalid, matched);
+    }
+    if (stamps) {
+      t1 = __builtin_readcyclecounter();
+      t_proc += t1 - t0;
+      t0 = t1;
+    }
+    lds_barrier();  // this round's appends are complete before the next round's flush
+    if (stamps) t_sync += __builtin_readcyclecounter() - t0;
+  }
+  if (stamps && threadIdx.x == 0) {
+    p.dbg[4 * blockIdx.x + 0] = t_stage;
+    p.dbg[4 * blockIdx.x + 1] = t_proc;
+    p.dbg[4 * blockIdx.x + 2] = t_sync;
+    p.dbg[4 * blockIdx.x + 3] = 1;
+  }
+  lds_barrier();
+  part_flush<REC64, kPartBlock>(p, smem, true);  // also writes the region record counts
+}
+
+template <int NG, int REC64, int HASV>
+static void launch_part_fast(const KParams& p, int grid, size_t lds, hipStream_t s) {
+  allow_lds(k_part_scan<NG, REC64, HASV>, lds);
+  hipLaunchKernelGGL((k_part_scan<NG, REC64, HASV>), dim3(grid), dim3(kPartBlock), lds, s, p);
+}
+
+template <int NG>
+static void launch_part_fast_ng(const KParams& p, int rec64, int grid, size_t lds, hipStream_t s) {
+  const int hasv = p.num_vals > 0;
+  if (rec64) {
+    if (hasv) launch_part_fast<NG, 1, 1>(p, grid, lds, s);
+    else launch_part_fast<NG, 1, 0>(p, grid, lds, s);
+  } else {
+    if (hasv) launch_part_fast<NG, 0, 1>(p, grid, lds, s);
+    else launch_part_fast<NG, 0, 0>(p, grid, lds, s);
+  }
+}
+
+void launch_scan_partition(const KParams& p, int ng, int rec64, int grid, size_t lds, hipStream_t s) {
+  if (!p.part_fast) {
+    launch_mode<MODE_PARTITION>(p, ng, rec64, grid, lds, s);
+    return;
+  }
+  switch (ng) {
+    case 1: launch_part_fast_ng<1>(p, rec64, grid, lds, s); break;
+    case 2: launch_part_fast_ng<2>(p, rec64, grid, lds, s); break;
+    case 3: launch_part_fast_ng<3>(p, rec64, grid, lds, s); break;
+    default: launch_part_fast_ng<4>(p, rec64, grid, lds, s); break;
+  }
+}
+
+// ------------------------------------------------------------------ kernel B: partition aggregation
+// One workgroup per (partition, slice): every record of the slice's regions goes through an LDS table of the
+// partition's keys, then the workgroup merges its key range into the dense result table (one slice: the
+// range has exactly one owner, plain read-modify-write; more slices: coalesced device atomics).  Region fill
+// levels are read once into LDS; each wave keeps 4 regions' 16-byte-per-lane record loads in flight.  Per key
+// the LDS table holds COUNT and the value-offset SUM in one 64-bit word (count << 40 | sum, pack_cs) and
+// MIN / MAX offsets in the two halves of a second 64-bit word.  A record reads that min/max word first and
+// issues an LDS atomic only when it improves one of them: over a key's records in random order that is
+// O(log n) atomics instead of 2 per record (min only falls and max only rises, so a stale read is safe).
+template <int REC64>
+__device__ __forceinline__ void part_agg_record(const PartAggParams& p, unsigned long long r, uint32_t vmask,
+                                                uint32_t* cnt, unsigned long long* cs, unsigned long long* sum,
+                                                uint32_t* mm) {
+  uint32_t k, v;
+  if (REC64) {
+    k = (uint32_t)(r >> 32);
+    v = (uint32_t)r;
+  } else {
+    k = (uint32_t)r >> p.part_vbits;
+    v = (uint32_t)r & vmask;
+  }
+  if (p.pack_cs) {
+    atomicAdd(&cs[k], (1ull << 40) | (unsigned long long)v);
+  } else {
+    atomicAdd(&cnt[k], 1u);
+    if (p.has_sum) atomicAdd(&sum[k], (unsigned long long)v);
+  }
+  if (p.has_min | p.has_max) {
+    const unsigned long long cur = *reinterpret_cast<const unsigned long long*>(mm + 2 * k);  // (max << 32 | min)
+    if (p.has_min && v < (uint32_t)cur) atomicMin(&mm[2 * k], v);
+    if (p.has_max && v > (uint32_t)(cur >> 32)) atomicMax(&mm[2 * k + 1], v);
+  }
+}
+
+template <int REC64>
+__global__ void __launch_bounds__(1024) k_part_agg(const PartAggParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int part = blockIdx.x / p.slices;
+  const int slice = blockIdx.x - part * p.slices;
+  const uint32_t KP = 1u << p.part_klo;
+  const int R = p.regions;
+  // this slice's regions [r0, r1)
+  const int r0 = (int)((int64_t)R * slice / p.slices), r1 = (int)((int64_t)R * (slice + 1) / p.slices);
+  const int NR = r1 - r0;
+  // LDS layout: [count u32 | count<<40|sum u64] [sum u64] [min|max u32 pairs] [region fill u32 x NR]
+  size_t off = 0;
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);
+  unsigned long long* cs = reinterpret_cast<unsigned long long*>(smem);
+  off += p.pack_cs ? 8 * (size_t)KP : 4 * (size_t)KP;
+  off = (off + 7) / 8 * 8;
+  unsigned long long* sum = reinterpret_cast<unsigned long long*>(smem + off);
+  off += (p.has_sum && !p.pack_cs) ? 8 * (size_t)KP : 0;
+  uint32_t* mm = reinterpret_cast<uint32_t*>(smem + off);
+  off += (p.has_min | p.has_max) ? 8 * (size_t)KP : 0;
+  uint32_t* fill = reinterpret_cast<uint32_t*>(smem + off);
+  for (uint32_t k = threadIdx.x; k < KP; k += blockDim.x) {
+    if (p.pack_cs) cs[k] = 0; else cnt[k] = 0;
+    if (p.has_sum && !p.pack_cs) sum[k] = 0;
+    if (p.has_min | p.has_max) {
+      mm[2 * k] = 0xffffffffu;
+      mm[2 * k + 1] = 0u;
+    }
+  }
+  for (int i = threadIdx.x; i < NR; i += blockDim.x) {
+    const uint32_t c = p.part_count[(size_t)part * R + r0 + i];
+    fill[i] = c < (uint32_t)p.part_cap ? c : (uint32_t)p.part_cap;
+  }
+  __syncthreads();
+  const uint32_t vmask = p.part_vbits ? ((p.part_vbits >= 32) ? 0xffffffffu : ((1u << p.part_vbits) - 1u)) : 0u;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nwaves = blockDim.x >> 6;
+  constexpr int RPW = 4;                          // regions per wave per step
+  constexpr int PER = REC64 ? 2 : 4;              // records per 16-byte lane load
+  constexpr uint32_t SPAN = 64 * PER;             // records per wave-load
+  using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
+  const Rec* buf = reinterpret_cast<const Rec*>(p.part_buf);
+  for (int b0 = wave * RPW; b0 < NR; b0 += nwaves * RPW) {
+    uint32_t nn[RPW];
+    uint32_t maxn = 0;
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      nn[q] = (b0 + q < NR) ? fill[b0 + q] : 0u;
+      maxn = nn[q] > maxn ? nn[q] : maxn;
+    }
+    for (uint32_t base = 0; base < maxn; base += SPAN) {
+      u32x4 v[RPW];
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const uint32_t i0 = base + lane * PER;
+        if (i0 < nn[q]) {
+          const Rec* src = buf + ((size_t)part * R + r0 + b0 + q) * (size_t)p.part_cap + i0;
+          v[q] = *reinterpret_cast<const u32x4*>(src);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        const uint32_t i0 = base + lane * PER;
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+          if (i0 + e >= nn[q]) continue;
+          const unsigned long long r = REC64 ? ((unsigned long long)v[q][2 * e + 1] << 32) | v[q][2 * e]
+                                             : (unsigned long long)v[q][e];
+          part_agg_record<REC64>(p, r, vmask, cnt, cs, sum, mm);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const bool shared_range = p.slices > 1;
+  for (uint32_t k = threadIdx.x; k < KP; k += blockDim.x) {
+    uint32_t c;
+    int64_t s = 0;
+    if (p.pack_cs) {
+      const unsigned long long x = cs[k];
+      c = (uint32_t)(x >> 40);
+      s = (int64_t)(x & ((1ull << 40) - 1ull));
+    } else {
+      c = cnt[k];
+      if (p.has_sum) s = (int64_t)sum[k];
+    }
+    if (!c) continue;
+    const int64_t g = ((int64_t)part << p.part_klo) | k;
+    if (g >= p.num_groups) continue;
+    const int64_t vs = s + (int64_t)c * p.part_vbase;
+    const int64_t vmin = p.part_vbase + (int64_t)mm[2 * k], vmax = p.part_vbase + (int64_t)mm[2 * k + 1];
+    if (shared_range) {
+      atomicAdd(&p.out_count[g], (unsigned long long)c);
+      if (p.has_sum) atomicAdd(reinterpret_cast<unsigned long long*>(p.out_sum) + g, (unsigned long long)vs);
+      if (p.has_min) atomicMin(reinterpret_cast<long long*>(p.out_min) + g, (long long)vmin);
+      if (p.has_max) atomicMax(reinterpret_cast<long long*>(p.out_max) + g, (long long)vmax);
+    } else {
+      p.out_count[g] += c;  // this block owns keys [part << klo, (part + 1) << klo)
+      if (p.has_sum) p.out_sum[g] += vs;
+      if (p.has_min && vmin < p.out_min[g]) p.out_min[g] = vmin;
+      if (p.has_max && vmax > p.out_max[g]) p.out_max[g] = vmax;
+    }
+  }
+}
+
+size_t part_agg_lds_bytes(const PartAggParams& p) {
+  const size_t KP = (size_t)1 << p.part_klo;
+  size_t o = p.pack_cs ? 8 * KP : 4 * KP;
+  o = (o + 7) / 8 * 8;
+  o += (p.has_sum && !p.pack_cs) ? 8 * KP : 0;
+  o += (p.has_min | p.has_max) ? 8 * KP : 0;
+  return o + 4 * (size_t)((p.regions + p.slices - 1) / p.slices);
+}
+
+void launch_part_agg(const PartAggParams& p, size_t lds, hipStream_t s) {
+  const dim3 grid((unsigned)(p.num_parts * p.slices));
+  if (p.rec64) {
+    allow_lds(k_part_agg<1>, lds);
+    hipLaunchKernelGGL(k_part_agg<1>, grid, dim3(1024), lds, s, p);
+  } else {
+    allow_lds(k_part_agg<0>, lds);
+    hipLaunchKernelGGL(k_part_agg<0>, grid, dim3(1024), lds, s, p);
+  }
+  PH_HIP_CHECK(hipGetLastError());
+}
+
+__global__ void k_merge_overflow(const MergeParams p) {
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < p.n; g += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long c = p.ovf_count[g];
+    if (!c) continue;
+    p.out_count[g] += c;
+    if (p.out_sum) p.out_sum[g] += p.ovf_sum[g];
+    if (p.out_min && p.ovf_min[g] < p.out_min[g]) p.out_min[g] = p.ovf_min[g];
+    if (p.out_max && p.ovf_max[g] > p.out_max[g]) p.out_max[g] = p.ovf_max[g];
+  }
+}
+
+void launch_merge_overflow(const MergeParams& p, hipStream_t s) {
+  const int grid = (int)std::min<int64_t>((p.n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_merge_overflow, dim3(grid), dim3(256), 0, s, p);
+  PH_HIP_CHECK(hipGetLastError());
+}
+
+
+}  // namespace ph

@@ -39,19 +39,25 @@ void DeviceBuffer::alloc(size_t n, int dev) {
 
 std::unique_ptr<DeviceBuffer> Context::scratch_acquire(size_t n) {
   n = std::max<size_t>(256, (n + 255) / 256 * 256);
-  auto it = scratch_free.lower_bound(n);
-  if (it != scratch_free.end() && it->first <= n + n / 2 + (1 << 20)) {
-    auto b = std::move(it->second);
-    scratch_free_bytes -= it->first;
-    scratch_free.erase(it);
-    return b;
+  {
+    std::lock_guard<std::mutex> lk(scratch_mu);
+    auto it = scratch_free.lower_bound(n);
+    if (it != scratch_free.end() && it->first <= n + n / 2 + (1 << 20)) {
+      auto b = std::move(it->second);
+      scratch_free_bytes -= it->first;
+      scratch_free.erase(it);
+      return b;
+    }
   }
   auto b = std::make_unique<DeviceBuffer>();
   try {
     b->alloc(n, device);
   } catch (const Error&) {
-    scratch_free.clear();  // give cached scratch back to the allocator and retry once
-    scratch_free_bytes = 0;
+    {
+      std::lock_guard<std::mutex> lk(scratch_mu);  // give cached scratch back to the allocator and retry once
+      scratch_free.clear();
+      scratch_free_bytes = 0;
+    }
     b->alloc(n, device);
   }
   return b;
@@ -61,6 +67,7 @@ void Context::scratch_release(std::unique_ptr<DeviceBuffer> b) {
   if (!b || !b->ptr) return;
   constexpr size_t kMaxCached = size_t(32) << 30;  // keep at most 32 GiB of idle scratch per context (of 288)
   if (b->bytes > kMaxCached) return;
+  std::lock_guard<std::mutex> lk(scratch_mu);
   while (scratch_free_bytes + b->bytes > kMaxCached && !scratch_free.empty()) {
     auto it = scratch_free.begin();
     scratch_free_bytes -= it->first;
@@ -71,15 +78,68 @@ void Context::scratch_release(std::unique_ptr<DeviceBuffer> b) {
   scratch_free.emplace(k, std::move(b));
 }
 
-void* Context::host_staging(size_t n) {
-  if (n > pinned_bytes) {
-    if (pinned) PH_HIP_CHECK(hipHostFree(pinned));
-    pinned = nullptr;
+// ------------------------------------------------------------------ execution lanes
+Lane::Lane(int dev) : device(dev) {
+  PH_HIP_CHECK(hipSetDevice(dev));
+  PH_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  PH_HIP_CHECK(hipStreamCreateWithFlags(&stream_b, hipStreamNonBlocking));
+  PH_HIP_CHECK(hipEventCreate(&ev_start));
+  PH_HIP_CHECK(hipEventCreate(&ev_stop));
+}
+
+Lane::~Lane() {
+  (void)hipSetDevice(device);
+  if (stream) (void)hipStreamSynchronize(stream);
+  if (stream_b) (void)hipStreamSynchronize(stream_b);
+  if (ev_start) (void)hipEventDestroy(ev_start);
+  if (ev_stop) (void)hipEventDestroy(ev_stop);
+  for (auto e : ev_pool) (void)hipEventDestroy(e);
+  if (stream) (void)hipStreamDestroy(stream);
+  if (stream_b) (void)hipStreamDestroy(stream_b);
+  if (staging) (void)hipHostFree(staging);
+}
+
+void* Lane::host_staging(size_t n) {
+  if (n > staging_bytes) {
+    if (staging) PH_HIP_CHECK(hipHostFree(staging));
+    staging = nullptr;
     size_t sz = std::max<size_t>(n, 1 << 20);
-    PH_HIP_CHECK(hipHostMalloc(&pinned, sz, hipHostMallocDefault));
-    pinned_bytes = sz;
+    PH_HIP_CHECK(hipHostMalloc(&staging, sz, hipHostMallocDefault));
+    staging_bytes = sz;
   }
-  return pinned;
+  return staging;
+}
+
+hipEvent_t Lane::event(size_t i) {
+  while (ev_pool.size() <= i) {
+    hipEvent_t e;
+    PH_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ev_pool.push_back(e);
+  }
+  return ev_pool[i];
+}
+
+std::unique_ptr<Lane> Context::lane_acquire() {
+  {
+    std::lock_guard<std::mutex> lk(lane_mu);
+    if (!lanes_free.empty()) {
+      auto l = std::move(lanes_free.back());
+      lanes_free.pop_back();
+      return l;
+    }
+  }
+  return std::make_unique<Lane>(device);
+}
+
+void Context::lane_release(std::unique_ptr<Lane> l) {
+  if (!l) return;
+  std::lock_guard<std::mutex> lk(lane_mu);
+  lanes_free.push_back(std::move(l));
+}
+
+Context::~Context() {
+  lanes_free.clear();
+  for (auto& kv : pinned_free) (void)hipHostFree(kv.second);
 }
 
 void* Context::pinned_acquire(size_t n, size_t* cap) {
@@ -320,6 +380,8 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
   if (!desc || desc->num_docs < 0 || desc->num_columns < 0 || (desc->num_columns && !desc->columns))
     fail(PH_ERR_INVALID_ARGUMENT, "bad segment descriptor");
   PH_HIP_CHECK(hipSetDevice(ctx->device));
+  LaneGuard lg(ctx);
+  const hipStream_t st = lg.lane->stream;  // a pin never runs on the caller's external stream
   auto seg = std::make_unique<ph_segment>();
   seg->ctx = ctx;
   seg->name = desc->name ? desc->name : "";
@@ -372,8 +434,8 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
     const size_t fwd_bytes = (size_t)((n * bits + 7) / 8);
     const size_t alloc = ((fwd_bytes + kFwdPadBytes + 255) / 256) * 256;
     col->d_fwd.alloc(alloc, ctx->device);
-    PH_HIP_CHECK(hipMemsetAsync(col->d_fwd.ptr, 0, alloc, ctx->stream));
-    PH_HIP_CHECK(hipMemcpyAsync(col->d_fwd.ptr, src, fwd_bytes, hipMemcpyHostToDevice, ctx->stream));
+    PH_HIP_CHECK(hipMemsetAsync(col->d_fwd.ptr, 0, alloc, st));
+    PH_HIP_CHECK(hipMemcpyAsync(col->d_fwd.ptr, src, fwd_bytes, hipMemcpyHostToDevice, st));
     seg->device_bytes += alloc;
     // dictionary values widened for arithmetic
     if (d.data_type != PH_STRING) {
@@ -381,7 +443,7 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
       const void* vsrc = (d.data_type == PH_INT || d.data_type == PH_LONG) ? (const void*)col->dict.ints.data()
                                                                            : (const void*)col->dict.reals.data();
       PH_HIP_CHECK(hipMemcpyAsync(col->d_values.ptr, vsrc, sizeof(int64_t) * d.cardinality, hipMemcpyHostToDevice,
-                                  ctx->stream));
+                                  st));
       seg->device_bytes += col->d_values.bytes;
     }
     if (d.inverted_index && d.inverted_index_size) {
@@ -390,11 +452,11 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
         fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": inverted index too small");
       col->inverted.assign(inv, inv + d.inverted_index_size);
       col->d_inverted.alloc(d.inverted_index_size, ctx->device);
-      PH_HIP_CHECK(hipMemcpyAsync(col->d_inverted.ptr, inv, d.inverted_index_size, hipMemcpyHostToDevice, ctx->stream));
+      PH_HIP_CHECK(hipMemcpyAsync(col->d_inverted.ptr, inv, d.inverted_index_size, hipMemcpyHostToDevice, st));
       seg->device_bytes += d.inverted_index_size;
     }
     // the caller's buffers may be released after pin returns
-    PH_HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    PH_HIP_CHECK(hipStreamSynchronize(st));
     seg->columns[col->name] = std::move(col);
   }
   seg->id = ctx->next_id++;

@@ -121,21 +121,32 @@ class DistributedQuery:
         self.group = group
 
     def execute(self, q, segments: Sequence, copy: bool = True):
+        """Returns (this rank's finalised key shard or None, (g0, g1), scan statistics of this rank).  The scan
+        statistics come from ph_query_execute_dense (device_ms = this rank's scan kernels); the shard's own
+        statistics describe only the finalisation."""
+        import time
+
         import torch
         dev = torch.device("cuda", self.ctx.device)
         # run the library on torch's current stream so RCCL and the scan are ordered without host syncs
         self.ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         import torch.distributed as dist
         world = dist.get_world_size(self.group) if dist.is_initialized() else 1
+        t0 = time.perf_counter()
         layout = Layout.from_native(self.ctx.dense_layout(q, segments))
         tables = alloc_tables(layout, world, dev)
-        self.ctx.execute_dense(q, segments, [t.data_ptr() for t in tables])
+        scan_stats = self.ctx.execute_dense(q, segments, [t.data_ptr() for t in tables])  # returns after the scan
+        t1 = time.perf_counter()
         shards, g0, g1 = reduce_tables(tables, layout, self.group)
         torch.cuda.current_stream(dev).synchronize()  # the collectives ran on torch's stream
-        if g1 <= g0:
-            return None, (g0, g1)
-        res = self.ctx.dense_finalize(q, segments, [t.data_ptr() for t in shards], g0, g1, copy=copy)
-        return res, (g0, g1)
+        t2 = time.perf_counter()
+        res = None
+        if g1 > g0:
+            res = self.ctx.dense_finalize(q, segments, [t.data_ptr() for t in shards], g0, g1, copy=copy)
+        # host-clock phase times of this rank (ms): plan + scan, cross-GPU reduction, shard finalisation
+        self.last_times = {"scan_ms": (t1 - t0) * 1e3, "reduce_ms": (t2 - t1) * 1e3,
+                           "finalize_ms": (time.perf_counter() - t2) * 1e3}
+        return res, (g0, g1), scan_stats
 
 
 def gather_to_root(res, group=None) -> Optional[list]:

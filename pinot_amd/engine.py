@@ -76,9 +76,10 @@ class IntermediateResult:
 
 
 class _QueryStruct:
-    """Builds the ph_query POD graph and keeps every buffer alive while the call runs."""
+    """Builds the ph_query POD graph and keeps every buffer alive while the call runs.  ``timeoutMs`` (query
+    option) becomes the call's end time; ``interrupt`` is a ctypes.c_int32 another thread may set."""
 
-    def __init__(self, q: QueryContext):
+    def __init__(self, q: QueryContext, interrupt=None):
         self.keep = []
         nodes: List[N.FilterNode] = []
         preds: List[N.Predicate] = []
@@ -124,10 +125,16 @@ class _QueryStruct:
         gb = (ctypes.c_char_p * max(1, len(q.group_by)))(*[s(g) for g in q.group_by])
         aggs = (N.Aggregation * max(1, len(q.aggregations)))(
             *[N.Aggregation(_AGG[a.function], s(a.column) if a.column else None,
-                            a.log2m if a.function == DISTINCTCOUNTHLL else 0) for a in q.aggregations])
+                            a.log2m if a.function == DISTINCTCOUNTHLL else 0,
+                            s(a.column2) if a.column2 else None, N.EXPR_CODES[a.op]) for a in q.aggregations])
         self.keep += [node_arr, pred_arr, gb, aggs]
+        end_ms = 0
+        if "timeoutMs" in q.options:
+            import time
+            end_ms = int(time.time() * 1000) + int(q.options["timeoutMs"])
         self.struct = N.Query(len(nodes), node_arr, root, len(preds), pred_arr, len(q.group_by), gb,
-                              len(q.aggregations), aggs, q.num_groups_limit)
+                              len(q.aggregations), aggs, q.num_groups_limit, end_ms,
+                              ctypes.pointer(interrupt) if interrupt is not None else None)
 
 
 _KEY_DTYPE = {N.PH_INT: np.int32, N.PH_LONG: np.int64, N.PH_FLOAT: np.float32, N.PH_DOUBLE: np.float64}
@@ -185,10 +192,12 @@ class GpuContext:
             width = buf.dtype.itemsize
         N.check(N.lib().ph_table_set_dictionary(self.handle, column.encode(), dt, buf.ctypes.data, len(values), width))
 
-    def execute(self, q: QueryContext, segments: Sequence[PinnedSegment], copy: bool = True) -> IntermediateResult:
+    def execute(self, q: QueryContext, segments: Sequence[PinnedSegment], copy: bool = True,
+                interrupt=None) -> IntermediateResult:
         """copy=False returns zero-copy views of the result's pinned columns; they stay valid while the
-        returned IntermediateResult is alive."""
-        qs = _QueryStruct(q)
+        returned IntermediateResult is alive.  ``interrupt``: optional ctypes.c_int32; setting it non-zero from
+        another thread cancels the call (CancelledError)."""
+        qs = _QueryStruct(q, interrupt)
         segs = (ctypes.c_void_p * max(1, len(segments)))(*[s.handle for s in segments])
         r = ctypes.c_void_p()
         N.check(N.lib().ph_query_execute(self.handle, ctypes.byref(qs.struct), segs, len(segments), ctypes.byref(r)))

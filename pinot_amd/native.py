@@ -17,6 +17,7 @@ PH_ERR_BAD_QUERY = 2
 PH_ERR_UNSUPPORTED = 3
 PH_ERR_DEVICE = 4
 PH_ERR_OUT_OF_MEMORY = 5
+PH_ERR_CANCELLED = 6
 
 PH_INT, PH_LONG, PH_FLOAT, PH_DOUBLE, PH_STRING = range(5)
 DATA_TYPES = {"INT": PH_INT, "LONG": PH_LONG, "FLOAT": PH_FLOAT, "DOUBLE": PH_DOUBLE, "STRING": PH_STRING}
@@ -38,6 +39,10 @@ class BadQueryError(PinotHipError):
 
 class UnsupportedError(PinotHipError):
     """Shape not on the GPU path; the caller falls back to the CPU plan."""
+
+
+class CancelledError(PinotHipError):
+    """Query interrupted or past its end time (QueryException EXECUTION_TIMEOUT / QUERY_CANCELLATION)."""
 
 
 class ColumnDesc(ctypes.Structure):
@@ -66,8 +71,13 @@ class FilterNode(ctypes.Structure):
                 ("children", ctypes.POINTER(ctypes.c_int32)), ("predicate", ctypes.c_int32)]
 
 
+PH_EXPR_NONE, PH_EXPR_MULT, PH_EXPR_SUB, PH_EXPR_ADD = range(4)
+EXPR_CODES = {None: PH_EXPR_NONE, "*": PH_EXPR_MULT, "-": PH_EXPR_SUB, "+": PH_EXPR_ADD}
+
+
 class Aggregation(ctypes.Structure):
-    _fields_ = [("type", ctypes.c_int32), ("column", ctypes.c_char_p), ("log2m", ctypes.c_int32)]
+    _fields_ = [("type", ctypes.c_int32), ("column", ctypes.c_char_p), ("log2m", ctypes.c_int32),
+                ("column2", ctypes.c_char_p), ("expr_op", ctypes.c_int32)]
 
 
 class Query(ctypes.Structure):
@@ -75,7 +85,8 @@ class Query(ctypes.Structure):
                 ("filter_root", ctypes.c_int32), ("num_predicates", ctypes.c_int32),
                 ("predicates", ctypes.POINTER(Predicate)), ("num_group_by", ctypes.c_int32),
                 ("group_by", ctypes.POINTER(ctypes.c_char_p)), ("num_aggregations", ctypes.c_int32),
-                ("aggregations", ctypes.POINTER(Aggregation)), ("num_groups_limit", ctypes.c_int64)]
+                ("aggregations", ctypes.POINTER(Aggregation)), ("num_groups_limit", ctypes.c_int64),
+                ("end_time_ms", ctypes.c_int64), ("interrupt", ctypes.POINTER(ctypes.c_int32))]
 
 
 PH_MAX_DENSE_TABLES = 16
@@ -105,7 +116,7 @@ EXPORTED_SYMBOLS = (
     "ph_result_destroy", "ph_result_stats", "ph_result_num_groups", "ph_result_key_entry_size", "ph_result_key_type",
     "ph_result_group_keys", "ph_result_aggregation", "ph_result_key_data", "ph_result_aggregation_data",
     "ph_query_dense_layout", "ph_query_execute_dense", "ph_dense_finalize", "ph_fixed_bit_pack", "ph_selftest_unpack",
-    "ph_last_error", "ph_version",
+    "ph_selftest_unpack_staged", "ph_last_error", "ph_version",
 )
 
 _lib = None
@@ -165,6 +176,7 @@ def lib():
                                ctypes.POINTER(vp)], ctypes.c_int),
         "ph_fixed_bit_pack": ([vp, i64, i32, vp, ctypes.c_uint64], ctypes.c_int),
         "ph_selftest_unpack": ([vp, vp, ctypes.c_uint64, i64, i32, vp], ctypes.c_int),
+        "ph_selftest_unpack_staged": ([vp, vp, ctypes.c_uint64, i64, i32, i32, vp], ctypes.c_int),
         "ph_last_error": ([], ctypes.c_char_p),
         "ph_version": ([], ctypes.c_char_p),
     }
@@ -184,4 +196,6 @@ def check(code: int):
         raise BadQueryError(code, msg)
     if code == PH_ERR_UNSUPPORTED:
         raise UnsupportedError(code, msg)
+    if code == PH_ERR_CANCELLED:
+        raise CancelledError(code, msg)
     raise PinotHipError(code, msg)

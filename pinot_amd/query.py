@@ -110,14 +110,28 @@ class FilterContext:
 
 
 # --------------------------------------------------------------------------- aggregations
+# 2-operand expressions inside aggregates (SSB Q1.x SUM(lo_extendedprice * lo_discount), Q4.x
+# SUM(lo_revenue - lo_supplycost)): MultiplicationTransformFunction "mult", SubtractionTransformFunction "sub",
+# AdditionTransformFunction "add" (pinot-core/.../operator/transform/function/*.java); the result is DOUBLE and
+# computed per row as double arithmetic (MultiplicationTransformFunction.java:89-104).
+EXPR_OPS = {"*": "mult", "-": "sub", "+": "add"}
+
+
 @dataclass(frozen=True)
 class AggregationSpec:
     function: str           # COUNT | SUM | MIN | MAX | DISTINCTCOUNTHLL
-    column: Optional[str]   # None for COUNT(*)
+    column: Optional[str]   # None for COUNT(*); the first operand of an expression
     log2m: int = DEFAULT_HLL_LOG2M
+    column2: Optional[str] = None  # second operand of `column <op> column2`
+    op: Optional[str] = None       # "*", "-" or "+" (None: plain column)
+
+    def columns(self) -> List[str]:
+        return [c for c in (self.column, self.column2) if c]
 
     def result_name(self) -> str:
         arg = "*" if self.column is None else self.column
+        if self.op:
+            arg = f"{EXPR_OPS[self.op]}({self.column},{self.column2})"
         if self.function == DISTINCTCOUNTHLL and self.log2m != DEFAULT_HLL_LOG2M:
             arg = f"{arg},{self.log2m}"
         return f"{self.function.lower()}({arg})"
@@ -173,7 +187,7 @@ class QueryContext:
 # --------------------------------------------------------------------------- SQL subset parser
 _TOKEN = re.compile(
     r"\s*(?:(?P<num>-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?)|(?P<str>'(?:[^']|'')*')|(?P<id>[A-Za-z_][A-Za-z0-9_.$]*)"
-    r"|(?P<op><>|!=|<=|>=|=|<|>|\(|\)|,|\*|;))")
+    r"|(?P<op><>|!=|<=|>=|=|<|>|\(|\)|,|\*|;|\+|-))")
 
 _KEYWORDS = {"SELECT", "FROM", "WHERE", "GROUP", "BY", "ORDER", "LIMIT", "AND", "OR", "NOT", "IN",
              "BETWEEN", "AS", "ASC", "DESC", "SET", "TOP"}
@@ -245,10 +259,18 @@ class _Parser:
         if t[0] == "id" and n == ("op", "(") and t[1].upper() in SUPPORTED_AGGREGATIONS:
             fn = t[1].upper()
             self.i += 2
+            col2 = op = None
             if self.accept("op", "*"):
                 col = None
             else:
                 col = self.ident()
+                t2 = self.peek()
+                if t2[0] == "op" and t2[1] in EXPR_OPS:
+                    self.i += 1
+                    op = t2[1]
+                    col2 = self.ident()
+                    if fn not in (SUM, MIN, MAX):
+                        raise SqlParseError(f"expressions are supported in SUM/MIN/MAX, not {fn}")
             log2m = DEFAULT_HLL_LOG2M
             if self.accept("op", ","):
                 log2m = int(self.literal())
@@ -257,7 +279,7 @@ class _Parser:
                 raise SqlParseError(f"{fn}(*) not supported")
             if fn == COUNT:
                 col = None
-            return AggregationSpec(fn, col, log2m)
+            return AggregationSpec(fn, col, log2m, col2, op)
         if t[0] == "id" and n == ("op", "("):
             raise SqlParseError(f"unsupported function {t[1]}")
         return None

@@ -103,9 +103,11 @@ def test_distributed_query_world1(ctx):
     os.environ.setdefault("MASTER_PORT", "29517")
     dist.init_process_group("gloo", rank=0, world_size=1)
     try:
-        res, (g0, g1) = DistributedQuery(ctx).execute(q, segs)
+        res, (g0, g1), scan = DistributedQuery(ctx).execute(q, segs)
         assert (g0, g1) == (0, 100_000)
         assert _rows(res) == _rows(ctx.execute(q, segs))
+        # the scan's device time is what bench.py's roofline divides by (it was dropped)
+        assert scan.device_ms > 0
     finally:
         dist.destroy_process_group()
         ctx.set_stream(0)

@@ -154,8 +154,8 @@ def test_every_bit_width_scan(ctx, bits):
 
 @pytest.mark.parametrize("bits", list(range(1, 32)))
 def test_device_unpack_every_width(ctx, bits):
-    # the kernel's unpack routine on raw packed streams of every width 1..31 (FixedBitIntReaderTest widths)
-    import ctypes
+    # the per-doc gather routine (generic filter programs, value re-encoding, HLL reads) on raw packed
+    # streams of every width 1..31 (FixedBitIntReaderTest widths, FixedBitIntReaderTest.java:43-81)
     from pinot_amd import native as N
     rng = np.random.default_rng(1000 + bits)
     for n in (1, 63, 64, 65, 100_003):
@@ -165,6 +165,25 @@ def test_device_unpack_every_width(ctx, bits):
         N.check(N.lib().ph_selftest_unpack(ctx.handle, packed.ctypes.data, packed.nbytes, n, bits,
                                            out.ctypes.data))
         assert np.array_equal(out, ids), (bits, n)
+
+
+@pytest.mark.parametrize("bits", list(range(1, 32)))
+def test_device_staged_unpack_every_width(ctx, bits):
+    # the scan kernels' own staged decode (tile_load -> tile_store -> BitCursor, the code k_scan runs) for every
+    # width 1..31 and every tile size the planner picks, on streams whose length is not a tile multiple
+    from pinot_amd import native as N
+    rng = np.random.default_rng(2000 + bits)
+    for tw in (4, 8, 16, 32):
+        if (tw * 8 * bits + 8 + 1023) // 1024 > 12:  # wider than the prefetch pool: the planner halves the tile
+            continue
+        for n in (1, 64, 64 * tw + 1, 200_003):
+            ids = rng.integers(0, 1 << bits, n, dtype=np.int64).astype(np.int32)
+            ids[:2] = [0, (1 << bits) - 1][: min(2, n)]
+            packed = O.fixed_bit_pack(ids, bits)
+            out = np.full(n, -7, np.int32)
+            N.check(N.lib().ph_selftest_unpack_staged(ctx.handle, packed.ctypes.data, packed.nbytes, n, bits, tw,
+                                                      out.ctypes.data))
+            assert np.array_equal(out, ids), (bits, tw, n)
 
 
 def test_wide_bits_31(ctx):

@@ -1,4 +1,8 @@
 #!/bin/bash
-for w in ${WORKLOADS:-config3 config2}; do
-  PH_DEBUG_STAMPS=1 PH_PART_SERIAL=1 timeout -k 10 300 python3 bench.py --workload $w --steps 2 --warmup 1 --no-cpu 2>&1 | grep -E "stamps|metric" | tail -3 | cut -c1-200
+# Where kernel A's waves spend their cycles (PH_DEBUG_STAMPS, wave 0 of each workgroup): one line per debug-flag
+# setting (flags as tools/gpu_sweep.sh; results invalid when != 0).
+mkdir -p gpurun_out
+for f in ${FLAGS:-0 16 8 6}; do
+  echo "flags=$f $(PH_DEBUG_FLAGS=$f PH_DEBUG_STAMPS=1 PH_PART_SERIAL=1 timeout -k 10 200 python3 bench.py --workload ${W:-config3} \
+    --steps 2 --warmup 1 --no-cpu --no-parity 2>&1 | grep -E "stamps" | tail -1)" | tee -a gpurun_out/stamps.txt || exit 1
 done
