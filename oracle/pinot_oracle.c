@@ -506,6 +506,8 @@ static void run_segment(const or_query* q, const or_segment* s, seg_result* r) {
     }
   }
   r->post_filter = r->docs_scanned * ncols_proj;
+  /* GroupByOperator.java:111: numGroupsLimitReached = getNumGroups() >= numGroupsLimit */
+  if (!no_group && r->ngroups >= q->num_groups_limit) r->limit_reached = 1;
   (void)card_product;
   free(doc_ids);
   free(dict_buf);

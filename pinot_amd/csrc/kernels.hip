@@ -9,13 +9,16 @@ void launch_scan_agg(const KParams& p, int mode, int grid, size_t lds, hipStream
 void launch_scan_group_lds(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);
 void launch_scan_group_global(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);
 void launch_scan_partition(const KParams& p, int ng, int rec64, int grid, size_t lds, hipStream_t s);
+void launch_scan_group_hash(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);
 
 void launch_scan(const KParams& p, int mode, int ng, int rec64, int grid, size_t lds, hipStream_t s) {
+  PH_HIP_CHECK(hipGetLastError());  // a failure left by an earlier unchecked call is reported as such, not as ours
   switch (mode) {
     case MODE_COUNT:
     case MODE_AGG: launch_scan_agg(p, mode, grid, lds, s); break;
     case MODE_GROUP_LDS: launch_scan_group_lds(p, ng, grid, lds, s); break;
     case MODE_GROUP_GLOBAL: launch_scan_group_global(p, ng, grid, lds, s); break;
+    case MODE_GROUP_HASH: launch_scan_group_hash(p, ng, grid, lds, s); break;
     default: launch_scan_partition(p, ng, rec64, grid, lds, s); break;
   }
   PH_HIP_CHECK(hipGetLastError());
@@ -48,6 +51,7 @@ void launch_encode_values(const uint32_t* fwd, int32_t bits, const int64_t* tabl
   const int64_t nwords = (n * vbits + 31) / 32;
   if (nwords <= 0) return;
   const int grid = (int)std::min<int64_t>((nwords + 255) / 256, 8192);
+  PH_HIP_CHECK(hipGetLastError());  // a failure left by an earlier unchecked call is reported as such, not as ours
   hipLaunchKernelGGL(k_encode_values, dim3(grid), dim3(256), 0, s, fwd, bits, table, base, vbits, n, out, nwords);
   PH_HIP_CHECK(hipGetLastError());
 }
@@ -145,7 +149,8 @@ __global__ void __launch_bounds__(256) k_compact_write(const CompactParams p) {
       }
       for (int j = 0; j < kMaxGroupCols; ++j) {
         if (j >= p.num_keys) continue;
-        const int64_t id = ((g + p.key_base) / p.key_stride[j]) % p.key_size[j];
+        const int64_t kid = p.hkeys ? (int64_t)p.hkeys[g] : g + p.key_base;
+        const int64_t id = (kid / p.key_stride[j]) % p.key_size[j];
         switch (p.key_type[j]) {
           case PH_INT:
             reinterpret_cast<int32_t*>(p.key_out[j])[r] = (int32_t)reinterpret_cast<const int64_t*>(p.key_table[j])[id];
@@ -174,6 +179,111 @@ void launch_compact(const CompactParams& p, hipStream_t s) {
   hipLaunchKernelGGL(k_compact_count, dim3(nblk), dim3(256), 0, s, p);
   hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(1024), 0, s, p, nblk);
   hipLaunchKernelGGL(k_compact_write, dim3(nblk), dim3(256), 0, s, p);
+  PH_HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------ numGroupsLimit (first-seen keys)
+// DictionaryBasedGroupKeyGenerator hands out group ids in first-seen doc order and drops the docs of every key
+// that arrives after numGroupsLimit ids were taken (IntGroupIdMap.getGroupId, :992-1017; INVALID_ID rows are
+// ignored by the result holders).  Given first[g] = the first matching doc of key g in one segment (UINT32_MAX:
+// absent), the kept keys are exactly the `limit` keys with the smallest first docs: distinct keys have distinct
+// first docs, so the keys kept are those whose first doc is below the doc of the limit-th set bit of the
+// first-doc bitmap.
+__global__ void __launch_bounds__(256) k_limit_mark(const uint32_t* __restrict__ first, int64_t G,
+                                                    uint32_t* __restrict__ docbits, unsigned long long* distinct) {
+  unsigned long long d = 0;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < G; g += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t f = first[g];
+    if (f != 0xffffffffu) {
+      ++d;
+      atomicOr(&docbits[f >> 5], 1u << (f & 31u));
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+  if ((threadIdx.x & 63) == 0 && d) atomicAdd(distinct, d);
+}
+
+// one workgroup: threshold = (doc of the limit-th set bit) + 1, or UINT32_MAX when distinct <= limit
+__global__ void __launch_bounds__(1024) k_limit_threshold(const uint32_t* __restrict__ docbits, int64_t nwords,
+                                                          int64_t limit, const unsigned long long* distinct,
+                                                          uint32_t* threshold, unsigned long long* reached) {
+  __shared__ unsigned long long wsum[1024];
+  __shared__ uint32_t found;
+  const int t = threadIdx.x;
+  const unsigned long long D = *distinct;
+  if (t == 0) {
+    found = 0xffffffffu;
+    if ((int64_t)D >= limit) *reached = 1;  // GroupByOperator: numGroups >= numGroupsLimit
+  }
+  if ((int64_t)D <= limit) {
+    if (t == 0) *threshold = 0xffffffffu;
+    return;
+  }
+  const int64_t per = (nwords + 1023) / 1024, w0 = t * per, w1 = min(nwords, w0 + per);
+  unsigned long long c = 0;
+  for (int64_t w = w0; w < w1; ++w) c += __popc(docbits[w]);
+  wsum[t] = c;
+  __syncthreads();
+  if (t == 0) {  // exclusive prefix (1024 entries, once per segment)
+    unsigned long long acc = 0;
+    for (int i = 0; i < 1024; ++i) {
+      const unsigned long long x = wsum[i];
+      wsum[i] = acc;
+      acc += x;
+    }
+  }
+  __syncthreads();
+  // the thread whose range holds the limit-th bit (1-based rank `limit`) walks its words
+  const unsigned long long before = wsum[t];
+  if (before < (unsigned long long)limit && before + c >= (unsigned long long)limit) {
+    unsigned long long need = (unsigned long long)limit - before;  // >= 1
+    for (int64_t w = w0; w < w1; ++w) {
+      uint32_t bits = docbits[w];
+      const uint32_t pc = __popc(bits);
+      if (need > pc) {
+        need -= pc;
+        continue;
+      }
+      for (;;) {
+        const uint32_t b = __ffs(bits) - 1;
+        if (--need == 0) {
+          found = (uint32_t)(w * 32 + b) + 1u;
+          break;
+        }
+        bits &= bits - 1;
+      }
+      break;
+    }
+  }
+  __syncthreads();
+  if (t == 0) *threshold = found;
+}
+
+// keep bit g  <=>  key g is present and its first doc is below the threshold
+__global__ void __launch_bounds__(256) k_limit_keep(const uint32_t* __restrict__ first, int64_t G,
+                                                    const uint32_t* threshold, uint32_t* __restrict__ keep) {
+  const uint32_t T = *threshold;
+  const int64_t nw = (G + 31) / 32;
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t bits = 0;
+    for (int i = 0; i < 32; ++i) {
+      const int64_t g = w * 32 + i;
+      if (g < G && first[g] < T) bits |= 1u << i;
+    }
+    keep[w] = bits;
+  }
+}
+
+void launch_limit_select(const uint32_t* first, int64_t G, int64_t limit, int32_t num_docs, uint32_t* docbits,
+                         uint32_t* keep, unsigned long long* scal, hipStream_t s) {
+  // scal: [0] distinct keys (zeroed by the caller), [1] threshold (u32), [2] limit reached flag (shared)
+  const int grid = (int)std::min<int64_t>((G + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_limit_mark, dim3(grid), dim3(256), 0, s, first, G, docbits, scal);
+  hipLaunchKernelGGL(k_limit_threshold, dim3(1), dim3(1024), 0, s, docbits, (int64_t)((num_docs + 31) / 32), limit,
+                     scal, reinterpret_cast<uint32_t*>(scal + 1), scal + 2);
+  const int grid2 = (int)std::min<int64_t>(((G + 31) / 32 + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_limit_keep, dim3(grid2), dim3(256), 0, s, first, G, reinterpret_cast<const uint32_t*>(scal + 1),
+                     keep);
   PH_HIP_CHECK(hipGetLastError());
 }
 

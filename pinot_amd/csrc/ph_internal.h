@@ -113,11 +113,11 @@ constexpr int kInterruptChunks = 8192;               // an interruptible scan ch
 // 16-byte-per-lane loads (1 KiB per wave-instruction) a wave keeps in flight per tile, over all streams
 constexpr int kPrefetchCount = 8;                    // MODE_COUNT: one stream
 constexpr int kPrefetchOther = 12;
-constexpr int kPrefetchPartition = 12;               // MODE_PARTITION prefetch pool (tile_words 16 needs 9 loads at 10+10+10+16 bits)
+constexpr int kPrefetchPartition = 6;                // MODE_PARTITION prefetch pool (r2: 8-word tiles need 5 loads at 10+10+10+20 bits; 12 cost 24 VGPRs)
 constexpr int stage_loads(int tile_words, int bits) { return (tile_words * 8 * bits + 8 + 1023) / 1024; }
-// staged span of one stream: 16-byte front pad (the decode reads dword j-1 and j) + whole 1 KiB pieces (every
-// lane of a piece stores its 16 bytes, those past the tile's bytes included, so the staging has no exec branches)
-constexpr int stage_stream_bytes(int tile_words, int bits) { return 16 + 1024 * stage_loads(tile_words, bits); }
+// staged span of one stream: 16-byte front pad (the decode reads dword j-1 and j) + the tile's bytes.  (r2: staging
+// whole 1 KiB pieces without exec branches measured slower -- config2 0.49 -> 0.55 ms -- from the extra LDS writes.)
+constexpr int stage_stream_bytes(int tile_words, int bits) { return 16 + (tile_words * 8 * bits + 8 + 15) / 16 * 16; }
 struct DevStream {
   const uint32_t* fwd;
   int32_t bits;
@@ -145,6 +145,7 @@ struct DevSegment {
   int32_t prog_len;
   int32_t pad;
   const uint32_t* fptr;  // FK_SET bitset over dictIds ; FK_BITMAP doc bitmap
+  const uint32_t* keep;  // numGroupsLimit: bitset over global keys this segment may aggregate (nullptr: all)
   DevColumn cols[kMaxCols];
   DevValCol vals[kMaxVals];
   DevValCol vals2[kMaxVals];       // second operand of a 2-operand expression term (KParams::val_op)
@@ -161,7 +162,16 @@ struct Chunk {
 
 enum : int32_t { AGG_COUNT = 0, AGG_SUM = 1, AGG_MIN = 2, AGG_MAX = 3, AGG_HLL = 4 };
 
-enum : int32_t { MODE_COUNT = 0, MODE_AGG = 1, MODE_GROUP_LDS = 2, MODE_GROUP_GLOBAL = 3, MODE_PARTITION = 4 };
+enum : int32_t {
+  MODE_COUNT = 0,
+  MODE_AGG = 1,
+  MODE_GROUP_LDS = 2,
+  MODE_GROUP_GLOBAL = 3,
+  MODE_PARTITION = 4,
+  MODE_GROUP_HASH = 5,  // key spaces beyond the dense budget: global open-addressing table keyed by the raw key
+};
+constexpr double kDenseTableBudget = 32e9;  // HBM bytes of dense (or hash) group tables one query may allocate
+constexpr unsigned long long kHashEmpty = ~0ull;  // empty slot of the MODE_GROUP_HASH key table
 
 constexpr int kPartUnroll = 4;     // 64-doc words per step of the partition append loop (independent LDS chains)
 constexpr int kPartSlots = 2048;    // LDS record slots per workgroup (partition p owns slots [p*C, (p+1)*C)); swept r1: small
@@ -210,6 +220,10 @@ struct KParams {
   int32_t hll_slot[kMaxHll];      // column slot of each HLL register set
   int32_t lds_hll_off;
   unsigned long long* out_count;  // [num_groups] matched docs per group
+  unsigned long long* matched_total;  // group-by plans: matched docs of the launch (numDocsScanned), or nullptr
+  uint32_t* first_doc;            // numGroupsLimit pass: [num_groups] first matching doc per key (atomicMin)
+  unsigned long long* hkeys;      // MODE_GROUP_HASH: [num_groups] slot keys (kHashEmpty = free); out_* by slot
+  int64_t hmask;                  // MODE_GROUP_HASH: slots - 1 (a power of two >= 2x the distinct keys possible)
   uint32_t* out_hll;              // [num_groups][num_hll][2^log2m]
   // MODE_PARTITION (kernel A) -- records to per-partition buffers
   int32_t part_klo;               // key bits kept in a record (keys per partition = 1 << part_klo)
@@ -443,6 +457,9 @@ struct RoaringContainer {
 void launch_roaring_or(const RoaringContainer* c, int n, const uint8_t* base, uint32_t* bitmap, int32_t num_docs,
                        hipStream_t s);
 void launch_selftest_unpack(const uint32_t* fwd, int64_t n, int bits, int32_t* out, hipStream_t s);
+// numGroupsLimit: from one segment's first-doc-per-key table, the bitset of the keys the reference keeps
+void launch_limit_select(const uint32_t* first, int64_t G, int64_t limit, int32_t num_docs, uint32_t* docbits,
+                         uint32_t* keep, unsigned long long* scal, hipStream_t s);
 void launch_selftest_staged(const DevSegment* seg, int32_t tile_words, int32_t stage_stride, int64_t n, int32_t* out,
                             hipStream_t s);
 // the 1 KiB wave-loads of a full tile of every staged stream of `d` (stage offsets per stream)
@@ -467,6 +484,7 @@ struct CompactParams {
   void* key_out[kMaxGroupCols];
   int64_t* count_out;
   int64_t key_base;          // group id of element 0 (finalizing one key shard of a dense table)
+  const unsigned long long* hkeys;  // MODE_GROUP_HASH: slot -> raw key (the key of row g is hkeys[g])
   unsigned long long* blk;   // [kCompactBlocks + 2] counts -> offsets, total at [kCompactBlocks], matched docs
                              // (sum of the group counts = numDocsScanned) at [kCompactBlocks + 1], zeroed by the host
   int32_t* flags;            // bit 0: an integer SUM reached 2^53

@@ -867,19 +867,27 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     gdicts.push_back(gd);
     const int64_t sz = std::max<int64_t>(1, gd->dict.size);
-    if (num_groups > (int64_t(1) << 40) / sz) fail(PH_ERR_UNSUPPORTED, "group key space too large");
+    // mixed-radix keys stay below 2^62 (int64 and never the hash table's empty marker)
+    if (num_groups > (int64_t(1) << 62) / sz) fail(PH_ERR_UNSUPPORTED, "group key space too large");
     num_groups *= sz;
   }
-  // numGroupsLimit: segments whose key space exceeds the limit may drop groups in the reference
-  // (first-seen order, IntGroupIdMap.getGroupId :992-1017); that emulation is not on the GPU path.
-  if (q->num_group_by > 0) {
-    const int64_t limit = q->num_groups_limit > 0 ? q->num_groups_limit : 100000;
-    for (auto* s : segs) {
+  // numGroupsLimit (per segment): a segment whose product of group-by cardinalities reaches the limit may hit it;
+  // such segments get a first-seen pass before the scan (DictionaryBasedGroupKeyGenerator keeps the first
+  // `limit` keys in doc order and drops the rest, IntGroupIdMap.getGroupId :992-1017; GroupByOperator.java:111
+  // reports numGroups >= limit)
+  const int64_t group_limit = q->num_groups_limit > 0 ? q->num_groups_limit : 100000;
+  std::vector<char> seg_limit(nseg, 0);
+  bool any_limit = false;
+  if (q->num_group_by > 0 && dop != DENSE_LAYOUT && !fin) {
+    for (int i = 0; i < nseg; ++i) {
+      if (!seg_live[i]) continue;
+      // a segment holds at most min(product of cardinalities, docs) distinct keys
       int64_t pp = 1;
-      for (auto& g : group_cols) pp = std::min<int64_t>(pp * s->columns.at(g)->cardinality, int64_t(1) << 40);
-      if (pp > limit)
-        fail(PH_ERR_UNSUPPORTED, "segment " + s->name + ": product of group-by cardinalities " + std::to_string(pp) +
-                                     " exceeds numGroupsLimit " + std::to_string(limit));
+      for (auto& g : group_cols) {
+        const int64_t c = std::max<int64_t>(1, segs[i]->columns.at(g)->cardinality);
+        pp = pp > (int64_t(1) << 40) / c ? int64_t(1) << 40 : pp * c;
+      }
+      if (std::min<int64_t>(pp, segs[i]->num_docs) >= group_limit) seg_limit[i] = any_limit = true;
     }
   }
   const int64_t G = num_groups;
@@ -972,7 +980,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
 
   int mode = -3;  // DENSE_FINALIZE: no scan
   float dev_ms = 0.f;
-  const int64_t hll_words = G * num_hll * (m ? m : 1);
+  int64_t TR = G;  // rows of the output tables: the key space, or the slots of the MODE_GROUP_HASH table
+  unsigned long long* hkeys = nullptr;
   if (fin) {
     // the tables hold the (already reduced) key shard [g0, g1): layout order of ph_query_dense_layout
     int t = 0;
@@ -996,7 +1005,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     lds_tables = (size_t)num_hll * (m ? m : 1) * 4 + 16;
   } else {
     kp.lds_cnt_off = 0;
-    size_t off = ((size_t)G * 4 + 15) / 16 * 16;
+    size_t off = G < (int64_t(1) << 24) ? ((size_t)G * 4 + 15) / 16 * 16 : SIZE_MAX / 2;
     for (int j = 0; j < nvals; ++j) {
       auto place = [&](int32_t& o) {
         o = (int32_t)std::min<size_t>(off, INT32_MAX);
@@ -1011,16 +1020,37 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     off += (size_t)G * num_hll * (m ? m : 1) * 4;
     const bool part_ok = num_hll == 0 && nvals <= 1 && (nvals == 0 || (val_is_int[0] && !val_exprs[0] && vmax >= vmin &&
                                                                        (uint64_t)(vmax - vmin) < (1ull << 32))) &&
-                         G <= ((int64_t)kPartMaxParts << kPartKeysLog2) && getenv("PH_DISABLE_PARTITION") == nullptr;
+                         G <= ((int64_t)kPartMaxParts << kPartKeysLog2) && !any_limit &&
+                         getenv("PH_DISABLE_PARTITION") == nullptr;
     if (off <= 64 * 1024) {
       mode = MODE_GROUP_LDS;
       lds_tables = off;
     } else if (part_ok && G >= 65536) {
       mode = MODE_PARTITION;
     } else {
-      mode = MODE_GROUP_GLOBAL;
-      const double bytes = (double)G * (8 + 8.0 * 3 * nvals + 4.0 * num_hll * (m ? m : 1));
-      if (bytes > 32e9) fail(PH_ERR_UNSUPPORTED, "dense group table too large for HBM budget");
+      int nout = 1;  // 8-byte tables per group
+      for (int j = 0; j < nvals; ++j) nout += __builtin_popcount(val_ops[j] & 7);
+      const double bytes = (double)G * (8.0 * nout + 4.0 * num_hll * (m ? m : 1));
+      if (bytes <= kDenseTableBudget) {
+        mode = MODE_GROUP_GLOBAL;
+      } else {
+        // key space beyond the dense budget: open-addressing table over the keys that can occur -- at most one
+        // per scanned doc -- with >= 2x slots (DictionaryBasedGroupKeyGenerator's map-based holders, :598/:778)
+        if (num_hll) fail(PH_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL group-by over a key space beyond the dense budget");
+        if (dop) fail(PH_ERR_UNSUPPORTED, "dense partials over a key space beyond the dense budget");
+        if (any_limit) fail(PH_ERR_UNSUPPORTED, "numGroupsLimit over a key space beyond the dense budget");
+        int64_t live_docs = 0;
+        for (int i = 0; i < nseg; ++i)
+          if (seg_live[i]) live_docs += segs[i]->num_docs;
+        int64_t H = 1024;
+        while (H < 2 * std::min<int64_t>(G, live_docs)) H <<= 1;
+        if ((double)H * (8.0 * nout + 8.0) > kDenseTableBudget)
+          fail(PH_ERR_UNSUPPORTED, "group-by hash table too large for HBM budget");
+        mode = MODE_GROUP_HASH;
+        TR = H;
+        kp.num_groups = H;
+        kp.hmask = H - 1;
+      }
     }
   }
 
@@ -1030,22 +1060,28 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     return scratch.alloc<uint8_t>(bytes);
   };
   int tix = 0;
-  kp.out_count = reinterpret_cast<unsigned long long*>(out_table(tix, 8 * (size_t)G));
-  PH_HIP_CHECK(hipMemsetAsync(kp.out_count, 0, sizeof(unsigned long long) * G, st));
+  kp.out_count = reinterpret_cast<unsigned long long*>(out_table(tix, 8 * (size_t)TR));
+  PH_HIP_CHECK(hipMemsetAsync(kp.out_count, 0, sizeof(unsigned long long) * TR, st));
   for (int j = 0; j < nvals; ++j) {
     if (val_ops[j] & 1) {
-      kp.out_sum[j] = out_table(tix, 8 * (size_t)G);
-      PH_HIP_CHECK(hipMemsetAsync(kp.out_sum[j], 0, 8 * G, st));
+      kp.out_sum[j] = out_table(tix, 8 * (size_t)TR);
+      PH_HIP_CHECK(hipMemsetAsync(kp.out_sum[j], 0, 8 * TR, st));
     }
     if (val_ops[j] & 2) {
-      kp.out_min[j] = reinterpret_cast<int64_t*>(out_table(tix, 8 * (size_t)G));
-      launch_fill_i64(kp.out_min[j], INT64_MAX, G, st);
+      kp.out_min[j] = reinterpret_cast<int64_t*>(out_table(tix, 8 * (size_t)TR));
+      launch_fill_i64(kp.out_min[j], INT64_MAX, TR, st);
     }
     if (val_ops[j] & 4) {
-      kp.out_max[j] = reinterpret_cast<int64_t*>(out_table(tix, 8 * (size_t)G));
-      launch_fill_i64(kp.out_max[j], INT64_MIN, G, st);
+      kp.out_max[j] = reinterpret_cast<int64_t*>(out_table(tix, 8 * (size_t)TR));
+      launch_fill_i64(kp.out_max[j], INT64_MIN, TR, st);
     }
   }
+  if (mode == MODE_GROUP_HASH) {
+    hkeys = scratch.alloc<unsigned long long>(TR);
+    PH_HIP_CHECK(hipMemsetAsync(hkeys, 0xFF, 8 * TR, st));  // kHashEmpty
+    kp.hkeys = hkeys;
+  }
+  const int64_t hll_words = TR * num_hll * (m ? m : 1);
   if (num_hll) {
     kp.out_hll = reinterpret_cast<uint32_t*>(out_table(tix, 4 * (size_t)hll_words));
     PH_HIP_CHECK(hipMemsetAsync(kp.out_hll, 0, 4 * hll_words, st));
@@ -1059,6 +1095,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<std::pair<size_t, int>> bitmap_fix;                     // global insn index -> bitmap leaf
   std::vector<std::pair<size_t, std::vector<uint32_t>>> fset_fix;     // segment index -> FK_SET bitset
   std::vector<std::pair<size_t, int>> fbitmap_fix;                    // segment index -> bitmap leaf
+  std::vector<std::pair<int32_t, int32_t>> dseg_chunks;                // device segment -> its chunk range
+  std::vector<int> dseg_src;                                           // device segment -> query segment index
   for (int i = 0; i < nseg; ++i) {
     if (!seg_live[i]) continue;
     ph_segment* s = segs[i];
@@ -1141,8 +1179,11 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
     }
     const int32_t words = (s->num_docs + 63) / 64;
+    dseg_chunks.push_back({(int32_t)chunks.size(), 0});
     for (int32_t w = 0; w < words; w += kChunkWords)
       chunks.push_back({(int32_t)si, w, std::min(words, w + kChunkWords), 0});
+    dseg_chunks.back().second = (int32_t)chunks.size();
+    dseg_src.push_back(i);
     dsegs.push_back(d);
     stats.num_segments_matched++;
   }
@@ -1180,6 +1221,24 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     for (int j = 0; j < nvals; ++j) g |= d.vals[j].kind != VK_PACKED || (val_exprs[j] && d.vals2[j].kind != VK_PACKED);
     if (g && mode != MODE_COUNT) kp.late_prefetch = 1;
     if (g && mode == MODE_COUNT && d.fkind != FK_RANGE && d.fkind != FK_ALL && d.fkind != FK_DOCRANGE) kp.late_prefetch = 1;
+  }
+  // numGroupsLimit: every segment that may reach the limit gets a keep bitset over the global keys (filled by
+  // the first-seen pass below, read by the scan: a gather, so the late prefetch)
+  std::vector<int> limit_segs;
+  unsigned long long* limit_scal = nullptr;  // [3] per limit segment: distinct, threshold, reached
+  if (any_limit && q->num_group_by > 0) {
+    for (size_t k = 0; k < dsegs.size(); ++k)
+      if (seg_limit[dseg_src[k]]) limit_segs.push_back((int)k);
+    const double keep_bytes = (double)limit_segs.size() * (double)((G + 31) / 32) * 4.0;
+    if (keep_bytes > 8e9) fail(PH_ERR_UNSUPPORTED, "numGroupsLimit emulation needs too many key bitsets");
+    for (int k : limit_segs) dsegs[k].keep = scratch.alloc<uint32_t>((size_t)(G + 31) / 32);
+    limit_scal = scratch.alloc<unsigned long long>(3 * limit_segs.size());
+    PH_HIP_CHECK(hipMemsetAsync(limit_scal, 0, 24 * limit_segs.size(), st));
+    if (!limit_segs.empty()) kp.late_prefetch = 1;
+  }
+  if (q->num_group_by > 0) {
+    kp.matched_total = scratch.alloc<unsigned long long>(1);
+    PH_HIP_CHECK(hipMemsetAsync(kp.matched_total, 0, 8, st));
   }
   // per-segment tile pieces: the 1 KiB wave-loads of a full tile, stream by stream
   for (auto& d : dsegs) fill_tile_pieces(d, kp.nstage, kp.stage_soff, kp.tile_words);
@@ -1247,9 +1306,34 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       int blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1)));
       if (mode == MODE_GROUP_LDS) blocks_per_cu = std::min(blocks_per_cu, 4);
       const int grid = (int)std::min<int64_t>((int64_t)chunks.size(), (int64_t)ctx->num_cus * blocks_per_cu);
+      if (!limit_segs.empty()) {
+        // first-seen pass per limit segment (MODE_GROUP_GLOBAL records each key's first matching doc), then the
+        // kept keys; stream-ordered, so one first-doc table and one doc bitmap serve every segment in turn
+        int32_t maxdocs = 0;
+        for (int k : limit_segs) maxdocs = std::max(maxdocs, dsegs[k].num_docs);
+        uint32_t* first = scratch.alloc<uint32_t>((size_t)G);
+        uint32_t* docbits = scratch.alloc<uint32_t>((size_t)maxdocs / 32 + 2);
+        KParams k1 = kp;
+        k1.matched_total = nullptr;
+        k1.late_prefetch = 1;
+        const size_t lds1 = (size_t)kWaves * kp.stage_stride + 16;
+        for (size_t t = 0; t < limit_segs.size(); ++t) {
+          const int k = limit_segs[t];
+          PH_HIP_CHECK(hipMemsetAsync(first, 0xff, 4 * (size_t)G, st));
+          PH_HIP_CHECK(hipMemsetAsync(docbits, 0, 4 * ((size_t)dsegs[k].num_docs / 32 + 2), st));
+          k1.first_doc = first;
+          k1.chunk_begin = dseg_chunks[k].first;
+          k1.chunk_end = dseg_chunks[k].second;
+          const int g1 = std::min<int>(k1.chunk_end - k1.chunk_begin, ctx->num_cus * 4);
+          if (g1 > 0) launch_scan(k1, MODE_GROUP_GLOBAL, q->num_group_by, 0, g1, lds1, st);
+          launch_limit_select(first, G, group_limit, dsegs[k].num_docs, docbits, const_cast<uint32_t*>(dsegs[k].keep),
+                              limit_scal + 3 * t, st);
+        }
+      }
       // an interruptible call scans in batches of kInterruptChunks chunks and checks between them
       const int32_t nchunks = (int32_t)chunks.size();
-      const int32_t step = interruptible ? kInterruptChunks : nchunks;
+      int32_t step = interruptible ? kInterruptChunks : nchunks;
+      if (const char* e = getenv("PH_INTERRUPT_CHUNKS")) if (interruptible) step = std::max(1, atoi(e));  // tests
       PH_HIP_CHECK(hipEventRecord(lane.lane->ev_start, st));
       for (int32_t cb = 0; cb < nchunks; cb += step) {
         kp.chunk_begin = cb;
@@ -1421,10 +1505,19 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   stats.device_ms = dev_ms;
   res->mode = mode;
   stats.plan_mode = mode;
+  if (kp.matched_total) {
+    // group-by: numDocsScanned = matched docs (docs of keys beyond numGroupsLimit included,
+    // GroupByOperator.java:106-107) and numGroupsLimitReached of any segment
+    std::vector<unsigned long long> sc(1 + 3 * limit_segs.size());
+    PH_HIP_CHECK(hipMemcpyAsync(sc.data(), kp.matched_total, 8, hipMemcpyDeviceToHost, st));
+    if (!limit_segs.empty())
+      PH_HIP_CHECK(hipMemcpyAsync(sc.data() + 1, limit_scal, 24 * limit_segs.size(), hipMemcpyDeviceToHost, st));
+    PH_HIP_CHECK(hipStreamSynchronize(st));
+    stats.num_docs_scanned = (int64_t)sc[0];
+    for (size_t t = 0; t < limit_segs.size(); ++t) stats.num_groups_limit_reached |= sc[1 + 3 * t + 2] != 0;
+  }
   if (dop == DENSE_EXECUTE) {
-    // partial tables stay on the device for the cross-GPU reduction; matched docs are counted when a key
-    // shard is finalised
-    stats.num_docs_scanned = -1;
+    // partial tables stay on the device for the cross-GPU reduction
     stats.host_ms = std::chrono::duration<double, std::milli>(clock::now() - t0).count() - dev_ms;
     return res.release();
   }
@@ -1432,7 +1525,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
 
   // ---- results (DENSE_FINALIZE: only the key shard [RB, RB + RG) of the tables)
   const int64_t RB = fin ? dn->g0 : 0;
-  const int64_t RG = fin ? dn->g1 - dn->g0 : G;
+  const int64_t RG = fin ? dn->g1 - dn->g0 : TR;
   const int64_t rhll_words = RG * num_hll * (m ? m : 1);
   const int ncols_proj = (int)projected.size();
   auto finish_value = [&](int k, int64_t raw, int64_t cnt_for_default, bool is_sum) -> double {
@@ -1512,6 +1605,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     cp.count_out = scratch.alloc<int64_t>(RG);
     cp.key_base = RB;
+    cp.hkeys = hkeys;
     cp.blk = scratch.alloc<unsigned long long>(kCompactBlocks + 2);
     PH_HIP_CHECK(hipMemsetAsync(cp.blk + kCompactBlocks + 1, 0, 8, st));
     launch_compact(cp, st);
@@ -1550,7 +1644,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
     }
     PH_HIP_CHECK(hipStreamSynchronize(st));
-    stats.num_docs_scanned = docs;  // sum of the group counts, reduced on the device by k_compact_count
+    // a finalised key shard has no scan: its matched docs are the sum of its group counts (k_compact_count)
+    if (fin) stats.num_docs_scanned = docs;
     for (int k = 0; k < nagg; ++k) {
       if (q->aggregations[k].type != PH_AGG_SUM || !val_is_int[agg_val[k]]) continue;
       if (!fin && sum_bounded[agg_val[k]]) continue;
@@ -1576,11 +1671,13 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     std::vector<unsigned long long> cnt(RG);
     PH_HIP_CHECK(hipMemcpy(cnt.data(), kp.out_count, 8 * RG, hipMemcpyDeviceToHost));
     std::vector<int64_t> live;
+    int64_t docs = 0;
     for (int64_t g = 0; g < RG; ++g)
       if (cnt[g]) {
         live.push_back(g);
-        stats.num_docs_scanned += (int64_t)cnt[g];
+        docs += (int64_t)cnt[g];
       }
+    if (fin) stats.num_docs_scanned = docs;
     const int64_t R = (int64_t)live.size();
     res->num_groups = R;
     init_row_results(R);

@@ -186,9 +186,6 @@ struct Prefetch {
   u32x4 r[NL];
 };
 
-// No exec branches: a lane whose 16 bytes lie past the bytes the tile needs re-loads the tile's first 16 bytes
-// (a line this wave reads anyway, never past the stream) and stores whatever it loaded into the staging area,
-// which holds whole pieces (stage_stream_bytes).
 template <int NL>
 __device__ __forceinline__ void tile_load(SegPtr S, int32_t w0, int32_t nvalid, int lane, Prefetch<NL>& pf) {
   if (nvalid <= 0) return;
@@ -197,11 +194,10 @@ __device__ __forceinline__ void tile_load(SegPtr S, int32_t w0, int32_t nvalid, 
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
     if (k < np) {
+      const uint8_t* fwd = S->pieces[k].fwd;
       const int32_t stride = S->pieces[k].stride, off = S->pieces[k].off;
-      const uint8_t* tile = S->pieces[k].fwd - off + (size_t)w0 * stride;  // wave-uniform
       // bytes of this stream the tile needs (+8: the decode reads the dword after the last value)
-      const bool need = off + lane * 16 < nvalid * stride + 8;
-      pf.r[k] = gld16a8(tile + (need ? off + lane * 16 : 0));
+      if (off + lane * 16 < nvalid * stride + 8) pf.r[k] = gld16a8(fwd + (size_t)w0 * stride + lane * 16);
     }
   }
 }
@@ -212,17 +208,22 @@ __device__ __forceinline__ void tile_store(SegPtr S, int32_t nvalid, uint8_t* ws
     const int np = S->npieces;
 #pragma unroll
     for (int k = 0; k < NL; ++k) {
-      if (k < np) {
+      const int32_t stride = S->pieces[k].stride, off = S->pieces[k].off, lds = S->pieces[k].lds;
+      if (k < np && off + lane * 16 < nvalid * stride + 8) {
         // byte-swap once here (the stream is big-endian) so the decode is one funnel shift per value
         u32x4 v = pf.r[k];
         v.x = __builtin_bswap32(v.x);
         v.y = __builtin_bswap32(v.y);
         v.z = __builtin_bswap32(v.z);
         v.w = __builtin_bswap32(v.w);
-        *reinterpret_cast<u32x4*>(wst + S->pieces[k].lds + lane * 16) = v;
+        *reinterpret_cast<u32x4*>(wst + lds + lane * 16) = v;
       }
     }
   }
+  // every load of this tile has been consumed; saying so explicitly keeps the waitcnt pass from
+  // assuming a predicated-off load into the pool is still pending (it would then put vmcnt(0) before
+  // each load of the next prefetch, serialising it)
+  __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
 }
 
 // Per-lane decode cursor over a staged (byte-swapped) stream.  Doc `lane` of 64-doc word u ends at bit
@@ -355,6 +356,8 @@ struct NumLoads {
 // Value columns the register state is sized for.  REC64 means 64-bit partition records in MODE_PARTITION; in
 // every other mode it selects the single-value-column variant, so a one-column query does not carry the
 // accumulators and cursors of kMaxVals columns (r1: 158 VGPRs / 3 waves per SIMD in MODE_AGG otherwise).
+// 2-operand expression terms run on the kMaxVals variant only (their second cursor costs the one-column
+// variant ~15 VGPRs: 90 -> 105 in r2).
 template <int MODE, int REC64>
 struct ValCap {
   // MODE_PARTITION is only planned for <= 1 value column (query.cpp part_ok)
@@ -406,7 +409,7 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
     vkind[j] = S->vals[j].kind;
     vbase[j] = S->vals[j].base;
     vtab[j] = S->vals[j].table;
-    if (MODE != MODE_PARTITION && p.val_op[j]) {
+    if (MODE != MODE_PARTITION && VC > 1 && p.val_op[j]) {  // expressions: the kMaxVals variant only
       vcur2[j] = bit_cursor(wst + p.stage_soff[p.v2_stream[j]], S->streams[p.v2_stream[j]].bits, lane);
       vkind2[j] = S->vals2[j].kind;
       vbase2[j] = S->vals2[j].base;
@@ -452,7 +455,7 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
         if (j < p.num_vals) {
           if (LATE) read_value(vkind[j], vbase[j], vtab[j], cursor_value(vcur[j], u), vi[j], vd[j]);
           else vi[j] = vbase[j] + (int64_t)cursor_value(vcur[j], u);  // VK_PACKED: no gather
-          const int eop = p.val_op[j];
+          const int eop = VC > 1 ? p.val_op[j] : 0;
           if (eop) {
             // `a <op> b` per row: exact int64 for integer terms, else double like the reference's
             // transformToDoubleValuesSV (MultiplicationTransformFunction.java:89-104)
@@ -482,9 +485,38 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
       return;
     } else {
       if (!hit) return;
-      const int64_t g = key;
+      int64_t g = key;
+      if constexpr (MODE == MODE_GROUP_HASH) {
+        // LongMapBasedHolder / ArrayMapBasedHolder regime (DictionaryBasedGroupKeyGenerator.java:598,778):
+        // linear probing on the raw mixed-radix key; the table has >= 2x the slots of the keys it can receive,
+        // so the probe always ends (bounded anyway)
+        unsigned long long h = (unsigned long long)key;
+        h ^= h >> 33;
+        h *= 0xff51afd7ed558ccdull;
+        h ^= h >> 33;
+        h *= 0xc4ceb9fe1a85ec53ull;
+        h ^= h >> 33;
+        int64_t slot = (int64_t)(h & (unsigned long long)p.hmask);
+        for (int64_t probe = 0; probe <= p.hmask; ++probe) {
+          // plain read first: a key already placed costs no atomic (the common case once the table warms up)
+          unsigned long long old = __hip_atomic_load(&p.hkeys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (old == (unsigned long long)key) break;
+          if (old == kHashEmpty) {
+            old = atomicCAS(&p.hkeys[slot], kHashEmpty, (unsigned long long)key);
+            if (old == kHashEmpty || old == (unsigned long long)key) break;
+          }
+          slot = (slot + 1) & p.hmask;
+        }
+        g = slot;
+      }
+      if (MODE == MODE_GROUP_GLOBAL && LATE && p.first_doc) {  // numGroupsLimit pass: first doc of every key
+        atomicMin(&p.first_doc[g], doc);
+        return;
+      }
+      if (MODE != MODE_GROUP_HASH && LATE && S->keep && !((gld(S->keep + (g >> 5)) >> (g & 31)) & 1u))
+        return;  // beyond numGroupsLimit
       if (MODE == MODE_GROUP_LDS) atomicAdd(&lds_cnt[g], 1u);
-      else if (MODE == MODE_GROUP_GLOBAL) atomicAdd(&p.out_count[g], 1ull);
+      else if (MODE == MODE_GROUP_GLOBAL || MODE == MODE_GROUP_HASH) atomicAdd(&p.out_count[g], 1ull);
 #pragma unroll
       for (int j = 0; j < VC; ++j) {
         if (j >= p.num_vals) continue;
@@ -756,6 +788,7 @@ __global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : kBlock) 
 
   // ---- workgroup epilogue
   if (MODE == MODE_PARTITION) {
+    if (lane == 0 && acc.matched && p.matched_total) atomicAdd(p.matched_total, acc.matched);
     lds_barrier();
     part_flush<REC64, BLOCK>(p, smem, true);  // also writes the region record counts
     return;
@@ -837,6 +870,7 @@ __global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : kBlock) 
   __syncthreads();
   if (threadIdx.x == 0 && s_matched && (MODE == MODE_COUNT || MODE == MODE_AGG))
     atomicAdd(&p.out_count[0], s_matched);
+  if (threadIdx.x == 0 && s_matched && p.matched_total) atomicAdd(p.matched_total, s_matched);
 }
 
 template <class K>

@@ -194,6 +194,7 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
     p.dbg[4 * blockIdx.x + 2] = t_sync;
     p.dbg[4 * blockIdx.x + 3] = 1;
   }
+  if (lane == 0 && matched && p.matched_total) atomicAdd(p.matched_total, matched);
   lds_barrier();
   part_flush<REC64, kPartBlock>(p, smem, true);  // also writes the region record counts
 }

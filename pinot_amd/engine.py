@@ -141,14 +141,20 @@ _KEY_DTYPE = {N.PH_INT: np.int32, N.PH_LONG: np.int64, N.PH_FLOAT: np.float32, N
 
 
 class _ResultHandle:
-    """Owns a ph_result; destroyed when the last IntermediateResult referencing it goes away."""
+    """Owns a ph_result; destroyed when the last IntermediateResult referencing it goes away, or by
+    GpuContext.close (a result must not outlive its context: it returns pinned blocks to the context's pool)."""
 
     def __init__(self, r):
         self.r = r
 
+    def destroy(self):
+        if self.r is not None:
+            N.lib().ph_result_destroy(self.r)
+            self.r = None
+
     def __del__(self):
         try:
-            N.lib().ph_result_destroy(self.r)
+            self.destroy()
         except Exception:
             pass
 
@@ -157,13 +163,21 @@ class GpuContext:
     """One context per GPU (ph_ctx)."""
 
     def __init__(self, device: int = 0):
+        import weakref
         h = ctypes.c_void_p()
         N.check(N.lib().ph_ctx_create(device, ctypes.byref(h)))
         self.handle = h
         self.device = device
+        # segments and results of this context: released before it (ph_ctx_destroy contract)
+        self._segments = weakref.WeakSet()
+        self._results = weakref.WeakSet()
 
     def close(self):
         if self.handle:
+            for r in list(self._results):
+                r.destroy()
+            for seg in list(self._segments):
+                seg.unpin()
             N.lib().ph_ctx_destroy(self.handle)
             self.handle = None
 
@@ -177,7 +191,9 @@ class GpuContext:
         N.check(N.lib().ph_ctx_set_stream(self.handle, ctypes.c_void_p(stream_ptr)))
 
     def pin(self, buffers: SegmentBuffers) -> PinnedSegment:
-        return PinnedSegment(self, buffers)
+        seg = PinnedSegment(self, buffers)
+        self._segments.add(seg)
+        return seg
 
     def set_table_dictionary(self, column: str, data_type: str, values: np.ndarray):
         dt = N.DATA_TYPES[data_type]
@@ -202,6 +218,7 @@ class GpuContext:
         r = ctypes.c_void_p()
         N.check(N.lib().ph_query_execute(self.handle, ctypes.byref(qs.struct), segs, len(segments), ctypes.byref(r)))
         handle = _ResultHandle(r)
+        self._results.add(handle)
         res = self._read_result(q, r, copy)
         if not copy:
             res._handle = handle
@@ -274,6 +291,7 @@ class GpuContext:
         N.check(N.lib().ph_dense_finalize(self.handle, ctypes.byref(qs.struct), segs, len(segments), tabs,
                                           group_begin, group_end, ctypes.byref(r)))
         handle = _ResultHandle(r)
+        self._results.add(handle)
         res = self._read_result(q, r, copy)
         if not copy:
             res._handle = handle

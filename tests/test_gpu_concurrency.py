@@ -100,11 +100,12 @@ def test_interrupt_before_and_deadline(setup):
     assert reduce_groups(q, r.keys, r.aggs).rows == expected[QUERIES[0]]
 
 
-def test_interrupt_during_long_scan(setup):
-    # a ~1.3G-doc scan (the same segments many times over) in batches: a thread sets the flag shortly after
-    # the call starts; the call must return CancelledError well before it could have finished
+def test_interrupt_during_long_scan(setup, monkeypatch):
+    # an interruptible scan checks between batches; with one chunk (16384 docs) per batch (PH_INTERRUPT_CHUNKS)
+    # a ~1.3G-doc scan takes seconds, so a flag set 50 ms after the start lands mid-scan
     import time
     ctx, gpu, _ = setup
+    monkeypatch.setenv("PH_INTERRUPT_CHUNKS", "1")
     flag = ctypes.c_int32(0)
     big = gpu * 2600
     q = parse_sql("SELECT COUNT(*), SUM(m) FROM t WHERE f BETWEEN 10 AND 900")

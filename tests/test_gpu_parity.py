@@ -258,13 +258,68 @@ def test_large_group_key_space_global_table(ctx):
                        "WHERE f BETWEEN 0 AND 499 GROUP BY g1, g2 ORDER BY g1, g2 LIMIT 2000000")
 
 
-def test_group_limit_unsupported_is_reported(ctx):
-    from pinot_amd.native import UnsupportedError
-    rng = np.random.default_rng(13)
-    t = {"g": (rng.integers(0, 5000, 10000).astype(np.int32), "INT")}
-    seg = ctx.pin(create_segment("x", t))
-    with pytest.raises(UnsupportedError):
-        ctx.execute(parse_sql("SET numGroupsLimit=100; SELECT g, COUNT(*) FROM t GROUP BY g"), [seg])
+@pytest.mark.parametrize("where", ["", " WHERE f < 300"])
+def test_hash_group_by_beyond_dense_budget(ctx, where):
+    # 3 columns of ~12 000 values each: a ~1.7e12 key space, far beyond any dense table -> MODE_GROUP_HASH
+    # (open addressing over the raw mixed-radix key, sized by the docs that can match; the map-based holders
+    # of DictionaryBasedGroupKeyGenerator.java:598/:778).  Segments hold fewer docs than numGroupsLimit, so the
+    # limit can never be reached and no group is dropped.
+    rng = np.random.default_rng(31)
+    tables = []
+    for n in (300_000, 123_457):
+        t = {c: (rng.integers(0, 12_000, n).astype(np.int32) * 3 + k, "INT") for k, c in enumerate(("g1", "g2", "g3"))}
+        t["m"] = (rng.integers(-1 << 20, 1 << 30, n).astype(np.int32), "INT")
+        t["f"] = (rng.integers(0, 1000, n).astype(np.int32), "INT")
+        # a few hot keys so that slots see repeated hits
+        t["g1"][0][: n // 10] = 5
+        t["g2"][0][: n // 10] = 7
+        t["g3"][0][: n // 10] = 11
+        tables.append(t)
+    sql = (f"SET numGroupsLimit=10000000; SELECT g1, g2, g3, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where} "
+           f"GROUP BY g1, g2, g3 ORDER BY g1, g2, g3 LIMIT 10000000")
+    r, got = _both(ctx, tables, sql)
+    assert r.stats.mode == 5  # MODE_GROUP_HASH
+    assert not r.stats.num_groups_limit_reached
+    assert len(got.rows) > 300_000
+
+
+@pytest.mark.parametrize("case", ["few", "many", "exact", "filtered", "three_cols"])
+def test_num_groups_limit_first_seen(ctx, case):
+    # DictionaryBasedGroupKeyGenerator keeps the first numGroupsLimit keys of each segment in doc order and drops
+    # the docs of later keys (IntGroupIdMap.getGroupId :992-1017); numGroupsLimitReached = numGroups >= limit
+    # (GroupByOperator.java:111).  Default limit 100 000, 2-column keys with a 1M cardinality product.
+    rng = np.random.default_rng(hash(case) % 2**32)
+    tables = []
+    for n in (400_000, 250_003):
+        if case == "few":  # 1 000 real groups (g2 follows g1) although the cardinality product is 1M
+            g1 = rng.integers(0, 1000, n)
+            g2 = (g1 * 7) % 1000
+        else:
+            g1 = rng.integers(0, 1000, n)
+            g2 = rng.integers(0, 1000, n)
+        t = {"g1": (g1.astype(np.int32), "INT"), "g2": (g2.astype(np.int32), "INT"),
+             "m": (rng.integers(-1000, 1 << 20, n).astype(np.int32), "INT"),
+             "f": (rng.integers(0, 100, n).astype(np.int32), "INT")}
+        if case == "three_cols":
+            t["g3"] = (rng.integers(0, 7, n).astype(np.int32), "INT")
+        tables.append(t)
+    # every value present in every segment, so dictionaries (and their cardinality products) are complete
+    for t in tables:
+        for c in ("g1", "g2"):
+            v = t[c][0]
+            v[:1000] = np.arange(1000) if c == "g1" or case != "few" else (np.arange(1000) * 7) % 1000
+    limit = {"exact": 2500, "few": None, "many": None, "filtered": 30_000, "three_cols": 50_000}[case]
+    opt = f"SET numGroupsLimit={limit}; " if limit else ""
+    where = " WHERE f < 40" if case == "filtered" else ""
+    cols = "g1, g2, g3" if case == "three_cols" else "g1, g2"
+    sql = (f"{opt}SELECT {cols}, COUNT(*), SUM(m), MAX(m) FROM t{where} GROUP BY {cols} ORDER BY {cols} "
+           f"LIMIT 2000000")
+    q = parse_sql(sql)
+    r, _ = _both(ctx, tables, sql)
+    e = O.execute(q, [O.build_segment(f"s{i}", t) for i, t in enumerate(tables)])
+    assert r.stats.num_groups_limit_reached == e.stats.num_groups_limit_reached
+    if case in ("many", "filtered", "three_cols"):
+        assert r.stats.num_groups_limit_reached
 
 
 def test_bad_query_is_reported(ctx, sv):
