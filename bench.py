@@ -181,6 +181,7 @@ def main():
     # table-level dictionaries: identical on every rank, so dense group ids line up for the RCCL merge
     for g in q.group_by:
         ctx.set_table_dictionary(g, "INT", np.arange(cols[g][0], dtype=np.int32))
+    ctx.set_schema({c: "INT" for c in cols})  # a rank without segments still builds the common dense layout
 
     runner = DistributedQuery(ctx)
     last = {}

@@ -173,6 +173,8 @@ int ph_ctx_set_stream(ph_ctx* ctx, void* hip_stream);
 /* ------------------------------------------------------------------ segments */
 int ph_segment_pin(ph_ctx* ctx, const ph_segment_desc* desc, ph_segment** out);
 int ph_segment_unpin(ph_segment* seg);
+/* HBM held for the segment: its pinned columns plus the per-column caches queries derived from them
+ * (re-encoded value streams, HLL hash tables, dictId remaps to table-level dictionaries). */
 int64_t ph_segment_device_bytes(const ph_segment* seg);
 int32_t ph_segment_num_docs(const ph_segment* seg);
 
@@ -180,6 +182,12 @@ int32_t ph_segment_num_docs(const ph_segment* seg);
  * Optional: without it the union of the queried segments' dictionaries is used. */
 int ph_table_set_dictionary(ph_ctx* ctx, const char* column, int32_t data_type, const void* values, int64_t count,
                             int32_t entry_size);
+
+/* Table schema type of a column (Schema / FieldSpec.getDataType, pinot-spi Schema.java).  Value columns take
+ * their type from the queried segments; a call that queries no segment holding the column (an empty rank of a
+ * multi-GPU query) takes it from here, so every rank builds the same dense layout.  A dense call that needs a
+ * value column's type and has neither fails with PH_ERR_INVALID_ARGUMENT. */
+int ph_table_set_column_type(ph_ctx* ctx, const char* column, int32_t data_type);
 
 /* ------------------------------------------------------------------ queries */
 int ph_query_execute(ph_ctx* ctx, const ph_query* query, ph_segment* const* segments, int32_t num_segments,

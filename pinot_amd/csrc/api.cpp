@@ -97,11 +97,55 @@ int ph_segment_unpin(ph_segment* seg) {
   return guarded([&] {
     if (!seg) return;
     (void)hipSetDevice(seg->ctx->device);
+    ph::Context& c = *seg->ctx;
+    {
+      // the segment's remaps to table / union dictionaries, and the unions that include it (never hit again:
+      // a re-pinned segment gets a new id)
+      std::lock_guard<std::mutex> lk(c.mu);
+      for (auto& kv : c.table_dicts) {
+        std::lock_guard<std::mutex> gl(kv.second->mu);
+        kv.second->remaps.erase(seg->id);
+      }
+      const std::string tag = std::to_string(seg->id) + ",";
+      auto holds = [&](const std::string& key) {
+        const size_t h = key.find('#');
+        for (size_t p = key.find(tag, h); p != std::string::npos; p = key.find(tag, p + 1))
+          if (key[p - 1] == '#' || key[p - 1] == ',') return true;
+        return false;
+      };
+      for (auto it = c.union_order.begin(); it != c.union_order.end();) {
+        if (holds(*it)) {
+          c.union_cache.erase(*it);
+          it = c.union_order.erase(it);
+        } else {
+          ++it;
+        }
+      }
+    }
     delete seg;  // hipFree waits for work in flight on the buffers
   });
 }
 
-int64_t ph_segment_device_bytes(const ph_segment* seg) { return seg ? seg->device_bytes : -1; }
+int64_t ph_segment_device_bytes(const ph_segment* seg) {
+  if (!seg) return -1;
+  int64_t n = seg->device_bytes;  // pinned columns, plus the caches queries built for them
+  for (auto& kv : seg->columns) {
+    ph::Column& c = *kv.second;
+    std::lock_guard<std::mutex> lk(c.cache_mu);
+    for (auto& h : c.hll_tables) n += h.second.buf ? (int64_t)h.second.buf->bytes : 0;
+    if (c.d_vpacked) n += (int64_t)c.d_vpacked->bytes;
+  }
+  ph::Context& c = *seg->ctx;  // remaps to table / union dictionaries
+  std::lock_guard<std::mutex> lk(c.mu);
+  auto add = [&](ph::GlobalDict& g) {
+    std::lock_guard<std::mutex> gl(g.mu);
+    auto it = g.remaps.find(seg->id);
+    if (it != g.remaps.end() && it->second) n += (int64_t)it->second->bytes;
+  };
+  for (auto& kv : c.table_dicts) add(*kv.second);
+  for (auto& kv : c.union_cache) add(*kv.second);
+  return n;
+}
 int32_t ph_segment_num_docs(const ph_segment* seg) { return seg ? seg->num_docs : -1; }
 
 int ph_table_set_dictionary(ph_ctx* ctx, const char* column, int32_t data_type, const void* values, int64_t count,
@@ -145,6 +189,15 @@ int ph_table_set_dictionary(ph_ctx* ctx, const char* column, int32_t data_type, 
     g->id = ctx->c.next_id++;
     std::lock_guard<std::mutex> lk(ctx->c.mu);
     ctx->c.table_dicts[column] = g;
+  });
+}
+
+int ph_table_set_column_type(ph_ctx* ctx, const char* column, int32_t data_type) {
+  return guarded([&] {
+    if (!ctx || !column) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
+    if (data_type < PH_INT || data_type > PH_STRING) fail(PH_ERR_INVALID_ARGUMENT, "data type");
+    std::lock_guard<std::mutex> lk(ctx->c.mu);
+    ctx->c.column_types[column] = data_type;
   });
 }
 

@@ -15,6 +15,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -170,6 +171,7 @@ enum : int32_t {
   MODE_PARTITION = 4,
   MODE_GROUP_HASH = 5,  // key spaces beyond the dense budget: global open-addressing table keyed by the raw key
 };
+constexpr size_t kUnionCacheEntries = 64;  // segment-set dictionary unions kept per context
 constexpr double kDenseTableBudget = 32e9;  // HBM bytes of dense (or hash) group tables one query may allocate
 constexpr unsigned long long kHashEmpty = ~0ull;  // empty slot of the MODE_GROUP_HASH key table
 
@@ -340,7 +342,6 @@ struct Column {
   std::unique_ptr<DeviceBuffer> d_vpacked;
   int64_t vbase = 0;
   int32_t vbits = 0;
-  std::map<uint64_t, std::shared_ptr<DeviceBuffer>> remaps;          // by global dictionary id
   bool has_inverted() const { return !inverted.empty(); }
 };
 
@@ -364,6 +365,9 @@ struct GlobalDict {
   Dictionary dict;
   std::mutex mu;
   std::unique_ptr<DeviceBuffer> d_values;  // int64 (INT/LONG) or float64 (FLOAT/DOUBLE) values, on demand
+  // dictId -> id remaps of the segments grouped over this dictionary, by segment id (nullptr = identity); they
+  // live and die with the dictionary, and ph_segment_unpin drops a segment's entries (guarded by mu)
+  std::map<uint64_t, std::shared_ptr<DeviceBuffer>> remaps;
 };
 
 // One execution lane = what a single call needs exclusively: a stream (and a second one for the partitioned
@@ -390,7 +394,9 @@ struct Context {
   std::atomic<hipStream_t> ext_stream{nullptr};  // ph_ctx_set_stream: run calls on the caller's stream
   std::mutex mu;  // guards table_dicts and union_cache (held only around their lookups / inserts)
   std::map<std::string, std::shared_ptr<GlobalDict>> table_dicts;   // ph_table_set_dictionary
+  std::map<std::string, int32_t> column_types;                      // ph_table_set_column_type (schema)
   std::map<std::string, std::shared_ptr<GlobalDict>> union_cache;   // column + segment-set -> union
+  std::deque<std::string> union_order;                              // union_cache keys, oldest first
   std::atomic<uint64_t> next_id{1};
   // execution lanes
   std::mutex lane_mu;

@@ -116,13 +116,14 @@ DictIdSet evaluate_predicate(const ph_predicate& p, const Column& c) {
     case PH_PRED_RANGE: {
       const std::string lo = lit(p.lower), hi = lit(p.upper);
       int64_t start, end;
-      if (lo == "*" || lo.empty()) {
+      // only "*" (RangePredicate.UNBOUNDED) or a missing bound is open: '' is a real (smallest) STRING literal
+      if (!p.lower || lo == "*") {
         start = 0;
       } else {
         int64_t ii = d.insertion_index_of(lo);
         start = ii < 0 ? -(ii + 1) : (p.lower_inclusive ? ii : ii + 1);
       }
-      if (hi == "*" || hi.empty()) {
+      if (!p.upper || hi == "*") {
         end = card;
       } else {
         int64_t ii = d.insertion_index_of(hi);
@@ -441,10 +442,10 @@ std::shared_ptr<GlobalDict> build_union(Context* ctx, const std::string& col, co
 }
 
 // dictId -> global id; nullptr when identity
-const int32_t* segment_remap(Context* ctx, Column& c, const GlobalDict& g) {
-  std::lock_guard<std::mutex> lk(c.cache_mu);
-  auto it = c.remaps.find(g.id);
-  if (it != c.remaps.end()) return it->second ? it->second->as<int32_t>() : nullptr;
+const int32_t* segment_remap(Context* ctx, const ph_segment& s, const Column& c, GlobalDict& g) {
+  std::lock_guard<std::mutex> lk(g.mu);
+  auto it = g.remaps.find(s.id);
+  if (it != g.remaps.end()) return it->second ? it->second->as<int32_t>() : nullptr;
   std::vector<int32_t> map(c.cardinality);
   bool identity = c.cardinality == g.dict.size;
   int64_t j = 0;
@@ -461,7 +462,7 @@ const int32_t* segment_remap(Context* ctx, Column& c, const GlobalDict& g) {
     buf->alloc(sizeof(int32_t) * map.size(), ctx->device);
     PH_HIP_CHECK(hipMemcpy(buf->ptr, map.data(), sizeof(int32_t) * map.size(), hipMemcpyHostToDevice));
   }
-  c.remaps[g.id] = buf;
+  g.remaps[s.id] = buf;
   return buf ? buf->as<int32_t>() : nullptr;
 }
 
@@ -750,6 +751,16 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           amax[o] = std::max(amax[o], std::fabs((double)c.dict.ints.back()));
         }
       }
+      if (col_int < 0) {  // no queried segment holds it: the schema type (ph_table_set_column_type)
+        std::lock_guard<std::mutex> dlk(ctx->mu);
+        auto ct = ctx->column_types.find(cn);
+        if (ct != ctx->column_types.end()) {
+          if (ct->second == PH_STRING) fail(PH_ERR_UNSUPPORTED, "numeric aggregation on STRING column " + cn);
+          col_int = ct->second == PH_INT || ct->second == PH_LONG;
+        } else if (dop) {
+          fail(PH_ERR_INVALID_ARGUMENT, "dense call without segments needs ph_table_set_column_type for " + cn);
+        }
+      }
       is_int &= col_int != 0;
     }
     double bound = amax[0];
@@ -861,8 +872,13 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         gd = ct->second;
       } else {
         gd = build_union(ctx, g, segs);
-        if (ctx->union_cache.size() > 256) ctx->union_cache.clear();
+        // bounded FIFO of unions; an evicted union's per-segment remaps go with it (segment_remap purges them)
+        while (ctx->union_cache.size() >= kUnionCacheEntries) {
+          ctx->union_cache.erase(ctx->union_order.front());
+          ctx->union_order.pop_front();
+        }
         ctx->union_cache[key] = gd;
+        ctx->union_order.push_back(key);
       }
     }
     gdicts.push_back(gd);
@@ -1144,7 +1160,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       dc.values = c.d_values.ptr;
     }
     for (int g = 0; g < q->num_group_by; ++g)
-      d.cols[kp.group_slot[g]].remap = segment_remap(ctx, *s->columns.at(group_cols[g]), *gdicts[g]);
+      d.cols[kp.group_slot[g]].remap = segment_remap(ctx, *s, *s->columns.at(group_cols[g]), *gdicts[g]);
     for (int h = 0; h < num_hll; ++h)
       d.cols[kp.hll_slot[h]].hll = segment_hll_table(ctx, *s->columns.at(hll_cols[h]), log2m, st);
     for (int j = 0; j < nvals; ++j) {
@@ -1267,6 +1283,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     lds = stage_bytes + lds_tables;
     kp.pl_misc_off = 0;
+    // 160 KiB of LDS per CU (gfx950); HLL registers of a large log2m do not fit beside the staging areas
+    if (lds > 160 * 1024) fail(PH_ERR_UNSUPPORTED, "aggregation state exceeds the LDS of one CU (HLL log2m too large)");
   }
   for (auto& pf : payload_fix) {
     uint32_t* dp = scratch.alloc<uint32_t>(pf.second.size() + 1);

@@ -195,6 +195,14 @@ class GpuContext:
         self._segments.add(seg)
         return seg
 
+    def set_column_type(self, column: str, data_type: str):
+        """Schema type of a column (ph_table_set_column_type): what a rank without segments uses for value columns."""
+        N.check(N.lib().ph_table_set_column_type(self.handle, column.encode(), N.DATA_TYPES[data_type]))
+
+    def set_schema(self, schema: dict):
+        for column, data_type in schema.items():
+            self.set_column_type(column, data_type)
+
     def set_table_dictionary(self, column: str, data_type: str, values: np.ndarray):
         dt = N.DATA_TYPES[data_type]
         if data_type == "STRING":

@@ -112,7 +112,7 @@ class ExecStats(ctypes.Structure):
 # every symbol declared in include/pinot_hip.h
 EXPORTED_SYMBOLS = (
     "ph_ctx_create", "ph_ctx_destroy", "ph_ctx_set_stream", "ph_segment_pin", "ph_segment_unpin",
-    "ph_segment_device_bytes", "ph_segment_num_docs", "ph_table_set_dictionary", "ph_query_execute",
+    "ph_segment_device_bytes", "ph_segment_num_docs", "ph_table_set_dictionary", "ph_table_set_column_type", "ph_query_execute",
     "ph_result_destroy", "ph_result_stats", "ph_result_num_groups", "ph_result_key_entry_size", "ph_result_key_type",
     "ph_result_group_keys", "ph_result_aggregation", "ph_result_key_data", "ph_result_aggregation_data",
     "ph_query_dense_layout", "ph_query_execute_dense", "ph_dense_finalize", "ph_fixed_bit_pack", "ph_selftest_unpack",
@@ -158,6 +158,7 @@ def lib():
         "ph_segment_device_bytes": ([vp], i64),
         "ph_segment_num_docs": ([vp], i32),
         "ph_table_set_dictionary": ([vp, ctypes.c_char_p, i32, vp, i64, i32], ctypes.c_int),
+        "ph_table_set_column_type": ([vp, ctypes.c_char_p, i32], ctypes.c_int),
         "ph_query_execute": ([vp, ctypes.POINTER(Query), ctypes.POINTER(vp), i32, ctypes.POINTER(vp)], ctypes.c_int),
         "ph_result_destroy": ([vp], ctypes.c_int),
         "ph_result_stats": ([vp, ctypes.POINTER(ExecStats)], ctypes.c_int),

@@ -92,6 +92,28 @@ def test_dense_matches_execute(ctx, sql, mode):
         _assert_rows_match(sorted(rows), _rows(ref), world)
 
 
+def test_empty_rank_layout_follows_schema(ctx):
+    # a rank holding no segment must build the same dense layout as the others: DOUBLE SUM reduces as f64 and
+    # MIN/MAX finalise as doubles (the value type defaulted to integer on an empty rank)
+    from pinot_amd import native as N
+    from pinot_amd.distributed import Layout, alloc_tables
+    import torch
+    segs = _segs(ctx, 6)
+    q = parse_sql("SELECT a, COUNT(*), SUM(d), MIN(d), MAX(m) FROM t GROUP BY a")
+    full = Layout.from_native(ctx.dense_layout(q, segs))
+    with pytest.raises(N.PinotHipError):
+        ctx.dense_layout(parse_sql("SELECT a, SUM(zz) FROM t GROUP BY a"), [])
+    ctx.set_schema({"d": "DOUBLE", "m": "INT"})
+    empty = Layout.from_native(ctx.dense_layout(q, []))
+    assert empty.reduce_ops == full.reduce_ops and empty.num_groups == full.num_groups
+    # the empty rank's tables are the reduction identities and finalise to no rows
+    tabs = alloc_tables(empty, 1, torch.device("cuda", 0))
+    ctx.execute_dense(q, [], [t.data_ptr() for t in tabs])
+    torch.cuda.synchronize()
+    res = ctx.dense_finalize(q, [], [t.data_ptr() for t in tabs], 0, empty.num_groups)
+    assert len(res.keys) == 0
+
+
 def test_distributed_query_world1(ctx):
     import torch.distributed as dist
 

@@ -121,6 +121,8 @@ FILTERS = [
     " WHERE a = 99",
     " WHERE a >= 0",
     " WHERE NOT (a IN (0, 1, 2, 3, 4, 5, 6))",
+    " WHERE str > ''",  # '' is a literal, not an open bound (RangePredicateEvaluatorFactory)
+    " WHERE str <= '' OR a = 1",
 ]
 
 
@@ -281,6 +283,32 @@ def test_hash_group_by_beyond_dense_budget(ctx, where):
     assert r.stats.mode == 5  # MODE_GROUP_HASH
     assert not r.stats.num_groups_limit_reached
     assert len(got.rows) > (300_000 if not where else 100_000)
+
+
+def test_remap_cache_bounded_over_segment_subsets(ctx):
+    # without a table dictionary every distinct segment set unions its own dictionary, and each segment gets a
+    # device remap to it; the union cache is a bounded FIFO (64 entries) and a segment's remaps must be released
+    # with their union (they accumulated without bound)
+    import itertools
+    rng = np.random.default_rng(8)
+    segs = []
+    for i in range(9):
+        vals = rng.choice(4000, 3000, replace=False).astype(np.int32)  # each segment its own value set
+        t = {"g": (vals[rng.integers(0, 3000, 20_000)], "INT"),
+             "m": (rng.integers(0, 100, 20_000).astype(np.int32), "INT")}
+        segs.append(ctx.pin(create_segment(f"rm{i}", t)))
+    ctx.execute(parse_sql("SELECT SUM(m) FROM t"), segs)  # value-stream caches, counted in device_bytes too
+    base = sum(s.device_bytes for s in segs)
+    q = parse_sql("SET numGroupsLimit=1000000; SELECT g, COUNT(*), SUM(m) FROM t GROUP BY g LIMIT 1000000")
+    subsets = list(itertools.combinations(range(9), 3)) + list(itertools.combinations(range(9), 4))  # 84 + 126
+    for sub in subsets:
+        ctx.execute(q, [segs[i] for i in sub])
+    # live remaps: at most the 64 cached unions x 4 segments each
+    grown = sum(s.device_bytes for s in segs) - base
+    per_remap = 3000 * 4
+    assert 0 < grown <= (64 + 1) * 4 * per_remap, grown
+    for s in segs:
+        s.unpin()
 
 
 @pytest.mark.parametrize("case", ["few", "many", "exact", "filtered", "three_cols"])
