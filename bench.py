@@ -51,6 +51,18 @@ WORKLOADS = {
     "config3-agg": ("SELECT SUM(m), COUNT(*), MIN(m), MAX(m) FROM t WHERE f BETWEEN 0 AND 499",
                     {"m": (65536, 16), "f": (1000, 10)}, "config3-agg: WHERE f BETWEEN 0 AND 499 SUM/COUNT/MIN/MAX(m)"),
 }
+# workloads whose segments come from tests/workloads.py value generators through create_segment (sorted columns,
+# inverted indexes): (query, builder(seg_index, rows) -> SegmentBuffers, distinct segments, default rows,
+# default segment rows, description)
+BUILT = {
+    # BASELINE.json configs[0]: the README AdAnalytics query on one 10M-row segment (sorted daysSinceEpoch)
+    "config1": ("ads", 1, 10_000_000, 10_000_000,
+                "config1: README AdAnalytics, sorted daysSinceEpoch range + accountId IN, GROUP BY day, one segment"),
+    # BASELINE.json configs[4] on one GPU: DISTINCTCOUNTHLL(u), u at b = 24, WHERE c IN (10 ids) on an inverted
+    # index (~1 % selectivity); 4 distinct 10M-row segments pinned 25 times each (segment build is ~6 s each)
+    "config5": ("hll", 4, 1_000_000_000, 10_000_000,
+                "config5: DISTINCTCOUNTHLL(u) (b=24) WHERE c IN (10 ids) via inverted bitmaps, 1 % selectivity"),
+}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 KERNEL_NAMES = {0: "k_scan<MODE_COUNT>", 1: "k_scan<MODE_AGG>", 2: "k_scan<MODE_GROUP_LDS>",
                 3: "k_scan<MODE_GROUP_GLOBAL>", 4: "k_scan<MODE_PARTITION> + k_part_agg"}
@@ -77,6 +89,34 @@ def make_segment_buffers(seg_index, rows, seed, cols):
         seg.columns[name] = ColumnBuffers(name, "INT", card, bits, False, fixed_bit_pack(ids, bits), dbytes, width,
                                           dictionary)
     return seg
+
+
+def built_workload(kind):
+    """(query, builder) of a BUILT workload; builder(i, rows) -> (SegmentBuffers, algorithmic bytes of one query
+    over that segment).  config1: the streams the scan reads, over the sorted range's docs only (accountId filter
+    ids, day keys, clicks / impressions values).  config5: SURVEY 8(d)'s figure -- the u stream in full plus the
+    roaring bytes of the IN list's bitmaps."""
+    sys.path.insert(0, ROOT)
+    from pinot_amd.segment import create_segment
+    from tests import workloads as W
+    if kind == "ads":
+        def build(i, rows):
+            cols = W.ads_columns(rows, seed=0xAD01 + i)
+            seg = create_segment(f"ads_{i}", cols)
+            days = cols["daysSinceEpoch"][0]
+            docs = int(np.count_nonzero((days >= 17849) & (days <= 17856)))
+            bits = sum(seg.columns[c].bits for c in ("accountId", "daysSinceEpoch", "clicks", "impressions"))
+            return seg, (docs * bits + 7) // 8
+        return W.ADS_SQL, build
+    ids = list(range(3, 1000, 100))
+
+    def build(i, rows):
+        seg = create_segment(f"hll_{i}", W.hll_columns(rows, seed=0xC005 + i), inverted=("c",))
+        c = seg.columns["c"]
+        offs = np.frombuffer(np.ascontiguousarray(c.inverted_index).tobytes()[:4 * (c.cardinality + 1)], ">u4")
+        roaring = sum(int(offs[k + 1]) - int(offs[k]) for k in ids if k < c.cardinality)
+        return seg, (rows * seg.columns["u"].bits + 7) // 8 + roaring
+    return W.hll_sql(ids), build
 
 
 def algorithmic_bytes(rows_per_seg, nseg, cols):
@@ -141,12 +181,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rows", type=int, default=1_000_000_000, help="table rows (sharded across the GPUs)")
-    ap.add_argument("--segment-rows", type=int, default=10_000_000)
+    ap.add_argument("--rows", type=int, default=None, help="table rows (sharded across the GPUs); default 1e9, "
+                                                           "config1 1e7")
+    ap.add_argument("--segment-rows", type=int, default=None, help="default 1e7")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample size in seconds of work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
-    ap.add_argument("--workload", default="config3", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="config3", choices=sorted(list(WORKLOADS) + list(BUILT)))
     args = ap.parse_args()
 
     import torch
@@ -164,24 +205,48 @@ def main():
     from pinot_amd.engine import GpuContext
     from pinot_amd.query import parse_sql
 
-    query, cols, wdesc = WORKLOADS[args.workload]
+    built = BUILT.get(args.workload)
+    if built:
+        kind, distinct, rows_default, seg_default, wdesc = built
+        query, builder = built_workload(kind)
+        cols = None
+    else:
+        query, cols, wdesc = WORKLOADS[args.workload]
+        rows_default, seg_default = 1_000_000_000, 10_000_000
+    rows_total = args.rows or rows_default
     q = parse_sql(query)
-    nseg = max(1, args.rows // args.segment_rows)
-    seg_rows = args.rows // nseg
+    nseg = max(1, rows_total // (args.segment_rows or seg_default))
+    seg_rows = rows_total // nseg
     mine = [i for i in range(nseg) if i % world == rank]  # this rank's shard of the table
     t0 = time.time()
     ctx = GpuContext(device)
-    bufs, pinned = [], []
+    bufs, pinned, seg_alg = [], [], []
+    distinct_bufs = {}
     for k, i in enumerate(mine):
-        b = make_segment_buffers(i, seg_rows, seed=1000, cols=cols)
+        if built:  # `distinct` different segments, each pinned as many times as the table needs
+            if i % distinct not in distinct_bufs:
+                distinct_bufs[i % distinct] = builder(i % distinct, seg_rows)
+            b, a = distinct_bufs[i % distinct]
+            seg_alg.append(a)
+        else:
+            b = make_segment_buffers(i, seg_rows, seed=1000, cols=cols)
         pinned.append(ctx.pin(b))
         bufs.append(b)
         if k % 20 == 19:
             log(f"[rank {rank}] pinned {k + 1}/{len(mine)} segments ({time.time() - t0:.1f}s)")
     # table-level dictionaries: identical on every rank, so dense group ids line up for the RCCL merge
-    for g in q.group_by:
-        ctx.set_table_dictionary(g, "INT", np.arange(cols[g][0], dtype=np.int32))
-    ctx.set_schema({c: "INT" for c in cols})  # a rank without segments still builds the common dense layout
+    if built:
+        # every rank builds the same distinct segments' dictionaries (deterministic seeds)
+        for g in q.group_by:
+            vals = set()
+            for j in range(min(distinct, nseg)):
+                vals.update((distinct_bufs.get(j) or builder(j, seg_rows))[0].columns[g].dictionary_values.tolist())
+            ctx.set_table_dictionary(g, "INT", np.array(sorted(vals), dtype=np.int32))
+        ctx.set_schema({c: "INT" for c in (bufs[0].columns if bufs else {})})
+    else:
+        for g in q.group_by:
+            ctx.set_table_dictionary(g, "INT", np.arange(cols[g][0], dtype=np.int32))
+        ctx.set_schema({c: "INT" for c in cols})  # a rank without segments still builds the common dense layout
 
     runner = DistributedQuery(ctx)
     last = {}
@@ -222,7 +287,7 @@ def main():
     # roofline of the dominant kernel: this rank's scan kernels (HIP events on their stream) over this rank's
     # algorithmic bytes
     kernel_ms = float(np.mean(dev_ms)) if dev_ms else 0.0
-    alg = algorithmic_bytes(seg_rows, len(mine), cols)
+    alg = sum(seg_alg) if built else algorithmic_bytes(seg_rows, len(mine), cols)
     achieved = alg / (kernel_ms / 1000.0) / 1e9 if kernel_ms > 0 else None
     traffic = load_traffic(args.workload, 1) if world == 1 else None
 
@@ -238,8 +303,10 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "int64",
-        "data": f"synthetic (seeded PCG64 dictIds, one {total_rows}-row table of {nseg} x {seg_rows}-doc segments, "
-                f"sharded over {world} GPU(s))",
+        "data": (f"synthetic (seeded PCG64 dictIds, one {total_rows}-row table of {nseg} x {seg_rows}-doc segments, "
+                 f"sharded over {world} GPU(s))" if not built else
+                 f"synthetic (tests/workloads.py generators, {min(built[1], nseg)} distinct {seg_rows}-doc segments "
+                 f"pinned as {nseg} segments, sharded over {world} GPU(s))"),
         "config": {"workload": wdesc, "table_rows": total_rows, "segments": nseg, "segments_per_gpu": len(mine),
                    "parallelism": f"segments sharded x{world}" + (", RCCL reduce-scatter by key range" if world > 1
                                                                   else "")},
@@ -263,7 +330,19 @@ def main():
                                             f"C restatement of the reference loop nest (one worker per segment, as "
                                             f"GroupByCombineOperator) on {threads} host threads, {dt:.2f}s; "
                                             f"value_t1 = one segment on one thread, {dt1:.2f}s"}
-        if not args.no_parity:
+        if not args.no_parity and built:
+            # parity on the sample: the GPU's reduced rows vs the oracle's (all columns bit-exact; HLL registers
+            # compared raw)
+            from oracle import oracle as O
+            from pinot_amd.reduce import reduce_groups
+            r = ctx.execute(q, pinned[:n])
+            e = O.execute(q, oracle_segments(bufs[:n]))
+            ok = reduce_groups(q, r.keys, r.aggs).rows == reduce_groups(q, e.keys, e.aggs).rows
+            for k, a in enumerate(q.aggregations):
+                if a.function == "DISTINCTCOUNTHLL":
+                    ok = ok and all(np.array_equal(x[k], y[k]) for x, y in zip(r.aggs, e.aggs))
+            result["parity_sample"] = {"segments": n, "groups": int(r.num_groups), "bit_exact": bool(ok)}
+        elif not args.no_parity:
             # parity on the sample: GPU over the same segments vs the oracle -- group keys, COUNT, integer SUM,
             # MIN, MAX bit-exact (synthetic group dictionaries are 0..C-1, so value == global id)
             r = ctx.execute(q, pinned[:n])

@@ -324,6 +324,14 @@ struct HllTable {
   std::unique_ptr<DeviceBuffer> buf;  // uint32 per dictId
 };
 
+struct RoaringContainer {
+  int32_t type;      // 0 array, 1 bitmap, 2 run
+  int32_t key;       // high 16 bits
+  int32_t card;      // array: cardinality; run: number of runs
+  int32_t pad;
+  uint64_t offset;   // byte offset of the payload in the device inverted buffer
+};
+
 struct Column {
   std::string name;
   int32_t data_type = PH_INT;
@@ -342,6 +350,11 @@ struct Column {
   std::unique_ptr<DeviceBuffer> d_vpacked;
   int64_t vbase = 0;
   int32_t vbits = 0;
+  // container directory of the inverted index, parsed once at pin (not per query): the containers of dictId i
+  // are dir[dir_begin[i] .. dir_begin[i + 1]); id_docs[i] = its bitmap's cardinality (FastFilteredCount)
+  std::vector<RoaringContainer> dir;
+  std::vector<int64_t> dir_begin;
+  std::vector<int64_t> id_docs;
   bool has_inverted() const { return !inverted.empty(); }
 };
 
@@ -453,13 +466,8 @@ void launch_encode_values(const uint32_t* fwd, int32_t bits, const int64_t* tabl
                           int64_t n, uint32_t* out, hipStream_t s);
 void launch_fill_i64(int64_t* p, int64_t v, int64_t n, hipStream_t s);
 void launch_hll_table(const void* values, int32_t is_int, int64_t n, int log2m, uint32_t* out, hipStream_t s);
-struct RoaringContainer {
-  int32_t type;      // 0 array, 1 bitmap, 2 run
-  int32_t key;       // high 16 bits
-  int32_t card;      // array: cardinality; run: number of runs
-  int32_t pad;
-  uint64_t offset;   // byte offset of the payload in the device inverted buffer
-};
+
+void build_bitmap_directory(Column& c);  // at pin, from c.inverted
 void launch_roaring_or(const RoaringContainer* c, int n, const uint8_t* base, uint32_t* bitmap, int32_t num_docs,
                        hipStream_t s);
 void launch_selftest_unpack(const uint32_t* fwd, int64_t n, int bits, int32_t* out, hipStream_t s);

@@ -27,6 +27,8 @@
 #include <set>
 #include <unordered_map>
 
+#include <functional>
+
 #include "ph_internal.h"
 
 namespace ph {
@@ -271,6 +273,33 @@ struct Planner {
   }
 };
 
+// [first, end) docs a segment's filter can match: sorted doc ranges bound it, an AND intersects, an OR takes the hull
+std::pair<int64_t, int64_t> doc_span(const PNode& n, int64_t docs) {
+  if (n.kind == L_NONE) return {0, 0};
+  if (n.kind == L_ALL) return {0, docs};
+  if (n.op == OP_DOCRANGES && !n.ranges.empty())
+    return {n.ranges.front(), std::min<int64_t>(docs, (int64_t)n.ranges.back() + 1)};
+  if (n.op == OP_AND) {
+    std::pair<int64_t, int64_t> r{0, docs};
+    for (auto& k : n.kids) {
+      auto x = doc_span(k, docs);
+      r = {std::max(r.first, x.first), std::min(r.second, x.second)};
+    }
+    if (r.second < r.first) r = {0, 0};
+    return r;
+  }
+  if (n.op == OP_OR) {
+    std::pair<int64_t, int64_t> r{docs, 0};
+    for (auto& k : n.kids) {
+      auto x = doc_span(k, docs);
+      if (x.second > x.first) r = {std::min(r.first, x.first), std::max(r.second, x.second)};
+    }
+    if (r.second < r.first) r = {0, 0};
+    return r;
+  }
+  return {0, docs};
+}
+
 int count_scan_leaves(const PNode& n) {
   if (n.kind != L_NODE) return 0;
   int s = n.scan ? 1 : 0;
@@ -379,17 +408,49 @@ void parse_roaring(const uint8_t* blob, uint64_t len, uint64_t blob_offset, std:
 }
 
 void collect_bitmap_containers(const Column& c, const std::vector<int32_t>& ids, std::vector<RoaringContainer>& out) {
+  for (int32_t id : ids) out.insert(out.end(), c.dir.begin() + c.dir_begin[id], c.dir.begin() + c.dir_begin[id + 1]);
+}
+
+// docs of the dictIds' bitmaps: a single-value column's bitmaps are disjoint, so the OR's cardinality is the sum
+// (InvertedIndexFilterOperator.getNumMatchingDocs :101-127)
+int64_t bitmap_docs(const Column& c, const std::vector<int32_t>& ids) {
+  int64_t n = 0;
+  for (int32_t id : ids) n += c.id_docs[id];
+  return n;
+}
+
+}  // namespace
+
+void build_bitmap_directory(Column& c) {
   // BitmapInvertedIndexReader.getDocIds: offsets are uint32 BE; normalise by the first offset
   // (absolute or relative formats, BitmapInvertedIndexReader.java:40-61)
   const uint8_t* b = c.inverted.data();
   const uint64_t off_end = 4ull * (c.cardinality + 1);
   const uint64_t first = be32u(b);
-  for (int32_t id : ids) {
+  c.dir.clear();
+  c.dir_begin.assign(1, 0);
+  c.id_docs.assign(c.cardinality, 0);
+  for (int32_t id = 0; id < c.cardinality; ++id) {
     uint64_t s = be32u(b + 4ull * id) - first, e = be32u(b + 4ull * (id + 1)) - first;
     if (off_end + e > c.inverted.size() || e < s) fail(PH_ERR_INVALID_ARGUMENT, "inverted index: bad offsets");
-    parse_roaring(b + off_end + s, e - s, off_end + s, out);
+    const size_t k0 = c.dir.size();
+    parse_roaring(b + off_end + s, e - s, off_end + s, c.dir);
+    int64_t docs = 0;
+    for (size_t k = k0; k < c.dir.size(); ++k) {
+      const RoaringContainer& rc = c.dir[k];
+      if (rc.type != 2) {
+        docs += rc.card;
+      } else {  // run container: (start, length - 1) pairs after the run count
+        const uint8_t* r = b + rc.offset + 2;
+        for (int32_t j = 0; j < rc.card; ++j) docs += (int64_t)le16(r + 4 * j + 2) + 1;
+      }
+    }
+    c.id_docs[id] = docs;
+    c.dir_begin.push_back((int64_t)c.dir.size());
   }
 }
+
+namespace {
 
 // ------------------------------------------------------------------ global dictionaries
 std::shared_ptr<GlobalDict> build_union(Context* ctx, const std::string& col, const std::vector<ph_segment*>& segs) {
@@ -837,23 +898,75 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     roots[i] = std::move(root);
   }
 
-  // ---- inverted-index leaves -> device doc bitmaps
-  std::vector<uint32_t*> bitmap_dev(pl.bitmaps.size(), nullptr);
-  for (size_t i = 0; i < pl.bitmaps.size() && dop != DENSE_LAYOUT && !fin; ++i) {
-    BitmapLeaf& b = pl.bitmaps[i];
-    const size_t words = ((size_t)b.seg->num_docs + 31) / 32 + 1;
-    uint32_t* bm = scratch.alloc<uint32_t>(words);
-    PH_HIP_CHECK(hipMemsetAsync(bm, 0, words * 4, st));
-    std::vector<RoaringContainer> cs;
-    collect_bitmap_containers(*b.col, b.dict_ids, cs);
-    if (!cs.empty()) {
-      RoaringContainer* dc = scratch.alloc<RoaringContainer>(cs.size());
-      PH_HIP_CHECK(hipMemcpyAsync(dc, cs.data(), sizeof(RoaringContainer) * cs.size(), hipMemcpyHostToDevice, st));
-      launch_roaring_or(dc, (int)cs.size(), b.col->d_inverted.as<uint8_t>(), bm, b.seg->num_docs, st);
-      PH_HIP_CHECK(hipStreamSynchronize(st));  // `cs` is pageable host memory
+  // ---- FastFilteredCountOperator (AggregationPlanNode.java:183-188): COUNT only, and every segment's filter
+  // answers getNumMatchingDocs from its index -- a sorted doc range, an inverted-index bitmap (disjoint per
+  // dictId in a single-value column) or their NOT -- so no doc is scanned
+  bool fast_count = q->num_group_by == 0 && nagg > 0 && q->filter_root >= 0 && !dop;
+  for (int k = 0; k < nagg && fast_count; ++k) fast_count = q->aggregations[k].type == PH_AGG_COUNT;
+  if (fast_count) {
+    std::function<int64_t(const PNode&, int64_t)> count_of = [&](const PNode& n, int64_t docs) -> int64_t {
+      if (n.kind == L_ALL) return docs;
+      if (n.kind == L_NONE) return 0;
+      if (n.op == OP_DOCRANGES) {
+        int64_t c = 0;
+        for (size_t r = 0; r + 1 < n.ranges.size(); r += 2) c += (int64_t)n.ranges[r + 1] - n.ranges[r] + 1;
+        return c;
+      }
+      if (n.op == OP_BITMAP) {
+        const BitmapLeaf& b = pl.bitmaps[n.bitmap_leaf];
+        return bitmap_docs(*b.col, b.dict_ids);
+      }
+      if (n.op == OP_NOT && n.kids.size() == 1) {
+        const int64_t c = count_of(n.kids[0], docs);
+        return c < 0 ? -1 : docs - c;
+      }
+      return -1;  // AND / OR / scan leaves: the scan counts them
+    };
+    int64_t total = 0;
+    for (int i = 0; i < nseg && fast_count; ++i) {
+      if (!seg_live[i]) continue;
+      const int64_t c = count_of(roots[i], segs[i]->num_docs);
+      if (c < 0) fast_count = false;
+      total += c;
     }
-    bitmap_dev[i] = bm;
+    if (fast_count) {
+      init_row_results(1);
+      for (int k = 0; k < nagg; ++k) memcpy(res->aggs[k].data(), &total, 8);
+      stats.num_docs_scanned = total;
+      for (int i = 0; i < nseg; ++i) stats.num_segments_matched += seg_live[i] ? 1 : 0;
+      stats.plan_mode = -2;
+      res->mode = -2;
+      stats.host_ms = std::chrono::duration<double, std::milli>(clock::now() - t0).count();
+      return res.release();
+    }
   }
+
+  // ---- inverted-index leaves -> device doc bitmaps
+  // (container lists from the directories cached at pin; one upload for all leaves)
+  std::vector<uint32_t*> bitmap_dev(pl.bitmaps.size(), nullptr);
+  auto build_bitmaps = [&]() {
+    if (pl.bitmaps.empty() || dop == DENSE_LAYOUT || fin) return;
+    std::vector<RoaringContainer> cs;
+    std::vector<size_t> first(pl.bitmaps.size() + 1, 0);
+    for (size_t i = 0; i < pl.bitmaps.size(); ++i) {
+      collect_bitmap_containers(*pl.bitmaps[i].col, pl.bitmaps[i].dict_ids, cs);
+      first[i + 1] = cs.size();
+    }
+    RoaringContainer* dc = cs.empty() ? nullptr : scratch.alloc<RoaringContainer>(cs.size());
+    if (dc) PH_HIP_CHECK(hipMemcpyAsync(dc, cs.data(), sizeof(RoaringContainer) * cs.size(), hipMemcpyHostToDevice, st));
+    for (size_t i = 0; i < pl.bitmaps.size(); ++i) {
+      BitmapLeaf& b = pl.bitmaps[i];
+      const size_t words = ((size_t)b.seg->num_docs + 31) / 32 + 1;
+      uint32_t* bm = scratch.alloc<uint32_t>(words);
+      PH_HIP_CHECK(hipMemsetAsync(bm, 0, words * 4, st));
+      if (first[i + 1] > first[i])
+        launch_roaring_or(dc + first[i], (int)(first[i + 1] - first[i]), b.col->d_inverted.as<uint8_t>(), bm,
+                          b.seg->num_docs, st);
+      bitmap_dev[i] = bm;
+    }
+    if (dc) PH_HIP_CHECK(hipStreamSynchronize(st));  // `cs` is pageable host memory
+  };
+  build_bitmaps();
 
   // ---- group-by key space over table-level dictionaries
   std::vector<std::shared_ptr<GlobalDict>> gdicts;
@@ -1194,9 +1307,12 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         d.streams[0] = DevStream{c.d_fwd.as<uint32_t>(), c.bits, 0};
       }
     }
-    const int32_t words = (s->num_docs + 63) / 64;
+    // chunks cover only the words the filter can match in (SortedIndexBasedFilterOperator: a sorted leaf, alone
+    // or under an AND, bounds the docs; r1 staged every stream of the whole segment)
+    const std::pair<int64_t, int64_t> span = doc_span(root, s->num_docs);
+    const int32_t w0 = (int32_t)(span.first / 64), words = (int32_t)((span.second + 63) / 64);
     dseg_chunks.push_back({(int32_t)chunks.size(), 0});
-    for (int32_t w = 0; w < words; w += kChunkWords)
+    for (int32_t w = w0; w < words; w += kChunkWords)
       chunks.push_back({(int32_t)si, w, std::min(words, w + kChunkWords), 0});
     dseg_chunks.back().second = (int32_t)chunks.size();
     dseg_src.push_back(i);

@@ -451,6 +451,7 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
       if (d.inverted_index_size < (uint64_t)4 * (d.cardinality + 1))
         fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": inverted index too small");
       col->inverted.assign(inv, inv + d.inverted_index_size);
+      build_bitmap_directory(*col);
       col->d_inverted.alloc(d.inverted_index_size, ctx->device);
       PH_HIP_CHECK(hipMemcpyAsync(col->d_inverted.ptr, inv, d.inverted_index_size, hipMemcpyHostToDevice, st));
       seg->device_bytes += d.inverted_index_size;

@@ -186,6 +186,11 @@ def test_fast_filtered_count_gpu(ctx, fast_seg, where, expected):
     q = parse_sql("SELECT COUNT(*) FROM testTable WHERE " + where)
     r = ctx.execute(q, [fast_seg])
     assert reduce_groups(q, r.keys, r.aggs).rows == [[expected]]
+    # FastFilteredCountOperator stats: docs "scanned" = the count, nothing read from the forward index
+    assert r.stats.num_docs_scanned == expected
+    assert r.stats.num_entries_scanned_in_filter == 0
+    if " AND " not in where and " OR " not in where:
+        assert r.stats.mode == -2  # answered from the sorted ranges / bitmap cardinalities, no scan
 
 
 def test_range_queries_closed_form_gpu(ctx):
