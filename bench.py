@@ -93,10 +93,11 @@ def make_segment_buffers(seg_index, rows, seed, cols):
 
 def built_workload(kind):
     """(query, builder) of a BUILT workload; builder(i, rows) -> (SegmentBuffers, algorithmic bytes of one query
-    over that segment).  config1: the streams the scan reads, over the sorted range's docs only (accountId filter
+    over that segment, oracle segment of the same values).  config1: the streams the scan reads, over the sorted range's docs only (accountId filter
     ids, day keys, clicks / impressions values).  config5: SURVEY 8(d)'s figure -- the u stream in full plus the
     roaring bytes of the IN list's bitmaps."""
     sys.path.insert(0, ROOT)
+    from oracle import oracle as O
     from pinot_amd.segment import create_segment
     from tests import workloads as W
     if kind == "ads":
@@ -106,16 +107,17 @@ def built_workload(kind):
             days = cols["daysSinceEpoch"][0]
             docs = int(np.count_nonzero((days >= 17849) & (days <= 17856)))
             bits = sum(seg.columns[c].bits for c in ("accountId", "daysSinceEpoch", "clicks", "impressions"))
-            return seg, (docs * bits + 7) // 8
+            return seg, (docs * bits + 7) // 8, lambda: O.build_segment(f"ads_{i}", cols)
         return W.ADS_SQL, build
     ids = list(range(3, 1000, 100))
 
     def build(i, rows):
-        seg = create_segment(f"hll_{i}", W.hll_columns(rows, seed=0xC005 + i), inverted=("c",))
+        cols = W.hll_columns(rows, seed=0xC005 + i)
+        seg = create_segment(f"hll_{i}", cols, inverted=("c",))
         c = seg.columns["c"]
         offs = np.frombuffer(np.ascontiguousarray(c.inverted_index).tobytes()[:4 * (c.cardinality + 1)], ">u4")
         roaring = sum(int(offs[k + 1]) - int(offs[k]) for k in ids if k < c.cardinality)
-        return seg, (rows * seg.columns["u"].bits + 7) // 8 + roaring
+        return seg, (rows * seg.columns["u"].bits + 7) // 8 + roaring, lambda: O.build_segment(f"hll_{i}", cols)
     return W.hll_sql(ids), build
 
 
@@ -150,15 +152,21 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(bufs, q, threads, target_s=10.0):
+def cpu_baseline(bufs, q, threads, target_s=10.0, makers=None):
     """The oracle (C restatement of the reference loop nest, one worker per segment on `threads` host threads,
     as GroupByCombineOperator) over a bounded sample of the same segments: calibrated on one segment on one
     thread (the T = 1 leg), then as many segments as make ~target_s seconds of CPU work on `threads`."""
     from oracle import oracle as O
-    dt1, _, _ = O.execute_timed(q, oracle_segments(bufs[:1]), 1)  # one segment on one thread
-    waves = max(1, int(target_s / max(dt1, 1e-3)))                 # segments per thread in ~target_s
+
+    def osegs(k):  # oracle segments of the first k (sorted columns / inverted indexes: from the values)
+        if makers:
+            built = {}
+            return [built.setdefault(id(mk), mk()) for mk in makers[:k]]
+        return oracle_segments(bufs[:k])
+    dt1, _, _ = O.execute_timed(q, osegs(1), 1)  # one segment on one thread
+    waves = max(1, int(target_s / max(dt1, 1e-3)))  # segments per thread in ~target_s
     n = int(max(1, min(len(bufs), waves * threads)))
-    segs = oracle_segments(bufs[:n])
+    segs = osegs(n)
     dt, keys, aggs = O.execute_timed(q, segs, threads)
     return n, dt, dt1, keys, aggs
 
@@ -220,14 +228,15 @@ def main():
     mine = [i for i in range(nseg) if i % world == rank]  # this rank's shard of the table
     t0 = time.time()
     ctx = GpuContext(device)
-    bufs, pinned, seg_alg = [], [], []
+    bufs, pinned, seg_alg, ora_makers = [], [], [], []
     distinct_bufs = {}
     for k, i in enumerate(mine):
         if built:  # `distinct` different segments, each pinned as many times as the table needs
             if i % distinct not in distinct_bufs:
                 distinct_bufs[i % distinct] = builder(i % distinct, seg_rows)
-            b, a = distinct_bufs[i % distinct]
+            b, a, mk = distinct_bufs[i % distinct]
             seg_alg.append(a)
+            ora_makers.append(mk)
         else:
             b = make_segment_buffers(i, seg_rows, seed=1000, cols=cols)
         pinned.append(ctx.pin(b))
@@ -321,7 +330,7 @@ def main():
         result["groups"] = last["res"].num_groups
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = host_threads()
-        n, dt, dt1, keys, aggs = cpu_baseline(bufs, q, threads, args.cpu_seconds)
+        n, dt, dt1, keys, aggs = cpu_baseline(bufs, q, threads, args.cpu_seconds, ora_makers or None)
         rows = n * seg_rows
         result["cpu_baseline"] = {"value": rows / dt, "unit": "rows/s", "cores": threads, "kind": "port",
                                   "value_t1": seg_rows / dt1, "host_cores": os.cpu_count(),
@@ -336,7 +345,8 @@ def main():
             from oracle import oracle as O
             from pinot_amd.reduce import reduce_groups
             r = ctx.execute(q, pinned[:n])
-            e = O.execute(q, oracle_segments(bufs[:n]))
+            built_o = {}
+            e = O.execute(q, [built_o.setdefault(id(mk), mk()) for mk in ora_makers[:n]])
             ok = reduce_groups(q, r.keys, r.aggs).rows == reduce_groups(q, e.keys, e.aggs).rows
             for k, a in enumerate(q.aggregations):
                 if a.function == "DISTINCTCOUNTHLL":

@@ -529,12 +529,24 @@ def execute_timed(q, segments: Sequence[OracleSegment], num_threads: int):
             oc = s.columns[c]
             cs = cols[ci]
             cs.cardinality, cs.bits = oc.cardinality, oc.bits
-            fwd = np.concatenate([oc.fwd, np.zeros(8, np.uint8)])
-            keep.append(fwd)
-            cs.fwd = fwd.ctypes.data
+            if oc.fwd is not None:
+                fwd = np.concatenate([oc.fwd, np.zeros(8, np.uint8)])
+                keep.append(fwd)
+                cs.fwd = fwd.ctypes.data
+            else:  # sorted column: doc ranges (SortedIndexReaderImpl), as execute()
+                sr = np.ascontiguousarray(oc.sorted_ranges, dtype=np.int32)
+                keep.append(sr)
+                cs.sorted = sr.ctypes.data
             vals = oc.dictionary.astype(np.float64)
             keep.append(vals)
             cs.values = vals.ctypes.data
+            if any(a.column == c and a.function == "DISTINCTCOUNTHLL" for a in q.aggregations):
+                hl, hi = _hash_arrays(oc)
+                keep.append(hl if hl is not None else hi)
+                if hl is not None:
+                    cs.hash_longs = hl.ctypes.data
+                else:
+                    cs.hash_ints = hi.ctypes.data
             if c in q.group_by:
                 gi = np.searchsorted(unions[q.group_by.index(c)], oc.dictionary).astype(np.int32)
                 keep.append(gi)
@@ -551,8 +563,9 @@ def execute_timed(q, segments: Sequence[OracleSegment], num_threads: int):
     group_cols = np.array([col_index[g] for g in q.group_by], dtype=np.int32)
     gcard = np.array([len(u) for u in unions], dtype=np.int64)
     agg_fn, agg_col, agg_col2, agg_op = _agg_arrays(q, col_index)
+    log2m = next((a.log2m for a in q.aggregations if a.function == "DISTINCTCOUNTHLL"), 8)
     qs = _Query(len(prog), ops, len(q.group_by), group_cols.ctypes.data, gcard.ctypes.data,
-                len(q.aggregations), agg_fn.ctypes.data, agg_col.ctypes.data, 8, q.num_groups_limit,
+                len(q.aggregations), agg_fn.ctypes.data, agg_col.ctypes.data, log2m, q.num_groups_limit,
                 agg_col2.ctypes.data, agg_op.ctypes.data)
     res = _Result()
     t0 = time.perf_counter()

@@ -1226,6 +1226,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<std::pair<size_t, int>> fbitmap_fix;                    // segment index -> bitmap leaf
   std::vector<std::pair<int32_t, int32_t>> dseg_chunks;                // device segment -> its chunk range
   std::vector<int> dseg_src;                                           // device segment -> query segment index
+  std::vector<std::pair<int32_t, int32_t>> seg_words;                  // device segment -> [first, end) words to scan
   for (int i = 0; i < nseg; ++i) {
     if (!seg_live[i]) continue;
     ph_segment* s = segs[i];
@@ -1310,14 +1311,24 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     // chunks cover only the words the filter can match in (SortedIndexBasedFilterOperator: a sorted leaf, alone
     // or under an AND, bounds the docs; r1 staged every stream of the whole segment)
     const std::pair<int64_t, int64_t> span = doc_span(root, s->num_docs);
-    const int32_t w0 = (int32_t)(span.first / 64), words = (int32_t)((span.second + 63) / 64);
-    dseg_chunks.push_back({(int32_t)chunks.size(), 0});
-    for (int32_t w = w0; w < words; w += kChunkWords)
-      chunks.push_back({(int32_t)si, w, std::min(words, w + kChunkWords), 0});
-    dseg_chunks.back().second = (int32_t)chunks.size();
+    seg_words.push_back({(int32_t)(span.first / 64), (int32_t)((span.second + 63) / 64)});
     dseg_src.push_back(i);
     dsegs.push_back(d);
     stats.num_segments_matched++;
+  }
+  {
+    // chunk size: 16384 docs, smaller when the whole scan has too few chunks to give every CU several (a single
+    // 10M-row segment clipped to an 8 % sorted range is ~50 full chunks: latency-bound on 50 workgroups)
+    int64_t total_words = 0;
+    for (auto& sw : seg_words) total_words += std::max(0, sw.second - sw.first);
+    const int32_t cw = (int32_t)std::max<int64_t>(
+        32, std::min<int64_t>(kChunkWords, (total_words + 4 * ctx->num_cus - 1) / (4 * ctx->num_cus)));
+    for (size_t si = 0; si < seg_words.size(); ++si) {
+      dseg_chunks.push_back({(int32_t)chunks.size(), 0});
+      for (int32_t w = seg_words[si].first; w < seg_words[si].second; w += cw)
+        chunks.push_back({(int32_t)si, w, std::min(seg_words[si].second, w + cw), 0});
+      dseg_chunks.back().second = (int32_t)chunks.size();
+    }
   }
   // ---- per-wave staging layout: one span per staged stream, sized by its widest segment; the tile is the
   // largest (<= 32 words) whose spans fit the kernel's prefetch register pool
@@ -1525,7 +1536,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       // region (partition, workgroup) capacity: a workgroup scans <= ceil(chunks / grid) chunks; uniform keys
       // put 1/P of its docs in each partition; 25 % headroom + 64, rounded to 64 records (16-byte aligned
       // regions).  Skew beyond that spills to the overflow table.
-      const int64_t wg_docs = (int64_t)((max_batch_chunks + grid_a - 1) / grid_a) * kChunkWords * 64;
+      int32_t max_chunk_words = 1;
+      for (auto& ch : chunks) max_chunk_words = std::max(max_chunk_words, ch.word_end - ch.word_begin);
+      const int64_t wg_docs = (int64_t)((max_batch_chunks + grid_a - 1) / grid_a) * max_chunk_words * 64;
       int64_t cap = (int64_t)((double)wg_docs * 1.25 / (double)P) + 64;
       cap = (cap + 63) / 64 * 64;
       // the ring word keeps flushed / chunk in 16 bits; ranks beyond the capacity go to the overflow table

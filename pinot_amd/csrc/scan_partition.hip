@@ -19,93 +19,183 @@ size_t partition_lds_bytes(KParams& p) {
   int cl = 5;
   if (const char* e = getenv("PH_PART_RING_LOG2")) cl = std::max(3, std::min(7, atoi(e)));  // tuning knob (<= 7: a partition's flush lanes stay in one wave)
   while (cl > 4 && (size_t)(p.num_parts << cl) * rec > 48 * 1024) --cl;
+  // the lean kernel's flush moves a partition's records with 16 lanes, one 16-byte quarter each
+  if (p.part_fast) cl = std::min(cl, rec == 4 ? 6 : 5);
   p.part_slot_log2 = cl;
   // + one scratch slot and one scratch word per lane: k_part_scan appends misses there (branch-free)
   place(p.pl_slot_off, ((size_t)(p.num_parts << cl) + 64) * rec);
-  place(p.pl_lcnt_off, 4 * ((size_t)p.num_parts + 64));  // (flushed / CH << 16 | pending) per partition
-  p.pl_bcnt_off = p.pl_lcnt_off;
+  // generic kernel: (flushed / CH << 16 | pending) per partition; lean kernel: pending per partition
+  place(p.pl_lcnt_off, 4 * ((size_t)p.num_parts + 64));
+  place(p.pl_bcnt_off, 4 * (size_t)p.num_parts);  // lean kernel: records flushed per partition (region position)
   place(p.pl_misc_off, 64);
   return o;
 }
 
 // ------------------------------------------------------------------ kernel A, lean form
 // k_part_scan is k_scan<MODE_PARTITION> for the common shapes (no gathers: identity key remaps, a packed value
-// stream; filter leaf ALL / RANGE / DOCRANGE) written for issue efficiency: per group of 4 words the filter,
-// key and value decodes of every lane are straight-line, keys are 24-bit multiply-adds, the 4 rank atomics
-// issue back to back (a miss increments its lane's scratch word instead of branching) and the ring stores
-// likewise (a miss stores to its lane's scratch slot).  r2 SQ counters on the generic form: 61 VALU + 44 SALU
-// per 64-doc word and 51 % of wave cycles waiting.
+// stream; filter leaf ALL / RANGE / DOCRANGE) written for issue efficiency:
+//  * per group of 4 words the filter, key and value decodes of every lane are straight-line; each stream keeps
+//    one per-lane LDS byte offset that advances by the stream's 8*b bytes per word (one add per value);
+//  * keys are 24-bit multiply-adds;
+//  * a partition's ring holds only its pending records, from slot 0 (the flush writes the whole 64-byte chunks
+//    and moves the < 16 leftovers to the front), so a record's slot is its partition's pending count: one
+//    returning LDS add, one compare, one shift-add.  The 4 rank atomics issue back to back, a miss increments
+//    its lane's scratch word and stores to its lane's scratch slot instead of branching.
+// r2 SQ counters on the generic form: 61 VALU + 44 SALU per 64-doc word and 51 % of wave cycles waiting.
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+
+// LDS address (not offset from the dynamic-LDS base: that add would be paid per value)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)(p);
+}
+
+// value of the staged stream whose bits for this lane sit in the dword pair at LDS address `a` (the last bit in
+// the second dword): one ds_read2 with non-negative offsets, one funnel shift, one AND
+__device__ __forceinline__ uint32_t lds_value(uint32_t a, uint32_t rsh, uint32_t mask) {
+  lds_cu32* w = reinterpret_cast<lds_cu32*>((uintptr_t)a);
+  return __builtin_amdgcn_alignbit(w[0], w[1], rsh) & mask;
+}
+
+struct LaneStream {
+  uint32_t off;   // LDS address of the dword before this lane's last-bit dword, in word 0 of the tile
+  uint32_t rsh;
+  uint32_t mask;
+  uint32_t step;  // bytes per 64-doc word = 8 * bits
+};
+
+__device__ __forceinline__ LaneStream lane_stream(uint32_t stage_base, int32_t bits, int lane) {
+  LaneStream c;
+  const uint32_t e1 = (uint32_t)lane * (uint32_t)bits + (uint32_t)bits - 1u;
+  c.off = stage_base + 12u + ((e1 >> 5) << 2);
+  c.rsh = 31u - (e1 & 31u);
+  c.mask = bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
+  c.step = 8u * (uint32_t)bits;
+  return c;
+}
+
 template <int NG, int REC64, int HASV, int FK>
-__device__ __forceinline__ void part_tile(const KParams& p, SegPtr S, uint8_t* smem, const uint8_t* wst, int lane,
-                                          int32_t w0, int32_t nvalid, unsigned long long& matched) {
+__device__ __forceinline__ void part_tile(const KParams& p, SegPtr S, uint8_t* smem, uint32_t wst_off, int lane,
+                                          int32_t w0, int32_t nvalid) {
   using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
-  constexpr uint32_t CH = 64 / sizeof(Rec);
   const uint32_t ndocs = (uint32_t)S->num_docs;
-  const int fbits = FK == FK_RANGE ? S->streams[p.f_stream].bits : 1;
-  const BitCursor fcur = bit_cursor(wst + p.stage_soff[p.f_stream], fbits, lane);
+  LaneStream fs = lane_stream(wst_off + (uint32_t)p.stage_soff[p.f_stream],
+                              FK == FK_RANGE ? S->streams[p.f_stream].bits : 1, lane);
   const uint32_t flo = S->flo, flen = S->flen;
-  BitCursor gcur[NG];
+  LaneStream gs[NG];
   uint32_t gstr[NG];
 #pragma unroll
   for (int g = 0; g < NG; ++g) {
-    gcur[g] = bit_cursor(wst + p.stage_soff[p.g_stream[g]], S->streams[p.g_stream[g]].bits, lane);
+    gs[g] = lane_stream(wst_off + (uint32_t)p.stage_soff[p.g_stream[g]], S->streams[p.g_stream[g]].bits, lane);
     gstr[g] = (uint32_t)p.group_stride[g];
   }
-  BitCursor vcur = fcur;
+  LaneStream vs = fs;
   uint32_t vadd = 0;
   if (HASV) {
-    vcur = bit_cursor(wst + p.stage_soff[p.v_stream[0]], S->streams[p.v_stream[0]].bits, lane);
+    vs = lane_stream(wst_off + (uint32_t)p.stage_soff[p.v_stream[0]], S->streams[p.v_stream[0]].bits, lane);
     vadd = (uint32_t)(S->vals[0].base - p.part_vbase);  // record value = packed offset + (base - vmin)
   }
   const uint32_t klo = (uint32_t)p.part_klo, kmask = (1u << klo) - 1u, vbits = (uint32_t)p.part_vbits;
   const int cl = p.part_slot_log2;
   const uint32_t C = 1u << cl;
-  uint32_t* words = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
+  uint32_t* pend = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
   Rec* slots = reinterpret_cast<Rec*>(smem + p.pl_slot_off);
   const uint32_t dummy_word = (uint32_t)p.num_parts + (uint32_t)lane;
   const uint32_t dummy_slot = ((uint32_t)p.num_parts << cl) + (uint32_t)lane;
-  const uint32_t docbase = (uint32_t)w0 * 64u + (uint32_t)lane;
+  uint32_t doc = (uint32_t)w0 * 64u + (uint32_t)lane;
   for (int u = 0; u < nvalid; u += 4) {
     bool h[4];
-    uint32_t tot = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t doc = docbase + (uint32_t)(u + q) * 64u;
-      bool hh = (u + q < nvalid) & (doc < ndocs);
-      if constexpr (FK == FK_RANGE) hh &= (cursor_value(fcur, u + q) - flo) < flen;
-      if constexpr (FK == FK_DOCRANGE) hh &= (doc - flo) < flen;
-      h[q] = hh;
-      tot += (uint32_t)__popcll(__ballot(hh));
-    }
-    matched += tot;
-    if (tot == 0) continue;
-    uint32_t bk[4], widx[4];
+    uint32_t widx[4], bk[4];
     Rec rec[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+      bool hh = (u + q < nvalid) & (doc < ndocs);
+      if constexpr (FK == FK_RANGE) hh &= (lds_value(fs.off, fs.rsh, fs.mask) - flo) < flen;
+      if constexpr (FK == FK_DOCRANGE) hh &= (doc - flo) < flen;
       uint32_t key = 0;
 #pragma unroll
-      for (int g = 0; g < NG; ++g) key += __umul24(cursor_value(gcur[g], u + q), gstr[g]);  // keys < 2^22
-      const uint32_t vo = HASV ? cursor_value(vcur, u + q) + vadd : 0u;
+      for (int g = 0; g < NG; ++g) {
+        key += __umul24(lds_value(gs[g].off, gs[g].rsh, gs[g].mask), gstr[g]);  // keys < 2^22
+        gs[g].off += gs[g].step;
+      }
+      const uint32_t vo = HASV ? lds_value(vs.off, vs.rsh, vs.mask) + vadd : 0u;
+      if (HASV) vs.off += vs.step;
+      if (FK == FK_RANGE) fs.off += fs.step;
+      doc += 64u;
+      h[q] = hh;
       bk[q] = key >> klo;
       rec[q] = REC64 ? (Rec)(((unsigned long long)(key & kmask) << 32) | vo) : (Rec)(((key & kmask) << vbits) | vo);
-      widx[q] = h[q] ? bk[q] : dummy_word;
+      widx[q] = hh ? bk[q] : dummy_word;
     }
     uint32_t w[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) w[q] = atomicAdd(&words[widx[q]], 1u);
+    for (int q = 0; q < 4; ++q) w[q] = atomicAdd(&pend[widx[q]], 1u);
     bool ovf = false;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const uint32_t pend = w[q] & 0xffffu, F = (w[q] >> 16) * CH;
-      const bool ok = h[q] & (pend < C);
-      ovf |= h[q] & (pend >= C);
-      slots[ok ? (bk[q] << cl) + ((F + pend) & (C - 1u)) : dummy_slot] = rec[q];
+      const bool ok = h[q] & (w[q] < C);
+      ovf |= h[q] & (w[q] >= C);
+      slots[ok ? (bk[q] << cl) + w[q] : dummy_slot] = rec[q];
     }
     if (__ballot(ovf)) {  // a skewed round filled a ring: those records aggregate into the overflow table
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (h[q] && (w[q] & 0xffffu) >= C) part_overflow<REC64>(p, bk[q], rec[q]);
+        if (h[q] && w[q] >= C) part_overflow<REC64>(p, bk[q], rec[q]);
+    }
+  }
+}
+
+// Flush of the lean kernel's rings: per partition (16 lanes of one wave) the whole 64-byte chunks of pending
+// records go to the partition's region at its flushed position with 16-byte stores, and the < 16 leftovers move
+// to the front of the ring.  Each lane reads before any lane of its wave writes (LDS ops of a wave execute in
+// order), so a leftover never overwrites a record still to be stored.  final: every pending record is stored
+// and the region's record count written.  `matched` gains the round's appends (pending before the flush minus
+// the leftovers of the previous one, summed over the rounds) = the matched docs, numDocsScanned.
+template <int REC64, int BLOCK>
+__device__ void part_flush_lean(const KParams& p, uint8_t* smem, bool final, unsigned long long& matched) {
+  using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
+  constexpr uint32_t CH = 64 / sizeof(Rec);  // records per 64-byte chunk
+  constexpr uint32_t PQ = 16 / sizeof(Rec);  // records per 16-byte quarter
+  Rec* slots = reinterpret_cast<Rec*>(smem + p.pl_slot_off);
+  uint32_t* pend = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
+  uint32_t* gpos = reinterpret_cast<uint32_t*>(smem + p.pl_bcnt_off);
+  const int cl = p.part_slot_log2;
+  const uint32_t C = 1u << cl;
+  const uint32_t cap = (uint32_t)p.part_cap;
+  const int total = p.num_parts * 16;
+  for (int t = threadIdx.x; t < total; t += BLOCK) {
+    const uint32_t b = (uint32_t)t >> 4, i = (uint32_t)t & 15u;
+    const uint32_t raw = pend[b];
+    const uint32_t n = min(raw, C);  // records beyond C went to the overflow table
+    const uint32_t out = final ? n : (n & ~(CH - 1u));
+    if (i == 0) matched += raw - (n - out);
+    const uint32_t g = gpos[b];
+    Rec* ring = slots + ((size_t)b << cl);
+    // reads: this lane's quarter of the outgoing records, and leftover record i
+    const uint32_t r = i * PQ;  // ring position of the quarter (C / PQ <= 16 quarters)
+    u32x4 qv = {0u, 0u, 0u, 0u};
+    if (r < out) qv = *reinterpret_cast<const u32x4*>(ring + r);
+    const bool mv = !final && i < n - out;
+    Rec left = 0;
+    if (mv) left = ring[out + i];
+    // writes
+    if (r < out) {
+      Rec* region = reinterpret_cast<Rec*>(p.part_buf) + ((size_t)b * gridDim.x + blockIdx.x) * (size_t)cap;
+      const uint32_t dst = g + r;
+      if (dst + PQ <= cap && r + PQ <= out) {
+        *reinterpret_cast<u32x4*>(region + dst) = qv;
+      } else {
+        const Rec* e = reinterpret_cast<const Rec*>(&qv);
+        for (uint32_t k = 0; k < PQ && r + k < out; ++k) part_store<REC64>(p, b, dst + k, e[k]);
+      }
+    }
+    if (mv) ring[i] = left;
+    if (i == 0) {
+      if (final) {
+        p.part_count[(size_t)b * gridDim.x + blockIdx.x] = g + out;  // records of region (b, blockIdx)
+      } else {
+        pend[b] = n - out;
+        gpos[b] = g + out;
+      }
     }
   }
 }
@@ -120,8 +210,11 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
   SegPtr segs = (SegPtr)p.segs;
   const PH_CONST Chunk* chunks = (const PH_CONST Chunk*)p.chunks;
   uint8_t* wst = smem + p.stage_off + (size_t)wave * p.stage_stride;
+  const uint32_t wst_off = lds_addr(wst);
   uint32_t* words = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
+  uint32_t* gpos = reinterpret_cast<uint32_t*>(smem + p.pl_bcnt_off);
   for (int i = threadIdx.x; i < p.num_parts + 64; i += kPartBlock) words[i] = 0;
+  for (int i = threadIdx.x; i < p.num_parts; i += kPartBlock) gpos[i] = 0;
   __syncthreads();
 
   unsigned long long matched = 0;
@@ -160,7 +253,7 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
     tile_store<NL>(S, nvalid, wst, lane, pf);
     // flush the chunks completed in the previous round before this round's prefetch: the stores complete
     // under the decode instead of stalling the next tile_store (stores count in vmcnt too)
-    part_flush<REC64, kPartBlock>(p, smem, false);
+    part_flush_lean<REC64, kPartBlock>(p, smem, false, matched);
     lds_barrier();  // ring words are final before anyone appends again
     SegPtr cs = S;
     const int32_t cw0 = w0, cnvalid = nvalid;
@@ -176,9 +269,9 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
     }
     if (cnvalid > 0) {
       const int fk = cs->fkind;
-      if (fk == FK_RANGE) part_tile<NG, REC64, HASV, FK_RANGE>(p, cs, smem, wst, lane, cw0, cnvalid, matched);
-      else if (fk == FK_DOCRANGE) part_tile<NG, REC64, HASV, FK_DOCRANGE>(p, cs, smem, wst, lane, cw0, cnvalid, matched);
-      else part_tile<NG, REC64, HASV, FK_ALL>(p, cs, smem, wst, lane, cw0, cnvalid, matched);
+      if (fk == FK_RANGE) part_tile<NG, REC64, HASV, FK_RANGE>(p, cs, smem, wst_off, lane, cw0, cnvalid);
+      else if (fk == FK_DOCRANGE) part_tile<NG, REC64, HASV, FK_DOCRANGE>(p, cs, smem, wst_off, lane, cw0, cnvalid);
+      else part_tile<NG, REC64, HASV, FK_ALL>(p, cs, smem, wst_off, lane, cw0, cnvalid);
     }
     if (stamps) {
       t1 = __builtin_readcyclecounter();
@@ -194,9 +287,9 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
     p.dbg[4 * blockIdx.x + 2] = t_sync;
     p.dbg[4 * blockIdx.x + 3] = 1;
   }
-  if (lane == 0 && matched && p.matched_total) atomicAdd(p.matched_total, matched);
   lds_barrier();
-  part_flush<REC64, kPartBlock>(p, smem, true);  // also writes the region record counts
+  part_flush_lean<REC64, kPartBlock>(p, smem, true, matched);  // also writes the region record counts
+  if (matched && p.matched_total) atomicAdd(p.matched_total, matched);
 }
 
 template <int NG, int REC64, int HASV>
