@@ -27,7 +27,8 @@ size_t partition_lds_bytes(KParams& p) {
   // generic kernel: (flushed / CH << 16 | pending) per partition; lean kernel: pending per partition
   place(p.pl_lcnt_off, 4 * ((size_t)p.num_parts + 64));
   place(p.pl_bcnt_off, 4 * (size_t)p.num_parts);  // lean kernel: records flushed per partition (region position)
-  place(p.pl_misc_off, 64);
+  // lean kernel: two lists (round parity) of the partitions whose ring reached a whole chunk, + their counts
+  place(p.pl_misc_off, 8 * (size_t)p.num_parts + 16);
   return o;
 }
 
@@ -75,8 +76,9 @@ __device__ __forceinline__ LaneStream lane_stream(uint32_t stage_base, int32_t b
 
 template <int NG, int REC64, int HASV, int FK>
 __device__ __forceinline__ void part_tile(const KParams& p, SegPtr S, uint8_t* smem, uint32_t wst_off, int lane,
-                                          int32_t w0, int32_t nvalid) {
+                                          int32_t w0, int32_t nvalid, uint32_t* flist, uint32_t* fcnt) {
   using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
+  constexpr uint32_t CH = 64 / sizeof(Rec);
   const uint32_t ndocs = (uint32_t)S->num_docs;
   LaneStream fs = lane_stream(wst_off + (uint32_t)p.stage_soff[p.f_stream],
                               FK == FK_RANGE ? S->streams[p.f_stream].bits : 1, lane);
@@ -129,12 +131,18 @@ __device__ __forceinline__ void part_tile(const KParams& p, SegPtr S, uint8_t* s
     uint32_t w[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) w[q] = atomicAdd(&pend[widx[q]], 1u);
-    bool ovf = false;
+    bool ovf = false, full = false;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const bool ok = h[q] & (w[q] < C);
       ovf |= h[q] & (w[q] >= C);
+      full |= h[q] & (w[q] == CH - 1u);
       slots[ok ? (bk[q] << cl) + w[q] : dummy_slot] = rec[q];
+    }
+    if (__ballot(full)) {  // this record completed its partition's first whole chunk of the round: list it
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (h[q] && w[q] == CH - 1u) flist[atomicAdd(fcnt, 1u)] = bk[q];
     }
     if (__ballot(ovf)) {  // a skewed round filled a ring: those records aggregate into the overflow table
 #pragma unroll
@@ -144,14 +152,15 @@ __device__ __forceinline__ void part_tile(const KParams& p, SegPtr S, uint8_t* s
   }
 }
 
-// Flush of the lean kernel's rings: per partition (16 lanes of one wave) the whole 64-byte chunks of pending
-// records go to the partition's region at its flushed position with 16-byte stores, and the < 16 leftovers move
-// to the front of the ring.  Each lane reads before any lane of its wave writes (LDS ops of a wave execute in
-// order), so a leftover never overwrites a record still to be stored.  final: every pending record is stored
-// and the region's record count written.  `matched` gains the round's appends (pending before the flush minus
-// the leftovers of the previous one, summed over the rounds) = the matched docs, numDocsScanned.
+// Flush of the lean kernel's rings, listed partitions only: a partition enters the round's list when an append
+// completes its first whole 64-byte chunk, so the flush touches ~(round records / 16) partitions instead of all P.
+// Per listed partition (8 lanes of one wave) the whole chunks go to the partition's region at its flushed
+// position with 16-byte stores, and the < 16 leftovers move to the front of the ring.  Every lane reads before
+// any lane of its wave writes (LDS ops of a wave execute in order), so a leftover never overwrites a record still
+// to be stored.  `matched` gains the appends that went to the overflow table (a full ring).
 template <int REC64, int BLOCK>
-__device__ void part_flush_lean(const KParams& p, uint8_t* smem, bool final, unsigned long long& matched) {
+__device__ void part_flush_listed(const KParams& p, uint8_t* smem, const uint32_t* flist, uint32_t nlisted,
+                                  unsigned long long& matched) {
   using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
   constexpr uint32_t CH = 64 / sizeof(Rec);  // records per 64-byte chunk
   constexpr uint32_t PQ = 16 / sizeof(Rec);  // records per 16-byte quarter
@@ -161,41 +170,67 @@ __device__ void part_flush_lean(const KParams& p, uint8_t* smem, bool final, uns
   const int cl = p.part_slot_log2;
   const uint32_t C = 1u << cl;
   const uint32_t cap = (uint32_t)p.part_cap;
-  const int total = p.num_parts * 16;
-  for (int t = threadIdx.x; t < total; t += BLOCK) {
-    const uint32_t b = (uint32_t)t >> 4, i = (uint32_t)t & 15u;
+  const uint32_t total = nlisted * 8u;
+  for (uint32_t t = threadIdx.x; t < total; t += BLOCK) {
+    const uint32_t b = flist[t >> 3], i = t & 7u;
     const uint32_t raw = pend[b];
     const uint32_t n = min(raw, C);  // records beyond C went to the overflow table
-    const uint32_t out = final ? n : (n & ~(CH - 1u));
-    if (i == 0) matched += raw - (n - out);
+    const uint32_t out = n & ~(CH - 1u), left = n - out;
     const uint32_t g = gpos[b];
     Rec* ring = slots + ((size_t)b << cl);
-    // reads: this lane's quarter of the outgoing records, and leftover record i
-    const uint32_t r = i * PQ;  // ring position of the quarter (C / PQ <= 16 quarters)
-    u32x4 qv = {0u, 0u, 0u, 0u};
-    if (r < out) qv = *reinterpret_cast<const u32x4*>(ring + r);
-    const bool mv = !final && i < n - out;
-    Rec left = 0;
-    if (mv) left = ring[out + i];
+    // reads: quarters i and i + 8 of the outgoing records (C / PQ <= 16), leftovers i and i + 8 (< CH <= 16)
+    u32x4 q0 = {0u, 0u, 0u, 0u}, q1 = {0u, 0u, 0u, 0u};
+    const uint32_t r0 = i * PQ, r1 = (i + 8u) * PQ;
+    if (r0 < out) q0 = *reinterpret_cast<const u32x4*>(ring + r0);
+    if (r1 < out) q1 = *reinterpret_cast<const u32x4*>(ring + r1);
+    Rec l0 = 0, l1 = 0;
+    if (i < left) l0 = ring[out + i];
+    if (i + 8u < left) l1 = ring[out + i + 8u];
     // writes
-    if (r < out) {
-      Rec* region = reinterpret_cast<Rec*>(p.part_buf) + ((size_t)b * gridDim.x + blockIdx.x) * (size_t)cap;
-      const uint32_t dst = g + r;
-      if (dst + PQ <= cap && r + PQ <= out) {
-        *reinterpret_cast<u32x4*>(region + dst) = qv;
+    Rec* region = reinterpret_cast<Rec*>(p.part_buf) + ((size_t)b * gridDim.x + blockIdx.x) * (size_t)cap;
+    if (r0 < out) {
+      if (g + r0 + PQ <= cap) {
+        *reinterpret_cast<u32x4*>(region + g + r0) = q0;
       } else {
-        const Rec* e = reinterpret_cast<const Rec*>(&qv);
-        for (uint32_t k = 0; k < PQ && r + k < out; ++k) part_store<REC64>(p, b, dst + k, e[k]);
+        const Rec* e = reinterpret_cast<const Rec*>(&q0);
+        for (uint32_t k = 0; k < PQ; ++k) part_store<REC64>(p, b, g + r0 + k, e[k]);
       }
     }
-    if (mv) ring[i] = left;
-    if (i == 0) {
-      if (final) {
-        p.part_count[(size_t)b * gridDim.x + blockIdx.x] = g + out;  // records of region (b, blockIdx)
+    if (r1 < out) {
+      if (g + r1 + PQ <= cap) {
+        *reinterpret_cast<u32x4*>(region + g + r1) = q1;
       } else {
-        pend[b] = n - out;
-        gpos[b] = g + out;
+        const Rec* e = reinterpret_cast<const Rec*>(&q1);
+        for (uint32_t k = 0; k < PQ; ++k) part_store<REC64>(p, b, g + r1 + k, e[k]);
       }
+    }
+    if (i < left) ring[i] = l0;
+    if (i + 8u < left) ring[i + 8u] = l1;
+    if (i == 0) {
+      pend[b] = left;
+      gpos[b] = g + out;
+      matched += raw - n;
+    }
+  }
+}
+
+// Final flush of the lean kernel (after the last listed flush): every partition's < 16 pending records, the
+// region record counts, and the matched docs = the regions' records (overflow appends counted already).
+template <int REC64, int BLOCK>
+__device__ void part_flush_final(const KParams& p, uint8_t* smem, unsigned long long& matched) {
+  using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
+  const Rec* slots = reinterpret_cast<const Rec*>(smem + p.pl_slot_off);
+  const uint32_t* pend = reinterpret_cast<const uint32_t*>(smem + p.pl_lcnt_off);
+  const uint32_t* gpos = reinterpret_cast<const uint32_t*>(smem + p.pl_bcnt_off);
+  const int cl = p.part_slot_log2;
+  const uint32_t total = (uint32_t)p.num_parts * 16u;
+  for (uint32_t t = threadIdx.x; t < total; t += BLOCK) {
+    const uint32_t b = t >> 4, i = t & 15u;
+    const uint32_t n = pend[b], g = gpos[b];  // n < 16 after the listed flushes
+    if (i < n) part_store<REC64>(p, b, g + i, slots[((size_t)b << cl) + i]);
+    if (i == 0) {
+      p.part_count[(size_t)b * gridDim.x + blockIdx.x] = g + n;  // records of region (b, blockIdx)
+      matched += g + n;
     }
   }
 }
@@ -213,9 +248,13 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
   const uint32_t wst_off = lds_addr(wst);
   uint32_t* words = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
   uint32_t* gpos = reinterpret_cast<uint32_t*>(smem + p.pl_bcnt_off);
+  uint32_t* lists = reinterpret_cast<uint32_t*>(smem + p.pl_misc_off);  // [2][P] listed partitions
+  uint32_t* lcnt = lists + 2 * p.num_parts;                            // [2] list lengths
   for (int i = threadIdx.x; i < p.num_parts + 64; i += kPartBlock) words[i] = 0;
   for (int i = threadIdx.x; i < p.num_parts; i += kPartBlock) gpos[i] = 0;
+  if (threadIdx.x < 2) lcnt[threadIdx.x] = 0;
   __syncthreads();
+  uint32_t par = 0;  // round parity: this round appends to list par, the flush reads list par ^ 1
 
   unsigned long long matched = 0;
   const int32_t tw = p.tile_words;
@@ -253,7 +292,12 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
     tile_store<NL>(S, nvalid, wst, lane, pf);
     // flush the chunks completed in the previous round before this round's prefetch: the stores complete
     // under the decode instead of stalling the next tile_store (stores count in vmcnt too)
-    part_flush_lean<REC64, kPartBlock>(p, smem, false, matched);
+    {
+      const uint32_t prev = par ^ 1u;
+      const uint32_t nl = lcnt[prev];
+      if (threadIdx.x == 0) lcnt[par] = 0;  // read by nobody now; this round's appends fill it
+      part_flush_listed<REC64, kPartBlock>(p, smem, lists + prev * p.num_parts, nl, matched);
+    }
     lds_barrier();  // ring words are final before anyone appends again
     SegPtr cs = S;
     const int32_t cw0 = w0, cnvalid = nvalid;
@@ -269,9 +313,11 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
     }
     if (cnvalid > 0) {
       const int fk = cs->fkind;
-      if (fk == FK_RANGE) part_tile<NG, REC64, HASV, FK_RANGE>(p, cs, smem, wst_off, lane, cw0, cnvalid);
-      else if (fk == FK_DOCRANGE) part_tile<NG, REC64, HASV, FK_DOCRANGE>(p, cs, smem, wst_off, lane, cw0, cnvalid);
-      else part_tile<NG, REC64, HASV, FK_ALL>(p, cs, smem, wst_off, lane, cw0, cnvalid);
+      uint32_t* fl = lists + par * p.num_parts;
+      uint32_t* fc = lcnt + par;
+      if (fk == FK_RANGE) part_tile<NG, REC64, HASV, FK_RANGE>(p, cs, smem, wst_off, lane, cw0, cnvalid, fl, fc);
+      else if (fk == FK_DOCRANGE) part_tile<NG, REC64, HASV, FK_DOCRANGE>(p, cs, smem, wst_off, lane, cw0, cnvalid, fl, fc);
+      else part_tile<NG, REC64, HASV, FK_ALL>(p, cs, smem, wst_off, lane, cw0, cnvalid, fl, fc);
     }
     if (stamps) {
       t1 = __builtin_readcyclecounter();
@@ -279,6 +325,7 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
       t0 = t1;
     }
     lds_barrier();  // this round's appends are complete before the next round's flush
+    par ^= 1u;
     if (stamps) t_sync += __builtin_readcyclecounter() - t0;
   }
   if (stamps && threadIdx.x == 0) {
@@ -287,8 +334,9 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
     p.dbg[4 * blockIdx.x + 2] = t_sync;
     p.dbg[4 * blockIdx.x + 3] = 1;
   }
+  part_flush_listed<REC64, kPartBlock>(p, smem, lists + (par ^ 1u) * p.num_parts, lcnt[par ^ 1u], matched);
   lds_barrier();
-  part_flush_lean<REC64, kPartBlock>(p, smem, true, matched);  // also writes the region record counts
+  part_flush_final<REC64, kPartBlock>(p, smem, matched);  // also writes the region record counts
   if (matched && p.matched_total) atomicAdd(p.matched_total, matched);
 }
 
