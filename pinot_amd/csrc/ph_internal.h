@@ -231,9 +231,10 @@ struct KParams {
   int32_t part_klo;               // key bits kept in a record (keys per partition = 1 << part_klo)
   int32_t part_vbits;             // value-offset bits in a record (0: COUNT only)
   int32_t num_parts;
+  int32_t part_load_first;        // lean kernel A: issue the next tile's loads before the flush (tuning)
   int32_t part_cap;               // records per (partition, workgroup) region
   int64_t part_vbase;             // record value = value - part_vbase
-  void* part_buf;                 // [num_parts][gridDim.x][part_cap] records: one region per workgroup
+  void* part_buf;                 // [gridDim.x][num_parts][part_cap] records: one region per (workgroup, partition)
   uint32_t* part_count;           // [num_parts][gridDim.x] records written per region (may exceed part_cap)
   int32_t pl_slot_off, pl_lcnt_off, pl_bcnt_off, pl_misc_off;  // LDS layout
   int32_t part_slot_log2;         // C = 1 << part_slot_log2 LDS ring slots per partition

@@ -187,7 +187,7 @@ __device__ void part_flush_listed(const KParams& p, uint8_t* smem, const uint32_
     if (i < left) l0 = ring[out + i];
     if (i + 8u < left) l1 = ring[out + i + 8u];
     // writes
-    Rec* region = reinterpret_cast<Rec*>(p.part_buf) + ((size_t)b * gridDim.x + blockIdx.x) * (size_t)cap;
+    Rec* region = reinterpret_cast<Rec*>(p.part_buf) + part_region(p, b, blockIdx.x) * (size_t)cap;
     if (r0 < out) {
       if (g + r0 + PQ <= cap) {
         *reinterpret_cast<u32x4*>(region + g + r0) = q0;
@@ -290,8 +290,14 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
   while (c < c_end) {
     if (stamps) t0 = __builtin_readcyclecounter();
     tile_store<NL>(S, nvalid, wst, lane, pf);
-    // flush the chunks completed in the previous round before this round's prefetch: the stores complete
-    // under the decode instead of stalling the next tile_store (stores count in vmcnt too)
+    SegPtr cs = S;
+    const int32_t cw0 = w0, cnvalid = nvalid;
+    advance();
+    locate();
+    const bool load_first = p.part_load_first;
+    if (load_first && c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
+    // flush the chunks completed in the previous round; the prefetch goes first (its loads get the flush's time
+    // to arrive; the flush's stores, issued after them, complete under the decode)
     {
       const uint32_t prev = par ^ 1u;
       const uint32_t nl = lcnt[prev];
@@ -299,11 +305,7 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
       part_flush_listed<REC64, kPartBlock>(p, smem, lists + prev * p.num_parts, nl, matched);
     }
     lds_barrier();  // ring words are final before anyone appends again
-    SegPtr cs = S;
-    const int32_t cw0 = w0, cnvalid = nvalid;
-    advance();
-    locate();
-    if (c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
+    if (!load_first && c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     if (stamps) {
@@ -462,7 +464,7 @@ __global__ void __launch_bounds__(1024) k_part_agg(const PartAggParams p) {
       for (int q = 0; q < RPW; ++q) {
         const uint32_t i0 = base + lane * PER;
         if (i0 < nn[q]) {
-          const Rec* src = buf + ((size_t)part * R + r0 + b0 + q) * (size_t)p.part_cap + i0;
+          const Rec* src = buf + ((size_t)(r0 + b0 + q) * p.num_parts + part) * (size_t)p.part_cap + i0;
           v[q] = *reinterpret_cast<const u32x4*>(src);
         }
       }
