@@ -232,6 +232,7 @@ struct KParams {
   int32_t part_vbits;             // value-offset bits in a record (0: COUNT only)
   int32_t num_parts;
   int32_t part_load_first;        // lean kernel A: issue the next tile's loads before the flush (tuning)
+  int32_t agg_fast;               // MODE_AGG: run k_agg_lean
   int32_t part_cap;               // records per (partition, workgroup) region
   int64_t part_vbase;             // record value = value - part_vbase
   void* part_buf;                 // [gridDim.x][num_parts][part_cap] records: one region per (workgroup, partition)

@@ -1389,8 +1389,16 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   kp.part_fast = !kp.late_prefetch && getenv("PH_PART_GENERIC") == nullptr;
   for (auto& d : dsegs)
     if (d.fkind != FK_ALL && d.fkind != FK_RANGE && d.fkind != FK_DOCRANGE) kp.part_fast = 0;
+  // the lean aggregation kernel (k_agg_lean) covers one packed integer value column with ALL / RANGE / DOCRANGE
+  // leaves; its 32-bit tile sums need value offsets below 2^26
+  kp.agg_fast = mode == MODE_AGG && nvals == 1 && !val_exprs[0] && num_hll == 0 && val_is_int[0] &&
+                !kp.late_prefetch && getenv("PH_AGG_GENERIC") == nullptr;
+  for (auto& d : dsegs)
+    if ((d.fkind != FK_ALL && d.fkind != FK_RANGE && d.fkind != FK_DOCRANGE) || d.vals[0].kind != VK_PACKED ||
+        d.streams[kp.v_stream[0]].bits > 26)
+      kp.agg_fast = 0;
   if (const char* e = getenv("PH_DEBUG_FLAGS")) kp.dbg_flags = atoi(e);
-  if (kp.dbg_flags) kp.part_fast = 0;  // timing experiments run on the generic form
+  if (kp.dbg_flags) kp.part_fast = kp.agg_fast = 0;  // timing experiments run on the generic form
   if (getenv("PH_DEBUG_STAMPS")) {
     kp.dbg = scratch.alloc<unsigned long long>(4 * (size_t)ctx->num_cus * 8);
     PH_HIP_CHECK(hipMemsetAsync(kp.dbg, 0, 32 * (size_t)ctx->num_cus * 8, st));

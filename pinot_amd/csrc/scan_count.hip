@@ -1,11 +1,133 @@
-// scan_count.hip -- k_scan instantiations of the aggregation-only plans (MODE_COUNT, MODE_AGG).
+// scan_count.hip -- k_scan instantiations of the aggregation-only plans (MODE_COUNT, MODE_AGG), and the lean
+// aggregation kernel k_agg_lean.
 #include "scan_kernel.h"
 
 namespace ph {
 
+// ------------------------------------------------------------------ lean MODE_AGG
+// k_agg_lean is k_scan<MODE_AGG> for the common shape -- one integer value column read from its packed
+// frame-of-reference stream, no HLL, filter leaf ALL / RANGE / DOCRANGE (AggregationOperator over SUM / MIN /
+// MAX / COUNT, AggregationPlanNode.java) -- written for issue efficiency: per word and lane the value offset is
+// folded into 32-bit tile accumulators (sum of offsets, min / max offset; offsets < 2^26 and <= 32 words per
+// tile, so the 32-bit sum cannot wrap), and the 64-bit absolute values are formed once per tile: SUM =
+// sum(offsets) + matches * base (the match count from the wave's ballots), MIN / MAX = base + min / max offset.
+// No LDS traffic beyond the wave's own staging, no barriers: every wave streams independently.
+template <int FK>
+__device__ __forceinline__ void agg_tile(const KParams& p, SegPtr S, uint32_t wst_off, int lane, int32_t w0,
+                                         int32_t nvalid, int64_t& asum, int64_t& amin, int64_t& amax,
+                                         unsigned long long& matched) {
+  const uint32_t ndocs = (uint32_t)S->num_docs;
+  LaneStream fs = lane_stream(wst_off + (uint32_t)p.stage_soff[p.f_stream],
+                              FK == FK_RANGE ? S->streams[p.f_stream].bits : 1, lane);
+  LaneStream vs = lane_stream(wst_off + (uint32_t)p.stage_soff[p.v_stream[0]], S->streams[p.v_stream[0]].bits, lane);
+  const uint32_t flo = S->flo, flen = S->flen;
+  uint32_t doc = (uint32_t)w0 * 64u + (uint32_t)lane;
+  uint32_t tsum = 0, tmin = 0xffffffffu, tmax = 0;
+  uint32_t tcnt = 0;  // wave-uniform
+  for (int u = 0; u < nvalid; u += 4) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bool hh = (u + q < nvalid) & (doc < ndocs);
+      if constexpr (FK == FK_RANGE) hh &= (lds_value(fs.off, fs.rsh, fs.mask) - flo) < flen;
+      if constexpr (FK == FK_DOCRANGE) hh &= (doc - flo) < flen;
+      const uint32_t v = lds_value(vs.off, vs.rsh, vs.mask);
+      const uint32_t m0 = hh ? v : 0u;
+      tsum += m0;
+      tmax = max(tmax, m0);
+      tmin = min(tmin, hh ? v : 0xffffffffu);
+      tcnt += (uint32_t)__popcll(__ballot(hh));
+      vs.off += vs.step;
+      if (FK == FK_RANGE) fs.off += fs.step;
+      doc += 64u;
+    }
+  }
+  const int64_t base = S->vals[0].base;
+  matched += tcnt;
+  asum += (int64_t)tsum;
+  if (lane == 0) asum += base * (int64_t)tcnt;  // the matches' common base, once per wave
+  if (tmin != 0xffffffffu) {                     // this lane matched in the tile
+    amin = min(amin, base + (int64_t)tmin);
+    amax = max(amax, base + (int64_t)tmax);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_agg_lean(const KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NL = kPrefetchOther;
+  constexpr int WAVES = kWaves;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  SegPtr segs = (SegPtr)p.segs;
+  const PH_CONST Chunk* chunks = (const PH_CONST Chunk*)p.chunks;
+  uint8_t* wst = smem + p.stage_off + (size_t)wave * p.stage_stride;
+  const uint32_t wst_off = lds_addr(wst);
+  int64_t asum = 0, amin = INT64_MAX, amax = INT64_MIN;
+  unsigned long long matched = 0;
+  const int32_t tw = p.tile_words;
+  const int32_t round_words = WAVES * tw;
+  const int64_t nch = p.chunk_end - p.chunk_begin;
+  int32_t c = p.chunk_begin + (int32_t)(nch * blockIdx.x / gridDim.x), r = 0;
+  const int32_t c_end = p.chunk_begin + (int32_t)(nch * (blockIdx.x + 1) / gridDim.x);
+  int32_t cbeg = 0, cend = 0;
+  SegPtr S = nullptr;
+  int32_t w0 = 0, nvalid = 0;
+  auto locate = [&]() {
+    if (c < c_end) {
+      cbeg = chunks[c].word_begin;
+      cend = chunks[c].word_end;
+      S = segs + chunks[c].seg;
+      w0 = cbeg + r * round_words + wave * tw;
+      nvalid = min(tw, cend - w0);
+    }
+  };
+  auto advance = [&]() {
+    if (cbeg + (r + 1) * round_words < cend) {
+      ++r;
+    } else {
+      ++c;
+      r = 0;
+    }
+  };
+  Prefetch<NL> pf;
+  locate();
+  if (c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
+  while (c < c_end) {
+    tile_store<NL>(S, nvalid, wst, lane, pf);
+    SegPtr cs = S;
+    const int32_t cw0 = w0, cnvalid = nvalid;
+    advance();
+    locate();
+    if (c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (cnvalid > 0) {
+      const int fk = cs->fkind;
+      if (fk == FK_RANGE) agg_tile<FK_RANGE>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched);
+      else if (fk == FK_DOCRANGE) agg_tile<FK_DOCRANGE>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched);
+      else agg_tile<FK_ALL>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // the staging area is rewritten by the next tile_store
+  }
+  // one set of device atomics per wave (a few thousand in all)
+  const int64_t si = wave_sum_i64(asum);
+  const int64_t mn = wave_min_i64(amin);
+  const int64_t mx = wave_max_i64(amax);
+  if (lane == 0) {
+    if (matched) atomicAdd(&p.out_count[0], matched);
+    const int ops = p.val_ops[0];
+    if (ops & OPS_SUM) atomicAdd(reinterpret_cast<unsigned long long*>(p.out_sum[0]), (unsigned long long)si);
+    if ((ops & OPS_MIN) && mn != INT64_MAX) atomicMin(reinterpret_cast<long long*>(p.out_min[0]), (long long)mn);
+    if ((ops & OPS_MAX) && mx != INT64_MIN) atomicMax(reinterpret_cast<long long*>(p.out_max[0]), (long long)mx);
+  }
+}
+
 void launch_scan_agg(const KParams& p, int mode, int grid, size_t lds, hipStream_t s) {
   if (mode == MODE_COUNT) {
     launch_late<MODE_COUNT, 0, 0>(p, grid, lds, s);
+  } else if (p.agg_fast) {
+    allow_lds(k_agg_lean, lds);
+    hipLaunchKernelGGL(k_agg_lean, dim3(grid), dim3(kBlock), lds, s, p);
   } else if (p.num_vals <= 1 && !p.val_op[0]) {
     launch_late<MODE_AGG, 0, 1>(p, grid, lds, s);  // ValCap 1
   } else {

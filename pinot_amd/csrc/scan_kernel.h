@@ -252,6 +252,39 @@ __device__ __forceinline__ uint32_t cursor_value(const BitCursor& c, int u) {
   return __builtin_amdgcn_alignbit(w[-1], w[0], c.rsh) & c.mask;
 }
 
+// ---- lean decode cursors (the lean kernels): the same decode as BitCursor on absolute LDS addresses, one per
+// stream and lane, advanced by the stream's 8*b bytes per word
+typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
+
+// LDS address (not offset from the dynamic-LDS base: that add would be paid per value)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)(p);
+}
+
+// value of the staged stream whose bits for this lane sit in the dword pair at LDS address `a` (the last bit in
+// the second dword): one ds_read2 with non-negative offsets, one funnel shift, one AND
+__device__ __forceinline__ uint32_t lds_value(uint32_t a, uint32_t rsh, uint32_t mask) {
+  lds_cu32* w = reinterpret_cast<lds_cu32*>((uintptr_t)a);
+  return __builtin_amdgcn_alignbit(w[0], w[1], rsh) & mask;
+}
+
+struct LaneStream {
+  uint32_t off;   // LDS address of the dword before this lane's last-bit dword, in word 0 of the tile
+  uint32_t rsh;
+  uint32_t mask;
+  uint32_t step;  // bytes per 64-doc word = 8 * bits
+};
+
+__device__ __forceinline__ LaneStream lane_stream(uint32_t stage_base, int32_t bits, int lane) {
+  LaneStream c;
+  const uint32_t e1 = (uint32_t)lane * (uint32_t)bits + (uint32_t)bits - 1u;
+  c.off = stage_base + 12u + ((e1 >> 5) << 2);
+  c.rsh = 31u - (e1 & 31u);
+  c.mask = bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
+  c.step = 8u * (uint32_t)bits;
+  return c;
+}
+
 // value of value-column j for a doc: int64 (integer columns) or float64 (real columns)
 __device__ __forceinline__ void read_value(int kind, int64_t base, const void* table, uint32_t x, int64_t& iv,
                                            double& dv) {

@@ -43,37 +43,6 @@ size_t partition_lds_bytes(KParams& p) {
 //    returning LDS add, one compare, one shift-add.  The 4 rank atomics issue back to back, a miss increments
 //    its lane's scratch word and stores to its lane's scratch slot instead of branching.
 // r2 SQ counters on the generic form: 61 VALU + 44 SALU per 64-doc word and 51 % of wave cycles waiting.
-typedef __attribute__((address_space(3))) const uint32_t lds_cu32;
-
-// LDS address (not offset from the dynamic-LDS base: that add would be paid per value)
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)(p);
-}
-
-// value of the staged stream whose bits for this lane sit in the dword pair at LDS address `a` (the last bit in
-// the second dword): one ds_read2 with non-negative offsets, one funnel shift, one AND
-__device__ __forceinline__ uint32_t lds_value(uint32_t a, uint32_t rsh, uint32_t mask) {
-  lds_cu32* w = reinterpret_cast<lds_cu32*>((uintptr_t)a);
-  return __builtin_amdgcn_alignbit(w[0], w[1], rsh) & mask;
-}
-
-struct LaneStream {
-  uint32_t off;   // LDS address of the dword before this lane's last-bit dword, in word 0 of the tile
-  uint32_t rsh;
-  uint32_t mask;
-  uint32_t step;  // bytes per 64-doc word = 8 * bits
-};
-
-__device__ __forceinline__ LaneStream lane_stream(uint32_t stage_base, int32_t bits, int lane) {
-  LaneStream c;
-  const uint32_t e1 = (uint32_t)lane * (uint32_t)bits + (uint32_t)bits - 1u;
-  c.off = stage_base + 12u + ((e1 >> 5) << 2);
-  c.rsh = 31u - (e1 & 31u);
-  c.mask = bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
-  c.step = 8u * (uint32_t)bits;
-  return c;
-}
-
 template <int NG, int REC64, int HASV, int FK>
 __device__ __forceinline__ void part_tile(const KParams& p, SegPtr S, uint8_t* smem, uint32_t wst_off, int lane,
                                           int32_t w0, int32_t nvalid, uint32_t* flist, uint32_t* fcnt) {
