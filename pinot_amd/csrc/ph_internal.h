@@ -233,6 +233,10 @@ struct KParams {
   int32_t num_parts;
   int32_t part_load_first;        // lean kernel A: issue the next tile's loads before the flush (tuning)
   int32_t agg_fast;               // MODE_AGG: run k_agg_lean
+  int32_t lds_fast;               // MODE_GROUP_LDS: run k_group_lds_lean
+  int32_t lds_pack;               //   COUNT << 40 | SUM in one 64-bit LDS word
+  int32_t lds_copies;             //   table copies (one per wave when they fit)
+  int32_t lds_copy_bytes;         //   bytes per copy
   int32_t part_cap;               // records per (partition, workgroup) region
   int64_t part_vbase;             // record value = value - part_vbase
   void* part_buf;                 // [gridDim.x][num_parts][part_cap] records: one region per (workgroup, partition)

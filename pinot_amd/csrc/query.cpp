@@ -1397,8 +1397,18 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if ((d.fkind != FK_ALL && d.fkind != FK_RANGE && d.fkind != FK_DOCRANGE) || d.vals[0].kind != VK_PACKED ||
         d.streams[kp.v_stream[0]].bits > 26)
       kp.agg_fast = 0;
+  // the lean LDS group-by (k_group_lds_lean): identity remaps, at most one packed integer value column whose
+  // offsets from the table-wide minimum fit 32 bits, ALL / RANGE / DOCRANGE leaves
+  kp.lds_fast = mode == MODE_GROUP_LDS && num_hll == 0 && nvals <= 1 && !kp.late_prefetch &&
+                getenv("PH_LDS_GENERIC") == nullptr;
+  if (nvals == 1)
+    kp.lds_fast = kp.lds_fast && val_is_int[0] && !val_exprs[0] && vmax >= vmin && (uint64_t)(vmax - vmin) < (1ull << 32);
+  for (auto& d : dsegs)
+    if ((d.fkind != FK_ALL && d.fkind != FK_RANGE && d.fkind != FK_DOCRANGE) ||
+        (nvals == 1 && d.vals[0].kind != VK_PACKED))
+      kp.lds_fast = 0;
   if (const char* e = getenv("PH_DEBUG_FLAGS")) kp.dbg_flags = atoi(e);
-  if (kp.dbg_flags) kp.part_fast = kp.agg_fast = 0;  // timing experiments run on the generic form
+  if (kp.dbg_flags) kp.part_fast = kp.agg_fast = kp.lds_fast = 0;  // timing experiments run on the generic form
   if (getenv("PH_DEBUG_STAMPS")) {
     kp.dbg = scratch.alloc<unsigned long long>(4 * (size_t)ctx->num_cus * 8);
     PH_HIP_CHECK(hipMemsetAsync(kp.dbg, 0, 32 * (size_t)ctx->num_cus * 8, st));
@@ -1418,6 +1428,27 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     lds = stage_bytes + lds_tables;
     kp.pl_misc_off = 0;
+    if (kp.lds_fast) {
+      // table copies (one per wave when they fit in 48 KiB); COUNT+SUM packed in one 64-bit word when a copy's
+      // docs (bounded by its workgroup's) keep count < 2^24 and the offset sum < 2^40
+      int32_t mcw = 1;
+      for (auto& ch : chunks) mcw = std::max(mcw, ch.word_end - ch.word_begin);
+      const uint64_t vrange = nvals ? (uint64_t)(vmax - vmin) : 0;
+      auto layout = [&](bool pack) {
+        kp.lds_copy_bytes = (int32_t)(((size_t)G * (pack ? 16 : 20) + 15) / 16 * 16);
+        kp.lds_copies = (size_t)kWaves * kp.lds_copy_bytes <= 48 * 1024 ? kWaves : 1;
+        return stage_bytes + (size_t)kp.lds_copies * kp.lds_copy_bytes;
+      };
+      size_t l = layout(true);
+      const int bpc = std::min<int>(4, (int)std::max<size_t>(1, (160 * 1024) / l));
+      const int64_t grid_est = std::max<int64_t>(1, std::min<int64_t>((int64_t)chunks.size(), (int64_t)ctx->num_cus * bpc));
+      const double wg_docs = (double)((int64_t)chunks.size() + grid_est - 1) / grid_est * mcw * 64.0;
+      kp.lds_pack = wg_docs < 16777216.0 && wg_docs * (double)vrange < 1099511627776.0;
+      if (!kp.lds_pack) l = layout(false);
+      kp.part_vbase = nvals ? vmin : 0;
+      if ((size_t)kp.lds_copy_bytes > 64 * 1024) kp.lds_fast = 0;  // not expected: G is an LDS-sized key space
+      else lds = std::max(lds, l);
+    }
     // 160 KiB of LDS per CU (gfx950); HLL registers of a large log2m do not fit beside the staging areas
     if (lds > 160 * 1024) fail(PH_ERR_UNSUPPORTED, "aggregation state exceeds the LDS of one CU (HLL log2m too large)");
   }
