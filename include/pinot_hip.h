@@ -172,6 +172,12 @@ int ph_ctx_set_stream(ph_ctx* ctx, void* hip_stream);
 
 /* ------------------------------------------------------------------ segments */
 int ph_segment_pin(ph_ctx* ctx, const ph_segment_desc* desc, ph_segment** out);
+/* Pin a segment straight from its on-disk directory (replaces ImmutableSegmentLoader.load's index-buffer path,
+ * ImmutableSegmentLoader.java / SingleFileIndexDirectory.java:72,213-305): V3 (<dir>/v3/: metadata.properties,
+ * index_map, columns.psf) or V1 (one file per index).  `columns` (NULL / 0: every single-value dictionary column)
+ * selects the columns to pin; a requested raw or multi-value column is PH_ERR_UNSUPPORTED. */
+int ph_segment_load_dir(ph_ctx* ctx, const char* segment_dir, const char* const* columns, int32_t num_columns,
+                        ph_segment** out);
 int ph_segment_unpin(ph_segment* seg);
 /* HBM held for the segment: its pinned columns plus the per-column caches queries derived from them
  * (re-encoded value streams, HLL hash tables, dictId remaps to table-level dictionaries). */

@@ -93,6 +93,15 @@ int ph_segment_pin(ph_ctx* ctx, const ph_segment_desc* desc, ph_segment** out) {
   });
 }
 
+int ph_segment_load_dir(ph_ctx* ctx, const char* segment_dir, const char* const* columns, int32_t num_columns,
+                        ph_segment** out) {
+  return guarded([&] {
+    if (!ctx || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    *out = segment_load_dir_impl(&ctx->c, segment_dir, columns, num_columns);
+  });
+}
+
 int ph_segment_unpin(ph_segment* seg) {
   return guarded([&] {
     if (!seg) return;

@@ -474,6 +474,8 @@ void launch_fill_i64(int64_t* p, int64_t v, int64_t n, hipStream_t s);
 void launch_hll_table(const void* values, int32_t is_int, int64_t n, int log2m, uint32_t* out, hipStream_t s);
 
 void build_bitmap_directory(Column& c);  // at pin, from c.inverted
+ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc);
+ph_segment* segment_load_dir_impl(Context* ctx, const char* dir, const char* const* columns, int32_t num_columns);
 void launch_roaring_or(const RoaringContainer* c, int n, const uint8_t* base, uint32_t* bitmap, int32_t num_docs,
                        hipStream_t s);
 void launch_selftest_unpack(const uint32_t* fwd, int64_t n, int bits, int32_t* out, hipStream_t s);

@@ -75,11 +75,29 @@ class IntermediateResult:
         return out
 
 
+def check_plan_supported(q: QueryContext):
+    """The plan maker's GPU gate for query options whose reference semantics the GPU path does not reproduce;
+    the caller then runs the CPU plan (GpuInstancePlanMaker falls back to InstancePlanMakerImplV2).
+
+    * Segment group trim (GroupByOperator.java:118-130): with ORDER BY and ``minSegmentGroupTrimSize`` > 0 each
+      segment keeps only its top max(5 * limit, minSegmentGroupTrimSize) groups by the ORDER BY values
+      (GroupByUtils.getTableCapacity) before the combine, so the reference's result is an approximation that
+      depends on per-segment partial aggregates.  The GPU aggregates all segments in one pass (exact), hence
+      UNSUPPORTED rather than a different answer.  The default (-1, InstancePlanMakerImplV2.java:97) is off.
+    * Server trim (IndexedTable.java:63-91, resize when the table exceeds ``groupTrimThreshold``) needs no gate:
+      its finish keeps the top records by the same ORDER BY, so the broker's final ORDER BY ... LIMIT over the
+      GPU's exact (untrimmed) groups is the same result whenever the reference's own merge is exact."""
+    seg_trim = int(q.options.get("minSegmentGroupTrimSize", -1))
+    if q.group_by and q.order_by and seg_trim > 0:
+        raise N.UnsupportedError(N.PH_ERR_UNSUPPORTED, "minSegmentGroupTrimSize > 0 (segment group trim)")
+
+
 class _QueryStruct:
     """Builds the ph_query POD graph and keeps every buffer alive while the call runs.  ``timeoutMs`` (query
     option) becomes the call's end time; ``interrupt`` is a ctypes.c_int32 another thread may set."""
 
     def __init__(self, q: QueryContext, interrupt=None):
+        check_plan_supported(q)
         self.keep = []
         nodes: List[N.FilterNode] = []
         preds: List[N.Predicate] = []
@@ -192,6 +210,12 @@ class GpuContext:
 
     def pin(self, buffers: SegmentBuffers) -> PinnedSegment:
         seg = PinnedSegment(self, buffers)
+        self._segments.add(seg)
+        return seg
+
+    def load_segment_dir(self, path: str, columns=None) -> PinnedSegment:
+        """Pin a segment straight from its on-disk directory (V3 columns.psf or V1 files)."""
+        seg = PinnedSegment.from_dir(self, path, columns)
         self._segments.add(seg)
         return seg
 

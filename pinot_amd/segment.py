@@ -202,6 +202,23 @@ def create_segment(name: str, columns: Dict[str, tuple], inverted: Sequence[str]
 class PinnedSegment:
     """An immutable segment resident in HBM (ph_segment)."""
 
+    @classmethod
+    def from_dir(cls, ctx, path: str, columns=None) -> "PinnedSegment":
+        """ph_segment_load_dir: pin a V3 / V1 segment directory (columns: names to pin, None = every single-value
+        dictionary column)."""
+        self = cls.__new__(cls)
+        self.ctx = ctx
+        self.buffers = None
+        self.handle = None
+        cols = list(columns or [])
+        arr = (ctypes.c_char_p * max(1, len(cols)))(*[c.encode() for c in cols])
+        h = ctypes.c_void_p()
+        N.check(N.lib().ph_segment_load_dir(ctx.handle, path.encode(), arr, len(cols), ctypes.byref(h)))
+        self.handle = h
+        self.num_docs = N.lib().ph_segment_num_docs(h)
+        self.name = path
+        return self
+
     def __init__(self, ctx, buffers: SegmentBuffers):
         self.ctx = ctx
         self.name = buffers.name

@@ -138,3 +138,17 @@ def test_sql_parser_shapes():
     assert [a.function for a in q.aggregations] == ["SUM", "COUNT", "MIN", "MAX"]
     q = parse_sql("SELECT COUNT(*) FROM t WHERE a NOT IN ('x', 'y') AND (b < 3 OR NOT c = 'q')")
     assert q.filter.type == "AND" and q.filter.children[1].type == "OR"
+
+
+def test_segment_group_trim_gate():
+    # minSegmentGroupTrimSize > 0 with ORDER BY: the reference trims per segment (an approximation), so the GPU
+    # plan declines (UNSUPPORTED -> CPU plan); -1 (the default) and queries without ORDER BY stay on the GPU path
+    from pinot_amd.engine import check_plan_supported
+    from pinot_amd.native import UnsupportedError
+    from pinot_amd.query import parse_sql
+    base = "SELECT a, SUM(m) FROM t GROUP BY a"
+    with pytest.raises(UnsupportedError):
+        check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=100; " + base + " ORDER BY SUM(m) DESC LIMIT 5"))
+    check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=-1; " + base + " ORDER BY SUM(m) DESC LIMIT 5"))
+    check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=100; " + base + " LIMIT 5"))
+    check_plan_supported(parse_sql(base + " ORDER BY a LIMIT 5"))
