@@ -159,8 +159,9 @@ typedef struct {
   int32_t sum_precision_flag;              /* 1 if an integer SUM reached 2^53 (double rounding differs) */
   double device_ms;                        /* kernel time of the query, HIP events */
   double host_ms;                          /* planning + result materialisation */
-  int32_t plan_mode;                       /* physical plan: -1 metadata, 0 count, 1 aggregation, 2 LDS
-                                              group table, 3 HBM atomic group table, 4 partitioned */
+  int32_t plan_mode;                       /* physical plan: -2 index-only count (FastFilteredCount), -1
+                                              metadata, 0 count, 1 aggregation, 2 LDS group table, 3 HBM
+                                              atomic group table, 4 partitioned, 5 HBM hash group table */
   int32_t reserved;
 } ph_exec_stats;
 

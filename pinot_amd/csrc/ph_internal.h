@@ -233,6 +233,7 @@ struct KParams {
   int32_t num_parts;
   int32_t part_load_first;        // lean kernel A: issue the next tile's loads before the flush (tuning)
   int32_t agg_fast;               // MODE_AGG: run k_agg_lean
+  int32_t agg_sparse;             // MODE_AGG over selective bitmap leaves: run k_agg_sparse
   int32_t lds_fast;               // MODE_GROUP_LDS: run k_group_lds_lean
   int32_t lds_pack;               //   COUNT << 40 | SUM in one 64-bit LDS word
   int32_t lds_copies;             //   table copies (one per wave when they fit)

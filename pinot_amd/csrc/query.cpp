@@ -1407,8 +1407,23 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if ((d.fkind != FK_ALL && d.fkind != FK_RANGE && d.fkind != FK_DOCRANGE) ||
         (nvals == 1 && d.vals[0].kind != VK_PACKED))
       kp.lds_fast = 0;
+  // selective inverted-index leaves (k_agg_sparse): every segment's filter is one bitmap leaf and together they
+  // match < 1/8 of the docs -> gather the matched docs' values instead of streaming the columns
+  {
+    bool all_bitmap = mode == MODE_AGG && !dsegs.empty();
+    for (int j = 0; j < nvals; ++j) all_bitmap = all_bitmap && !val_exprs[j];
+    for (auto& d : dsegs) all_bitmap = all_bitmap && d.fkind == FK_BITMAP;
+    int64_t docs = 0, hits = 0;
+    if (all_bitmap) {
+      for (auto& d : dsegs) docs += d.num_docs;
+      for (auto& fb : fbitmap_fix) hits += bitmap_docs(*pl.bitmaps[fb.second].col, pl.bitmaps[fb.second].dict_ids);
+    }
+    kp.agg_sparse = all_bitmap && hits * 8 < docs;
+    if (const char* e = getenv("PH_AGG_SPARSE")) kp.agg_sparse = all_bitmap && atoi(e) != 0;  // tuning knob
+    if (kp.agg_sparse) kp.agg_fast = 0;
+  }
   if (const char* e = getenv("PH_DEBUG_FLAGS")) kp.dbg_flags = atoi(e);
-  if (kp.dbg_flags) kp.part_fast = kp.agg_fast = kp.lds_fast = 0;  // timing experiments run on the generic form
+  if (kp.dbg_flags) kp.part_fast = kp.agg_fast = kp.lds_fast = kp.agg_sparse = 0;  // timing experiments: generic form
   if (getenv("PH_DEBUG_STAMPS")) {
     kp.dbg = scratch.alloc<unsigned long long>(4 * (size_t)ctx->num_cus * 8);
     PH_HIP_CHECK(hipMemsetAsync(kp.dbg, 0, 32 * (size_t)ctx->num_cus * 8, st));
@@ -1448,6 +1463,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       kp.part_vbase = nvals ? vmin : 0;
       if ((size_t)kp.lds_copy_bytes > 64 * 1024) kp.lds_fast = 0;  // not expected: G is an LDS-sized key space
       else lds = std::max(lds, l);
+    }
+    if (kp.agg_sparse) {  // no staging: only the HLL registers live in LDS
+      kp.lds_hll_off = 0;
+      lds = (size_t)num_hll * (m ? m : 1) * 4 + 16;
     }
     // 160 KiB of LDS per CU (gfx950); HLL registers of a large log2m do not fit beside the staging areas
     if (lds > 160 * 1024) fail(PH_ERR_UNSUPPORTED, "aggregation state exceeds the LDS of one CU (HLL log2m too large)");

@@ -122,7 +122,106 @@ __global__ void __launch_bounds__(kBlock) k_agg_lean(const KParams p) {
   }
 }
 
+// ------------------------------------------------------------------ sparse MODE_AGG (selective bitmap leaves)
+// k_agg_sparse serves aggregation-only queries whose every segment is filtered by an inverted-index bitmap that
+// matches few docs (InvertedIndexFilterOperator -> DocIdSetOperator -> AggregationOperator): instead of streaming
+// the aggregated columns through the staging tiles, a wave walks the doc bitmap 64 docs at a time, skips empty
+// words, and gathers the value / HLL entry of each matched doc straight from its packed stream.  At 1 %
+// selectivity a 24-bit column is touched on ~19 % of its 64-byte sectors instead of all
+// of them.  Values: read_value on the gathered code (packed offset or dictId); HLL: the segment's per-dictId
+// (register, rank) table, registers in LDS (as k_scan<MODE_AGG>).
+__global__ void __launch_bounds__(kBlock) k_agg_sparse(const KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int WAVES = kWaves;
+  constexpr int UW = 4;  // words per wave per step: independent gathers in flight
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int m = 1 << p.log2m;
+  SegPtr segs = (SegPtr)p.segs;
+  const PH_CONST Chunk* chunks = (const PH_CONST Chunk*)p.chunks;
+  uint32_t* lds_hll = reinterpret_cast<uint32_t*>(smem + p.lds_hll_off);
+  for (int i = threadIdx.x; i < p.num_hll * m; i += kBlock) lds_hll[i] = 0;
+  __syncthreads();
+  int64_t isum[kMaxVals], vmin[kMaxVals], vmax[kMaxVals];
+  double dsum[kMaxVals];
+#pragma unroll
+  for (int j = 0; j < kMaxVals; ++j) {
+    isum[j] = 0;
+    dsum[j] = 0.0;
+    vmin[j] = INT64_MAX;
+    vmax[j] = INT64_MIN;
+  }
+  unsigned long long matched = 0;
+  const int64_t nch = p.chunk_end - p.chunk_begin;
+  const int32_t c0 = p.chunk_begin + (int32_t)(nch * blockIdx.x / gridDim.x);
+  const int32_t c1 = p.chunk_begin + (int32_t)(nch * (blockIdx.x + 1) / gridDim.x);
+  for (int32_t c = c0; c < c1; ++c) {
+    SegPtr S = segs + chunks[c].seg;
+    const uint32_t ndocs = (uint32_t)S->num_docs;
+    const uint32_t* bm = S->fptr;
+    for (int32_t w = chunks[c].word_begin + wave * UW; w < chunks[c].word_end; w += WAVES * UW) {
+      uint32_t hitmask = 0;
+#pragma unroll
+      for (int u = 0; u < UW; ++u) {
+        const uint32_t doc = (uint32_t)(w + u) * 64u + (uint32_t)lane;
+        const bool in = (w + u < chunks[c].word_end) & (doc < ndocs);
+        const bool hit = in && ((gld(bm + (min(doc, ndocs - 1) >> 5)) >> (doc & 31u)) & 1u);
+        matched += (uint32_t)__popcll(__ballot(hit));
+        hitmask |= (hit ? 1u : 0u) << u;
+      }
+      if (!__ballot(hitmask != 0)) continue;
+#pragma unroll
+      for (int u = 0; u < UW; ++u) {
+        if (!((hitmask >> u) & 1u)) continue;
+        const uint32_t doc = (uint32_t)(w + u) * 64u + (uint32_t)lane;
+        for (int j = 0; j < p.num_vals && j < kMaxVals; ++j) {
+          const PH_CONST DevValCol& vc = S->vals[j];
+          int64_t iv;
+          double dv;
+          read_value(vc.kind, vc.base, vc.table, unpack_bits(vc.fwd, vc.bits, doc), iv, dv);
+          const int ops = p.val_ops[j];
+          if (ops & OPS_SUM) {
+            if (p.val_is_int[j]) isum[j] += iv; else dsum[j] += dv;
+          }
+          if (ops & OPS_MIN) vmin[j] = iv < vmin[j] ? iv : vmin[j];
+          if (ops & OPS_MAX) vmax[j] = iv > vmax[j] ? iv : vmax[j];
+        }
+        for (int h = 0; h < p.num_hll && h < kMaxHll; ++h) {
+          ColRef col = S->cols[p.hll_slot[h]];
+          const uint32_t e = gld(col.hll + unpack_col(col, doc));
+          atomicMax(&lds_hll[h * m + (e >> 8)], e & 0xffu);
+        }
+      }
+    }
+  }
+  // epilogue: one set of device atomics per wave, registers once per workgroup
+  for (int j = 0; j < p.num_vals && j < kMaxVals; ++j) {
+    const int64_t si = wave_sum_i64(isum[j]);
+    const double sd = wave_sum_f64(dsum[j]);
+    const int64_t mn = wave_min_i64(vmin[j]);
+    const int64_t mx = wave_max_i64(vmax[j]);
+    if (lane == 0) {
+      const int ops = p.val_ops[j];
+      if (ops & OPS_SUM) {
+        if (p.val_is_int[j]) atomicAdd(reinterpret_cast<unsigned long long*>(p.out_sum[j]), (unsigned long long)si);
+        else atomicAdd(reinterpret_cast<double*>(p.out_sum[j]), sd);
+      }
+      if ((ops & OPS_MIN) && mn != INT64_MAX) atomicMin(reinterpret_cast<long long*>(p.out_min[j]), (long long)mn);
+      if ((ops & OPS_MAX) && mx != INT64_MIN) atomicMax(reinterpret_cast<long long*>(p.out_max[j]), (long long)mx);
+    }
+  }
+  if (lane == 0 && matched) atomicAdd(&p.out_count[0], matched);
+  __syncthreads();
+  for (int i = threadIdx.x; i < p.num_hll * m; i += kBlock)
+    if (lds_hll[i]) atomicMax(&p.out_hll[i], lds_hll[i]);
+}
+
 void launch_scan_agg(const KParams& p, int mode, int grid, size_t lds, hipStream_t s) {
+  if (mode == MODE_AGG && p.agg_sparse) {
+    allow_lds(k_agg_sparse, lds);
+    hipLaunchKernelGGL(k_agg_sparse, dim3(grid), dim3(kBlock), lds, s, p);
+    return;
+  }
   if (mode == MODE_COUNT) {
     launch_late<MODE_COUNT, 0, 0>(p, grid, lds, s);
   } else if (p.agg_fast) {
