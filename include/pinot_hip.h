@@ -79,6 +79,12 @@ typedef struct {
    * (BitmapInvertedIndexWriter.java:33-96); NULL when the column has none */
   const void* inverted_index;
   uint64_t inverted_index_size;
+  /* 1: forward_index is a raw (no-dictionary) single-value chunk forward index of a fixed-width stored type
+   * (FixedByteChunkSVForwardIndexReader / FixedBytePower2ChunkSVForwardIndexReader format,
+   * BaseChunkForwardIndexReader.java:57-105; PASS_THROUGH, LZ4, LZ4_LENGTH_PREFIXED or SNAPPY chunks), as
+   * ForwardIndexReaderFactory.createRawIndexReader (:75-82) reads it; cardinality, bits_per_element and the
+   * dictionary are then ignored (the pin decodes the values once and dictionary-encodes them in HBM) */
+  int32_t raw_forward_index;
 } ph_column_desc;
 
 typedef struct {
@@ -175,8 +181,9 @@ int ph_ctx_set_stream(ph_ctx* ctx, void* hip_stream);
 int ph_segment_pin(ph_ctx* ctx, const ph_segment_desc* desc, ph_segment** out);
 /* Pin a segment straight from its on-disk directory (replaces ImmutableSegmentLoader.load's index-buffer path,
  * ImmutableSegmentLoader.java / SingleFileIndexDirectory.java:72,213-305): V3 (<dir>/v3/: metadata.properties,
- * index_map, columns.psf) or V1 (one file per index).  `columns` (NULL / 0: every single-value dictionary column)
- * selects the columns to pin; a requested raw or multi-value column is PH_ERR_UNSUPPORTED. */
+ * index_map, columns.psf) or V1 (one file per index).  `columns`
+ * selects the columns to pin (NULL / 0: every single-value dictionary or fixed-width raw column); a requested
+ * multi-value or variable-width raw column is PH_ERR_UNSUPPORTED. */
 int ph_segment_load_dir(ph_ctx* ctx, const char* segment_dir, const char* const* columns, int32_t num_columns,
                         ph_segment** out);
 int ph_segment_unpin(ph_segment* seg);
@@ -256,6 +263,12 @@ int ph_dense_finalize(ph_ctx* ctx, const ph_query* query, ph_segment* const* seg
                       const void* const* device_tables, int64_t group_begin, int64_t group_end, ph_result** out);
 
 /* ------------------------------------------------------------------ segment creation helper */
+/* Raw forward index reader (BaseChunkForwardIndexReader / FixedByteChunkSVForwardIndexReader.getInt/getLong/
+ * getFloat/getDouble over docs [0, num_docs)): decodes `buf` into num_docs native-endian values of `data_type`
+ * (INT int32, LONG int64, FLOAT float, DOUBLE double) at `out`.  Host-only; what ph_segment_pin runs on a raw
+ * column. */
+int ph_raw_forward_index_read(const void* buf, uint64_t size, int32_t data_type, int32_t num_docs, void* out);
+
 /* FixedBitSVForwardIndexWriter: packs n dictIds with `bits` bits, MSB-first big-endian; out_size >=
  * (n*bits+7)/8 */
 int ph_fixed_bit_pack(const int32_t* dict_ids, int64_t n, int32_t bits, uint8_t* out, uint64_t out_size);

@@ -345,6 +345,13 @@ int ph_selftest_unpack_staged(ph_ctx* ctx, const uint8_t* packed, uint64_t packe
   });
 }
 
+int ph_raw_forward_index_read(const void* buf, uint64_t size, int32_t data_type, int32_t num_docs, void* out) {
+  return guarded([&] {
+    if (!buf || !out || num_docs < 0) ph::fail(PH_ERR_INVALID_ARGUMENT, "null buffer or negative num_docs");
+    ph::raw_forward_index_decode(static_cast<const uint8_t*>(buf), size, data_type, num_docs, out);
+  });
+}
+
 int ph_fixed_bit_pack(const int32_t* dict_ids, int64_t n, int32_t bits, uint8_t* out, uint64_t out_size) {
   return guarded([&] {
     if (n < 0 || bits < 1 || bits > 31 || (n > 0 && (!dict_ids || !out)))

@@ -7,7 +7,7 @@
 //     0xdeadbeefdeafbead followed by the payload; `size` counts the magic (SingleFileIndexDirectory.java:72,
 //     170-204, 213-305).
 //   V1 (older segments): one file per index, <col>.dict, <col>.sv.unsorted.fwd / <col>.sv.sorted.fwd,
-//     <col>.bitmap.inv (V1Constants.java Indexes / Dict).
+//     <col>.sv.raw.fwd (no-dictionary columns), <col>.bitmap.inv (V1Constants.java Indexes / Dict).
 //
 // metadata.properties keys (V1Constants.MetadataKeys, SegmentColumnarIndexCreator.addColumnMetadataInfo
 // :519-541): segment.name, segment.total.docs, column.<col>.{cardinality, dataType, bitsPerElement,
@@ -225,16 +225,27 @@ ph_segment* segment_load_dir_impl(Context* ctx, const char* dir_c, const char* c
     const std::string* hd = prop("hasDictionary");
     const bool single = !sv || *sv == "true";
     const bool dict = !hd || *hd == "true";
-    if (!single || !dict) {
-      if (explicit_cols)
-        fail(PH_ERR_UNSUPPORTED, "column " + c + ": only single-value dictionary-encoded columns are on the GPU path");
-      continue;  // stays with the CPU plan (raw / multi-value columns)
-    }
     const std::string* dt = prop("dataType");
     if (!dt) fail(PH_ERR_INVALID_ARGUMENT, "column " + c + " without dataType");
+    const bool fixed_raw = !dict && *dt != "STRING" && *dt != "BYTES" && *dt != "JSON" && *dt != "BIG_DECIMAL";
+    if (!single || (!dict && !fixed_raw)) {
+      if (explicit_cols)
+        fail(PH_ERR_UNSUPPORTED, "column " + c + ": only single-value dictionary or fixed-width raw columns are on the GPU path");
+      continue;  // stays with the CPU plan (multi-value / variable-width raw columns)
+    }
     ph_column_desc d{};
     d.name = c.c_str();
     d.data_type = data_type_of(*dt, c);
+    if (!dict) {
+      // raw forward index (ForwardIndexReaderFactory.createRawIndexReader): V3 index "forward_index", V1
+      // <col>.sv.raw.fwd (V1Constants.Indexes.RAW_SV_FORWARD_INDEX_FILE_EXTENSION)
+      d.raw_forward_index = 1;
+      const bool ok = v3 ? v3_buffer(c, "forward_index", &d.forward_index, &d.forward_index_size)
+                         : v1_buffer(c + ".sv.raw.fwd", false, &d.forward_index, &d.forward_index_size);
+      if (!ok) fail(PH_ERR_INVALID_ARGUMENT, "column " + c + ": raw forward index missing");
+      descs.push_back(d);
+      continue;
+    }
     d.cardinality = (int32_t)std::stol(*prop("cardinality"));
     d.bits_per_element = prop("bitsPerElement") ? (int32_t)std::stol(*prop("bitsPerElement")) : 0;
     d.is_sorted = prop("isSorted") && *prop("isSorted") == "true";

@@ -345,6 +345,7 @@ struct Column {
   int32_t cardinality = 0;
   int32_t bits = 1;
   bool is_sorted = false;
+  bool is_raw = false;                // pinned from a raw forward index (dictionary-encoded at pin)
   Dictionary dict;
   std::vector<int32_t> sorted_ranges;  // [card][2] (sorted columns)
   std::vector<uint8_t> inverted;       // host copy of the inverted index (offsets + roaring blobs)
@@ -519,6 +520,10 @@ int32_t murmur_hash_long(int64_t v);
 int32_t murmur_hash_bytes(const uint8_t* data, int32_t len, int32_t seed);
 uint32_t hll_entry(int32_t hash, int log2m);
 void fixed_bit_pack_host(const int32_t* ids, int64_t n, int bits, uint8_t* out);
+// raw (no-dictionary) forward indexes (rawfwd.cpp): decode a chunk forward index to native values, and
+// dictionary-encode native values (sorted distinct values + per-doc ids)
+void raw_forward_index_decode(const uint8_t* buf, uint64_t size, int32_t data_type, int64_t num_docs, void* out);
+void raw_dictionary_encode(int32_t data_type, const void* values, int64_t n, Dictionary* dict, std::vector<int32_t>* ids);
 
 }  // namespace ph
 

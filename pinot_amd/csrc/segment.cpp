@@ -396,18 +396,37 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
     col->data_type = d.data_type;
     col->cardinality = d.cardinality;
     col->is_sorted = d.is_sorted != 0;
-    if (d.cardinality <= 0 && n > 0) fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": cardinality <= 0");
-    if (!d.dictionary) fail(PH_ERR_UNSUPPORTED, "column " + col->name + ": raw (no-dictionary) columns are not on the GPU path");
-    parse_dictionary(d, &col->dict);
-    // PinotDataBitSet.getNumBitsPerValue(cardinality - 1)
-    int bits = 1;
-    while (bits < 31 && ((int64_t)1 << bits) < (int64_t)d.cardinality) bits++;
+    col->is_raw = d.raw_forward_index != 0;
     const uint8_t* fwd = static_cast<const uint8_t*>(d.forward_index);
     if (!fwd) fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": missing forward index");
     std::vector<uint8_t> packed;
     const uint8_t* src = fwd;
     uint64_t src_bytes = d.forward_index_size;
-    if (col->is_sorted) {
+    int64_t card = d.cardinality;
+    if (col->is_raw) {
+      // raw (no-dictionary) column: decode the chunks once, dictionary-encode (rawfwd.cpp) and pin the packed form
+      if (d.inverted_index) fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": raw column with an inverted index");
+      col->is_sorted = false;
+      const int w = (d.data_type == PH_LONG || d.data_type == PH_DOUBLE) ? 8 : 4;
+      std::vector<uint8_t> vals((size_t)n * w);
+      raw_forward_index_decode(fwd, d.forward_index_size, d.data_type, n, vals.data());
+      raw_dictionary_encode(d.data_type, vals.data(), n, &col->dict, &ids);
+      card = col->dict.size;
+      col->cardinality = (int32_t)card;
+    } else {
+      if (d.cardinality <= 0 && n > 0) fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": cardinality <= 0");
+      if (!d.dictionary) fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": no dictionary and not marked raw");
+      parse_dictionary(d, &col->dict);
+    }
+    // PinotDataBitSet.getNumBitsPerValue(cardinality - 1)
+    int bits = 1;
+    while (bits < 31 && ((int64_t)1 << bits) < card) bits++;
+    if (col->is_raw) {
+      packed.assign((size_t)((n * bits + 7) / 8), 0);
+      fixed_bit_pack_host(ids.data(), n, bits, packed.data());
+      src = packed.data();
+      src_bytes = packed.size();
+    } else if (col->is_sorted) {
       // SortedIndexReaderImpl: int32 BE (start, end) per dictId; expand to the packed fixed-bit form
       if (d.forward_index_size < (uint64_t)8 * d.cardinality)
         fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": sorted index too small");
@@ -439,16 +458,16 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
     seg->device_bytes += alloc;
     // dictionary values widened for arithmetic
     if (d.data_type != PH_STRING) {
-      col->d_values.alloc(sizeof(int64_t) * std::max<int64_t>(1, d.cardinality), ctx->device);
+      col->d_values.alloc(sizeof(int64_t) * std::max<int64_t>(1, card), ctx->device);
       const void* vsrc = (d.data_type == PH_INT || d.data_type == PH_LONG) ? (const void*)col->dict.ints.data()
                                                                            : (const void*)col->dict.reals.data();
-      PH_HIP_CHECK(hipMemcpyAsync(col->d_values.ptr, vsrc, sizeof(int64_t) * d.cardinality, hipMemcpyHostToDevice,
+      PH_HIP_CHECK(hipMemcpyAsync(col->d_values.ptr, vsrc, sizeof(int64_t) * card, hipMemcpyHostToDevice,
                                   st));
       seg->device_bytes += col->d_values.bytes;
     }
     if (d.inverted_index && d.inverted_index_size) {
       const uint8_t* inv = static_cast<const uint8_t*>(d.inverted_index);
-      if (d.inverted_index_size < (uint64_t)4 * (d.cardinality + 1))
+      if (d.inverted_index_size < (uint64_t)4 * (card + 1))
         fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": inverted index too small");
       col->inverted.assign(inv, inv + d.inverted_index_size);
       build_bitmap_directory(*col);

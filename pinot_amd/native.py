@@ -51,7 +51,8 @@ class ColumnDesc(ctypes.Structure):
                 ("forward_index", ctypes.c_void_p), ("forward_index_size", ctypes.c_uint64),
                 ("dictionary", ctypes.c_void_p), ("dictionary_size", ctypes.c_uint64),
                 ("dictionary_entry_size", ctypes.c_int32),
-                ("inverted_index", ctypes.c_void_p), ("inverted_index_size", ctypes.c_uint64)]
+                ("inverted_index", ctypes.c_void_p), ("inverted_index_size", ctypes.c_uint64),
+                ("raw_forward_index", ctypes.c_int32)]
 
 
 class SegmentDesc(ctypes.Structure):
@@ -115,7 +116,8 @@ EXPORTED_SYMBOLS = (
     "ph_segment_device_bytes", "ph_segment_num_docs", "ph_table_set_dictionary", "ph_table_set_column_type", "ph_query_execute",
     "ph_result_destroy", "ph_result_stats", "ph_result_num_groups", "ph_result_key_entry_size", "ph_result_key_type",
     "ph_result_group_keys", "ph_result_aggregation", "ph_result_key_data", "ph_result_aggregation_data",
-    "ph_query_dense_layout", "ph_query_execute_dense", "ph_dense_finalize", "ph_fixed_bit_pack", "ph_selftest_unpack",
+    "ph_query_dense_layout", "ph_query_execute_dense", "ph_dense_finalize", "ph_fixed_bit_pack",
+    "ph_raw_forward_index_read", "ph_selftest_unpack",
     "ph_selftest_unpack_staged", "ph_last_error", "ph_version",
 )
 
@@ -178,6 +180,7 @@ def lib():
         "ph_dense_finalize": ([vp, ctypes.POINTER(Query), ctypes.POINTER(vp), i32, ctypes.POINTER(vp), i64, i64,
                                ctypes.POINTER(vp)], ctypes.c_int),
         "ph_fixed_bit_pack": ([vp, i64, i32, vp, ctypes.c_uint64], ctypes.c_int),
+        "ph_raw_forward_index_read": ([vp, ctypes.c_uint64, i32, i32, vp], ctypes.c_int),
         "ph_selftest_unpack": ([vp, vp, ctypes.c_uint64, i64, i32, vp], ctypes.c_int),
         "ph_selftest_unpack_staged": ([vp, vp, ctypes.c_uint64, i64, i32, i32, vp], ctypes.c_int),
         "ph_last_error": ([], ctypes.c_char_p),

@@ -134,6 +134,7 @@ class ColumnBuffers:
     entry_size: int
     dictionary_values: np.ndarray   # native values (for tests / reduce)
     inverted_index: Optional[np.ndarray] = None
+    raw: bool = False               # forward_index is a raw chunk forward index (no dictionary)
 
 
 @dataclass
@@ -184,13 +185,152 @@ def create_column(name: str, values, data_type: str, inverted: bool = False, run
                                        run_optimize=run_optimize)
 
 
+# --------------------------------------------------------------------------- raw (no-dictionary) columns
+COMPRESSION = {"PASS_THROUGH": 0, "SNAPPY": 1, "ZSTANDARD": 2, "LZ4": 3, "LZ4_LENGTH_PREFIXED": 4}
+
+
+def _lz4_block(data: bytes) -> bytes:
+    """LZ4 block format (greedy 4-byte hash matches; the last 5 bytes stay literals, as the format requires)."""
+    n, out, anchor, i, table = len(data), bytearray(), 0, 0, {}
+
+    def lengths(v):
+        b = bytearray()
+        while v >= 255:
+            b.append(255)
+            v -= 255
+        b.append(v)
+        return b
+    while i + 12 <= n:
+        key = data[i:i + 4]
+        j = table.get(key)
+        table[key] = i
+        if j is None or i - j > 65535:
+            i += 1
+            continue
+        m = 4
+        while i + m < n - 5 and data[j + m] == data[i + m]:
+            m += 1
+        lit = i - anchor
+        out.append((min(lit, 15) << 4) | min(m - 4, 15))
+        if lit >= 15:
+            out += lengths(lit - 15)
+        out += data[anchor:i]
+        out += (i - j).to_bytes(2, "little")
+        if m - 4 >= 15:
+            out += lengths(m - 4 - 15)
+        i += m
+        anchor = i
+    lit = n - anchor
+    out.append(min(lit, 15) << 4)
+    if lit >= 15:
+        out += lengths(lit - 15)
+    out += data[anchor:]
+    return bytes(out)
+
+
+def _snappy(data: bytes) -> bytes:
+    """Snappy raw format: varint length, then literals and 2-byte-offset copies (greedy 4-byte hash matches)."""
+    n, out = len(data), bytearray()
+    v = n
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+
+    def literal(a, b):
+        ln = b - a - 1
+        if ln < 60:
+            out.append(ln << 2)
+        else:
+            nb = (ln.bit_length() + 7) // 8
+            out.append((59 + nb) << 2)
+            out.extend(ln.to_bytes(nb, "little"))
+        out.extend(data[a:b])
+    anchor, i, table = 0, 0, {}
+    while i + 4 <= n:
+        key = data[i:i + 4]
+        j = table.get(key)
+        table[key] = i
+        if j is None or i - j > 65535:
+            i += 1
+            continue
+        m = 4
+        while i + m < n and m < 64 and data[j + m] == data[i + m]:
+            m += 1
+        if anchor < i:
+            literal(anchor, i)
+        out.append(((m - 1) << 2) | 2)
+        out.extend((i - j).to_bytes(2, "little"))
+        i += m
+        anchor = i
+    if anchor < n:
+        literal(anchor, n)
+    return bytes(out)
+
+
+def write_raw_forward_index(values, data_type: str, compression: str = "PASS_THROUGH", version: int = 2,
+                            docs_per_chunk: int = 1000) -> np.ndarray:
+    """FixedByteChunkForwardIndexWriter / BaseChunkForwardIndexWriter (SingleValueFixedByteRawIndexCreator:
+    NUM_DOCS_PER_CHUNK 1000; version 4 rounds docs per chunk up to a power of 2): header, chunk offsets, chunks."""
+    vals = np.asarray(values, dtype=_NP[data_type])
+    width = vals.dtype.itemsize
+    if version >= 4 and docs_per_chunk & (docs_per_chunk - 1):
+        docs_per_chunk = 1 << (docs_per_chunk - 1).bit_length()
+    n = len(vals)
+    nchunks = (n + docs_per_chunk - 1) // docs_per_chunk
+    off_size = 4 if version == 2 else 8
+    header = 7 * 4 + nchunks * off_size
+    raw = vals.tobytes()
+    chunks, offsets, pos = [], [], header
+    for c in range(nchunks):
+        body = raw[c * docs_per_chunk * width:(c + 1) * docs_per_chunk * width]
+        if compression == "LZ4":
+            body = _lz4_block(body)
+        elif compression == "LZ4_LENGTH_PREFIXED":
+            body = len(body).to_bytes(4, "little") + _lz4_block(body)
+        elif compression == "SNAPPY":
+            body = _snappy(body)
+        elif compression != "PASS_THROUGH":
+            raise ValueError(compression)
+        offsets.append(pos)
+        chunks.append(body)
+        pos += len(body)
+    head = np.array([version, nchunks, docs_per_chunk, width, n, COMPRESSION[compression], 28], ">i4").tobytes()
+    head += np.array(offsets, ">i4" if off_size == 4 else ">i8").tobytes()
+    return np.frombuffer(head + b"".join(chunks), dtype=np.uint8)
+
+
+def read_raw_forward_index(buf: np.ndarray, data_type: str, num_docs: int) -> np.ndarray:
+    """ph_raw_forward_index_read: the library's host decoder of a raw forward index (native-endian values)."""
+    out = np.empty(num_docs, dtype=_NATIVE[data_type])
+    b = np.ascontiguousarray(buf, dtype=np.uint8)
+    N.check(N.lib().ph_raw_forward_index_read(b.ctypes.data, b.nbytes, N.DATA_TYPES[data_type], num_docs,
+                                              out.ctypes.data))
+    return out
+
+
+def create_raw_column(name: str, values, data_type: str, compression: str = "PASS_THROUGH", version: int = 2):
+    """A no-dictionary SV column (SingleValueFixedByteRawIndexCreator); dictionary_values keeps the sorted distinct
+    values for tests."""
+    vals = np.asarray(values, dtype=_NATIVE[data_type])
+    fwd = write_raw_forward_index(vals, data_type, compression, version)
+    uniq = np.unique(vals)
+    return ColumnBuffers(name, data_type, len(uniq), num_bits_per_value(len(uniq) - 1), False, fwd,
+                         np.zeros(0, np.uint8), vals.dtype.itemsize, uniq, None, True)
+
+
 def create_segment(name: str, columns: Dict[str, tuple], inverted: Sequence[str] = (),
-                   run_optimize: bool = False) -> SegmentBuffers:
-    """columns: name -> (values, data_type) -- SegmentIndexCreationDriverImpl for dictionary SV columns."""
+                   run_optimize: bool = False, raw: Sequence[str] = (), raw_compression: str = "PASS_THROUGH",
+                   raw_version: int = 2) -> SegmentBuffers:
+    """columns: name -> (values, data_type) -- SegmentIndexCreationDriverImpl for SV columns (dictionary-encoded, or
+    raw for the names in ``raw``: noDictionaryColumns)."""
     seg = SegmentBuffers(name, 0)
     n = None
     for c, (vals, dt) in columns.items():
-        seg.columns[c] = create_column(c, vals, dt, c in inverted, run_optimize)
+        if c in raw:
+            seg.columns[c] = create_raw_column(c, vals, dt, raw_compression, raw_version)
+        else:
+            seg.columns[c] = create_column(c, vals, dt, c in inverted, run_optimize)
         n = len(vals) if n is None else n
         if n != len(vals):
             raise ValueError("columns of different lengths")
@@ -243,6 +383,7 @@ class PinnedSegment:
             d.dictionary = dic.ctypes.data
             d.dictionary_size = dic.nbytes
             d.dictionary_entry_size = cb.entry_size
+            d.raw_forward_index = int(cb.raw)
             if cb.inverted_index is not None:
                 inv = np.ascontiguousarray(cb.inverted_index)
                 keep.append(inv)

@@ -4,7 +4,7 @@
   V3 = ``v3/metadata.properties`` + ``v3/index_map`` + ``v3/columns.psf`` with an 8-byte magic
   0xdeadbeefdeafbead before every buffer, ``size`` counting the magic (SingleFileIndexDirectory.java:72,170-204);
   V1 = one file per index (V1Constants.Indexes / Dict: ``.dict``, ``.sv.unsorted.fwd``, ``.sv.sorted.fwd``,
-  ``.bitmap.inv``).  Metadata keys: V1Constants.MetadataKeys, SegmentColumnarIndexCreator.addColumnMetadataInfo.
+  ``.sv.raw.fwd``, ``.bitmap.inv``); raw columns carry ``hasDictionary = false`` and only a forward index.  Metadata keys: V1Constants.MetadataKeys, SegmentColumnarIndexCreator.addColumnMetadataInfo.
 * ``read_dir`` is an independent reader of either layout that builds the CPU oracle's segment (the checker for
   ph_segment_load_dir).  ``tests/golden/v1_padding*`` are two V1 segments the reference itself wrote
   (pinot-core/src/test/resources/data/padding{Null,Old}.tar.gz).
@@ -16,6 +16,7 @@ import os
 import numpy as np
 
 from oracle import oracle as O
+from tests import raw_codecs as RC
 
 MAGIC = (0xDEADBEEFDEAFBEAD).to_bytes(8, "big")
 _NP = {"INT": ">i4", "LONG": ">i8", "FLOAT": ">f4", "DOUBLE": ">f8"}
@@ -31,7 +32,7 @@ def _metadata(seg, extra=None):
                   f"column.{key}.dataType = {cb.data_type}", f"column.{key}.bitsPerElement = {cb.bits}",
                   f"column.{key}.lengthOfEachEntry = {entry}", f"column.{key}.columnType = DIMENSION",
                   f"column.{key}.isSorted = {'true' if cb.is_sorted else 'false'}",
-                  f"column.{key}.hasDictionary = true",
+                  f"column.{key}.hasDictionary = {'false' if cb.raw else 'true'}",
                   f"column.{key}.hasInvertedIndex = {'true' if cb.inverted_index is not None else 'false'}",
                   f"column.{key}.isSingleValues = true"]
     for k, v in (extra or {}).items():
@@ -40,6 +41,8 @@ def _metadata(seg, extra=None):
 
 
 def _buffers(cb):
+    if cb.raw:  # no-dictionary column: the raw chunk forward index only
+        return [("forward_index", np.ascontiguousarray(cb.forward_index).tobytes())]
     out = [("dictionary", np.ascontiguousarray(cb.dictionary).tobytes()),
            ("forward_index", np.ascontiguousarray(cb.forward_index).tobytes())]
     if cb.inverted_index is not None:
@@ -66,7 +69,8 @@ def write_v1(seg, path):
     os.makedirs(path, exist_ok=True)
     open(os.path.join(path, "metadata.properties"), "w").write(_metadata(seg))
     for c, cb in seg.columns.items():
-        ext = {"dictionary": ".dict", "forward_index": ".sv.sorted.fwd" if cb.is_sorted else ".sv.unsorted.fwd",
+        ext = {"dictionary": ".dict", "forward_index": ".sv.raw.fwd" if cb.raw else
+               (".sv.sorted.fwd" if cb.is_sorted else ".sv.unsorted.fwd"),
                "inverted_index": ".bitmap.inv"}
         for idx, payload in _buffers(cb):
             open(os.path.join(path, c + ext[idx]), "wb").write(payload)
@@ -104,6 +108,13 @@ def read_dir(path):
         g = lambda k: meta[f"column.{c}.{k}"]  # noqa: E731
         dt, card, bits = g("dataType"), int(g("cardinality")), int(g("bitsPerElement"))
         srt = g("isSorted") == "true"
+        if meta.get(f"column.{c}.hasDictionary") == "false":  # raw: values -> sorted distinct dictionary + ids
+            fwd = buf(c, "forward_index") if v3 else open(os.path.join(d, c + ".sv.raw.fwd"), "rb").read()
+            values, ids = np.unique(RC.read_raw(fwd, dt, n), return_inverse=True)
+            b = O.num_bits_per_value(len(values) - 1) if len(values) > 1 else 1
+            out[c] = dict(dictionary=values, fwd=O.fixed_bit_pack(ids.astype(np.int32), b), bits=b, data_type=dt,
+                          num_docs=n)
+            continue
         if v3:
             dic, fwd = buf(c, "dictionary"), buf(c, "forward_index")
         else:

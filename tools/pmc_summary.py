@@ -12,7 +12,7 @@ import json
 import os
 import sys
 
-SCAN_KERNELS = ("k_scan", "k_part_agg", "k_merge_overflow", "k_compact")
+SCAN_KERNELS = ("k_scan", "k_part_scan", "k_part_agg", "k_agg", "k_group", "k_merge_overflow", "k_compact", "k_roaring", "k_hll")
 
 
 def totals(d, counter):
