@@ -225,6 +225,20 @@ const void* ph_result_key_data(const ph_result* r, int32_t group_by_index);
 int ph_result_aggregation(const ph_result* r, int32_t aggregation_index, void* out);
 const void* ph_result_aggregation_data(const ph_result* r, int32_t aggregation_index);
 
+/* ------------------------------------------------------------------ server -> broker DataTable */
+/* The result as the DataTable V4 bytes the reference's server returns for it (InstanceResponseBlock.toDataTable:
+ * GroupByResultsBlock.getDataTable :170 / AggregationResultsBlock.getDataTable, DataTableBuilderV4,
+ * DataTableImplV4.toBytes): group-by identifiers + one intermediate-result column per aggregation, results metadata
+ * (BaseResultsBlock.getResultsMetadata) followed by the caller's `extra` entries (e.g. numSegmentsQueried,
+ * timeUsedMs, requestId; MetadataKey names, DataTable.java:103-137), in java.util.HashMap order.  `q` is the query
+ * the result came from (column names).  out == NULL: only *size is set; otherwise capacity must be >= *size. */
+typedef struct {
+  const char* key;
+  const char* value;
+} ph_metadata_entry;
+int ph_result_datatable(const ph_result* r, const ph_query* q, const ph_metadata_entry* extra, int32_t num_extra,
+                        void* out, uint64_t capacity, uint64_t* size);
+
 /* ------------------------------------------------------------------ multi-GPU combine: dense partials */
 /* GroupByCombineOperator.mergeResults (GroupByCombineOperator.java:169-181) and
  * AggregationResultsBlockMerger (:33-45) merge per-segment results keyed by group VALUES.  Over table-level

@@ -345,6 +345,19 @@ int ph_selftest_unpack_staged(ph_ctx* ctx, const uint8_t* packed, uint64_t packe
   });
 }
 
+int ph_result_datatable(const ph_result* r, const ph_query* q, const ph_metadata_entry* extra, int32_t num_extra,
+                        void* out, uint64_t capacity, uint64_t* size) {
+  return guarded([&] {
+    if (!size || num_extra < 0 || (num_extra > 0 && !extra)) ph::fail(PH_ERR_INVALID_ARGUMENT, "bad arguments");
+    const auto bytes = ph::result_to_datatable(r, q, extra, num_extra);
+    *size = bytes.size();
+    if (out) {
+      if (capacity < bytes.size()) ph::fail(PH_ERR_INVALID_ARGUMENT, "DataTable buffer too small");
+      memcpy(out, bytes.data(), bytes.size());
+    }
+  });
+}
+
 int ph_raw_forward_index_read(const void* buf, uint64_t size, int32_t data_type, int32_t num_docs, void* out) {
   return guarded([&] {
     if (!buf || !out || num_docs < 0) ph::fail(PH_ERR_INVALID_ARGUMENT, "null buffer or negative num_docs");

@@ -232,6 +232,7 @@ struct KParams {
   int32_t part_vbits;             // value-offset bits in a record (0: COUNT only)
   int32_t num_parts;
   int32_t part_load_first;        // lean kernel A: issue the next tile's loads before the flush (tuning)
+  int32_t part_dbg;               // lean kernel A timing experiments (PH_PART_DBG; results invalid when set)
   int32_t agg_fast;               // MODE_AGG: run k_agg_lean
   int32_t agg_sparse;             // MODE_AGG over selective bitmap leaves: run k_agg_sparse
   int32_t lds_fast;               // MODE_GROUP_LDS: run k_group_lds_lean
@@ -523,6 +524,8 @@ void fixed_bit_pack_host(const int32_t* ids, int64_t n, int bits, uint8_t* out);
 // raw (no-dictionary) forward indexes (rawfwd.cpp): decode a chunk forward index to native values, and
 // dictionary-encode native values (sorted distinct values + per-doc ids)
 void raw_forward_index_decode(const uint8_t* buf, uint64_t size, int32_t data_type, int64_t num_docs, void* out);
+std::vector<uint8_t> result_to_datatable(const ph_result* r, const ph_query* q, const ph_metadata_entry* extra,
+                                         int32_t num_extra);
 void raw_dictionary_encode(int32_t data_type, const void* values, int64_t n, Dictionary* dict, std::vector<int32_t>* ids);
 
 }  // namespace ph

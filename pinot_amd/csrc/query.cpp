@@ -1585,6 +1585,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       // the next tile's loads go out before the flush (r2: 3.78 vs 4.39 ms on one box); PH_PART_FLUSH_FIRST
       // restores the r1 order
       kp.part_load_first = getenv("PH_PART_FLUSH_FIRST") == nullptr;
+      kp.part_dbg = getenv("PH_PART_DBG") ? atoi(getenv("PH_PART_DBG")) : 0;  // timing experiments only
       kp.part_vbits = vbits;
       kp.num_parts = (int32_t)P;
       const size_t lds_a = partition_lds_bytes(kp);

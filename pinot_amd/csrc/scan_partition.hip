@@ -73,6 +73,7 @@ __device__ __forceinline__ void part_tile(const KParams& p, SegPtr S, uint8_t* s
   const uint32_t dummy_word = (uint32_t)p.num_parts + (uint32_t)lane;
   const uint32_t dummy_slot = ((uint32_t)p.num_parts << cl) + (uint32_t)lane;
   uint32_t doc = (uint32_t)w0 * 64u + (uint32_t)lane;
+  const int dbg = p.part_dbg;  // timing experiments: 1 = no key/value decode, 2 = no appends
   for (int u = 0; u < nvalid; u += 4) {
     bool h[4];
     uint32_t widx[4], bk[4];
@@ -82,13 +83,18 @@ __device__ __forceinline__ void part_tile(const KParams& p, SegPtr S, uint8_t* s
       bool hh = (u + q < nvalid) & (doc < ndocs);
       if constexpr (FK == FK_RANGE) hh &= (lds_value(fs.off, fs.rsh, fs.mask) - flo) < flen;
       if constexpr (FK == FK_DOCRANGE) hh &= (doc - flo) < flen;
+      if (dbg & 2) hh = false;
       uint32_t key = 0;
+      uint32_t vo = 0;
+      if (!(dbg & 1)) {
 #pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        key += __umul24(lds_value(gs[g].off, gs[g].rsh, gs[g].mask), gstr[g]);  // keys < 2^22
-        gs[g].off += gs[g].step;
+        for (int g = 0; g < NG; ++g) key += __umul24(lds_value(gs[g].off, gs[g].rsh, gs[g].mask), gstr[g]);  // keys < 2^22
+        vo = HASV ? lds_value(vs.off, vs.rsh, vs.mask) + vadd : 0u;
+      } else {
+        key = ((doc * 2654435761u) >> 8) % ((uint32_t)p.num_parts << klo);  // in range, spread like real keys
       }
-      const uint32_t vo = HASV ? lds_value(vs.off, vs.rsh, vs.mask) + vadd : 0u;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) gs[g].off += gs[g].step;
       if (HASV) vs.off += vs.step;
       if (FK == FK_RANGE) fs.off += fs.step;
       doc += 64u;

@@ -256,6 +256,27 @@ class GpuContext:
             res._handle = handle
         return res
 
+    def execute_datatable(self, q: QueryContext, segments: Sequence[PinnedSegment], extra=None) -> bytes:
+        """The query's server response: ph_query_execute then ph_result_datatable (DataTable V4 bytes, as
+        InstanceResponseBlock.toDataTable).  ``extra``: metadata entries appended to the results metadata."""
+        qs = _QueryStruct(q)
+        segs = (ctypes.c_void_p * max(1, len(segments)))(*[s.handle for s in segments])
+        r = ctypes.c_void_p()
+        L = N.lib()
+        N.check(L.ph_query_execute(self.handle, ctypes.byref(qs.struct), segs, len(segments), ctypes.byref(r)))
+        try:
+            items = list((extra or {}).items())
+            keep = [(k.encode(), str(v).encode()) for k, v in items]
+            ents = (N.MetadataEntry * max(1, len(keep)))(*[N.MetadataEntry(k, v) for k, v in keep])
+            size = ctypes.c_uint64()
+            N.check(L.ph_result_datatable(r, ctypes.byref(qs.struct), ents, len(keep), None, 0, ctypes.byref(size)))
+            buf = (ctypes.c_uint8 * size.value)()
+            N.check(L.ph_result_datatable(r, ctypes.byref(qs.struct), ents, len(keep), buf, size.value,
+                                          ctypes.byref(size)))
+            return bytes(buf)
+        finally:
+            L.ph_result_destroy(r)
+
     @staticmethod
     def _read_result(q: QueryContext, r, copy: bool = True) -> IntermediateResult:
         L = N.lib()

@@ -55,6 +55,10 @@ class ColumnDesc(ctypes.Structure):
                 ("raw_forward_index", ctypes.c_int32)]
 
 
+class MetadataEntry(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_char_p), ("value", ctypes.c_char_p)]
+
+
 class SegmentDesc(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char_p), ("num_docs", ctypes.c_int32), ("num_columns", ctypes.c_int32),
                 ("columns", ctypes.POINTER(ColumnDesc))]
@@ -117,7 +121,7 @@ EXPORTED_SYMBOLS = (
     "ph_result_destroy", "ph_result_stats", "ph_result_num_groups", "ph_result_key_entry_size", "ph_result_key_type",
     "ph_result_group_keys", "ph_result_aggregation", "ph_result_key_data", "ph_result_aggregation_data",
     "ph_query_dense_layout", "ph_query_execute_dense", "ph_dense_finalize", "ph_fixed_bit_pack",
-    "ph_raw_forward_index_read", "ph_selftest_unpack",
+    "ph_raw_forward_index_read", "ph_result_datatable", "ph_selftest_unpack",
     "ph_selftest_unpack_staged", "ph_last_error", "ph_version",
 )
 
@@ -181,6 +185,8 @@ def lib():
                                ctypes.POINTER(vp)], ctypes.c_int),
         "ph_fixed_bit_pack": ([vp, i64, i32, vp, ctypes.c_uint64], ctypes.c_int),
         "ph_raw_forward_index_read": ([vp, ctypes.c_uint64, i32, i32, vp], ctypes.c_int),
+        "ph_result_datatable": ([vp, ctypes.POINTER(Query), ctypes.POINTER(MetadataEntry), i32, vp, ctypes.c_uint64,
+                                 ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
         "ph_selftest_unpack": ([vp, vp, ctypes.c_uint64, i64, i32, vp], ctypes.c_int),
         "ph_selftest_unpack_staged": ([vp, vp, ctypes.c_uint64, i64, i32, i32, vp], ctypes.c_int),
         "ph_last_error": ([], ctypes.c_char_p),
