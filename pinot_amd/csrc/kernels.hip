@@ -399,9 +399,12 @@ uint32_t hll_entry(int32_t hash, int log2m) { return hll_entry_of(hash, log2m); 
 // container payloads need not be 2-byte aligned inside the inverted-index buffer).
 __device__ __forceinline__ uint32_t ld_u16(const uint8_t* b) { return (uint32_t)b[0] | ((uint32_t)b[1] << 8); }
 
-__global__ void k_roaring_or(const RoaringContainer* __restrict__ cs, const uint8_t* __restrict__ base,
-                             uint32_t* __restrict__ bitmap, int32_t num_docs) {
+__global__ void k_roaring_or(const RoaringContainer* __restrict__ cs, const RoaringTarget* __restrict__ targets) {
   const RoaringContainer c = cs[blockIdx.x];
+  const RoaringTarget t = targets[c.target];
+  const uint8_t* base = t.base;
+  uint32_t* bitmap = t.bitmap;
+  const int32_t num_docs = t.num_docs;
   const uint8_t* pay = base + c.offset;
   const uint32_t hi = (uint32_t)c.key << 16;
   const uint32_t nwords = ((uint32_t)num_docs + 31u) >> 5;
@@ -432,10 +435,9 @@ __global__ void k_roaring_or(const RoaringContainer* __restrict__ cs, const uint
   }
 }
 
-void launch_roaring_or(const RoaringContainer* c, int n, const uint8_t* base, uint32_t* bitmap, int32_t num_docs,
-                       hipStream_t s) {
+void launch_roaring_or(const RoaringContainer* c, int n, const RoaringTarget* targets, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_roaring_or, dim3(n), dim3(256), 0, s, c, base, bitmap, num_docs);
+  hipLaunchKernelGGL(k_roaring_or, dim3(n), dim3(256), 0, s, c, targets);
   PH_HIP_CHECK(hipGetLastError());
 }
 

@@ -109,6 +109,7 @@ constexpr int kWaves = kBlock / 64;
 // the big LDS item: 8 waves per ring set doubles the resident waves per CU at the same ring footprint)
 constexpr int kPartBlock = 512;
 constexpr int kPartWaves = kPartBlock / 64;
+constexpr int kSparseStepWords = 64;              // k_agg_sparse: bitmap words (4096 docs) per wave step
 constexpr int kChunkWords = 256;                     // 16384 docs per chunk (a multiple of every round)
 constexpr int kInterruptChunks = 8192;               // an interruptible scan checks every 8192 chunks (~134M docs)
 // 16-byte-per-lane loads (1 KiB per wave-instruction) a wave keeps in flight per tile, over all streams
@@ -336,8 +337,16 @@ struct RoaringContainer {
   int32_t type;      // 0 array, 1 bitmap, 2 run
   int32_t key;       // high 16 bits
   int32_t card;      // array: cardinality; run: number of runs
-  int32_t pad;
+  int32_t target;    // launch time: index of the leaf's RoaringTarget (its inverted buffer and doc bitmap)
   uint64_t offset;   // byte offset of the payload in the device inverted buffer
+};
+
+// one inverted-index leaf of a query: the device inverted buffer its containers point into and its doc bitmap
+struct RoaringTarget {
+  const uint8_t* base;
+  uint32_t* bitmap;
+  int32_t num_docs;
+  int32_t pad;
 };
 
 struct Column {
@@ -479,8 +488,8 @@ void launch_hll_table(const void* values, int32_t is_int, int64_t n, int log2m, 
 void build_bitmap_directory(Column& c);  // at pin, from c.inverted
 ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc);
 ph_segment* segment_load_dir_impl(Context* ctx, const char* dir, const char* const* columns, int32_t num_columns);
-void launch_roaring_or(const RoaringContainer* c, int n, const uint8_t* base, uint32_t* bitmap, int32_t num_docs,
-                       hipStream_t s);
+// every container of every inverted leaf of a query in one launch (one workgroup per container)
+void launch_roaring_or(const RoaringContainer* c, int n, const RoaringTarget* targets, hipStream_t s);
 void launch_selftest_unpack(const uint32_t* fwd, int64_t n, int bits, int32_t* out, hipStream_t s);
 // numGroupsLimit: from one segment's first-doc-per-key table, the bitset of the keys the reference keeps
 void launch_limit_select(const uint32_t* first, int64_t G, int64_t limit, int32_t num_docs, uint32_t* docbits,

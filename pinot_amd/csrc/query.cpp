@@ -946,25 +946,34 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<uint32_t*> bitmap_dev(pl.bitmaps.size(), nullptr);
   auto build_bitmaps = [&]() {
     if (pl.bitmaps.empty() || dop == DENSE_LAYOUT || fin) return;
+    // all leaves' bitmaps in one zeroed block (each padded to whole 64-doc words + one), every container of every
+    // leaf OR-ed in by ONE launch
     std::vector<RoaringContainer> cs;
-    std::vector<size_t> first(pl.bitmaps.size() + 1, 0);
+    std::vector<RoaringTarget> tg(pl.bitmaps.size());
+    std::vector<size_t> woff(pl.bitmaps.size() + 1, 0);
     for (size_t i = 0; i < pl.bitmaps.size(); ++i) {
+      const size_t before = cs.size();
       collect_bitmap_containers(*pl.bitmaps[i].col, pl.bitmaps[i].dict_ids, cs);
-      first[i + 1] = cs.size();
+      for (size_t k = before; k < cs.size(); ++k) cs[k].target = (int32_t)i;
+      woff[i + 1] = woff[i] + (((size_t)pl.bitmaps[i].seg->num_docs + 63) / 64 + 1) * 2;
     }
-    RoaringContainer* dc = cs.empty() ? nullptr : scratch.alloc<RoaringContainer>(cs.size());
-    if (dc) PH_HIP_CHECK(hipMemcpyAsync(dc, cs.data(), sizeof(RoaringContainer) * cs.size(), hipMemcpyHostToDevice, st));
+    uint32_t* block = scratch.alloc<uint32_t>(std::max<size_t>(2, woff.back()));
+    PH_HIP_CHECK(hipMemsetAsync(block, 0, 4 * std::max<size_t>(2, woff.back()), st));
     for (size_t i = 0; i < pl.bitmaps.size(); ++i) {
-      BitmapLeaf& b = pl.bitmaps[i];
-      const size_t words = ((size_t)b.seg->num_docs + 31) / 32 + 1;
-      uint32_t* bm = scratch.alloc<uint32_t>(words);
-      PH_HIP_CHECK(hipMemsetAsync(bm, 0, words * 4, st));
-      if (first[i + 1] > first[i])
-        launch_roaring_or(dc + first[i], (int)(first[i + 1] - first[i]), b.col->d_inverted.as<uint8_t>(), bm,
-                          b.seg->num_docs, st);
-      bitmap_dev[i] = bm;
+      bitmap_dev[i] = block + woff[i];
+      tg[i] = RoaringTarget{pl.bitmaps[i].col->d_inverted.as<uint8_t>(), bitmap_dev[i], pl.bitmaps[i].seg->num_docs, 0};
     }
-    if (dc) PH_HIP_CHECK(hipStreamSynchronize(st));  // `cs` is pageable host memory
+    if (!cs.empty()) {
+      const size_t b1 = sizeof(RoaringContainer) * cs.size(), b2 = sizeof(RoaringTarget) * tg.size();
+      uint8_t* dev = scratch.alloc<uint8_t>(b1 + b2);
+      uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(b1 + b2));
+      memcpy(stage, cs.data(), b1);
+      memcpy(stage + b1, tg.data(), b2);
+      PH_HIP_CHECK(hipMemcpyAsync(dev, stage, b1 + b2, hipMemcpyHostToDevice, st));
+      launch_roaring_or(reinterpret_cast<RoaringContainer*>(dev), (int)cs.size(),
+                        reinterpret_cast<RoaringTarget*>(dev + b1), st);
+      PH_HIP_CHECK(hipStreamSynchronize(st));  // the staging buffer is reused below
+    }
   };
   build_bitmaps();
 
@@ -1464,9 +1473,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       if ((size_t)kp.lds_copy_bytes > 64 * 1024) kp.lds_fast = 0;  // not expected: G is an LDS-sized key space
       else lds = std::max(lds, l);
     }
-    if (kp.agg_sparse) {  // no staging: only the HLL registers live in LDS
+    if (kp.agg_sparse) {  // no staging: the HLL registers and one matched-doc list (uint16 offsets) per wave
       kp.lds_hll_off = 0;
-      lds = (size_t)num_hll * (m ? m : 1) * 4 + 16;
+      kp.pl_misc_off = (int32_t)(((size_t)num_hll * (m ? m : 1) * 4 + 16 + 15) / 16 * 16);
+      lds = (size_t)kp.pl_misc_off + (size_t)kWaves * kSparseStepWords * 64 * sizeof(uint16_t);
     }
     // 160 KiB of LDS per CU (gfx950); HLL registers of a large log2m do not fit beside the staging areas
     if (lds > 160 * 1024) fail(PH_ERR_UNSUPPORTED, "aggregation state exceeds the LDS of one CU (HLL log2m too large)");

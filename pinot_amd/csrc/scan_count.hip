@@ -125,21 +125,25 @@ __global__ void __launch_bounds__(kBlock) k_agg_lean(const KParams p) {
 // ------------------------------------------------------------------ sparse MODE_AGG (selective bitmap leaves)
 // k_agg_sparse serves aggregation-only queries whose every segment is filtered by an inverted-index bitmap that
 // matches few docs (InvertedIndexFilterOperator -> DocIdSetOperator -> AggregationOperator): instead of streaming
-// the aggregated columns through the staging tiles, a wave walks the doc bitmap 64 docs at a time, skips empty
-// words, and gathers the value / HLL entry of each matched doc straight from its packed stream.  At 1 %
-// selectivity a 24-bit column is touched on ~19 % of its 64-byte sectors instead of all
-// of them.  Values: read_value on the gathered code (packed offset or dictId); HLL: the segment's per-dictId
-// (register, rank) table, registers in LDS (as k_scan<MODE_AGG>).
+// the aggregated columns through the staging tiles, it gathers the value / HLL entry of each matched doc straight
+// from its packed stream.  At 1 % selectivity a 24-bit column is touched on ~19 % of its 64-byte sectors
+//  instead of all of them.
+// A wave step covers 64 bitmap words = 4096 docs: one 8-byte load per lane (the next step's is issued before this
+// one is processed), a wave prefix sum of the lanes' popcounts places every matched doc's offset in a per-wave LDS
+// list, and the list is gathered 64 docs per round with every lane busy -- so a wave pays the dependent gather
+// latency once per ~41 matched docs (1 %), not once per 64-doc word.  Values: read_value on the gathered code
+// (packed offset or dictId); HLL: the segment's per-dictId (register, rank) table, registers in LDS.
 __global__ void __launch_bounds__(kBlock) k_agg_sparse(const KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int WAVES = kWaves;
-  constexpr int UW = 4;  // words per wave per step: independent gathers in flight
+  constexpr int SW = kSparseStepWords;  // bitmap words per wave step
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int m = 1 << p.log2m;
   SegPtr segs = (SegPtr)p.segs;
   const PH_CONST Chunk* chunks = (const PH_CONST Chunk*)p.chunks;
   uint32_t* lds_hll = reinterpret_cast<uint32_t*>(smem + p.lds_hll_off);
+  uint16_t* list = reinterpret_cast<uint16_t*>(smem + p.pl_misc_off) + (size_t)wave * (SW * 64);
   for (int i = threadIdx.x; i < p.num_hll * m; i += kBlock) lds_hll[i] = 0;
   __syncthreads();
   int64_t isum[kMaxVals], vmin[kMaxVals], vmax[kMaxVals];
@@ -158,22 +162,37 @@ __global__ void __launch_bounds__(kBlock) k_agg_sparse(const KParams p) {
   for (int32_t c = c0; c < c1; ++c) {
     SegPtr S = segs + chunks[c].seg;
     const uint32_t ndocs = (uint32_t)S->num_docs;
-    const uint32_t* bm = S->fptr;
-    for (int32_t w = chunks[c].word_begin + wave * UW; w < chunks[c].word_end; w += WAVES * UW) {
-      uint32_t hitmask = 0;
+    const unsigned long long* bm = reinterpret_cast<const unsigned long long*>(S->fptr);  // 64 docs per word
+    const int32_t wb = chunks[c].word_begin, we = chunks[c].word_end;
+    int32_t w = wb + wave * SW;
+    unsigned long long nxt = (w + lane < we) ? bm[w + lane] : 0ull;
+    for (; w < we; w += WAVES * SW) {
+      unsigned long long bits = nxt;
+      const int32_t wn = w + WAVES * SW;
+      nxt = (wn + lane < we) ? bm[wn + lane] : 0ull;  // the next step's bitmap words are in flight meanwhile
+      const uint32_t d0 = (uint32_t)(w + lane) * 64u;
+      if (d0 + 64u > ndocs) bits &= d0 >= ndocs ? 0ull : ((1ull << (ndocs - d0)) - 1ull);
+      const uint32_t cnt = (uint32_t)__popcll(bits);
+      uint32_t incl = cnt;
 #pragma unroll
-      for (int u = 0; u < UW; ++u) {
-        const uint32_t doc = (uint32_t)(w + u) * 64u + (uint32_t)lane;
-        const bool in = (w + u < chunks[c].word_end) & (doc < ndocs);
-        const bool hit = in && ((gld(bm + (min(doc, ndocs - 1) >> 5)) >> (doc & 31u)) & 1u);
-        matched += (uint32_t)__popcll(__ballot(hit));
-        hitmask |= (hit ? 1u : 0u) << u;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
       }
-      if (!__ballot(hitmask != 0)) continue;
-#pragma unroll
-      for (int u = 0; u < UW; ++u) {
-        if (!((hitmask >> u) & 1u)) continue;
-        const uint32_t doc = (uint32_t)(w + u) * 64u + (uint32_t)lane;
+      const uint32_t total = __shfl(incl, 63, 64);
+      if (total == 0) continue;
+      uint32_t pos = incl - cnt;
+      while (bits) {
+        list[pos++] = (uint16_t)(lane * 64 + __builtin_ctzll(bits));
+        bits &= bits - 1ull;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      matched += total;
+      for (uint32_t base = 0; base < total; base += 64) {
+        if (base + (uint32_t)lane >= total) continue;
+        const uint32_t doc = (uint32_t)w * 64u + list[base + lane];
         for (int j = 0; j < p.num_vals && j < kMaxVals; ++j) {
           const PH_CONST DevValCol& vc = S->vals[j];
           int64_t iv;
@@ -192,6 +211,10 @@ __global__ void __launch_bounds__(kBlock) k_agg_sparse(const KParams p) {
           atomicMax(&lds_hll[h * m + (e >> 8)], e & 0xffu);
         }
       }
+      // every lane has read its list entries before the next step rewrites the list
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
   // epilogue: one set of device atomics per wave, registers once per workgroup
