@@ -267,6 +267,7 @@ struct PartAggParams {
   int32_t has_sum, has_min, has_max;
   int32_t pack_cs;        // count and value-offset sum share one 64-bit LDS word (count << 40 | sum)
   int32_t slices;         // workgroups per partition (each aggregates a contiguous range of the regions)
+  int32_t dbg;            // timing experiments (PH_PART_DBG bits 4: loads only, 8: no MIN/MAX); results invalid
   int64_t part_vbase;
   int64_t num_groups;
   unsigned long long* out_count;

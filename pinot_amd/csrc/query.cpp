@@ -1669,6 +1669,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       int slices = (int)std::max<int64_t>(1, std::min<int64_t>(8, (2 * (int64_t)ctx->num_cus + P - 1) / P));
       if (const char* e = getenv("PH_PART_SLICES")) slices = std::max(1, std::min(16, atoi(e)));  // tuning knob
       bp.slices = slices;
+      bp.dbg = kp.part_dbg;
       bp.regions = grid_a;
       const size_t lds_b = part_agg_lds_bytes(bp);
       Lane& L = *lane.lane;
