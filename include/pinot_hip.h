@@ -22,6 +22,12 @@
  *   ph_result_*
  *       GroupByResultsBlock / AggregationResultsBlock contents (GroupByResultsBlock.java:62,86;
  *       AggregationResultsBlock.java:50) and ExecutionStatistics (GroupByOperator.java:143-148).
+ *   ph_result_datatable
+ *       DataTableImplV4.toBytes of GroupByResultsBlock.getDataTable / AggregationResultsBlock.getDataTable
+ *       (pinot-common/.../datatable/DataTableImplV4.java, GroupByResultsBlock.java:170).
+ *   ph_raw_forward_index_read (+ ph_column_desc.raw_forward_index)
+ *       FixedByteChunkSVForwardIndexReader / BaseChunkForwardIndexReader (pinot-segment-local/.../readers/
+ *       forward/BaseChunkForwardIndexReader.java:57-105) behind ForwardIndexReaderFactory.createRawIndexReader.
  *   ph_fixed_bit_pack
  *       FixedBitSVForwardIndexWriter.putDictId (pinot-segment-local/.../io/writer/impl/
  *       FixedBitSVForwardIndexWriter.java:39-50) -- the on-disk forward-index format.

@@ -680,6 +680,11 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   const bool fin = dop == DENSE_FINALIZE;
   using clock = std::chrono::steady_clock;
   const auto t0 = clock::now();
+  const bool host_times = getenv("PH_HOST_TIMES") != nullptr;  // per-phase host clock (tuning)
+  auto stamp = [&](const char* what) {
+    if (host_times)
+      fprintf(stderr, "[ph host] %-12s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(clock::now() - t0).count());
+  };
   if (!q) fail(PH_ERR_INVALID_ARGUMENT, "null query");
   if (nseg < 0 || (nseg > 0 && !segs_in)) fail(PH_ERR_INVALID_ARGUMENT, "bad segment list");
   if (q->num_aggregations > kMaxAggs) fail(PH_ERR_UNSUPPORTED, "too many aggregations");
@@ -975,7 +980,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       PH_HIP_CHECK(hipStreamSynchronize(st));  // the staging buffer is reused below
     }
   };
+  stamp("plan");
   build_bitmaps();
+  stamp("bitmaps");
 
   // ---- group-by key space over table-level dictionaries
   std::vector<std::shared_ptr<GlobalDict>> gdicts;
@@ -1493,9 +1500,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     dsegs[ff.first].fptr = dp;
   }
   for (auto& fb : fbitmap_fix) dsegs[fb.first].fptr = bitmap_dev[fb.second];
-  PH_HIP_CHECK(hipStreamSynchronize(st));  // pageable payload copies above
+  if (!payload_fix.empty() || !fset_fix.empty()) PH_HIP_CHECK(hipStreamSynchronize(st));  // pageable copies above
 
   check_interrupt();
+  stamp("setup");
   if (!chunks.empty()) {
     DevSegment* d_segs = scratch.alloc<DevSegment>(dsegs.size());
     FilterInsn* d_prog = scratch.alloc<FilterInsn>(std::max<size_t>(1, all_insns.size()));
@@ -1708,7 +1716,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       PH_HIP_CHECK(hipStreamWaitEvent(st, L.event(2 * batches.size() + 1), 0));
       PH_HIP_CHECK(hipEventRecord(L.ev_stop, st));
     }
+    stamp("launched");
     PH_HIP_CHECK(hipStreamSynchronize(st));  // staging buffer reuse + results
+    stamp("kernels done");
     PH_HIP_CHECK(hipEventElapsedTime(&dev_ms, lane.lane->ev_start, lane.lane->ev_stop));
     if (kp.dbg) {  // PH_DEBUG_STAMPS: where wave 0 of each workgroup spent its cycles (last launch)
       std::vector<unsigned long long> h(4 * (size_t)ctx->num_cus * 8);
@@ -1773,8 +1783,27 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   };
   if (q->num_group_by == 0) {
     init_row_results(1);
+    // every scalar (and HLL register block) in one round trip: async copies into one pinned block, one sync
+    std::vector<size_t> at(nagg + 1, 0);
+    size_t need = 8;
+    for (int k = 0; k < nagg; ++k) {
+      at[k] = need;
+      const int t = q->aggregations[k].type;
+      need += t == PH_AGG_COUNT ? 0 : (t == PH_AGG_DISTINCTCOUNTHLL ? 4 * (size_t)m : 8);
+    }
+    size_t blk_cap = 0;
+    uint8_t* blk = static_cast<uint8_t*>(ctx->pinned_acquire(need, &blk_cap));
+    PH_HIP_CHECK(hipMemcpyAsync(blk, kp.out_count, 8, hipMemcpyDeviceToHost, st));
+    for (int k = 0; k < nagg; ++k) {
+      const int t = q->aggregations[k].type;
+      if (t == PH_AGG_DISTINCTCOUNTHLL)
+        PH_HIP_CHECK(hipMemcpyAsync(blk + at[k], kp.out_hll + (size_t)agg_hll[k] * m, 4 * m, hipMemcpyDeviceToHost, st));
+      else if (t != PH_AGG_COUNT)
+        PH_HIP_CHECK(hipMemcpyAsync(blk + at[k], src_of(k), 8, hipMemcpyDeviceToHost, st));
+    }
+    PH_HIP_CHECK(hipStreamSynchronize(st));
     unsigned long long matched = 0;
-    PH_HIP_CHECK(hipMemcpy(&matched, kp.out_count, 8, hipMemcpyDeviceToHost));
+    memcpy(&matched, blk, 8);
     stats.num_docs_scanned = (int64_t)matched;
     for (int k = 0; k < nagg; ++k) {
       const int t = q->aggregations[k].type;
@@ -1783,16 +1812,16 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         int64_t v = (int64_t)matched;
         memcpy(dst, &v, 8);
       } else if (t == PH_AGG_DISTINCTCOUNTHLL) {
-        std::vector<uint32_t> r(m);
-        PH_HIP_CHECK(hipMemcpy(r.data(), kp.out_hll + (size_t)agg_hll[k] * m, 4 * m, hipMemcpyDeviceToHost));
+        const uint32_t* r = reinterpret_cast<const uint32_t*>(blk + at[k]);
         for (int j = 0; j < m; ++j) dst[j] = (uint8_t)r[j];
       } else {
         int64_t raw;
-        PH_HIP_CHECK(hipMemcpy(&raw, src_of(k), 8, hipMemcpyDeviceToHost));
+        memcpy(&raw, blk + at[k], 8);
         double v = finish_value(k, raw, (int64_t)matched, t == PH_AGG_SUM);
         memcpy(dst, &v, 8);
       }
     }
+    ctx->pinned_release(blk, blk_cap);
   } else if (num_hll == 0) {
     // device-side compaction: non-empty groups in key order, keys decoded, values converted to double,
     // copied straight into pinned result columns
@@ -1948,6 +1977,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
   }
   stats.num_entries_scanned_post_filter = stats.num_docs_scanned * ncols_proj;
+  stamp("done");
   stats.host_ms = std::chrono::duration<double, std::milli>(clock::now() - t0).count() - dev_ms;
   return res.release();
 }
