@@ -63,6 +63,10 @@ BUILT = {
     "config5": ("hll", 4, 1_000_000_000, 10_000_000,
                 "config5: DISTINCTCOUNTHLL(u) (b=24) WHERE c IN (10 ids) via inverted bitmaps, 1 % selectivity"),
 }
+# BASELINE.json configs[3]: the 13 SSB queries as one flight over a denormalised lineorder table (SF100 = 600M rows,
+# 60 x 10M-row segments: 4 distinct segments built in dictId form by tests/workloads.py, pinned 15 times each)
+FLIGHTS = {"config4": (4, 600_000_000, 10_000_000,
+                       "config4: SSB lineorder SF100 flight Q1.1-Q4.3 (13 queries), string dimensions as dictId scans")}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 KERNEL_NAMES = {0: "k_scan<MODE_COUNT>", 1: "k_scan<MODE_AGG>", 2: "k_scan<MODE_GROUP_LDS>",
                 3: "k_scan<MODE_GROUP_GLOBAL>", 4: "k_scan<MODE_PARTITION> + k_part_agg"}
@@ -128,8 +132,123 @@ def algorithmic_bytes(rows_per_seg, nseg, cols):
 def oracle_segments(bufs):
     from oracle import oracle as O
     return [O.segment_from_dict_ids(b.name, {c: dict(dictionary=cb.dictionary_values, fwd=cb.forward_index,
-                                                     bits=cb.bits, data_type="INT", num_docs=b.num_docs)
+                                                     bits=cb.bits, data_type=cb.data_type, num_docs=b.num_docs)
                                            for c, cb in b.columns.items()}) for b in bufs]
+
+
+def query_columns(q):
+    cols = list(q.group_by)
+    for a in q.aggregations:
+        cols += a.columns()
+    if q.filter is not None:
+        cols += q.filter.columns()
+    return list(dict.fromkeys(cols))
+
+
+def flight_main(args, world, rank, dist, device):
+    """config4: every step runs the 13 SSB queries over the whole table (one launch set per query); value = rows
+    scanned per second summed over the flight (13 x table rows / flight time)."""
+    import torch
+    from oracle import oracle as O
+    from pinot_amd.distributed import DistributedQuery
+    from pinot_amd.engine import GpuContext
+    from pinot_amd.query import parse_sql
+    from pinot_amd.reduce import reduce_groups
+    from tests import workloads as W
+    distinct, rows_default, seg_default, wdesc = FLIGHTS[args.workload]
+    queries = [parse_sql(sql) for sql in W.SSB_QUERIES.values()]
+    rows_total = args.rows or rows_default
+    nseg = max(1, rows_total // (args.segment_rows or seg_default))
+    seg_rows = rows_total // nseg
+    mine = [i for i in range(nseg) if i % world == rank]
+    t0 = time.time()
+    built = {j: W.ssb_segment_buffers(f"ssb_{j}", seg_rows, seed=0xC004 + j) for j in range(min(distinct, nseg))}
+    log(f"[rank {rank}] built {len(built)} distinct segments ({time.time() - t0:.1f}s)")
+    ctx = GpuContext(device)
+    pinned = [ctx.pin(built[i % distinct]) for i in mine]
+    bufs = [built[i % distinct] for i in mine]
+    any_buf = built[0]
+    for g in dict.fromkeys(g for q in queries for g in q.group_by):  # table-level dictionaries for dense partials
+        vals = np.unique(np.concatenate([b.columns[g].dictionary_values for b in built.values()]))
+        ctx.set_table_dictionary(g, any_buf.columns[g].data_type, vals)
+    ctx.set_schema({c: cb.data_type for c, cb in any_buf.columns.items()})
+    runner = DistributedQuery(ctx)
+    alg = sum(sum((seg_rows * any_buf.columns[c].bits + 7) // 8 for c in query_columns(q)) * len(mine)
+              for q in queries)
+
+    def step():
+        ms = 0.0
+        for q in queries:
+            if world > 1:
+                _, _, scan = runner.execute(q, pinned, copy=False)
+                ms += scan.device_ms
+            else:
+                ms += ctx.execute(q, pinned, copy=False).stats.device_ms
+        return ms
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dev_ms = []
+    ts = time.perf_counter()
+    for _ in range(args.steps):
+        dev_ms.append(step())
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - ts
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed * 1000.0 / args.steps
+    total_rows = nseg * seg_rows
+    kernel_ms = float(np.mean(dev_ms))
+    achieved = alg / (kernel_ms / 1000.0) / 1e9 if kernel_ms > 0 else None
+    result = {
+        "metric": "filter+group-by rows/s and achieved HBM GB/s, 1B rows",
+        "value": len(queries) * total_rows / (ms_per_step / 1000.0), "unit": "rows/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "int64",
+        "data": (f"synthetic (tests/workloads.py ssb_segment_buffers, {len(built)} distinct {seg_rows}-doc segments "
+                 f"pinned as {nseg} segments, sharded over {world} GPU(s))"),
+        "config": {"workload": wdesc, "table_rows": total_rows, "segments": nseg, "segments_per_gpu": len(mine),
+                   "queries_per_step": len(queries),
+                   "parallelism": f"segments sharded x{world}" + (", RCCL reduce-scatter by key range" if world > 1
+                                                                  else "")},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                     "kernel": "13 SSB queries (k_scan MODE_AGG / MODE_GROUP_LDS / lean forms)", "kernel_ms": kernel_ms,
+                     "algorithmic_bytes_per_launch": alg},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads = host_threads()
+        osegs = oracle_segments([built[0]])
+        t1 = time.perf_counter()
+        exp = [O.execute(q, osegs, 1) for q in queries]  # one segment, one thread, every query
+        dt1 = time.perf_counter() - t1
+        n = int(max(1, min(len(bufs), args.cpu_seconds / max(dt1, 1e-3) * threads)))
+        sample = oracle_segments(bufs[:n])
+        t2 = time.perf_counter()
+        for q in queries:
+            O.execute(q, sample, threads)
+        dt = time.perf_counter() - t2
+        result["cpu_baseline"] = {
+            "value": len(queries) * n * seg_rows / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+            "value_t1": len(queries) * seg_rows / dt1, "host_cores": os.cpu_count(), "cpu_model": cpu_model(),
+            "sample": f"the 13 queries over {n} of {nseg} segments x {seg_rows} rows, oracle C restatement on "
+                      f"{threads} host threads, {dt:.2f}s; value_t1 = one segment on one thread, {dt1:.2f}s"}
+        if not args.no_parity:  # every query of the flight on one segment, bit-exact (SUM of integer expressions)
+            ok = True
+            for q, e in zip(queries, exp):
+                r = ctx.execute(q, pinned[:1])
+                ok = ok and reduce_groups(q, r.keys, r.aggs).rows == reduce_groups(q, e.keys, e.aggs).rows
+            result["parity_sample"] = {"segments": 1, "queries": len(queries), "bit_exact": bool(ok)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 def host_threads():
@@ -195,7 +314,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample size in seconds of work")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
-    ap.add_argument("--workload", default="config3", choices=sorted(list(WORKLOADS) + list(BUILT)))
+    ap.add_argument("--workload", default="config3", choices=sorted(list(WORKLOADS) + list(BUILT) + list(FLIGHTS)))
     args = ap.parse_args()
 
     import torch
@@ -208,6 +327,8 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = local_rank
+    if args.workload in FLIGHTS:
+        return flight_main(args, world, rank, dist, device)
 
     from pinot_amd.distributed import DistributedQuery
     from pinot_amd.engine import GpuContext

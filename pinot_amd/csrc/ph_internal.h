@@ -78,7 +78,11 @@ struct FilterInsn {
 };
 
 // Single-leaf filters are specialised (the common shapes); anything else runs the postfix program.
-enum : int32_t { FK_ALL = 0, FK_RANGE = 1, FK_SET = 2, FK_BITMAP = 3, FK_DOCRANGE = 4, FK_GENERIC = 5 };
+enum : int32_t { FK_ALL = 0, FK_RANGE = 1, FK_SET = 2, FK_BITMAP = 3, FK_DOCRANGE = 4, FK_GENERIC = 5, FK_CONJ = 6 };
+// FK_CONJ: an AND of up to kMaxConj scan leaves (dictId range or bitset), each on its own LDS-staged stream -- the
+// FilterPlanNode shape of multi-predicate WHERE clauses (AndFilterOperator over ScanBasedFilterOperators), decoded
+// from the staged tile like a single leaf instead of gathered per doc by the generic program
+constexpr int kMaxConj = 4;
 
 // How an aggregated numeric column is read:
 //   VK_PACKED   frame-of-reference stream (value - base) in `bits`, built once per column in HBM from the
@@ -148,6 +152,10 @@ struct DevSegment {
   int32_t pad;
   const uint32_t* fptr;  // FK_SET bitset over dictIds ; FK_BITMAP doc bitmap
   const uint32_t* keep;  // numGroupsLimit: bitset over global keys this segment may aggregate (nullptr: all)
+  int32_t nconj;                    // FK_CONJ leaves
+  int32_t cstream[kMaxConj];        // FK_CONJ: staged stream of leaf k
+  uint32_t clo[kMaxConj], clen[kMaxConj];  // FK_CONJ range leaf k: [clo, clo + clen)
+  const uint32_t* cset[kMaxConj];   // FK_CONJ set leaf k: bitset over dictIds (nullptr: range leaf)
   DevColumn cols[kMaxCols];
   DevValCol vals[kMaxVals];
   DevValCol vals2[kMaxVals];       // second operand of a 2-operand expression term (KParams::val_op)

@@ -300,6 +300,96 @@ std::pair<int64_t, int64_t> doc_span(const PNode& n, int64_t docs) {
   return {0, docs};
 }
 
+// Same-column scan leaves under one AND / OR combine into one leaf (intersection / union of their dictId sets:
+// `d_year >= 1992 AND d_year <= 1997` -> one range, `c_city = 'A' OR c_city = 'B'` -> one set), the dictId-space
+// form of what the reference evaluates as separate ScanBasedFilterOperators; results are unchanged.  A set whose
+// ids are contiguous becomes a range.
+std::vector<uint32_t> leaf_bits(const PNode& k, int64_t card) {
+  if (k.op == OP_SET) {
+    std::vector<uint32_t> b = k.set;
+    b.resize((size_t)(card + 31) / 32, 0u);
+    return b;
+  }
+  std::vector<uint32_t> b((size_t)(card + 31) / 32, 0u);
+  for (int64_t i = k.lo; i < (int64_t)k.lo + k.len && i < card; ++i) b[i >> 5] |= 1u << (i & 31);
+  return b;
+}
+
+void leaf_from_bits(PNode& n, const std::vector<uint32_t>& b, int64_t card) {
+  int64_t first = -1, last = -1, count = 0;
+  for (int64_t i = 0; i < card; ++i)
+    if ((b[i >> 5] >> (i & 31)) & 1u) {
+      if (first < 0) first = i;
+      last = i;
+      ++count;
+    }
+  if (count == 0) {
+    n = PNode{};
+    n.kind = L_NONE;
+    return;
+  }
+  if (count == card) {
+    n = PNode{};
+    n.kind = L_ALL;
+    return;
+  }
+  if (count == last - first + 1) {
+    n.op = OP_RANGE;
+    n.lo = (uint32_t)first;
+    n.len = (uint32_t)count;
+    n.set.clear();
+  } else {
+    n.op = OP_SET;
+    n.set = b;
+  }
+}
+
+template <class CardOf>
+void merge_same_column_leaves(PNode& n, const CardOf& card_of) {
+  if (n.kind != L_NODE) return;
+  for (auto& k : n.kids) merge_same_column_leaves(k, card_of);
+  if (n.op != OP_AND && n.op != OP_OR) return;
+  const bool is_and = n.op == OP_AND;
+  std::map<int, size_t> first_of;  // column slot -> index of its first scan leaf
+  std::vector<PNode> kids;
+  for (auto& k : n.kids) {
+    if (k.kind == L_NODE && k.scan && (k.op == OP_RANGE || k.op == OP_SET)) {
+      auto it = first_of.find(k.col);
+      if (it != first_of.end()) {
+        PNode& a = kids[it->second];
+        const int64_t card = card_of(k.col);
+        std::vector<uint32_t> x = leaf_bits(a, card), y = leaf_bits(k, card);
+        for (size_t w = 0; w < x.size(); ++w) x[w] = is_and ? (x[w] & y[w]) : (x[w] | y[w]);
+        leaf_from_bits(a, x, card);
+        continue;
+      }
+      first_of[k.col] = kids.size();
+    }
+    kids.push_back(std::move(k));
+  }
+  std::vector<PNode> out;
+  for (auto& k : kids) {
+    if (k.kind == (is_and ? L_NONE : L_ALL)) {  // AND with an empty child / OR with an all child
+      n = PNode{};
+      n.kind = is_and ? L_NONE : L_ALL;
+      return;
+    }
+    if (k.kind == (is_and ? L_ALL : L_NONE)) continue;
+    out.push_back(std::move(k));
+  }
+  if (out.empty()) {
+    n = PNode{};
+    n.kind = is_and ? L_ALL : L_NONE;
+    return;
+  }
+  if (out.size() == 1) {
+    PNode only = std::move(out[0]);
+    n = std::move(only);
+    return;
+  }
+  n.kids = std::move(out);
+}
+
 int count_scan_leaves(const PNode& n) {
   if (n.kind != L_NODE) return 0;
   int s = n.scan ? 1 : 0;
@@ -899,6 +989,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     root.kind = L_ALL;
     if (q->filter_root >= 0) root = pl.build(segs[i], q->filter_root, 0);
     stats.num_entries_scanned_in_filter += (int64_t)segs[i]->num_docs * count_scan_leaves(root);
+    merge_same_column_leaves(root, [&](int slot) { return (int64_t)segs[i]->columns.at(slot_names[slot])->cardinality; });
     if (root.kind == L_NONE || segs[i]->num_docs == 0) seg_live[i] = 0;
     roots[i] = std::move(root);
   }
@@ -1104,6 +1195,48 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     kp.v2_stream[j] = val_exprs[j] ? stream_of(val_cols2[j], "val") : kp.v_stream[j];
   }
   if ((int)stream_cols.size() > kMaxStreams) fail(PH_ERR_UNSUPPORTED, "too many column streams in one query");
+  // FK_CONJ candidates: a WHERE that is an AND of predicates (or of ORs of predicates on one column) gets one staged
+  // dictId stream per filter column, when they fit beside the group / value streams
+  std::map<int, int> conj_stream;  // column slot -> staged stream
+  if (q->filter_root >= 0 && q->filter_nodes[q->filter_root].type == PH_FILTER_AND) {
+    std::vector<std::string> fcols;
+    bool shape = true;
+    const ph_filter_node& r = q->filter_nodes[q->filter_root];
+    for (int i = 0; i < r.num_children && shape; ++i) {
+      const ph_filter_node& k = q->filter_nodes[r.children[i]];
+      std::string col;
+      if (k.type == PH_FILTER_PREDICATE) {
+        col = q->predicates[k.predicate].column;
+      } else if (k.type == PH_FILTER_OR) {
+        for (int j = 0; j < k.num_children && shape; ++j) {
+          const ph_filter_node& g = q->filter_nodes[k.children[j]];
+          if (g.type != PH_FILTER_PREDICATE) shape = false;
+          else if (j == 0) col = q->predicates[g.predicate].column;
+          else shape = col == q->predicates[g.predicate].column;
+        }
+      } else {
+        shape = false;
+      }
+      if (shape && std::find(fcols.begin(), fcols.end(), col) == fcols.end()) fcols.push_back(col);
+    }
+    if (shape && fcols.size() >= 2 && (int)fcols.size() <= kMaxConj) {
+      std::vector<std::string> trial = stream_cols;
+      std::map<int, int> cs;
+      for (auto& c : fcols) {
+        const std::string key = "id:" + c;
+        auto it = std::find(trial.begin(), trial.end(), key);
+        if (it == trial.end()) {
+          trial.push_back(key);
+          it = trial.end() - 1;
+        }
+        cs[pl.slot.at(c)] = (int)(it - trial.begin());
+      }
+      if ((int)trial.size() <= kMaxStreams) {
+        stream_cols = trial;
+        conj_stream = cs;
+      }
+    }
+  }
   kp.nstage = (int)stream_cols.size();  // <= kMaxStreams == kMaxStage: every stream is staged
 
   // value column encodings + the table-wide value range (partitioned records carry value - vmin)
@@ -1240,6 +1373,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<std::pair<size_t, int>> bitmap_fix;                     // global insn index -> bitmap leaf
   std::vector<std::pair<size_t, std::vector<uint32_t>>> fset_fix;     // segment index -> FK_SET bitset
   std::vector<std::pair<size_t, int>> fbitmap_fix;                    // segment index -> bitmap leaf
+  std::vector<std::pair<size_t, std::vector<uint32_t>>> conj_set_fix; // segment index * kMaxConj + leaf -> bitset
   std::vector<std::pair<int32_t, int32_t>> dseg_chunks;                // device segment -> its chunk range
   std::vector<int> dseg_src;                                           // device segment -> query segment index
   std::vector<std::pair<int32_t, int32_t>> seg_words;                  // device segment -> [first, end) words to scan
@@ -1268,6 +1402,19 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       d.fkind = FK_DOCRANGE;
       d.flo = (uint32_t)root.ranges[0];
       d.flen = (uint32_t)(root.ranges[1] - root.ranges[0] + 1);
+    } else if (root.op == OP_AND && (int)root.kids.size() <= kMaxConj &&
+               std::all_of(root.kids.begin(), root.kids.end(), [&](const PNode& k) {
+                 return k.kind == L_NODE && k.scan && (k.op == OP_RANGE || k.op == OP_SET) && conj_stream.count(k.col);
+               })) {
+      d.fkind = FK_CONJ;
+      d.nconj = (int32_t)root.kids.size();
+      for (int k = 0; k < d.nconj; ++k) {
+        const PNode& leaf = root.kids[k];
+        d.cstream[k] = conj_stream.at(leaf.col);
+        d.clo[k] = leaf.lo;
+        d.clen[k] = leaf.len;
+        if (leaf.op == OP_SET) conj_set_fix.push_back({si * kMaxConj + k, leaf.set});
+      }
     } else {
       d.fkind = FK_GENERIC;
       emit(root, progs[i]);
@@ -1315,6 +1462,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     for (int g = 0; g < q->num_group_by; ++g) {
       Column& c = *s->columns.at(group_cols[g]);
       d.streams[kp.g_stream[g]] = DevStream{c.d_fwd.as<uint32_t>(), c.bits, 0};
+    }
+    for (int k = 0; d.fkind == FK_CONJ && k < d.nconj; ++k) {
+      Column& c = *s->columns.at(slot_names[root.kids[k].col]);
+      d.streams[d.cstream[k]] = DevStream{c.d_fwd.as<uint32_t>(), c.bits, 0};
     }
     if (q->filter_root >= 0) {
       // bits = 0: nothing to stage for this segment's filter (FK_ALL / bitmap / doc range / program)
@@ -1376,6 +1527,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // would wait behind an early prefetch
   for (auto& d : dsegs) {
     bool g = d.fkind == FK_SET || d.fkind == FK_BITMAP || d.fkind == FK_GENERIC || num_hll > 0;
+    for (int k = 0; d.fkind == FK_CONJ && k < d.nconj; ++k) g |= d.cset[k] != nullptr || d.clen[k] == 0;
     for (int gi = 0; gi < q->num_group_by; ++gi) g |= d.cols[kp.group_slot[gi]].remap != nullptr;
     for (int j = 0; j < nvals; ++j) g |= d.vals[j].kind != VK_PACKED || (val_exprs[j] && d.vals2[j].kind != VK_PACKED);
     if (g && mode != MODE_COUNT) kp.late_prefetch = 1;
@@ -1500,7 +1652,13 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     dsegs[ff.first].fptr = dp;
   }
   for (auto& fb : fbitmap_fix) dsegs[fb.first].fptr = bitmap_dev[fb.second];
-  if (!payload_fix.empty() || !fset_fix.empty()) PH_HIP_CHECK(hipStreamSynchronize(st));  // pageable copies above
+  for (auto& cf : conj_set_fix) {
+    uint32_t* dp = scratch.alloc<uint32_t>(cf.second.size() + 1);
+    PH_HIP_CHECK(hipMemcpyAsync(dp, cf.second.data(), 4 * cf.second.size(), hipMemcpyHostToDevice, st));
+    dsegs[cf.first / kMaxConj].cset[cf.first % kMaxConj] = dp;
+  }
+  if (!payload_fix.empty() || !fset_fix.empty() || !conj_set_fix.empty())
+    PH_HIP_CHECK(hipStreamSynchronize(st));  // pageable copies above
 
   check_interrupt();
   stamp("setup");

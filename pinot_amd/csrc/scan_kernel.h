@@ -425,6 +425,22 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
   const BitCursor fcur = bit_cursor(wst + p.stage_soff[p.f_stream], fbits, lane);
   const uint32_t flo = S->flo, flen = S->flen;
   const uint32_t* fptr = S->fptr;
+  // conjunctive scan leaves (FK_CONJ)
+  BitCursor ccur[FK == FK_CONJ ? kMaxConj : 1];
+  uint32_t clo[FK == FK_CONJ ? kMaxConj : 1], clen[FK == FK_CONJ ? kMaxConj : 1];
+  const uint32_t* cset[FK == FK_CONJ ? kMaxConj : 1];
+  const int nconj = FK == FK_CONJ ? S->nconj : 0;
+  if constexpr (FK == FK_CONJ) {
+#pragma unroll
+    for (int k = 0; k < kMaxConj; ++k) {
+      if (k >= nconj) continue;
+      const int cs = S->cstream[k];
+      ccur[k] = bit_cursor(wst + p.stage_soff[cs], S->streams[cs].bits, lane);
+      clo[k] = S->clo[k];
+      clen[k] = S->clen[k];
+      cset[k] = S->cset[k];
+    }
+  }
   // group-by key streams
   BitCursor gcur[NG > 0 ? NG : 1];
   const int32_t* gremap[NG > 0 ? NG : 1];
@@ -475,6 +491,14 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
       hit &= (doc - flo) < flen;
     } else if constexpr (FK == FK_GENERIC && LATE) {
       if (hit) hit = eval_filter((const PH_CONST FilterInsn*)p.prog + S->prog_off, S->prog_len, S, doc);
+    } else if constexpr (FK == FK_CONJ) {
+#pragma unroll
+      for (int k = 0; k < kMaxConj; ++k) {
+        if (k >= nconj) continue;
+        const uint32_t v = cursor_value(ccur[k], u);
+        if (LATE && cset[k]) hit &= (bool)((gld(cset[k] + (v >> 5)) >> (v & 31u)) & 1u);
+        else hit &= (v - clo[k]) < clen[k];
+      }
     }
     return hit;
   };
@@ -806,6 +830,7 @@ __global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : kBlock) 
         case FK_DOCRANGE:
           process_tile<MODE, NG, REC64, FK_DOCRANGE, LATE>(p, cs, smem, wst, lane, cw0, cnvalid, acc);
           break;
+        case FK_CONJ: process_tile<MODE, NG, REC64, FK_CONJ, LATE>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
         default: process_tile<MODE, NG, REC64, FK_GENERIC, LATE>(p, cs, smem, wst, lane, cw0, cnvalid, acc); break;
       }
     }

@@ -431,3 +431,31 @@ def test_value_stream_reencoding_wide_values(ctx):
     t2 = {"m": (rng.integers(-2**40, 2**40, 50_000, dtype=np.int64), "LONG"),
           "a": (rng.integers(0, 5, 50_000).astype(np.int32), "INT")}
     _both(ctx, [t2], "SELECT a, SUM(m), MIN(m), MAX(m) FROM t GROUP BY a ORDER BY a")
+
+
+# AND of scan leaves on different columns (FK_CONJ: every leaf decoded from its own staged stream), including
+# same-column ORs / ANDs merged into one leaf (sets, ranges, contiguous sets -> ranges), exclusive sets, a leaf
+# that is always true and an AND that matches nothing -- no inverted indexes, so every leaf is a scan
+CONJ_FILTERS = [
+    " WHERE a = 3 AND b > 0",
+    " WHERE b BETWEEN -500 AND 250 AND m < 536870912 AND s IN (3, 7, 30)",
+    " WHERE (a = 1 OR a = 5) AND (str = 'gFuH' OR str = 't') AND b >= -100",
+    " WHERE b >= -100 AND b <= 300 AND a <> 2",
+    " WHERE a NOT IN (0, 6) AND str > 'o' AND d > 0.5 AND c < 0",
+    " WHERE a = 99 AND b > 0",
+    " WHERE a >= 0 AND b > 0",
+    " WHERE (a = 1 OR a = 2 OR a = 3) AND s BETWEEN 10 AND 20",
+]
+
+
+@pytest.mark.parametrize("where", CONJ_FILTERS)
+@pytest.mark.parametrize("group", ["", "a, str", "s", "b"])
+def test_conjunctive_scan_leaves(ctx, where, group):
+    rng = np.random.default_rng((abs(hash(where + group))) % 2**32)
+    tables = [_random_table(rng, n) for n in (12_345, 64 * 500 + 3)]
+    if group:
+        sql = (f"SET numGroupsLimit=10000000; SELECT {group}, COUNT(*), SUM(m), MIN(d), MAX(b) FROM t{where} "
+               f"GROUP BY {group} ORDER BY {group} LIMIT 100000")
+    else:
+        sql = "SELECT COUNT(*), SUM(m), MIN(b), MAX(b), SUM(d), SUM(m * b) FROM t" + where
+    _both(ctx, tables, sql, inverted=())

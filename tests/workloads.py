@@ -150,3 +150,60 @@ SSB_QUERIES = {
 }
 SSB_INVERTED = ("c_region", "s_region", "c_nation", "s_nation", "c_city", "s_city", "p_mfgr", "p_category",
                 "p_brand1")
+
+
+def ssb_segment_buffers(name: str, n: int, seed: int = 0xC004):
+    """A denormalised lineorder segment of n rows built straight in dictionary-id form (no string arrays of n
+    entries): the same column set, value domains and dictionaries as ``ssb_columns`` (sorted distinct values),
+    drawn from its own seeded PCG64 stream.  For bench-sized segments (10M rows in seconds); no inverted indexes, so
+    the string predicates run as dictId scans."""
+    from pinot_amd.segment import SegmentBuffers, create_column, create_column_from_dict_ids
+    rng = np.random.default_rng(seed)
+    seg = SegmentBuffers(name, n)
+
+    def put(col, dictionary, ids, dt):
+        dictionary = np.asarray(dictionary)
+        used = np.zeros(len(dictionary), bool)
+        used[np.unique(ids)] = True  # dictionary = values present (sorted), ids renumbered
+        remap = np.cumsum(used) - 1
+        seg.columns[col] = create_column_from_dict_ids(col, dictionary[used], remap[ids].astype(np.int32), dt,
+                                                       allow_sorted=False)
+    day = rng.integers(0, 2557, n)
+    base = np.datetime64("1992-01-01")
+    all_days = base + np.arange(2557).astype("timedelta64[D]")
+    yr = all_days.astype("datetime64[Y]").astype(np.int64) + 1970
+    mo = all_days.astype("datetime64[M]").astype(np.int64) % 12 + 1
+    wk = (all_days - all_days.astype("datetime64[Y]")).astype(np.int64) // 7 + 1
+    ym = yr * 100 + mo
+    for col, per_day in (("d_year", yr), ("d_yearmonthnum", ym), ("d_weeknuminyear", wk)):
+        dic, inv = np.unique(per_day, return_inverse=True)
+        put(col, dic.astype(np.int32), inv.reshape(-1)[day], "INT")
+    nat_names = [x[0] for x in NATIONS]
+    regions = sorted(REGIONS)
+    nations = sorted(nat_names)
+    cities = sorted({(nm + " " * 9)[:9] + str(d) for nm in nat_names for d in range(10)})
+    region_of = np.array([regions.index(REGIONS[x[1]]) for x in NATIONS])
+    nation_rank = np.array([nations.index(nm) for nm in nat_names])
+    city_rank = np.array([[cities.index((nm + " " * 9)[:9] + str(d)) for d in range(10)] for nm in nat_names])
+    for pfx in ("c", "s"):
+        nat = rng.integers(0, 25, n)
+        digit = rng.integers(0, 10, n)
+        put(f"{pfx}_region", np.array(regions), region_of[nat], "STRING")
+        put(f"{pfx}_nation", np.array(nations), nation_rank[nat], "STRING")
+        put(f"{pfx}_city", np.array(cities), city_rank[nat, digit], "STRING")
+    mfgr = rng.integers(1, 6, n)
+    cat = rng.integers(1, 6, n)
+    brand = rng.integers(1, 41, n)
+    put("p_mfgr", np.array([f"MFGR#{i}" for i in range(1, 6)]), mfgr - 1, "STRING")
+    cats = [m * 10 + c for m in range(1, 6) for c in range(1, 6)]
+    put("p_category", np.array([f"MFGR#{v}" for v in cats]), (mfgr - 1) * 5 + (cat - 1), "STRING")
+    brands = [m * 1000 + c * 100 + b for m in range(1, 6) for c in range(1, 6) for b in range(1, 41)]
+    put("p_brand1", np.array([f"MFGR#{v}" for v in brands]), ((mfgr - 1) * 5 + (cat - 1)) * 40 + (brand - 1), "STRING")
+    qty = rng.integers(1, 51, n)
+    price = rng.integers(90_000, 200_001, n)
+    disc = rng.integers(0, 11, n)
+    ext = qty * price // 100
+    for col, v in (("lo_quantity", qty), ("lo_discount", disc), ("lo_extendedprice", ext),
+                   ("lo_revenue", ext * (100 - disc) // 100), ("lo_supplycost", price * 6 // 1000)):
+        seg.columns[col] = create_column(col, v.astype(np.int32), "INT")
+    return seg
