@@ -189,8 +189,13 @@ void launch_compact(const CompactParams& p, hipStream_t s) {
 // absent), the kept keys are exactly the `limit` keys with the smallest first docs: distinct keys have distinct
 // first docs, so the keys kept are those whose first doc is below the doc of the limit-th set bit of the
 // first-doc bitmap.
+// (blockIdx.y = limit segment: its first-doc table, doc bitmap, scalars and keep bitset)
 __global__ void __launch_bounds__(256) k_limit_mark(const uint32_t* __restrict__ first, int64_t G,
-                                                    uint32_t* __restrict__ docbits, unsigned long long* distinct) {
+                                                    uint32_t* __restrict__ docbits, int64_t dbw,
+                                                    unsigned long long* distinct) {
+  first += (int64_t)blockIdx.y * G;
+  docbits += (int64_t)blockIdx.y * dbw;
+  distinct += 3 * (int64_t)blockIdx.y;
   unsigned long long d = 0;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < G; g += (int64_t)gridDim.x * blockDim.x) {
     const uint32_t f = first[g];
@@ -205,8 +210,11 @@ __global__ void __launch_bounds__(256) k_limit_mark(const uint32_t* __restrict__
 
 // one workgroup: threshold = (doc of the limit-th set bit) + 1, or UINT32_MAX when distinct <= limit
 __global__ void __launch_bounds__(1024) k_limit_threshold(const uint32_t* __restrict__ docbits, int64_t nwords,
-                                                          int64_t limit, const unsigned long long* distinct,
-                                                          uint32_t* threshold, unsigned long long* reached) {
+                                                          int64_t limit, unsigned long long* scal) {
+  docbits += (int64_t)blockIdx.x * nwords;
+  const unsigned long long* distinct = scal + 3 * (int64_t)blockIdx.x;
+  uint32_t* threshold = reinterpret_cast<uint32_t*>(scal + 3 * (int64_t)blockIdx.x + 1);
+  unsigned long long* reached = scal + 3 * (int64_t)blockIdx.x + 2;
   __shared__ unsigned long long wsum[1024];
   __shared__ uint32_t found;
   const int t = threadIdx.x;
@@ -261,9 +269,11 @@ __global__ void __launch_bounds__(1024) k_limit_threshold(const uint32_t* __rest
 
 // keep bit g  <=>  key g is present and its first doc is below the threshold
 __global__ void __launch_bounds__(256) k_limit_keep(const uint32_t* __restrict__ first, int64_t G,
-                                                    const uint32_t* threshold, uint32_t* __restrict__ keep) {
-  const uint32_t T = *threshold;
+                                                    const unsigned long long* scal, uint32_t* __restrict__ keep) {
   const int64_t nw = (G + 31) / 32;
+  first += (int64_t)blockIdx.y * G;
+  keep += (int64_t)blockIdx.y * nw;
+  const uint32_t T = *reinterpret_cast<const uint32_t*>(scal + 3 * (int64_t)blockIdx.y + 1);
   for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < nw; w += (int64_t)gridDim.x * blockDim.x) {
     uint32_t bits = 0;
     for (int i = 0; i < 32; ++i) {
@@ -274,16 +284,14 @@ __global__ void __launch_bounds__(256) k_limit_keep(const uint32_t* __restrict__
   }
 }
 
-void launch_limit_select(const uint32_t* first, int64_t G, int64_t limit, int32_t num_docs, uint32_t* docbits,
+void launch_limit_select(const uint32_t* first, int64_t G, int64_t limit, int nseg, int64_t dbw, uint32_t* docbits,
                          uint32_t* keep, unsigned long long* scal, hipStream_t s) {
-  // scal: [0] distinct keys (zeroed by the caller), [1] threshold (u32), [2] limit reached flag (shared)
+  if (nseg <= 0) return;
   const int grid = (int)std::min<int64_t>((G + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_limit_mark, dim3(grid), dim3(256), 0, s, first, G, docbits, scal);
-  hipLaunchKernelGGL(k_limit_threshold, dim3(1), dim3(1024), 0, s, docbits, (int64_t)((num_docs + 31) / 32), limit,
-                     scal, reinterpret_cast<uint32_t*>(scal + 1), scal + 2);
+  hipLaunchKernelGGL(k_limit_mark, dim3(grid, nseg), dim3(256), 0, s, first, G, docbits, dbw, scal);
+  hipLaunchKernelGGL(k_limit_threshold, dim3(nseg), dim3(1024), 0, s, docbits, dbw, limit, scal);
   const int grid2 = (int)std::min<int64_t>(((G + 31) / 32 + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_limit_keep, dim3(grid2), dim3(256), 0, s, first, G, reinterpret_cast<const uint32_t*>(scal + 1),
-                     keep);
+  hipLaunchKernelGGL(k_limit_keep, dim3(grid2, nseg), dim3(256), 0, s, first, G, scal, keep);
   PH_HIP_CHECK(hipGetLastError());
 }
 

@@ -156,6 +156,7 @@ struct DevSegment {
   int32_t cstream[kMaxConj];        // FK_CONJ: staged stream of leaf k
   uint32_t clo[kMaxConj], clen[kMaxConj];  // FK_CONJ range leaf k: [clo, clo + clen)
   const uint32_t* cset[kMaxConj];   // FK_CONJ set leaf k: bitset over dictIds (nullptr: range leaf)
+  uint32_t* first_doc;              // numGroupsLimit pass: this segment's [num_groups] first matching doc per key
   DevColumn cols[kMaxCols];
   DevValCol vals[kMaxVals];
   DevValCol vals2[kMaxVals];       // second operand of a 2-operand expression term (KParams::val_op)
@@ -232,7 +233,7 @@ struct KParams {
   int32_t lds_hll_off;
   unsigned long long* out_count;  // [num_groups] matched docs per group
   unsigned long long* matched_total;  // group-by plans: matched docs of the launch (numDocsScanned), or nullptr
-  uint32_t* first_doc;            // numGroupsLimit pass: [num_groups] first matching doc per key (atomicMin)
+  uint32_t* first_doc;            // non-null: this launch is the numGroupsLimit first-seen pass (DevSegment.first_doc)
   unsigned long long* hkeys;      // MODE_GROUP_HASH: [num_groups] slot keys (kHashEmpty = free); out_* by slot
   int64_t hmask;                  // MODE_GROUP_HASH: slots - 1 (a power of two >= 2x the distinct keys possible)
   uint32_t* out_hll;              // [num_groups][num_hll][2^log2m]
@@ -500,8 +501,10 @@ ph_segment* segment_load_dir_impl(Context* ctx, const char* dir, const char* con
 // every container of every inverted leaf of a query in one launch (one workgroup per container)
 void launch_roaring_or(const RoaringContainer* c, int n, const RoaringTarget* targets, hipStream_t s);
 void launch_selftest_unpack(const uint32_t* fwd, int64_t n, int bits, int32_t* out, hipStream_t s);
-// numGroupsLimit: from one segment's first-doc-per-key table, the bitset of the keys the reference keeps
-void launch_limit_select(const uint32_t* first, int64_t G, int64_t limit, int32_t num_docs, uint32_t* docbits,
+// numGroupsLimit: from each limit segment's first-doc-per-key table (nseg tables of G entries, back to back), the
+// bitsets of the keys the reference keeps (nseg x ceil(G/32) words); docbits: nseg x dbw zeroed words; scal: 3 per
+// segment (distinct, threshold, reached; zeroed)
+void launch_limit_select(const uint32_t* first, int64_t G, int64_t limit, int nseg, int64_t dbw, uint32_t* docbits,
                          uint32_t* keep, unsigned long long* scal, hipStream_t s);
 void launch_selftest_staged(const DevSegment* seg, int32_t tile_words, int32_t stage_stride, int64_t n, int32_t* out,
                             hipStream_t s);

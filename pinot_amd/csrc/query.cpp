@@ -1178,28 +1178,11 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   for (int h = 0; h < num_hll; ++h) kp.hll_slot[h] = pl.slot.at(hll_cols[h]);
 
   // packed streams of the hot loop: slot 0 = the single-leaf filter column of each segment (if any),
-  // then the group-by columns, then the aggregated value columns; all of them are LDS-staged
-  std::vector<std::string> stream_cols;  // "" for the per-segment filter slot
-  if (q->filter_root >= 0) stream_cols.push_back("");
-  kp.f_stream = 0;
-  auto stream_of = [&](const std::string& c, const char* kind) {
-    std::string key = std::string(kind) + ":" + c;
-    for (size_t i = 0; i < stream_cols.size(); ++i)
-      if (stream_cols[i] == key) return (int)i;
-    stream_cols.push_back(key);
-    return (int)stream_cols.size() - 1;
-  };
-  for (int g = 0; g < q->num_group_by; ++g) kp.g_stream[g] = stream_of(group_cols[g], "id");
-  for (int j = 0; j < nvals; ++j) {
-    kp.v_stream[j] = stream_of(val_cols[j], "val");
-    kp.v2_stream[j] = val_exprs[j] ? stream_of(val_cols2[j], "val") : kp.v_stream[j];
-  }
-  if ((int)stream_cols.size() > kMaxStreams) fail(PH_ERR_UNSUPPORTED, "too many column streams in one query");
-  // FK_CONJ candidates: a WHERE that is an AND of predicates (or of ORs of predicates on one column) gets one staged
-  // dictId stream per filter column, when they fit beside the group / value streams
-  std::map<int, int> conj_stream;  // column slot -> staged stream
+  // then the group-by columns, then the aggregated value columns; all of them are LDS-staged.
+  // FK_CONJ queries (a WHERE that is an AND of predicates, or of ORs of predicates on one column) instead get one
+  // staged dictId stream per filter column and no per-segment filter slot, when they all fit kMaxStreams.
+  std::vector<std::string> fcols;
   if (q->filter_root >= 0 && q->filter_nodes[q->filter_root].type == PH_FILTER_AND) {
-    std::vector<std::string> fcols;
     bool shape = true;
     const ph_filter_node& r = q->filter_nodes[q->filter_root];
     for (int i = 0; i < r.num_children && shape; ++i) {
@@ -1219,24 +1202,33 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
       if (shape && std::find(fcols.begin(), fcols.end(), col) == fcols.end()) fcols.push_back(col);
     }
-    if (shape && fcols.size() >= 2 && (int)fcols.size() <= kMaxConj) {
-      std::vector<std::string> trial = stream_cols;
-      std::map<int, int> cs;
-      for (auto& c : fcols) {
-        const std::string key = "id:" + c;
-        auto it = std::find(trial.begin(), trial.end(), key);
-        if (it == trial.end()) {
-          trial.push_back(key);
-          it = trial.end() - 1;
-        }
-        cs[pl.slot.at(c)] = (int)(it - trial.begin());
-      }
-      if ((int)trial.size() <= kMaxStreams) {
-        stream_cols = trial;
-        conj_stream = cs;
-      }
-    }
+    if (!shape || (int)fcols.size() > kMaxConj) fcols.clear();
   }
+  std::vector<std::string> stream_cols;  // "" for the per-segment filter slot
+  std::map<int, int> conj_stream;        // FK_CONJ: column slot -> staged stream
+  auto stream_of = [&](const std::string& c, const char* kind) {
+    std::string key = std::string(kind) + ":" + c;
+    for (size_t i = 0; i < stream_cols.size(); ++i)
+      if (stream_cols[i] == key) return (int)i;
+    stream_cols.push_back(key);
+    return (int)stream_cols.size() - 1;
+  };
+  auto assign_streams = [&](bool conj) {
+    stream_cols.clear();
+    conj_stream.clear();
+    if (q->filter_root >= 0 && !conj) stream_cols.push_back("");
+    for (int g = 0; g < q->num_group_by; ++g) kp.g_stream[g] = stream_of(group_cols[g], "id");
+    for (int j = 0; j < nvals; ++j) {
+      kp.v_stream[j] = stream_of(val_cols[j], "val");
+      kp.v2_stream[j] = val_exprs[j] ? stream_of(val_cols2[j], "val") : kp.v_stream[j];
+    }
+    for (auto& c : fcols)
+      if (conj) conj_stream[pl.slot.at(c)] = stream_of(c, "id");
+    return (int)stream_cols.size() <= kMaxStreams;
+  };
+  const bool conj_query = !fcols.empty() && assign_streams(true);
+  if (!conj_query && !assign_streams(false)) fail(PH_ERR_UNSUPPORTED, "too many column streams in one query");
+  kp.f_stream = 0;  // the per-segment filter slot (unused by FK_CONJ queries, which have none)
   kp.nstage = (int)stream_cols.size();  // <= kMaxStreams == kMaxStage: every stream is staged
 
   // value column encodings + the table-wide value range (partitioned records carry value - vmin)
@@ -1384,8 +1376,25 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     d.num_docs = s->num_docs;
     const PNode& root = roots[i];
     const size_t si = dsegs.size();
+    auto conj_leaf = [&](const PNode& k) {
+      return k.kind == L_NODE && k.scan && (k.op == OP_RANGE || k.op == OP_SET) && conj_stream.count(k.col);
+    };
+    const bool single_conj = conj_query && conj_leaf(root);
     if (root.kind == L_ALL) {
       d.fkind = FK_ALL;
+    } else if (single_conj || (conj_query && root.op == OP_AND && (int)root.kids.size() <= kMaxConj &&
+                               std::all_of(root.kids.begin(), root.kids.end(), conj_leaf))) {
+      d.fkind = FK_CONJ;
+      d.nconj = single_conj ? 1 : (int32_t)root.kids.size();
+      for (int k = 0; k < d.nconj; ++k) {
+        const PNode& leaf = single_conj ? root : root.kids[k];
+        d.cstream[k] = conj_stream.at(leaf.col);
+        d.clo[k] = leaf.lo;
+        d.clen[k] = leaf.len;
+        if (leaf.op == OP_SET) conj_set_fix.push_back({si * kMaxConj + k, leaf.set});
+      }
+    } else if (conj_query && root.scan) {
+      fail(PH_ERR_INVALID_ARGUMENT, "scan leaf without a staged stream");  // not reached: every filter column has one
     } else if (root.op == OP_RANGE) {
       d.fkind = FK_RANGE;
       d.fslot = root.col;
@@ -1402,19 +1411,6 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       d.fkind = FK_DOCRANGE;
       d.flo = (uint32_t)root.ranges[0];
       d.flen = (uint32_t)(root.ranges[1] - root.ranges[0] + 1);
-    } else if (root.op == OP_AND && (int)root.kids.size() <= kMaxConj &&
-               std::all_of(root.kids.begin(), root.kids.end(), [&](const PNode& k) {
-                 return k.kind == L_NODE && k.scan && (k.op == OP_RANGE || k.op == OP_SET) && conj_stream.count(k.col);
-               })) {
-      d.fkind = FK_CONJ;
-      d.nconj = (int32_t)root.kids.size();
-      for (int k = 0; k < d.nconj; ++k) {
-        const PNode& leaf = root.kids[k];
-        d.cstream[k] = conj_stream.at(leaf.col);
-        d.clo[k] = leaf.lo;
-        d.clen[k] = leaf.len;
-        if (leaf.op == OP_SET) conj_set_fix.push_back({si * kMaxConj + k, leaf.set});
-      }
     } else {
       d.fkind = FK_GENERIC;
       emit(root, progs[i]);
@@ -1464,10 +1460,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       d.streams[kp.g_stream[g]] = DevStream{c.d_fwd.as<uint32_t>(), c.bits, 0};
     }
     for (int k = 0; d.fkind == FK_CONJ && k < d.nconj; ++k) {
-      Column& c = *s->columns.at(slot_names[root.kids[k].col]);
+      Column& c = *s->columns.at(slot_names[(d.nconj == 1 && root.op != OP_AND) ? root.col : root.kids[k].col]);
       d.streams[d.cstream[k]] = DevStream{c.d_fwd.as<uint32_t>(), c.bits, 0};
     }
-    if (q->filter_root >= 0) {
+    if (q->filter_root >= 0 && !conj_query) {
       // bits = 0: nothing to stage for this segment's filter (FK_ALL / bitmap / doc range / program)
       d.streams[0] = DevStream{nullptr, 0, 0};
       if (d.fkind == FK_RANGE || d.fkind == FK_SET) {
@@ -1537,12 +1533,24 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // the first-seen pass below, read by the scan: a gather, so the late prefetch)
   std::vector<int> limit_segs;
   unsigned long long* limit_scal = nullptr;  // [3] per limit segment: distinct, threshold, reached
+  uint32_t* limit_keep = nullptr;             // [limit segments][ceil(G / 32)] keep bitsets
+  uint32_t* limit_first = nullptr;            // [limit segments][G] first matching doc per key
   if (any_limit && q->num_group_by > 0) {
     for (size_t k = 0; k < dsegs.size(); ++k)
       if (seg_limit[dseg_src[k]]) limit_segs.push_back((int)k);
     const double keep_bytes = (double)limit_segs.size() * (double)((G + 31) / 32) * 4.0;
     if (keep_bytes > 8e9) fail(PH_ERR_UNSUPPORTED, "numGroupsLimit emulation needs too many key bitsets");
-    for (int k : limit_segs) dsegs[k].keep = scratch.alloc<uint32_t>((size_t)(G + 31) / 32);
+    // one block each for the limit segments' keep bitsets and first-doc tables (every segment's pass runs in one
+    // launch, the selections in one launch per step)
+    const double first_bytes = (double)limit_segs.size() * (double)G * 4.0;
+    if (first_bytes > 16e9) fail(PH_ERR_UNSUPPORTED, "numGroupsLimit emulation needs too many first-doc tables");
+    const size_t kw = (size_t)(G + 31) / 32;
+    limit_keep = scratch.alloc<uint32_t>(std::max<size_t>(1, kw * limit_segs.size()));
+    limit_first = scratch.alloc<uint32_t>(std::max<size_t>(1, (size_t)G * limit_segs.size()));
+    for (size_t t = 0; t < limit_segs.size(); ++t) {
+      dsegs[limit_segs[t]].keep = limit_keep + t * kw;
+      dsegs[limit_segs[t]].first_doc = limit_first + t * (size_t)G;
+    }
     limit_scal = scratch.alloc<unsigned long long>(3 * limit_segs.size());
     PH_HIP_CHECK(hipMemsetAsync(limit_scal, 0, 24 * limit_segs.size(), st));
     if (!limit_segs.empty()) kp.late_prefetch = 1;
@@ -1665,13 +1673,17 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   if (!chunks.empty()) {
     DevSegment* d_segs = scratch.alloc<DevSegment>(dsegs.size());
     FilterInsn* d_prog = scratch.alloc<FilterInsn>(std::max<size_t>(1, all_insns.size()));
-    Chunk* d_chunks = scratch.alloc<Chunk>(chunks.size());
+    std::vector<Chunk> all_chunks = chunks;  // + the numGroupsLimit pass's chunks (limit segments only)
+    for (int k : limit_segs)
+      all_chunks.insert(all_chunks.end(), chunks.begin() + dseg_chunks[k].first, chunks.begin() + dseg_chunks[k].second);
+    const size_t n_limit_chunks = all_chunks.size() - chunks.size();
+    Chunk* d_chunks = scratch.alloc<Chunk>(all_chunks.size());
     const size_t b1 = sizeof(DevSegment) * dsegs.size(), b2 = sizeof(FilterInsn) * all_insns.size(),
-                 b3 = sizeof(Chunk) * chunks.size();
+                 b3 = sizeof(Chunk) * all_chunks.size();
     uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(b1 + b2 + b3));
     memcpy(stage, dsegs.data(), b1);
     memcpy(stage + b1, all_insns.data(), b2);
-    memcpy(stage + b1 + b2, chunks.data(), b3);
+    memcpy(stage + b1 + b2, all_chunks.data(), b3);
     PH_HIP_CHECK(hipMemcpyAsync(d_segs, stage, b1, hipMemcpyHostToDevice, st));
     if (b2) PH_HIP_CHECK(hipMemcpyAsync(d_prog, stage + b1, b2, hipMemcpyHostToDevice, st));
     PH_HIP_CHECK(hipMemcpyAsync(d_chunks, stage + b1 + b2, b3, hipMemcpyHostToDevice, st));
@@ -1686,28 +1698,26 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       if (mode == MODE_GROUP_LDS) blocks_per_cu = std::min(blocks_per_cu, 4);
       const int grid = (int)std::min<int64_t>((int64_t)chunks.size(), (int64_t)ctx->num_cus * blocks_per_cu);
       if (!limit_segs.empty()) {
-        // first-seen pass per limit segment (MODE_GROUP_GLOBAL records each key's first matching doc), then the
-        // kept keys; stream-ordered, so one first-doc table and one doc bitmap serve every segment in turn
+        // first-seen pass over every limit segment in ONE launch (MODE_GROUP_GLOBAL records each key's first
+        // matching doc in the segment's own table), then the kept keys of every segment in one select step; the
+        // pass walks the limit segments' chunks, appended after the main chunk list
         int32_t maxdocs = 0;
         for (int k : limit_segs) maxdocs = std::max(maxdocs, dsegs[k].num_docs);
-        uint32_t* first = scratch.alloc<uint32_t>((size_t)G);
-        uint32_t* docbits = scratch.alloc<uint32_t>((size_t)maxdocs / 32 + 2);
+        const int64_t dbw = (int64_t)maxdocs / 32 + 2;
+        uint32_t* docbits = scratch.alloc<uint32_t>((size_t)dbw * limit_segs.size());
+        PH_HIP_CHECK(hipMemsetAsync(limit_first, 0xff, 4 * (size_t)G * limit_segs.size(), st));
+        PH_HIP_CHECK(hipMemsetAsync(docbits, 0, 4 * (size_t)dbw * limit_segs.size(), st));
         KParams k1 = kp;
         k1.matched_total = nullptr;
         k1.late_prefetch = 1;
+        k1.first_doc = limit_first;  // the pass flag; each segment writes its own table
+        k1.chunk_begin = (int32_t)chunks.size();
+        k1.chunk_end = (int32_t)(chunks.size() + n_limit_chunks);
         const size_t lds1 = (size_t)kWaves * kp.stage_stride + 16;
-        for (size_t t = 0; t < limit_segs.size(); ++t) {
-          const int k = limit_segs[t];
-          PH_HIP_CHECK(hipMemsetAsync(first, 0xff, 4 * (size_t)G, st));
-          PH_HIP_CHECK(hipMemsetAsync(docbits, 0, 4 * ((size_t)dsegs[k].num_docs / 32 + 2), st));
-          k1.first_doc = first;
-          k1.chunk_begin = dseg_chunks[k].first;
-          k1.chunk_end = dseg_chunks[k].second;
-          const int g1 = std::min<int>(k1.chunk_end - k1.chunk_begin, ctx->num_cus * 4);
-          if (g1 > 0) launch_scan(k1, MODE_GROUP_GLOBAL, q->num_group_by, 0, g1, lds1, st);
-          launch_limit_select(first, G, group_limit, dsegs[k].num_docs, docbits, const_cast<uint32_t*>(dsegs[k].keep),
-                              limit_scal + 3 * t, st);
-        }
+        const int g1 = std::min<int>(k1.chunk_end - k1.chunk_begin, ctx->num_cus * 4);
+        if (g1 > 0) launch_scan(k1, MODE_GROUP_GLOBAL, q->num_group_by, 0, g1, lds1, st);
+        launch_limit_select(limit_first, G, group_limit, (int)limit_segs.size(), dbw, docbits, limit_keep, limit_scal,
+                            st);
       }
       // an interruptible call scans in batches of kInterruptChunks chunks and checks between them
       const int32_t nchunks = (int32_t)chunks.size();

@@ -575,7 +575,7 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
         g = slot;
       }
       if (MODE == MODE_GROUP_GLOBAL && LATE && p.first_doc) {  // numGroupsLimit pass: first doc of every key
-        atomicMin(&p.first_doc[g], doc);
+        atomicMin(&S->first_doc[g], doc);
         return;
       }
       if (MODE != MODE_GROUP_HASH && LATE && S->keep && !((gld(S->keep + (g >> 5)) >> (g & 31)) & 1u))
