@@ -252,6 +252,8 @@ void launch_scan_agg(const KParams& p, int mode, int grid, size_t lds, hipStream
     hipLaunchKernelGGL(k_agg_lean, dim3(grid), dim3(kBlock), lds, s, p);
   } else if (p.num_vals <= 1 && !p.val_op[0]) {
     launch_late<MODE_AGG, 0, 1>(p, grid, lds, s);  // ValCap 1
+  } else if (p.num_vals <= 1) {
+    launch_late<MODE_AGG, 0, 2>(p, grid, lds, s);  // ValCap 1 + a 2-operand expression
   } else {
     launch_late<MODE_AGG, 0, 0>(p, grid, lds, s);
   }

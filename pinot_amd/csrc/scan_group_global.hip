@@ -4,7 +4,7 @@
 namespace ph {
 
 void launch_scan_group_global(const KParams& p, int ng, int grid, size_t lds, hipStream_t s) {
-  launch_mode<MODE_GROUP_GLOBAL>(p, ng, (p.num_vals <= 1 && !p.val_op[0]) ? 1 : 0, grid, lds, s);
+  launch_mode<MODE_GROUP_GLOBAL>(p, ng, value_variant(p), grid, lds, s);
 }
 
 }  // namespace ph

@@ -207,7 +207,7 @@ void launch_scan_group_lds(const KParams& p, int ng, int grid, size_t lds, hipSt
     }
     return;
   }
-  launch_mode<MODE_GROUP_LDS>(p, ng, (p.num_vals <= 1 && !p.val_op[0]) ? 1 : 0, grid, lds, s);
+  launch_mode<MODE_GROUP_LDS>(p, ng, value_variant(p), grid, lds, s);
 }
 
 }  // namespace ph

@@ -397,8 +397,8 @@ struct NumLoads {
 // Value columns the register state is sized for.  REC64 means 64-bit partition records in MODE_PARTITION; in
 // every other mode it selects the single-value-column variant, so a one-column query does not carry the
 // accumulators and cursors of kMaxVals columns (r1: 158 VGPRs / 3 waves per SIMD in MODE_AGG otherwise).
-// 2-operand expression terms run on the kMaxVals variant only (their second cursor costs the one-column
-// variant ~15 VGPRs: 90 -> 105 in r2).
+// 2-operand expression terms run on the kMaxVals variant, or on REC64 = 2: the one-column variant with the
+// expression's second cursor (~15 VGPRs more than REC64 = 1; SSB Q1.x / Q4.x: one SUM(a*b) / SUM(a-b) column).
 template <int MODE, int REC64>
 struct ValCap {
   // MODE_PARTITION is only planned for <= 1 value column (query.cpp part_ok)
@@ -466,7 +466,7 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
     vkind[j] = S->vals[j].kind;
     vbase[j] = S->vals[j].base;
     vtab[j] = S->vals[j].table;
-    if (MODE != MODE_PARTITION && VC > 1 && p.val_op[j]) {  // expressions: the kMaxVals variant only
+    if (MODE != MODE_PARTITION && (VC > 1 || REC64 == 2) && p.val_op[j]) {  // expressions: kMaxVals or REC64 2
       vcur2[j] = bit_cursor(wst + p.stage_soff[p.v2_stream[j]], S->streams[p.v2_stream[j]].bits, lane);
       vkind2[j] = S->vals2[j].kind;
       vbase2[j] = S->vals2[j].base;
@@ -520,7 +520,7 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
         if (j < p.num_vals) {
           if (LATE) read_value(vkind[j], vbase[j], vtab[j], cursor_value(vcur[j], u), vi[j], vd[j]);
           else vi[j] = vbase[j] + (int64_t)cursor_value(vcur[j], u);  // VK_PACKED: no gather
-          const int eop = VC > 1 ? p.val_op[j] : 0;
+          const int eop = (MODE != MODE_PARTITION && (VC > 1 || REC64 == 2)) ? p.val_op[j] : 0;
           if (eop) {
             // `a <op> b` per row: exact int64 for integer terms, else double like the reference's
             // transformToDoubleValuesSV (MultiplicationTransformFunction.java:89-104)
@@ -960,9 +960,18 @@ inline void launch_late(const KParams& p, int grid, size_t lds, hipStream_t s) {
 
 template <int MODE, int NG>
 inline void launch_ng(const KParams& p, int rec64, int grid, size_t lds, hipStream_t s) {
+  if constexpr (MODE != MODE_PARTITION) {
+    if (rec64 == 2) {
+      launch_late<MODE, NG, 2>(p, grid, lds, s);
+      return;
+    }
+  }
   if (rec64) launch_late<MODE, NG, 1>(p, grid, lds, s);
   else launch_late<MODE, NG, 0>(p, grid, lds, s);
 }
+
+// the value-column variant of a non-partition launch: 1 = one plain column, 2 = one 2-operand expression, 0 = any
+inline int value_variant(const KParams& p) { return p.num_vals <= 1 ? (p.val_op[0] ? 2 : 1) : 0; }
 
 template <int MODE>
 inline void launch_mode(const KParams& p, int ng, int rec64, int grid, size_t lds, hipStream_t s) {

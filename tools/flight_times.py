@@ -19,7 +19,10 @@ def main():
     ctx = GpuContext(0)
     pinned = [ctx.pin(built[i % distinct]) for i in range(nseg)]
     only = os.environ.get("FLIGHT_ONLY")
-    for name, sql in W.SSB_QUERIES.items():
+    queries = dict(W.SSB_QUERIES)
+    if os.environ.get("FLIGHT_SQL"):  # ad-hoc variants: "sql;;sql;;..."
+        queries = {f"X{i}": q for i, q in enumerate(os.environ["FLIGHT_SQL"].split(";;"))}
+    for name, sql in queries.items():
         if only and name not in only.split(","):
             continue
         q = parse_sql(sql)
