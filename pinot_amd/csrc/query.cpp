@@ -1292,6 +1292,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
                                                                        (uint64_t)(vmax - vmin) < (1ull << 32))) &&
                          G <= ((int64_t)kPartMaxParts << kPartKeysLog2) && !any_limit &&
                          getenv("PH_DISABLE_PARTITION") == nullptr;
+    // LDS-private tables up to 64 KiB; r2 measured 96 KiB tables (one workgroup per CU) slower than the HBM table
+    // for selective filters (SSB Q2.1, 7000 keys x COUNT + SUM: 3.9 vs 3.2 ms; Q2.3 3.2 vs 1.6 ms)
     if (off <= 64 * 1024) {
       mode = MODE_GROUP_LDS;
       lds_tables = off;
@@ -1510,6 +1512,15 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       return n;
     };
     while (tw > 4 && loads(tw) > pool) tw /= 2;
+    if (mode == MODE_GROUP_LDS) {  // staging + the LDS tables within one CU's 160 KiB
+      auto stage = [&](int t) {
+        size_t b = 0;
+        for (int s2 = 0; s2 < kp.nstage; ++s2) b += maxbits[s2] ? stage_stream_bytes(t, maxbits[s2]) : 0;
+        return (size_t)kWaves * std::max<size_t>(16, b);
+      };
+      while (tw > 4 && stage(tw) + lds_tables > 160 * 1024) tw /= 2;
+      if (stage(tw) + lds_tables > 160 * 1024) fail(PH_ERR_UNSUPPORTED, "LDS group table and staging exceed 160 KiB");
+    }
     if (loads(tw) > pool) fail(PH_ERR_UNSUPPORTED, "staged streams too wide for the prefetch pool");
     kp.tile_words = tw;
     int32_t soff = 0;
