@@ -324,8 +324,15 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # one process per GPU over RCCL; PH_DIST_BACKEND=gloo rehearses the N > 1 path on a box with fewer GPUs than
+        # ranks (ranks share devices round-robin; gloo all-reduces and slices where RCCL reduce-scatters)
+        local_rank = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        backend = os.environ.get("PH_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
     device = local_rank
     if args.workload in FLIGHTS:
         return flight_main(args, world, rank, dist, device)
