@@ -211,7 +211,9 @@ struct KParams {
                                   // 1 no record stores, 2 no flush, 4 no record append
   unsigned long long* dbg;        // PH_DEBUG_STAMPS: per-workgroup cycle totals [grid][4] (wave 0)
   int32_t stage_soff[kMaxStage];  // byte offset of staged stream s inside a wave's area
-  int32_t lds_cnt_off;            // MODE_GROUP_LDS: byte offset of the count table
+  int32_t lds_cnt_off;            // MODE_GROUP_LDS: byte offset of the count table (MODE_GROUP_GLOBAL: cache counts)
+  int32_t gc_slots;               // MODE_GROUP_GLOBAL: LDS group cache slots (power of 2; 0 = off)
+  int32_t gc_key_off;             // MODE_GROUP_GLOBAL: byte offset of the cache's key array (uint32, ~0u = empty)
   int32_t num_group_cols;
   int32_t group_slot[kMaxGroupCols];
   int64_t group_stride[kMaxGroupCols];

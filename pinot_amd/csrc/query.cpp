@@ -1305,6 +1305,25 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       const double bytes = (double)G * (8.0 * nout + 4.0 * num_hll * (m ? m : 1));
       if (bytes <= kDenseTableBudget) {
         mode = MODE_GROUP_GLOBAL;
+        // per-workgroup LDS cache of the groups it meets (open addressing, 1024 slots): repeated keys aggregate in
+        // LDS and reach the HBM table once per workgroup at the end; a key that finds no slot within 8 probes goes
+        // straight to the HBM table.  Device atomics from 64 lanes at 64 scattered addresses are the slow part of
+        // this mode (r2: SSB Q2.1, 7000 keys, 3.2 ms of which ~2.2 ms atomics)
+        if (num_hll == 0 && nvals <= 1 && G < (int64_t)0xffffffffu && getenv("PH_NO_GROUP_CACHE") == nullptr) {
+          const size_t S = 1024;
+          size_t o = 0;
+          kp.gc_key_off = (int32_t)o;
+          o += 4 * S;
+          kp.lds_cnt_off = (int32_t)o;
+          o += 4 * S;
+          for (int j = 0; j < nvals; ++j) {
+            if (val_ops[j] & 1) { kp.lds_sum_off[j] = (int32_t)o; o += 8 * S; }
+            if (val_ops[j] & 2) { kp.lds_min_off[j] = (int32_t)o; o += 8 * S; }
+            if (val_ops[j] & 4) { kp.lds_max_off[j] = (int32_t)o; o += 8 * S; }
+          }
+          kp.gc_slots = (int32_t)S;
+          lds_tables = o;
+        }
       } else {
         // key space beyond the dense budget: open-addressing table over the keys that can occur -- at most one
         // per scanned doc -- with >= 2x slots (DictionaryBasedGroupKeyGenerator's map-based holders, :598/:778)
@@ -1504,7 +1523,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     const int pool = mode == MODE_COUNT ? kPrefetchCount : (mode == MODE_PARTITION ? kPrefetchPartition : kPrefetchOther);
     // r1/r2 sweeps: MODE_PARTITION rounds (8 waves x 8 words) append ~2048 records, which keeps a
     // partition's ring (32 slots) from overflowing
-    int tw = mode == MODE_PARTITION ? 8 : (mode == MODE_GROUP_LDS ? 16 : kMaxTileWords);
+    int tw = mode == MODE_PARTITION ? 8 : ((mode == MODE_GROUP_LDS || kp.gc_slots) ? 16 : kMaxTileWords);
     if (const char* e = getenv("PH_TILE_WORDS")) tw = std::max(4, std::min(kMaxTileWords, atoi(e)));  // tuning knob
     auto loads = [&](int t) {
       int n = 0;
@@ -1623,6 +1642,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     kp.stage_off = 0;
     kp.lds_cnt_off += (int32_t)stage_bytes;
     kp.lds_hll_off += (int32_t)stage_bytes;
+    kp.gc_key_off += (int32_t)stage_bytes;
     for (int j = 0; j < nvals; ++j) {
       kp.lds_sum_off[j] += (int32_t)stage_bytes;
       kp.lds_min_off[j] += (int32_t)stage_bytes;
@@ -1722,6 +1742,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         k1.matched_total = nullptr;
         k1.late_prefetch = 1;
         k1.first_doc = limit_first;  // the pass flag; each segment writes its own table
+        k1.gc_slots = 0;             // the pass aggregates nothing (and its LDS holds only the staging)
         k1.chunk_begin = (int32_t)chunks.size();
         k1.chunk_end = (int32_t)(chunks.size() + n_limit_chunks);
         const size_t lds1 = (size_t)kWaves * kp.stage_stride + 16;

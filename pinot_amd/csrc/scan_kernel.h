@@ -580,7 +580,26 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
       }
       if (MODE != MODE_GROUP_HASH && LATE && S->keep && !((gld(S->keep + (g >> 5)) >> (g & 31)) & 1u))
         return;  // beyond numGroupsLimit
-      if (MODE == MODE_GROUP_LDS) atomicAdd(&lds_cnt[g], 1u);
+      // MODE_GROUP_GLOBAL: the workgroup's LDS group cache first (slot found -> aggregate in LDS like MODE_GROUP_LDS)
+      bool local = MODE == MODE_GROUP_LDS;
+      if (MODE == MODE_GROUP_GLOBAL && p.gc_slots) {
+        uint32_t* gkeys = reinterpret_cast<uint32_t*>(smem + p.gc_key_off);
+        const uint32_t k32 = (uint32_t)g;
+        const uint32_t smask = (uint32_t)p.gc_slots - 1u;
+        uint32_t h = (k32 * 2654435761u) & smask;
+#pragma unroll 1
+        for (int probe = 0; probe < 8; ++probe) {
+          uint32_t k = gkeys[h];
+          if (k == 0xffffffffu) k = atomicCAS(&gkeys[h], 0xffffffffu, k32);
+          if (k == 0xffffffffu || k == k32) {
+            local = true;
+            g = h;
+            break;
+          }
+          h = (h + 1u) & smask;
+        }
+      }
+      if (local) atomicAdd(&lds_cnt[g], 1u);
       else if (MODE == MODE_GROUP_GLOBAL || MODE == MODE_GROUP_HASH) atomicAdd(&p.out_count[g], 1ull);
 #pragma unroll
       for (int j = 0; j < VC; ++j) {
@@ -594,11 +613,11 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
           if (ops & OPS_MIN) acc.vmin[j] = iv < acc.vmin[j] ? iv : acc.vmin[j];
           if (ops & OPS_MAX) acc.vmax[j] = iv > acc.vmax[j] ? iv : acc.vmax[j];
         } else {
-          void* sb = MODE == MODE_GROUP_LDS ? (void*)(smem + p.lds_sum_off[j]) : p.out_sum[j];
-          long long* mnb = MODE == MODE_GROUP_LDS ? reinterpret_cast<long long*>(smem + p.lds_min_off[j])
-                                                  : reinterpret_cast<long long*>(p.out_min[j]);
-          long long* mxb = MODE == MODE_GROUP_LDS ? reinterpret_cast<long long*>(smem + p.lds_max_off[j])
-                                                  : reinterpret_cast<long long*>(p.out_max[j]);
+          void* sb = local ? (void*)(smem + p.lds_sum_off[j]) : p.out_sum[j];
+          long long* mnb = local ? reinterpret_cast<long long*>(smem + p.lds_min_off[j])
+                                 : reinterpret_cast<long long*>(p.out_min[j]);
+          long long* mxb = local ? reinterpret_cast<long long*>(smem + p.lds_max_off[j])
+                                 : reinterpret_cast<long long*>(p.out_max[j]);
           if (ops & OPS_SUM) {
             if (p.val_is_int[j]) atomicAdd(reinterpret_cast<unsigned long long*>(sb) + g, (unsigned long long)iv);
             else atomicAdd(reinterpret_cast<double*>(sb) + g, vd[j]);
@@ -745,6 +764,22 @@ __global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : kBlock) 
     for (int64_t i = threadIdx.x; i < nh; i += kBlock) lds_hll[i] = 0;
   } else if (MODE == MODE_AGG) {
     for (int i = threadIdx.x; i < p.num_hll * m; i += kBlock) lds_hll[i] = 0;
+  } else if (MODE == MODE_GROUP_GLOBAL) {
+    if (p.gc_slots) {  // LDS group cache: empty keys, zero counts / sums, min / max identities
+      uint32_t* gkeys = reinterpret_cast<uint32_t*>(smem + p.gc_key_off);
+      for (int i = threadIdx.x; i < p.gc_slots; i += kBlock) {
+        gkeys[i] = 0xffffffffu;
+        lds_cnt[i] = 0;
+#pragma unroll
+        for (int j = 0; j < VC; ++j) {
+          if (j >= p.num_vals) continue;
+          const int ops = p.val_ops[j];
+          if (ops & OPS_SUM) reinterpret_cast<int64_t*>(smem + p.lds_sum_off[j])[i] = 0;
+          if (ops & OPS_MIN) reinterpret_cast<int64_t*>(smem + p.lds_min_off[j])[i] = INT64_MAX;
+          if (ops & OPS_MAX) reinterpret_cast<int64_t*>(smem + p.lds_max_off[j])[i] = INT64_MIN;
+        }
+      }
+    }
   } else if (MODE == MODE_PARTITION) {
     uint32_t* words = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
     for (int i = threadIdx.x; i < p.num_parts; i += BLOCK) words[i] = 0;
@@ -932,6 +967,32 @@ __global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : kBlock) 
     const int64_t nh = p.num_groups * p.num_hll * m;
     for (int64_t i = threadIdx.x; i < nh; i += kBlock)
       if (lds_hll[i]) atomicMax(&p.out_hll[i], lds_hll[i]);
+  }
+  if (MODE == MODE_GROUP_GLOBAL && p.gc_slots) {  // the workgroup's cached groups -> the HBM table, once each
+    __syncthreads();
+    const uint32_t* gkeys = reinterpret_cast<const uint32_t*>(smem + p.gc_key_off);
+    for (int i = threadIdx.x; i < p.gc_slots; i += kBlock) {
+      const uint32_t key = gkeys[i];
+      const uint32_t cnt = lds_cnt[i];
+      if (key == 0xffffffffu || !cnt) continue;
+      atomicAdd(&p.out_count[key], (unsigned long long)cnt);
+#pragma unroll
+      for (int j = 0; j < VC; ++j) {
+        if (j >= p.num_vals) continue;
+        const int ops = p.val_ops[j];
+        if (ops & OPS_SUM) {
+          if (p.val_is_int[j])
+            atomicAdd(reinterpret_cast<unsigned long long*>(p.out_sum[j]) + key,
+                      reinterpret_cast<const unsigned long long*>(smem + p.lds_sum_off[j])[i]);
+          else
+            atomicAdd(reinterpret_cast<double*>(p.out_sum[j]) + key, reinterpret_cast<const double*>(smem + p.lds_sum_off[j])[i]);
+        }
+        if (ops & OPS_MIN)
+          atomicMin(reinterpret_cast<long long*>(p.out_min[j]) + key, reinterpret_cast<const long long*>(smem + p.lds_min_off[j])[i]);
+        if (ops & OPS_MAX)
+          atomicMax(reinterpret_cast<long long*>(p.out_max[j]) + key, reinterpret_cast<const long long*>(smem + p.lds_max_off[j])[i]);
+      }
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0 && s_matched && (MODE == MODE_COUNT || MODE == MODE_AGG))
