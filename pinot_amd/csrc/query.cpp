@@ -1294,7 +1294,13 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
                          getenv("PH_DISABLE_PARTITION") == nullptr;
     // LDS-private tables up to 64 KiB; r2 measured 96 KiB tables (one workgroup per CU) slower than the HBM table
     // for selective filters (SSB Q2.1, 7000 keys x COUNT + SUM: 3.9 vs 3.2 ms; Q2.3 3.2 vs 1.6 ms)
-    if (off <= 64 * 1024) {
+    // Dense LDS tables up to 64 KiB (PH_LDS_TABLE_MAX: tuning knob).  r2: routing 32-64 KiB tables to the cached
+    // HBM table instead did not speed up SSB Q3.1 / Q4.2 and made an unfiltered 4375-key group-by 22x slower
+    // (38.8 vs 1.7 ms: the cache cannot hold every key, the rest pays device atomics)
+    size_t lds_table_max = 64 * 1024;
+    if (const char* e = getenv("PH_LDS_TABLE_MAX")) lds_table_max = (size_t)std::max(0, atoi(e));
+    const bool cache_ok = num_hll == 0 && nvals <= 1 && getenv("PH_NO_GROUP_CACHE") == nullptr;
+    if (off <= (cache_ok ? lds_table_max : (size_t)64 * 1024)) {
       mode = MODE_GROUP_LDS;
       lds_tables = off;
     } else if (part_ok && G >= 65536) {
@@ -1309,8 +1315,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         // LDS and reach the HBM table once per workgroup at the end; a key that finds no slot within 8 probes goes
         // straight to the HBM table.  Device atomics from 64 lanes at 64 scattered addresses are the slow part of
         // this mode (r2: SSB Q2.1, 7000 keys, 3.2 ms of which ~2.2 ms atomics)
-        if (num_hll == 0 && nvals <= 1 && G < (int64_t)0xffffffffu && getenv("PH_NO_GROUP_CACHE") == nullptr) {
-          const size_t S = 1024;
+        if (cache_ok && G < (int64_t)0xffffffffu) {
+          const size_t S = G <= 65536 ? 2048 : 1024;
           size_t o = 0;
           kp.gc_key_off = (int32_t)o;
           o += 4 * S;
