@@ -1879,8 +1879,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       bp.out_sum = has_sum ? reinterpret_cast<int64_t*>(kp.out_sum[0]) : nullptr;
       bp.out_min = has_min ? kp.out_min[0] : nullptr;
       bp.out_max = has_max ? kp.out_max[0] : nullptr;
-      // kernel B slices: enough (partition, slice) workgroups to give every CU two
-      int slices = (int)std::max<int64_t>(1, std::min<int64_t>(8, (2 * (int64_t)ctx->num_cus + P - 1) / P));
+      // kernel B slices: about one (partition, slice) workgroup per CU; a single slice owns its key range (no
+      // device atomics in the merge).  r2 sweep, config 3 (P = 245): 1 slice 3.89, 2 slices 3.90, 3 slices 3.99 ms
+      int slices = (int)std::max<int64_t>(1, std::min<int64_t>(8, (int64_t)ctx->num_cus / P));
       if (const char* e = getenv("PH_PART_SLICES")) slices = std::max(1, std::min(16, atoi(e)));  // tuning knob
       bp.slices = slices;
       bp.dbg = kp.part_dbg;
