@@ -459,3 +459,21 @@ def test_conjunctive_scan_leaves(ctx, where, group):
     else:
         sql = "SELECT COUNT(*), SUM(m), MIN(b), MAX(b), SUM(d), SUM(m * b) FROM t" + where
     _both(ctx, tables, sql, inverted=())
+
+
+# MODE_GROUP_GLOBAL's per-workgroup LDS group cache (one value column): keys that all fit the cache, key spaces
+# that overflow it (spilled keys go straight to the HBM table), integer and DOUBLE values with SUM / MIN / MAX,
+# selective and unfiltered; a numGroupsLimit that truncates runs through the same path
+@pytest.mark.parametrize("sql", [
+    "SET numGroupsLimit=10000000; SELECT b, c, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t WHERE a < 4 GROUP BY b, c "
+    "ORDER BY b, c LIMIT 1000000",
+    "SET numGroupsLimit=10000000; SELECT b, c, SUM(d), MIN(d), MAX(d) FROM t GROUP BY b, c ORDER BY b, c LIMIT 1000000",
+    "SET numGroupsLimit=10000000; SELECT a, b, COUNT(*), SUM(m) FROM t WHERE s > 25 GROUP BY a, b ORDER BY a, b "
+    "LIMIT 1000000",
+    "SET numGroupsLimit=300; SELECT b, c, COUNT(*), SUM(m) FROM t WHERE a IN (1, 2) AND m > 0 GROUP BY b, c "
+    "ORDER BY b, c LIMIT 1000000",
+])
+def test_group_cache_global_table(ctx, sql):
+    rng = np.random.default_rng(abs(hash(sql)) % 2**32)
+    tables = [_random_table(rng, n) for n in (40_000, 64 * 700 + 9)]
+    _both(ctx, tables, sql, inverted=())
