@@ -1529,7 +1529,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     const int pool = mode == MODE_COUNT ? kPrefetchCount : (mode == MODE_PARTITION ? kPrefetchPartition : kPrefetchOther);
     // r1/r2 sweeps: MODE_PARTITION rounds (8 waves x 8 words) append ~2048 records, which keeps a
     // partition's ring (32 slots) from overflowing
-    int tw = mode == MODE_PARTITION ? 8 : ((mode == MODE_GROUP_LDS || kp.gc_slots) ? 16 : kMaxTileWords);
+    // (r2 interleaved sweep, config 3: partition tiles of 12 words 3.80-3.82 ms, 8 words 3.89-3.93, 10 words 4.36)
+    int tw = mode == MODE_PARTITION ? 12 : ((mode == MODE_GROUP_LDS || kp.gc_slots) ? 16 : kMaxTileWords);
     if (const char* e = getenv("PH_TILE_WORDS")) tw = std::max(4, std::min(kMaxTileWords, atoi(e)));  // tuning knob
     auto loads = [&](int t) {
       int n = 0;
