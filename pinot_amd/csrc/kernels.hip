@@ -403,49 +403,57 @@ void launch_hll_table(const void* values, int32_t is_int, int64_t n, int log2m, 
 int32_t murmur_hash_long(int64_t v) { return murmur_long(v); }
 uint32_t hll_entry(int32_t hash, int log2m) { return hll_entry_of(hash, log2m); }
 
-// Portable-roaring containers -> doc bitmap (one workgroup per container; bytes read individually because
-// container payloads need not be 2-byte aligned inside the inverted-index buffer).
+// Portable-roaring containers -> doc bitmap (bytes read individually because container payloads need not be
+// 2-byte aligned inside the inverted-index buffer).
 __device__ __forceinline__ uint32_t ld_u16(const uint8_t* b) { return (uint32_t)b[0] | ((uint32_t)b[1] << 8); }
 
-__global__ void k_roaring_or(const RoaringContainer* __restrict__ cs, const RoaringTarget* __restrict__ targets) {
-  const RoaringContainer c = cs[blockIdx.x];
-  const RoaringTarget t = targets[c.target];
-  const uint8_t* base = t.base;
-  uint32_t* bitmap = t.bitmap;
-  const int32_t num_docs = t.num_docs;
+// one workgroup per work item (a leaf's dictId, up to kRoaringWorkContainers of its containers): the 4 waves take
+// the containers round-robin, each OR-ed by one wave (the directory is device-resident since pin, so a query
+// uploads only its work items)
+__device__ __forceinline__ void roaring_or_container(const RoaringContainer& c, const uint8_t* __restrict__ base,
+                                                     uint32_t* __restrict__ bitmap, int32_t num_docs, int lane) {
   const uint8_t* pay = base + c.offset;
   const uint32_t hi = (uint32_t)c.key << 16;
   const uint32_t nwords = ((uint32_t)num_docs + 31u) >> 5;
   if (c.type == 0) {  // array container: card x uint16 LE
-    for (int i = threadIdx.x; i < c.card; i += blockDim.x) {
+    for (int i = lane; i < c.card; i += 64) {
       const uint32_t doc = hi | ld_u16(pay + 2 * i);
       if (doc < (uint32_t)num_docs) atomicOr(&bitmap[doc >> 5], 1u << (doc & 31u));
     }
   } else if (c.type == 1) {  // bitmap container: 1024 x uint64 LE = 2048 x uint32 LE
-    for (int i = threadIdx.x; i < 2048; i += blockDim.x) {
+    for (int i = lane; i < 2048; i += 64) {
       const uint8_t* q = pay + 4 * i;
       const uint32_t v = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
       const uint32_t wi = (hi >> 5) + i;
       if (v && wi < nwords) atomicOr(&bitmap[wi], v);
     }
   } else {  // run container: uint16 numRuns, then (start, length-1) pairs
-    for (int r = threadIdx.x; r < c.card; r += blockDim.x) {
+    for (int r = lane; r < c.card; r += 64) {
       const uint32_t start = hi | ld_u16(pay + 2 + 4 * r);
       const uint32_t end = start + ld_u16(pay + 4 + 4 * r);  // inclusive
       for (uint32_t d = start; d <= end && d < (uint32_t)num_docs;) {
-        const uint32_t bit = d & 31u;
-        const uint32_t take = min(32u - bit, end - d + 1u);
-        const uint32_t mask = take == 32u ? 0xffffffffu : (((1u << take) - 1u) << bit);
-        atomicOr(&bitmap[d >> 5], mask);
-        d += take;
+        const uint32_t w = d >> 5, b0 = d & 31u;
+        const uint32_t last = min(end, min((uint32_t)num_docs - 1u, (w << 5) + 31u));
+        const uint32_t nb = last - d + 1u;
+        const uint32_t m = (nb >= 32u ? 0xffffffffu : ((1u << nb) - 1u)) << b0;
+        atomicOr(&bitmap[w], m);
+        d = last + 1u;
       }
     }
   }
 }
 
-void launch_roaring_or(const RoaringContainer* c, int n, const RoaringTarget* targets, hipStream_t s) {
+__global__ void __launch_bounds__(256) k_roaring_or(const RoaringWork* __restrict__ work,
+                                                    const RoaringTarget* __restrict__ targets) {
+  const RoaringWork w = work[blockIdx.x];
+  const RoaringTarget t = targets[w.target];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int k = wave; k < w.count; k += 4) roaring_or_container(w.dir[w.first + k], t.base, t.bitmap, t.num_docs, lane);
+}
+
+void launch_roaring_or(const RoaringWork* w, int n, const RoaringTarget* targets, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_roaring_or, dim3(n), dim3(256), 0, s, c, targets);
+  hipLaunchKernelGGL(k_roaring_or, dim3(n), dim3(256), 0, s, w, targets);
   PH_HIP_CHECK(hipGetLastError());
 }
 

@@ -361,6 +361,16 @@ struct RoaringTarget {
   int32_t pad;
 };
 
+// one dictId of one inverted leaf: its containers dir[first, first + count) of the leaf's column directory
+constexpr int64_t kRoaringWorkContainers = 16;  // containers per RoaringWork item (4 waves x 4)
+struct RoaringWork {
+  const RoaringContainer* dir;
+  int32_t target;  // RoaringTarget index
+  int32_t first;
+  int32_t count;
+  int32_t pad;
+};
+
 struct Column {
   std::string name;
   int32_t data_type = PH_INT;
@@ -384,6 +394,7 @@ struct Column {
   // are dir[dir_begin[i] .. dir_begin[i + 1]); id_docs[i] = its bitmap's cardinality (FastFilteredCount)
   std::vector<RoaringContainer> dir;
   std::vector<int64_t> dir_begin;
+  DeviceBuffer d_dir;                  // `dir` in HBM (uploaded at pin): queries name (dictId -> container range) only
   std::vector<int64_t> id_docs;
   bool has_inverted() const { return !inverted.empty(); }
 };
@@ -500,8 +511,8 @@ void launch_hll_table(const void* values, int32_t is_int, int64_t n, int log2m, 
 void build_bitmap_directory(Column& c);  // at pin, from c.inverted
 ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc);
 ph_segment* segment_load_dir_impl(Context* ctx, const char* dir, const char* const* columns, int32_t num_columns);
-// every container of every inverted leaf of a query in one launch (one workgroup per container)
-void launch_roaring_or(const RoaringContainer* c, int n, const RoaringTarget* targets, hipStream_t s);
+// every container of every (leaf, dictId) work item of a query in one launch (one wave per container)
+void launch_roaring_or(const RoaringWork* w, int n, const RoaringTarget* targets, hipStream_t s);
 void launch_selftest_unpack(const uint32_t* fwd, int64_t n, int bits, int32_t* out, hipStream_t s);
 // numGroupsLimit: from each limit segment's first-doc-per-key table (nseg tables of G entries, back to back), the
 // bitsets of the keys the reference keeps (nseg x ceil(G/32) words); docbits: nseg x dbw zeroed words; scal: 3 per

@@ -497,10 +497,6 @@ void parse_roaring(const uint8_t* blob, uint64_t len, uint64_t blob_offset, std:
   }
 }
 
-void collect_bitmap_containers(const Column& c, const std::vector<int32_t>& ids, std::vector<RoaringContainer>& out) {
-  for (int32_t id : ids) out.insert(out.end(), c.dir.begin() + c.dir_begin[id], c.dir.begin() + c.dir_begin[id + 1]);
-}
-
 // docs of the dictIds' bitmaps: a single-value column's bitmaps are disjoint, so the OR's cardinality is the sum
 // (InvertedIndexFilterOperator.getNumMatchingDocs :101-127)
 int64_t bitmap_docs(const Column& c, const std::vector<int32_t>& ids) {
@@ -1044,13 +1040,17 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if (pl.bitmaps.empty() || dop == DENSE_LAYOUT || fin) return;
     // all leaves' bitmaps in one zeroed block (each padded to whole 64-doc words + one), every container of every
     // leaf OR-ed in by ONE launch
-    std::vector<RoaringContainer> cs;
+    std::vector<RoaringWork> cs;  // one item per (leaf, dictId); the containers stay in the pinned directories
     std::vector<RoaringTarget> tg(pl.bitmaps.size());
     std::vector<size_t> woff(pl.bitmaps.size() + 1, 0);
     for (size_t i = 0; i < pl.bitmaps.size(); ++i) {
-      const size_t before = cs.size();
-      collect_bitmap_containers(*pl.bitmaps[i].col, pl.bitmaps[i].dict_ids, cs);
-      for (size_t k = before; k < cs.size(); ++k) cs[k].target = (int32_t)i;
+      const Column& col = *pl.bitmaps[i].col;
+      for (int32_t id : pl.bitmaps[i].dict_ids) {
+        const int64_t f = col.dir_begin[id], n = col.dir_begin[id + 1] - f;
+        for (int64_t k = 0; k < n; k += kRoaringWorkContainers)  // 4 containers per wave keeps the grid wide
+          cs.push_back(RoaringWork{col.d_dir.as<RoaringContainer>(), (int32_t)i, (int32_t)(f + k),
+                                   (int32_t)std::min<int64_t>(kRoaringWorkContainers, n - k), 0});
+      }
       woff[i + 1] = woff[i] + (((size_t)pl.bitmaps[i].seg->num_docs + 63) / 64 + 1) * 2;
     }
     uint32_t* block = scratch.alloc<uint32_t>(std::max<size_t>(2, woff.back()));
@@ -1060,14 +1060,14 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       tg[i] = RoaringTarget{pl.bitmaps[i].col->d_inverted.as<uint8_t>(), bitmap_dev[i], pl.bitmaps[i].seg->num_docs, 0};
     }
     if (!cs.empty()) {
-      const size_t b1 = sizeof(RoaringContainer) * cs.size(), b2 = sizeof(RoaringTarget) * tg.size();
+      const size_t b1 = sizeof(RoaringWork) * cs.size(), b2 = sizeof(RoaringTarget) * tg.size();
       uint8_t* dev = scratch.alloc<uint8_t>(b1 + b2);
       uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(b1 + b2));
       memcpy(stage, cs.data(), b1);
       memcpy(stage + b1, tg.data(), b2);
       PH_HIP_CHECK(hipMemcpyAsync(dev, stage, b1 + b2, hipMemcpyHostToDevice, st));
-      launch_roaring_or(reinterpret_cast<RoaringContainer*>(dev), (int)cs.size(),
-                        reinterpret_cast<RoaringTarget*>(dev + b1), st);
+      launch_roaring_or(reinterpret_cast<RoaringWork*>(dev), (int)cs.size(), reinterpret_cast<RoaringTarget*>(dev + b1),
+                        st);
       PH_HIP_CHECK(hipStreamSynchronize(st));  // the staging buffer is reused below
     }
   };

@@ -474,6 +474,12 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
       col->d_inverted.alloc(d.inverted_index_size, ctx->device);
       PH_HIP_CHECK(hipMemcpyAsync(col->d_inverted.ptr, inv, d.inverted_index_size, hipMemcpyHostToDevice, st));
       seg->device_bytes += d.inverted_index_size;
+      // the container directory too, so a query's inverted leaves upload only (dictId -> container range) items
+      col->d_dir.alloc(sizeof(RoaringContainer) * std::max<size_t>(1, col->dir.size()), ctx->device);
+      if (!col->dir.empty())
+        PH_HIP_CHECK(hipMemcpyAsync(col->d_dir.ptr, col->dir.data(), sizeof(RoaringContainer) * col->dir.size(),
+                                    hipMemcpyHostToDevice, st));
+      seg->device_bytes += col->d_dir.bytes;
     }
     // the caller's buffers may be released after pin returns
     PH_HIP_CHECK(hipStreamSynchronize(st));
