@@ -407,33 +407,32 @@ uint32_t hll_entry(int32_t hash, int log2m) { return hll_entry_of(hash, log2m); 
 // 2-byte aligned inside the inverted-index buffer).
 __device__ __forceinline__ uint32_t ld_u16(const uint8_t* b) { return (uint32_t)b[0] | ((uint32_t)b[1] << 8); }
 
-// one workgroup per work item (a leaf's dictId, up to kRoaringWorkContainers of its containers): the 4 waves take
-// the containers round-robin, each OR-ed by one wave (the directory is device-resident since pin, so a query
-// uploads only its work items)
+// ORs one container's docs (hi | low 16 bits) below `limit` into `bitmap` (word = doc / 32); `bitmap` is the
+// device doc bitmap (hi = key << 16, limit = num_docs) or a workgroup's LDS chunk (hi = 0, limit = docs in chunk)
 __device__ __forceinline__ void roaring_or_container(const RoaringContainer& c, const uint8_t* __restrict__ base,
-                                                     uint32_t* __restrict__ bitmap, int32_t num_docs, int lane) {
+                                                     uint32_t* bitmap, uint32_t hi, uint32_t limit, int lane) {
   const uint8_t* pay = base + c.offset;
-  const uint32_t hi = (uint32_t)c.key << 16;
-  const uint32_t nwords = ((uint32_t)num_docs + 31u) >> 5;
   if (c.type == 0) {  // array container: card x uint16 LE
     for (int i = lane; i < c.card; i += 64) {
       const uint32_t doc = hi | ld_u16(pay + 2 * i);
-      if (doc < (uint32_t)num_docs) atomicOr(&bitmap[doc >> 5], 1u << (doc & 31u));
+      if (doc < limit) atomicOr(&bitmap[doc >> 5], 1u << (doc & 31u));
     }
   } else if (c.type == 1) {  // bitmap container: 1024 x uint64 LE = 2048 x uint32 LE
     for (int i = lane; i < 2048; i += 64) {
+      const uint32_t d0 = hi + 32u * (uint32_t)i;
+      if (d0 >= limit) break;
       const uint8_t* q = pay + 4 * i;
-      const uint32_t v = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-      const uint32_t wi = (hi >> 5) + i;
-      if (v && wi < nwords) atomicOr(&bitmap[wi], v);
+      uint32_t v = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+      if (limit - d0 < 32u) v &= (1u << (limit - d0)) - 1u;
+      if (v) atomicOr(&bitmap[d0 >> 5], v);
     }
   } else {  // run container: uint16 numRuns, then (start, length-1) pairs
     for (int r = lane; r < c.card; r += 64) {
       const uint32_t start = hi | ld_u16(pay + 2 + 4 * r);
       const uint32_t end = start + ld_u16(pay + 4 + 4 * r);  // inclusive
-      for (uint32_t d = start; d <= end && d < (uint32_t)num_docs;) {
+      for (uint32_t d = start; d <= end && d < limit;) {
         const uint32_t w = d >> 5, b0 = d & 31u;
-        const uint32_t last = min(end, min((uint32_t)num_docs - 1u, (w << 5) + 31u));
+        const uint32_t last = min(end, min(limit - 1u, (w << 5) + 31u));
         const uint32_t nb = last - d + 1u;
         const uint32_t m = (nb >= 32u ? 0xffffffffu : ((1u << nb) - 1u)) << b0;
         atomicOr(&bitmap[w], m);
@@ -443,17 +442,67 @@ __device__ __forceinline__ void roaring_or_container(const RoaringContainer& c, 
   }
 }
 
+// one workgroup per work item (a leaf's dictId, up to kRoaringWorkContainers of its containers): the 4 waves take
+// the containers round-robin, each OR-ed by one wave straight into the zeroed device bitmap (device atomics)
 __global__ void __launch_bounds__(256) k_roaring_or(const RoaringWork* __restrict__ work,
                                                     const RoaringTarget* __restrict__ targets) {
   const RoaringWork w = work[blockIdx.x];
   const RoaringTarget t = targets[w.target];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int k = wave; k < w.count; k += 4) roaring_or_container(w.dir[w.first + k], t.base, t.bitmap, t.num_docs, lane);
+  for (int k = wave; k < w.count; k += 4) {
+    const RoaringContainer c = w.dir[w.first + k];
+    roaring_or_container(c, t.base, t.bitmap, (uint32_t)c.key << 16, (uint32_t)t.num_docs, lane);
+  }
 }
 
 void launch_roaring_or(const RoaringWork* w, int n, const RoaringTarget* targets, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_roaring_or, dim3(n), dim3(256), 0, s, w, targets);
+  PH_HIP_CHECK(hipGetLastError());
+}
+
+// One workgroup per (65536-doc chunk, leaf): each wave finds, for its share of the leaf's dictIds, the container
+// whose key is the chunk (64 keys per ballot, 4 ballots in flight), ORs it into the chunk's 8 KiB LDS bitmap, and
+// the workgroup then stores the chunk's words (padding words included) with plain coalesced stores -- no memset,
+// and LDS atomics instead of one device atomic per matched doc.
+__global__ void __launch_bounds__(256) k_roaring_chunk(const RoaringLeaf* __restrict__ leaves,
+                                                       const RoaringRange* __restrict__ ranges) {
+  __shared__ uint32_t bm[2048];
+  const RoaringLeaf L = leaves[blockIdx.y];
+  const uint32_t chunk = blockIdx.x, w0 = chunk * 2048u;
+  if (w0 >= (uint32_t)L.padded_words) return;  // whole workgroup
+  for (int i = threadIdx.x; i < 2048; i += 256) bm[i] = 0u;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t nd = (uint32_t)L.num_docs, d0 = chunk << 16;
+  const uint32_t limit = nd > d0 ? min(nd - d0, 65536u) : 0u;
+  for (int r = wave; r < L.ids_count; r += 4) {
+    const RoaringRange rg = ranges[L.ids_first + r];
+    int found = -1;
+    for (int b = 0; b < rg.count && found < 0; b += 256) {
+      int key[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = b + 64 * q + lane;
+        key[q] = i < rg.count ? L.dir[rg.first + i].key : -1;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const unsigned long long m = __ballot(key[q] == (int)chunk);
+        if (m && found < 0) found = b + 64 * q + (int)__ffsll((long long)m) - 1;
+      }
+    }
+    if (found >= 0) roaring_or_container(L.dir[rg.first + found], L.base, bm, 0u, limit, lane);
+  }
+  __syncthreads();
+  const uint32_t nw = min(2048u, (uint32_t)L.padded_words - w0);
+  for (uint32_t i = threadIdx.x; i < nw; i += 256) L.bitmap[w0 + i] = bm[i];
+}
+
+void launch_roaring_chunk(const RoaringLeaf* leaves, int nleaves, int max_chunks, const RoaringRange* ranges,
+                          hipStream_t s) {
+  if (nleaves <= 0 || max_chunks <= 0) return;
+  hipLaunchKernelGGL(k_roaring_chunk, dim3(max_chunks, nleaves), dim3(256), 0, s, leaves, ranges);
   PH_HIP_CHECK(hipGetLastError());
 }
 

@@ -371,6 +371,23 @@ struct RoaringWork {
   int32_t pad;
 };
 
+// chunked bitmap build (k_roaring_chunk): one leaf's target and its dictIds' directory ranges
+struct RoaringRange {
+  int32_t first;  // dir[first, first + count): one dictId's containers, ascending keys
+  int32_t count;
+};
+struct RoaringLeaf {
+  const uint8_t* base;            // device inverted buffer
+  const RoaringContainer* dir;    // the column's device directory
+  uint32_t* bitmap;               // doc bitmap, padded_words words
+  int32_t num_docs;
+  int32_t padded_words;
+  int32_t ids_first;              // ranges[ids_first, ids_first + ids_count)
+  int32_t ids_count;
+};
+// the chunked build applies when every dictId has at most this many containers (each wave scans them 256 at a time)
+constexpr int64_t kRoaringChunkMaxContainers = 1024;
+
 struct Column {
   std::string name;
   int32_t data_type = PH_INT;
@@ -513,6 +530,8 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc);
 ph_segment* segment_load_dir_impl(Context* ctx, const char* dir, const char* const* columns, int32_t num_columns);
 // every container of every (leaf, dictId) work item of a query in one launch (one wave per container)
 void launch_roaring_or(const RoaringWork* w, int n, const RoaringTarget* targets, hipStream_t s);
+void launch_roaring_chunk(const RoaringLeaf* leaves, int nleaves, int max_chunks, const RoaringRange* ranges,
+                          hipStream_t s);
 void launch_selftest_unpack(const uint32_t* fwd, int64_t n, int bits, int32_t* out, hipStream_t s);
 // numGroupsLimit: from each limit segment's first-doc-per-key table (nseg tables of G entries, back to back), the
 // bitsets of the keys the reference keeps (nseg x ceil(G/32) words); docbits: nseg x dbw zeroed words; scal: 3 per

@@ -1038,12 +1038,50 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<uint32_t*> bitmap_dev(pl.bitmaps.size(), nullptr);
   auto build_bitmaps = [&]() {
     if (pl.bitmaps.empty() || dop == DENSE_LAYOUT || fin) return;
-    // all leaves' bitmaps in one zeroed block (each padded to whole 64-doc words + one), every container of every
-    // leaf OR-ed in by ONE launch
-    std::vector<RoaringWork> cs;  // one item per (leaf, dictId); the containers stay in the pinned directories
-    std::vector<RoaringTarget> tg(pl.bitmaps.size());
-    std::vector<size_t> woff(pl.bitmaps.size() + 1, 0);
-    for (size_t i = 0; i < pl.bitmaps.size(); ++i) {
+    // all leaves' bitmaps in one block, each padded to whole 64-doc words + one
+    const size_t nl = pl.bitmaps.size();
+    std::vector<size_t> woff(nl + 1, 0);
+    bool chunked = getenv("PH_ROARING_ATOMIC") == nullptr;  // PH_ROARING_ATOMIC=1: device-atomic build (tests)
+    for (size_t i = 0; i < nl; ++i) {
+      woff[i + 1] = woff[i] + (((size_t)pl.bitmaps[i].seg->num_docs + 63) / 64 + 1) * 2;
+      const Column& col = *pl.bitmaps[i].col;
+      for (int32_t id : pl.bitmaps[i].dict_ids)
+        chunked = chunked && col.dir_begin[id + 1] - col.dir_begin[id] <= kRoaringChunkMaxContainers;
+    }
+    uint32_t* block = scratch.alloc<uint32_t>(std::max<size_t>(2, woff.back()));
+    for (size_t i = 0; i < nl; ++i) bitmap_dev[i] = block + woff[i];
+    if (chunked) {
+      // k_roaring_chunk: one workgroup per (65536-doc chunk, leaf) builds the chunk in LDS and stores every word
+      std::vector<RoaringLeaf> lv(nl);
+      std::vector<RoaringRange> rg;
+      int max_chunks = 0;
+      for (size_t i = 0; i < nl; ++i) {
+        const Column& col = *pl.bitmaps[i].col;
+        const int32_t first = (int32_t)rg.size();
+        for (int32_t id : pl.bitmaps[i].dict_ids) {
+          const int64_t f = col.dir_begin[id], n = col.dir_begin[id + 1] - f;
+          if (n > 0) rg.push_back(RoaringRange{(int32_t)f, (int32_t)n});
+        }
+        const int32_t pw = (int32_t)(woff[i + 1] - woff[i]);
+        lv[i] = RoaringLeaf{col.d_inverted.as<uint8_t>(), col.d_dir.as<RoaringContainer>(), bitmap_dev[i],
+                            pl.bitmaps[i].seg->num_docs, pw, first, (int32_t)rg.size() - first};
+        max_chunks = std::max(max_chunks, (pw + 2047) / 2048);
+      }
+      const size_t b1 = sizeof(RoaringLeaf) * nl, b2 = sizeof(RoaringRange) * std::max<size_t>(1, rg.size());
+      uint8_t* dev = scratch.alloc<uint8_t>(b1 + b2);
+      uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(b1 + b2));
+      memcpy(stage, lv.data(), b1);
+      if (!rg.empty()) memcpy(stage + b1, rg.data(), sizeof(RoaringRange) * rg.size());
+      PH_HIP_CHECK(hipMemcpyAsync(dev, stage, b1 + b2, hipMemcpyHostToDevice, st));
+      launch_roaring_chunk(reinterpret_cast<RoaringLeaf*>(dev), (int)nl, max_chunks,
+                           reinterpret_cast<RoaringRange*>(dev + b1), st);
+      PH_HIP_CHECK(hipStreamSynchronize(st));  // the staging buffer is reused below
+      return;
+    }
+    // device-atomic build: a zeroed block, every container of every leaf OR-ed in by ONE launch
+    std::vector<RoaringWork> cs;  // items of (leaf, dictId, <= 16 containers); the containers stay in the directories
+    std::vector<RoaringTarget> tg(nl);
+    for (size_t i = 0; i < nl; ++i) {
       const Column& col = *pl.bitmaps[i].col;
       for (int32_t id : pl.bitmaps[i].dict_ids) {
         const int64_t f = col.dir_begin[id], n = col.dir_begin[id + 1] - f;
@@ -1051,14 +1089,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           cs.push_back(RoaringWork{col.d_dir.as<RoaringContainer>(), (int32_t)i, (int32_t)(f + k),
                                    (int32_t)std::min<int64_t>(kRoaringWorkContainers, n - k), 0});
       }
-      woff[i + 1] = woff[i] + (((size_t)pl.bitmaps[i].seg->num_docs + 63) / 64 + 1) * 2;
+      tg[i] = RoaringTarget{col.d_inverted.as<uint8_t>(), bitmap_dev[i], pl.bitmaps[i].seg->num_docs, 0};
     }
-    uint32_t* block = scratch.alloc<uint32_t>(std::max<size_t>(2, woff.back()));
     PH_HIP_CHECK(hipMemsetAsync(block, 0, 4 * std::max<size_t>(2, woff.back()), st));
-    for (size_t i = 0; i < pl.bitmaps.size(); ++i) {
-      bitmap_dev[i] = block + woff[i];
-      tg[i] = RoaringTarget{pl.bitmaps[i].col->d_inverted.as<uint8_t>(), bitmap_dev[i], pl.bitmaps[i].seg->num_docs, 0};
-    }
     if (!cs.empty()) {
       const size_t b1 = sizeof(RoaringWork) * cs.size(), b2 = sizeof(RoaringTarget) * tg.size();
       uint8_t* dev = scratch.alloc<uint8_t>(b1 + b2);

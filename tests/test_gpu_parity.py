@@ -226,6 +226,24 @@ def test_inverted_index_containers(ctx):
             _both(ctx, [t], f"SELECT COUNT(*), SUM(m) FROM t WHERE {where}", inverted=("a",), run_opt=run_opt)
 
 
+@pytest.mark.parametrize("atomic", [False, True])
+@pytest.mark.parametrize("n", [131072, 131172, 65536 * 3 - 1])
+def test_inverted_bitmap_chunk_edges(ctx, monkeypatch, n, atomic):
+    # the chunked LDS build (65536-doc chunks, padding words stored by the last chunk) and the device-atomic build
+    # (PH_ROARING_ATOMIC) on segments that end on, just past and just before a chunk boundary
+    if atomic:
+        monkeypatch.setenv("PH_ROARING_ATOMIC", "1")
+    rng = np.random.default_rng(n)
+    a = rng.integers(0, 40, n).astype(np.int32)
+    a[: n // 3] = 7  # dense run -> bitmap / run containers
+    a[-40:] = 9
+    t = {"a": (a, "INT"), "m": (rng.integers(0, 1000, n).astype(np.int32), "INT")}
+    for run_opt in (False, True):
+        for where in ("a = 7", "a IN (9, 3, 11)", "a NOT IN (7)", "a = 9"):
+            _both(ctx, [t, t], f"SELECT COUNT(*), SUM(m), MAX(m) FROM t WHERE {where}", inverted=("a",),
+                  run_opt=run_opt)
+
+
 def rng_idx(n, k):
     return np.random.default_rng(1).choice(n, k, replace=False)
 
