@@ -451,11 +451,11 @@ struct Lane {
   hipStream_t stream_b = nullptr;
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
   std::vector<hipEvent_t> ev_pool;
-  void* staging = nullptr;
-  size_t staging_bytes = 0;
+  void* staging[2] = {nullptr, nullptr};  // slot 0: launch parameters; slot 1: the bitmap build's work items
+  size_t staging_bytes[2] = {0, 0};
   explicit Lane(int dev);
   ~Lane();
-  void* host_staging(size_t n);
+  void* host_staging(size_t n, int slot = 0);  // valid until the lane's stream passes this call's uploads
   hipEvent_t event(size_t i);  // hand-off event i (created on demand)
 };
 

@@ -1069,13 +1069,13 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
       const size_t b1 = sizeof(RoaringLeaf) * nl, b2 = sizeof(RoaringRange) * std::max<size_t>(1, rg.size());
       uint8_t* dev = scratch.alloc<uint8_t>(b1 + b2);
-      uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(b1 + b2));
+      // staging slot 1: nothing else in this call writes it, so the build overlaps the rest of the host setup
+      uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(b1 + b2, 1));
       memcpy(stage, lv.data(), b1);
       if (!rg.empty()) memcpy(stage + b1, rg.data(), sizeof(RoaringRange) * rg.size());
       PH_HIP_CHECK(hipMemcpyAsync(dev, stage, b1 + b2, hipMemcpyHostToDevice, st));
       launch_roaring_chunk(reinterpret_cast<RoaringLeaf*>(dev), (int)nl, max_chunks,
                            reinterpret_cast<RoaringRange*>(dev + b1), st);
-      PH_HIP_CHECK(hipStreamSynchronize(st));  // the staging buffer is reused below
       return;
     }
     // device-atomic build: a zeroed block, every container of every leaf OR-ed in by ONE launch
@@ -1095,13 +1095,12 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if (!cs.empty()) {
       const size_t b1 = sizeof(RoaringWork) * cs.size(), b2 = sizeof(RoaringTarget) * tg.size();
       uint8_t* dev = scratch.alloc<uint8_t>(b1 + b2);
-      uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(b1 + b2));
+      uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(b1 + b2, 1));
       memcpy(stage, cs.data(), b1);
       memcpy(stage + b1, tg.data(), b2);
       PH_HIP_CHECK(hipMemcpyAsync(dev, stage, b1 + b2, hipMemcpyHostToDevice, st));
       launch_roaring_or(reinterpret_cast<RoaringWork*>(dev), (int)cs.size(), reinterpret_cast<RoaringTarget*>(dev + b1),
                         st);
-      PH_HIP_CHECK(hipStreamSynchronize(st));  // the staging buffer is reused below
     }
   };
   stamp("plan");

@@ -96,18 +96,21 @@ Lane::~Lane() {
   for (auto e : ev_pool) (void)hipEventDestroy(e);
   if (stream) (void)hipStreamDestroy(stream);
   if (stream_b) (void)hipStreamDestroy(stream_b);
-  if (staging) (void)hipHostFree(staging);
+  for (void* p : staging)
+    if (p) (void)hipHostFree(p);
 }
 
-void* Lane::host_staging(size_t n) {
-  if (n > staging_bytes) {
-    if (staging) PH_HIP_CHECK(hipHostFree(staging));
-    staging = nullptr;
+void* Lane::host_staging(size_t n, int slot) {
+  if (n > staging_bytes[slot]) {
+    // a pending upload may still read the old block: drain the lane before freeing it
+    PH_HIP_CHECK(hipStreamSynchronize(stream));
+    if (staging[slot]) PH_HIP_CHECK(hipHostFree(staging[slot]));
+    staging[slot] = nullptr;
     size_t sz = std::max<size_t>(n, 1 << 20);
-    PH_HIP_CHECK(hipHostMalloc(&staging, sz, hipHostMallocDefault));
-    staging_bytes = sz;
+    PH_HIP_CHECK(hipHostMalloc(&staging[slot], sz, hipHostMallocDefault));
+    staging_bytes[slot] = sz;
   }
-  return staging;
+  return staging[slot];
 }
 
 hipEvent_t Lane::event(size_t i) {
