@@ -1282,6 +1282,11 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
 
   int mode = -3;  // DENSE_FINALIZE: no scan
   float dev_ms = 0.f;
+  // a plain group-by's scan completion, matched-doc count and limit flags are read at the compaction's sync
+  // (one host round trip instead of three)
+  const bool defer_sync = q->num_group_by > 0 && num_hll == 0 && dop != DENSE_EXECUTE && !fin;
+  unsigned long long* dsc = nullptr;  // pinned: matched total, then 3 words per limit segment
+  size_t dsc_cap = 0, dsc_nlim = 0;
   int64_t TR = G;  // rows of the output tables: the key space, or the slots of the MODE_GROUP_HASH table
   unsigned long long* hkeys = nullptr;
   if (fin) {
@@ -1957,9 +1962,11 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       PH_HIP_CHECK(hipEventRecord(L.ev_stop, st));
     }
     stamp("launched");
-    PH_HIP_CHECK(hipStreamSynchronize(st));  // staging buffer reuse + results
-    stamp("kernels done");
-    PH_HIP_CHECK(hipEventElapsedTime(&dev_ms, lane.lane->ev_start, lane.lane->ev_stop));
+    if (!defer_sync || kp.dbg) {
+      PH_HIP_CHECK(hipStreamSynchronize(st));  // staging buffer reuse + results
+      stamp("kernels done");
+      PH_HIP_CHECK(hipEventElapsedTime(&dev_ms, lane.lane->ev_start, lane.lane->ev_stop));
+    }
     if (kp.dbg) {  // PH_DEBUG_STAMPS: where wave 0 of each workgroup spent its cycles (last launch)
       std::vector<unsigned long long> h(4 * (size_t)ctx->num_cus * 8);
       PH_HIP_CHECK(hipMemcpy(h.data(), kp.dbg, 8 * h.size(), hipMemcpyDeviceToHost));
@@ -1975,7 +1982,12 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   stats.device_ms = dev_ms;
   res->mode = mode;
   stats.plan_mode = mode;
-  if (kp.matched_total) {
+  if (kp.matched_total && defer_sync) {
+    dsc_nlim = limit_segs.size();
+    dsc = static_cast<unsigned long long*>(ctx->pinned_acquire(8 * (1 + 3 * dsc_nlim), &dsc_cap));
+    PH_HIP_CHECK(hipMemcpyAsync(dsc, kp.matched_total, 8, hipMemcpyDeviceToHost, st));
+    if (dsc_nlim) PH_HIP_CHECK(hipMemcpyAsync(dsc + 1, limit_scal, 24 * dsc_nlim, hipMemcpyDeviceToHost, st));
+  } else if (kp.matched_total) {
     // group-by: numDocsScanned = matched docs (docs of keys beyond numGroupsLimit included,
     // GroupByOperator.java:106-107) and numGroupsLimitReached of any segment
     std::vector<unsigned long long> sc(1 + 3 * limit_segs.size());
@@ -2102,6 +2114,17 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     unsigned long long* tot = static_cast<unsigned long long*>(ctx->pinned_acquire(16, &tot_cap));
     PH_HIP_CHECK(hipMemcpyAsync(tot, cp.blk + kCompactBlocks, 16, hipMemcpyDeviceToHost, st));
     PH_HIP_CHECK(hipStreamSynchronize(st));
+    if (defer_sync && !kp.dbg) {
+      stamp("kernels done");
+      PH_HIP_CHECK(hipEventElapsedTime(&dev_ms, lane.lane->ev_start, lane.lane->ev_stop));
+      stats.device_ms = dev_ms;
+    }
+    if (dsc) {
+      stats.num_docs_scanned = (int64_t)dsc[0];
+      for (size_t t = 0; t < dsc_nlim; ++t) stats.num_groups_limit_reached |= dsc[1 + 3 * t + 2] != 0;
+      ctx->pinned_release(dsc, dsc_cap);
+      dsc = nullptr;
+    }
     const int64_t R = (int64_t)tot[0];
     const int64_t docs = (int64_t)tot[1];
     ctx->pinned_release(tot, tot_cap);
