@@ -1287,6 +1287,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   const bool defer_sync = q->num_group_by > 0 && num_hll == 0 && dop != DENSE_EXECUTE && !fin;
   unsigned long long* dsc = nullptr;  // pinned: matched total, then 3 words per limit segment
   size_t dsc_cap = 0, dsc_nlim = 0;
+  bool timed = false;  // this call recorded ev_start / ev_stop (some chunk was scanned)
   int64_t TR = G;  // rows of the output tables: the key space, or the slots of the MODE_GROUP_HASH table
   unsigned long long* hkeys = nullptr;
   if (fin) {
@@ -1962,6 +1963,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       PH_HIP_CHECK(hipEventRecord(L.ev_stop, st));
     }
     stamp("launched");
+    timed = true;
     if (!defer_sync || kp.dbg) {
       PH_HIP_CHECK(hipStreamSynchronize(st));  // staging buffer reuse + results
       stamp("kernels done");
@@ -2033,6 +2035,20 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     const int t = q->aggregations[k].type;
     return t == PH_AGG_SUM ? kp.out_sum[j] : (t == PH_AGG_MIN ? (void*)kp.out_min[j] : (void*)kp.out_max[j]);
   };
+  // after the first sync of the result path: the deferred scan timing and group-by statistics
+  auto resolve_deferred = [&]() {
+    if (defer_sync && !kp.dbg && timed) {
+      stamp("kernels done");
+      PH_HIP_CHECK(hipEventElapsedTime(&dev_ms, lane.lane->ev_start, lane.lane->ev_stop));
+      stats.device_ms = dev_ms;
+    }
+    if (dsc) {
+      stats.num_docs_scanned = (int64_t)dsc[0];
+      for (size_t t = 0; t < dsc_nlim; ++t) stats.num_groups_limit_reached |= dsc[1 + 3 * t + 2] != 0;
+      ctx->pinned_release(dsc, dsc_cap);
+      dsc = nullptr;
+    }
+  };
   if (q->num_group_by == 0) {
     init_row_results(1);
     // every scalar (and HLL register block) in one round trip: async copies into one pinned block, one sync
@@ -2054,6 +2070,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         PH_HIP_CHECK(hipMemcpyAsync(blk + at[k], src_of(k), 8, hipMemcpyDeviceToHost, st));
     }
     PH_HIP_CHECK(hipStreamSynchronize(st));
+    resolve_deferred();
     unsigned long long matched = 0;
     memcpy(&matched, blk, 8);
     stats.num_docs_scanned = (int64_t)matched;
@@ -2114,17 +2131,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     unsigned long long* tot = static_cast<unsigned long long*>(ctx->pinned_acquire(16, &tot_cap));
     PH_HIP_CHECK(hipMemcpyAsync(tot, cp.blk + kCompactBlocks, 16, hipMemcpyDeviceToHost, st));
     PH_HIP_CHECK(hipStreamSynchronize(st));
-    if (defer_sync && !kp.dbg) {
-      stamp("kernels done");
-      PH_HIP_CHECK(hipEventElapsedTime(&dev_ms, lane.lane->ev_start, lane.lane->ev_stop));
-      stats.device_ms = dev_ms;
-    }
-    if (dsc) {
-      stats.num_docs_scanned = (int64_t)dsc[0];
-      for (size_t t = 0; t < dsc_nlim; ++t) stats.num_groups_limit_reached |= dsc[1 + 3 * t + 2] != 0;
-      ctx->pinned_release(dsc, dsc_cap);
-      dsc = nullptr;
-    }
+    resolve_deferred();
     const int64_t R = (int64_t)tot[0];
     const int64_t docs = (int64_t)tot[1];
     ctx->pinned_release(tot, tot_cap);
