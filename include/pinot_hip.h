@@ -174,7 +174,9 @@ typedef struct {
   int32_t plan_mode;                       /* physical plan: -2 index-only count (FastFilteredCount), -1
                                               metadata, 0 count, 1 aggregation, 2 LDS group table, 3 HBM
                                               atomic group table, 4 partitioned, 5 HBM hash group table */
-  int32_t reserved;
+  int32_t limit_pass;                      /* numGroupsLimit emulation: 0 no segment could reach the limit, 1 the
+                                              untruncated scan's table held < limit keys (no pass needed), 2 the
+                                              first-seen pass and the truncating scan ran */
 } ph_exec_stats;
 
 /* ------------------------------------------------------------------ context */

@@ -38,20 +38,55 @@ JNIEXPORT jlong JNICALL FN(ctxCreate)(JNIEnv* env, jclass c, jint device) {
 
 JNIEXPORT void JNICALL FN(ctxDestroy)(JNIEnv* env, jclass c, jlong ctx) { throw_ph(env, ph_ctx_destroy(PTR(ctx))); }
 
+/* Strings of a Java String[] as UTF-8 for the duration of one call.  The element references are local refs held in
+ * `refs` (the caller brackets the call in Push/PopLocalFrame, so many strings never overflow the local-reference
+ * table); a null element stays NULL. */
+typedef struct {
+  jsize n;
+  jstring* refs;
+  const char** strs;
+} utf_strings;
+
+static int utf_strings_get(JNIEnv* env, jobjectArray arr, utf_strings* u) {
+  u->n = arr ? (*env)->GetArrayLength(env, arr) : 0;
+  u->refs = (jstring*)calloc((size_t)(u->n ? u->n : 1), sizeof(jstring));
+  u->strs = (const char**)calloc((size_t)(u->n ? u->n : 1), sizeof(char*));
+  if (!u->refs || !u->strs) return 0;
+  for (jsize i = 0; i < u->n; ++i) {
+    u->refs[i] = (jstring)(*env)->GetObjectArrayElement(env, arr, i);
+    u->strs[i] = u->refs[i] ? (*env)->GetStringUTFChars(env, u->refs[i], NULL) : NULL;
+    if (u->refs[i] && !u->strs[i]) return 0;  /* OutOfMemoryError pending */
+  }
+  return 1;
+}
+
+static void utf_strings_release(JNIEnv* env, utf_strings* u) {
+  for (jsize i = 0; u->refs && u->strs && i < u->n; ++i)
+    if (u->refs[i] && u->strs[i]) (*env)->ReleaseStringUTFChars(env, u->refs[i], u->strs[i]);
+  free(u->refs);
+  free(u->strs);
+}
+
+static void throw_illegal(JNIEnv* env, const char* msg) {
+  jclass c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
+  if (c) (*env)->ThrowNew(env, c, msg);
+}
+
 /* ImmutableSegmentLoader.load -> pin the segment's directory (ph_segment_load_dir); columns == null: all */
 JNIEXPORT jlong JNICALL FN(segmentLoadDir)(JNIEnv* env, jclass c, jlong ctx, jstring dir, jobjectArray columns) {
-  const char* d = (*env)->GetStringUTFChars(env, dir, NULL);
   const jsize n = columns ? (*env)->GetArrayLength(env, columns) : 0;
-  const char** cols = n ? (const char**)calloc((size_t)n, sizeof(char*)) : NULL;
-  for (jsize i = 0; i < n; ++i)
-    cols[i] = (*env)->GetStringUTFChars(env, (jstring)(*env)->GetObjectArrayElement(env, columns, i), NULL);
+  if ((*env)->PushLocalFrame(env, n + 16) != 0) return 0;
+  const char* d = (*env)->GetStringUTFChars(env, dir, NULL);
+  utf_strings cols = {0, NULL, NULL};
   ph_segment* seg = NULL;
-  const int rc = ph_segment_load_dir(PTR(ctx), d, cols, (int32_t)n, &seg);
-  for (jsize i = 0; i < n; ++i)
-    (*env)->ReleaseStringUTFChars(env, (jstring)(*env)->GetObjectArrayElement(env, columns, i), cols[i]);
-  free(cols);
-  (*env)->ReleaseStringUTFChars(env, dir, d);
-  throw_ph(env, rc);
+  int rc = PH_ERR_INVALID_ARGUMENT;
+  if (d && utf_strings_get(env, columns, &cols)) {
+    rc = ph_segment_load_dir(PTR(ctx), d, n ? cols.strs : NULL, (int32_t)n, &seg);
+  }
+  utf_strings_release(env, &cols);
+  if (d) (*env)->ReleaseStringUTFChars(env, dir, d);
+  (*env)->PopLocalFrame(env, NULL);
+  if (!(*env)->ExceptionCheck(env)) throw_ph(env, rc);
   return (jlong)(intptr_t)seg;
 }
 
@@ -86,74 +121,120 @@ JNIEXPORT void JNICALL FN(tableSetColumnType)(JNIEnv* env, jclass c, jlong ctx, 
  *    per aggregation: type, column, log2m, column2, exprOp]                                                      */
 JNIEXPORT jlong JNICALL FN(queryExecute)(JNIEnv* env, jclass c, jlong ctx, jintArray descArr, jobjectArray strArr,
                                          jlong numGroupsLimit, jlong endTimeMs, jlongArray segArr) {
-  const jsize nd = (*env)->GetArrayLength(env, descArr), ns = (*env)->GetArrayLength(env, strArr);
+  const jsize nd = (*env)->GetArrayLength(env, descArr);
+  const jsize ns0 = strArr ? (*env)->GetArrayLength(env, strArr) : 0;
+  if ((*env)->PushLocalFrame(env, ns0 + 16) != 0) return 0;
   jint* desc = (*env)->GetIntArrayElements(env, descArr, NULL);
-  const char** strs = (const char**)calloc((size_t)(ns ? ns : 1), sizeof(char*));
-  for (jsize i = 0; i < ns; ++i)
-    strs[i] = (*env)->GetStringUTFChars(env, (jstring)(*env)->GetObjectArrayElement(env, strArr, i), NULL);
+  utf_strings us = {0, NULL, NULL};
+  const int strs_ok = utf_strings_get(env, strArr, &us);
+  const jsize ns = us.n;
+  const char** strs = us.strs;
 #define S(i) ((i) >= 0 && (i) < ns ? strs[(i)] : NULL)
-  int k = 0;
+  /* every read of the descriptor is bounds-checked: a malformed one throws IllegalArgumentException */
+#define NEXT(dst)              \
+  do {                         \
+    if (k >= nd) goto bad;     \
+    (dst) = desc[k++];         \
+  } while (0)
+  int k = 0, tmp = 0;
   ph_query q;
   memset(&q, 0, sizeof q);
-  q.num_filter_nodes = desc[k++];
-  q.filter_root = desc[k++];
-  q.num_predicates = desc[k++];
-  q.num_group_by = desc[k++];
-  q.num_aggregations = desc[k++];
-  ph_filter_node* nodes = (ph_filter_node*)calloc((size_t)q.num_filter_nodes + 1, sizeof(ph_filter_node));
-  ph_predicate* preds = (ph_predicate*)calloc((size_t)q.num_predicates + 1, sizeof(ph_predicate));
-  const char** gby = (const char**)calloc((size_t)q.num_group_by + 1, sizeof(char*));
-  ph_aggregation* aggs = (ph_aggregation*)calloc((size_t)q.num_aggregations + 1, sizeof(ph_aggregation));
-  int32_t* ints = (int32_t*)calloc((size_t)nd + 1, sizeof(int32_t));  /* children lists live here */
-  const char** vals = (const char**)calloc((size_t)nd + 1, sizeof(char*));
-  int ki = 0, kv = 0;
-  for (int i = 0; i < q.num_filter_nodes; ++i) {
-    nodes[i].type = desc[k++];
-    nodes[i].num_children = desc[k++];
-    nodes[i].predicate = desc[k++];
-    nodes[i].children = ints + ki;
-    for (int j = 0; j < nodes[i].num_children; ++j) ints[ki++] = desc[k++];
+  ph_filter_node* nodes = NULL;
+  ph_predicate* preds = NULL;
+  const char** gby = NULL;
+  ph_aggregation* aggs = NULL;
+  int32_t* ints = NULL;
+  const char** vals = NULL;
+  ph_result* res = NULL;
+  int rc = PH_ERR_INVALID_ARGUMENT;
+  if (!desc || !strs_ok) goto done;
+  NEXT(q.num_filter_nodes);
+  NEXT(q.filter_root);
+  NEXT(q.num_predicates);
+  NEXT(q.num_group_by);
+  NEXT(q.num_aggregations);
+  /* every entity takes at least one descriptor int, so a count beyond nd is malformed */
+  if (q.num_filter_nodes < 0 || q.num_predicates < 0 || q.num_group_by < 0 || q.num_aggregations < 0 ||
+      q.num_filter_nodes > nd || q.num_predicates > nd || q.num_group_by > nd || q.num_aggregations > nd)
+    goto bad;
+  nodes = (ph_filter_node*)calloc((size_t)q.num_filter_nodes + 1, sizeof(ph_filter_node));
+  preds = (ph_predicate*)calloc((size_t)q.num_predicates + 1, sizeof(ph_predicate));
+  gby = (const char**)calloc((size_t)q.num_group_by + 1, sizeof(char*));
+  aggs = (ph_aggregation*)calloc((size_t)q.num_aggregations + 1, sizeof(ph_aggregation));
+  ints = (int32_t*)calloc((size_t)nd + 1, sizeof(int32_t)); /* children lists live here (<= nd entries) */
+  vals = (const char**)calloc((size_t)nd + 1, sizeof(char*));
+  if (!nodes || !preds || !gby || !aggs || !ints || !vals) goto done;
+  {
+    int ki = 0, kv = 0;
+    for (int i = 0; i < q.num_filter_nodes; ++i) {
+      NEXT(nodes[i].type);
+      NEXT(nodes[i].num_children);
+      NEXT(nodes[i].predicate);
+      if (nodes[i].num_children < 0 || nodes[i].num_children > nd - k) goto bad;
+      nodes[i].children = ints + ki;
+      for (int j = 0; j < nodes[i].num_children; ++j) NEXT(ints[ki++]);
+    }
+    for (int i = 0; i < q.num_predicates; ++i) {
+      NEXT(preds[i].type);
+      NEXT(tmp);
+      preds[i].column = S(tmp);
+      NEXT(preds[i].num_values);
+      if (preds[i].num_values < 0 || preds[i].num_values > nd - k) goto bad;
+      preds[i].values = vals + kv;
+      for (int j = 0; j < preds[i].num_values; ++j) {
+        NEXT(tmp);
+        vals[kv++] = S(tmp);
+      }
+      NEXT(tmp);
+      preds[i].lower = S(tmp);
+      NEXT(tmp);
+      preds[i].upper = S(tmp);
+      NEXT(preds[i].lower_inclusive);
+      NEXT(preds[i].upper_inclusive);
+    }
+    for (int i = 0; i < q.num_group_by; ++i) {
+      NEXT(tmp);
+      gby[i] = S(tmp);
+    }
+    for (int i = 0; i < q.num_aggregations; ++i) {
+      NEXT(aggs[i].type);
+      NEXT(tmp);
+      aggs[i].column = S(tmp);
+      NEXT(aggs[i].log2m);
+      NEXT(tmp);
+      aggs[i].column2 = S(tmp);
+      NEXT(aggs[i].expr_op);
+    }
   }
-  for (int i = 0; i < q.num_predicates; ++i) {
-    preds[i].type = desc[k++];
-    preds[i].column = S(desc[k]); k++;
-    preds[i].num_values = desc[k++];
-    preds[i].values = vals + kv;
-    for (int j = 0; j < preds[i].num_values; ++j) vals[kv++] = S(desc[k++]);
-    preds[i].lower = S(desc[k]); k++;
-    preds[i].upper = S(desc[k]); k++;
-    preds[i].lower_inclusive = desc[k++];
-    preds[i].upper_inclusive = desc[k++];
-  }
-  for (int i = 0; i < q.num_group_by; ++i) gby[i] = S(desc[k++]);
-  for (int i = 0; i < q.num_aggregations; ++i) {
-    aggs[i].type = desc[k++];
-    aggs[i].column = S(desc[k]); k++;
-    aggs[i].log2m = desc[k++];
-    aggs[i].column2 = S(desc[k]); k++;
-    aggs[i].expr_op = desc[k++];
-  }
+  /* indices inside the query (children, predicates, root) are range-checked by ph_query_execute itself */
   q.filter_nodes = nodes;
   q.predicates = preds;
   q.group_by = gby;
   q.aggregations = aggs;
   q.num_groups_limit = numGroupsLimit;
   q.end_time_ms = endTimeMs;
-  const jsize nseg = (*env)->GetArrayLength(env, segArr);
-  jlong* segs = (*env)->GetLongArrayElements(env, segArr, NULL);
-  ph_segment** sp = (ph_segment**)calloc((size_t)(nseg ? nseg : 1), sizeof(ph_segment*));
-  for (jsize i = 0; i < nseg; ++i) sp[i] = (ph_segment*)PTR(segs[i]);
-  ph_result* res = NULL;
-  const int rc = ph_query_execute(PTR(ctx), &q, sp, (int32_t)nseg, &res);
-  free(sp);
-  (*env)->ReleaseLongArrayElements(env, segArr, segs, JNI_ABORT);
+  {
+    const jsize nseg = (*env)->GetArrayLength(env, segArr);
+    jlong* segs = (*env)->GetLongArrayElements(env, segArr, NULL);
+    ph_segment** sp = (ph_segment**)calloc((size_t)(nseg ? nseg : 1), sizeof(ph_segment*));
+    if (segs && sp) {
+      for (jsize i = 0; i < nseg; ++i) sp[i] = (ph_segment*)PTR(segs[i]);
+      rc = ph_query_execute(PTR(ctx), &q, sp, (int32_t)nseg, &res);
+    }
+    free(sp);
+    if (segs) (*env)->ReleaseLongArrayElements(env, segArr, segs, JNI_ABORT);
+  }
+  goto done;
+bad:
+  throw_illegal(env, "malformed GPU query descriptor");
+done:
   free(nodes); free(preds); free(gby); free(aggs); free(ints); free(vals);
-  for (jsize i = 0; i < ns; ++i)
-    (*env)->ReleaseStringUTFChars(env, (jstring)(*env)->GetObjectArrayElement(env, strArr, i), strs[i]);
-  free(strs);
-  (*env)->ReleaseIntArrayElements(env, descArr, desc, JNI_ABORT);
+  utf_strings_release(env, &us);
+  if (desc) (*env)->ReleaseIntArrayElements(env, descArr, desc, JNI_ABORT);
+  (*env)->PopLocalFrame(env, NULL);
+#undef NEXT
 #undef S
-  throw_ph(env, rc);
+  if (!(*env)->ExceptionCheck(env)) throw_ph(env, rc);
   return (jlong)(intptr_t)res;
 }
 

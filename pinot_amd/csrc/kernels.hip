@@ -295,6 +295,25 @@ void launch_limit_select(const uint32_t* first, int64_t G, int64_t limit, int ns
   PH_HIP_CHECK(hipGetLastError());
 }
 
+// Non-empty groups of a dense / hash count table (the optimistic numGroupsLimit check: when the merged table has
+// fewer than `limit` groups, no segment can have reached the limit, so its first-seen pass is not needed)
+__global__ void __launch_bounds__(256) k_count_nonzero(const unsigned long long* __restrict__ cnt, int64_t n,
+                                                       unsigned long long* out) {
+  unsigned long long d = 0;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < n; g += (int64_t)gridDim.x * blockDim.x)
+    d += cnt[g] != 0;
+  for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+  if ((threadIdx.x & 63) == 0 && d) atomicAdd(out, d);
+}
+
+void launch_count_nonzero(const unsigned long long* cnt, int64_t n, unsigned long long* out, hipStream_t s) {
+  PH_HIP_CHECK(hipMemsetAsync(out, 0, 8, s));
+  if (n <= 0) return;
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_count_nonzero, dim3(grid), dim3(256), 0, s, cnt, n, out);
+  PH_HIP_CHECK(hipGetLastError());
+}
+
 // ------------------------------------------------------------------ helpers
 // Self-test of the scan kernels' staged decode: the same tile_load / tile_store / BitCursor code k_scan runs
 // (one stream, stage offset 0), writing every decoded dictId out.

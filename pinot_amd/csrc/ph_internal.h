@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <exception>
 #include <cstdint>
 #include <deque>
 #include <map>
@@ -258,6 +259,7 @@ struct KParams {
   int32_t pl_slot_off, pl_lcnt_off, pl_bcnt_off, pl_misc_off;  // LDS layout
   int32_t part_slot_log2;         // C = 1 << part_slot_log2 LDS ring slots per partition
   int32_t part_fast;              // kernel A may run the lean k_part_scan (no gathers; ALL / RANGE / DOCRANGE leaves)
+  int32_t part_depth;             // lean kernel A: tiles of loads in flight per wave (1: k_part_scan, 2: k_part_scan2)
   unsigned long long* ovf_count;  // overflow table (same layout as out_*), merged at the end
   int64_t* ovf_sum;
   int64_t* ovf_min;
@@ -450,6 +452,7 @@ struct Lane {
   hipStream_t stream = nullptr;
   hipStream_t stream_b = nullptr;
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  hipEvent_t ev_bm0 = nullptr, ev_bm1 = nullptr;  // around the inverted-leaf bitmap build (part of device_ms)
   std::vector<hipEvent_t> ev_pool;
   void* staging[2] = {nullptr, nullptr};  // slot 0: launch parameters; slot 1: the bitmap build's work items
   size_t staging_bytes[2] = {0, 0};
@@ -487,6 +490,27 @@ struct Context {
   std::unique_ptr<DeviceBuffer> scratch_acquire(size_t n);
   void scratch_release(std::unique_ptr<DeviceBuffer> b);
   ~Context();
+};
+
+// A pinned host block of the context's pool held by one call, returned to the pool when the call's scope ends --
+// also when it ends by a throw, after draining `st` so no copy into the block is still in flight
+struct PinnedBlock {
+  Context* ctx;
+  hipStream_t st;
+  void* p = nullptr;
+  size_t cap = 0;
+  PinnedBlock(Context* c, hipStream_t s, size_t n) : ctx(c), st(s) { p = c->pinned_acquire(n, &cap); }
+  ~PinnedBlock() { release(); }
+  void release() {
+    if (!p) return;
+    if (std::uncaught_exceptions() > 0) (void)hipStreamSynchronize(st);
+    ctx->pinned_release(p, cap);
+    p = nullptr;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+  PinnedBlock(const PinnedBlock&) = delete;
+  PinnedBlock& operator=(const PinnedBlock&) = delete;
 };
 
 // RAII lane of one call; stream() is the caller's external stream when one is set (ph_ctx_set_stream)
@@ -538,6 +562,8 @@ void launch_selftest_unpack(const uint32_t* fwd, int64_t n, int bits, int32_t* o
 // segment (distinct, threshold, reached; zeroed)
 void launch_limit_select(const uint32_t* first, int64_t G, int64_t limit, int nseg, int64_t dbw, uint32_t* docbits,
                          uint32_t* keep, unsigned long long* scal, hipStream_t s);
+// number of non-zero entries of cnt[0, n) into *out (zeroed by the call)
+void launch_count_nonzero(const unsigned long long* cnt, int64_t n, unsigned long long* out, hipStream_t s);
 void launch_selftest_staged(const DevSegment* seg, int32_t tile_words, int32_t stage_stride, int64_t n, int32_t* out,
                             hipStream_t s);
 // the 1 KiB wave-loads of a full tile of every staged stream of `d` (stage offsets per stream)

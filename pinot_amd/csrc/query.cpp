@@ -1104,7 +1104,14 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
   };
   stamp("plan");
-  build_bitmaps();
+  // the bitmap build's device time is part of the query's device_ms (its own event pair: host setup follows it)
+  bool bm_timed = false;
+  if (!pl.bitmaps.empty() && dop != DENSE_LAYOUT && !fin) {
+    PH_HIP_CHECK(hipEventRecord(lane.lane->ev_bm0, st));
+    build_bitmaps();
+    PH_HIP_CHECK(hipEventRecord(lane.lane->ev_bm1, st));
+    bm_timed = true;
+  }
   stamp("bitmaps");
 
   // ---- group-by key space over table-level dictionaries
@@ -1285,9 +1292,17 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // a plain group-by's scan completion, matched-doc count and limit flags are read at the compaction's sync
   // (one host round trip instead of three)
   const bool defer_sync = q->num_group_by > 0 && num_hll == 0 && dop != DENSE_EXECUTE && !fin;
-  unsigned long long* dsc = nullptr;  // pinned: matched total, then 3 words per limit segment
-  size_t dsc_cap = 0, dsc_nlim = 0;
+  std::unique_ptr<PinnedBlock> dsc;  // pinned: matched total, then 3 words per limit segment
+  size_t dsc_nlim = 0;
   bool timed = false;  // this call recorded ev_start / ev_stop (some chunk was scanned)
+  // device time of the call: the scan launches (ev_start .. ev_stop, including a numGroupsLimit pass) + the
+  // inverted-leaf bitmap build (ev_bm0 .. ev_bm1); read after a sync of the stream
+  auto device_elapsed = [&]() {
+    float a = 0.f, b = 0.f;
+    if (timed) PH_HIP_CHECK(hipEventElapsedTime(&a, lane.lane->ev_start, lane.lane->ev_stop));
+    if (bm_timed) PH_HIP_CHECK(hipEventElapsedTime(&b, lane.lane->ev_bm0, lane.lane->ev_bm1));
+    return a + b;
+  };
   int64_t TR = G;  // rows of the output tables: the key space, or the slots of the MODE_GROUP_HASH table
   unsigned long long* hkeys = nullptr;
   if (fin) {
@@ -1373,7 +1388,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         // per scanned doc -- with >= 2x slots (DictionaryBasedGroupKeyGenerator's map-based holders, :598/:778)
         if (num_hll) fail(PH_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL group-by over a key space beyond the dense budget");
         if (dop) fail(PH_ERR_UNSUPPORTED, "dense partials over a key space beyond the dense budget");
-        if (any_limit) fail(PH_ERR_UNSUPPORTED, "numGroupsLimit over a key space beyond the dense budget");
+        // numGroupsLimit here runs optimistically only: the scan goes ahead without truncation and the call fails
+        // UNSUPPORTED afterwards if the table ends up with `limit` keys or more (see the launch below)
         int64_t live_docs = 0;
         for (int i = 0; i < nseg; ++i)
           if (seg_live[i]) live_docs += segs[i]->num_docs;
@@ -1395,32 +1411,30 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     return scratch.alloc<uint8_t>(bytes);
   };
   int tix = 0;
+  const int64_t hll_words = TR * num_hll * (m ? m : 1);
   kp.out_count = reinterpret_cast<unsigned long long*>(out_table(tix, 8 * (size_t)TR));
-  PH_HIP_CHECK(hipMemsetAsync(kp.out_count, 0, sizeof(unsigned long long) * TR, st));
   for (int j = 0; j < nvals; ++j) {
-    if (val_ops[j] & 1) {
-      kp.out_sum[j] = out_table(tix, 8 * (size_t)TR);
-      PH_HIP_CHECK(hipMemsetAsync(kp.out_sum[j], 0, 8 * TR, st));
-    }
-    if (val_ops[j] & 2) {
-      kp.out_min[j] = reinterpret_cast<int64_t*>(out_table(tix, 8 * (size_t)TR));
-      launch_fill_i64(kp.out_min[j], INT64_MAX, TR, st);
-    }
-    if (val_ops[j] & 4) {
-      kp.out_max[j] = reinterpret_cast<int64_t*>(out_table(tix, 8 * (size_t)TR));
-      launch_fill_i64(kp.out_max[j], INT64_MIN, TR, st);
-    }
+    if (val_ops[j] & 1) kp.out_sum[j] = out_table(tix, 8 * (size_t)TR);
+    if (val_ops[j] & 2) kp.out_min[j] = reinterpret_cast<int64_t*>(out_table(tix, 8 * (size_t)TR));
+    if (val_ops[j] & 4) kp.out_max[j] = reinterpret_cast<int64_t*>(out_table(tix, 8 * (size_t)TR));
   }
   if (mode == MODE_GROUP_HASH) {
     hkeys = scratch.alloc<unsigned long long>(TR);
-    PH_HIP_CHECK(hipMemsetAsync(hkeys, 0xFF, 8 * TR, st));  // kHashEmpty
     kp.hkeys = hkeys;
   }
-  const int64_t hll_words = TR * num_hll * (m ? m : 1);
-  if (num_hll) {
-    kp.out_hll = reinterpret_cast<uint32_t*>(out_table(tix, 4 * (size_t)hll_words));
-    PH_HIP_CHECK(hipMemsetAsync(kp.out_hll, 0, 4 * hll_words, st));
-  }
+  if (num_hll) kp.out_hll = reinterpret_cast<uint32_t*>(out_table(tix, 4 * (size_t)hll_words));
+  // identities of every output table (again before a numGroupsLimit rescan)
+  auto init_tables = [&]() {
+    PH_HIP_CHECK(hipMemsetAsync(kp.out_count, 0, sizeof(unsigned long long) * TR, st));
+    for (int j = 0; j < nvals; ++j) {
+      if (val_ops[j] & 1) PH_HIP_CHECK(hipMemsetAsync(kp.out_sum[j], 0, 8 * TR, st));
+      if (val_ops[j] & 2) launch_fill_i64(kp.out_min[j], INT64_MAX, TR, st);
+      if (val_ops[j] & 4) launch_fill_i64(kp.out_max[j], INT64_MIN, TR, st);
+    }
+    if (hkeys) PH_HIP_CHECK(hipMemsetAsync(hkeys, 0xFF, 8 * TR, st));  // kHashEmpty
+    if (num_hll) PH_HIP_CHECK(hipMemsetAsync(kp.out_hll, 0, 4 * hll_words, st));
+  };
+  init_tables();
 
   // ---- device segment table, programs, chunks
   std::vector<DevSegment> dsegs;
@@ -1610,9 +1624,17 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   unsigned long long* limit_scal = nullptr;  // [3] per limit segment: distinct, threshold, reached
   uint32_t* limit_keep = nullptr;             // [limit segments][ceil(G / 32)] keep bitsets
   uint32_t* limit_first = nullptr;            // [limit segments][G] first matching doc per key
+  const int base_late = kp.late_prefetch;     // the scan's prefetch order without the keep-bitset gathers
+  // numGroupsLimit, optimistic form: scan without truncation first; only when the merged table then holds >= limit
+  // keys can a segment have reached the limit, and only then do the first-seen pass and the truncating rescan run
+  // (r2 ran the pass whenever a segment's cardinality product reached the limit: SSB Q3.2-Q4.3, products of
+  // 0.4-1.75M keys over a few hundred real groups).  PH_LIMIT_EAGER=1 restores the pass-first order (tests).
+  const bool limit_opt = getenv("PH_LIMIT_EAGER") == nullptr || mode == MODE_GROUP_HASH;
   if (any_limit && q->num_group_by > 0) {
     for (size_t k = 0; k < dsegs.size(); ++k)
       if (seg_limit[dseg_src[k]]) limit_segs.push_back((int)k);
+  }
+  if (!limit_segs.empty() && mode != MODE_GROUP_HASH) {
     const double keep_bytes = (double)limit_segs.size() * (double)((G + 31) / 32) * 4.0;
     if (keep_bytes > 8e9) fail(PH_ERR_UNSUPPORTED, "numGroupsLimit emulation needs too many key bitsets");
     // one block each for the limit segments' keep bitsets and first-doc tables (every segment's pass runs in one
@@ -1636,6 +1658,12 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   }
   // per-segment tile pieces: the 1 KiB wave-loads of a full tile, stream by stream
   for (auto& d : dsegs) fill_tile_pieces(d, kp.nstage, kp.stage_soff, kp.tile_words);
+  // the optimistic numGroupsLimit scan's segment table: no keep bitsets, no first-doc tables
+  std::vector<DevSegment> dsegs_opt;
+  if (!limit_segs.empty() && limit_opt) {
+    dsegs_opt = dsegs;
+    for (auto& d : dsegs_opt) d.keep = nullptr, d.first_doc = nullptr;
+  }
   // the lean kernel A (k_part_scan) covers gather-free tiles with ALL / RANGE / DOCRANGE filter leaves
   kp.part_fast = !kp.late_prefetch && getenv("PH_PART_GENERIC") == nullptr;
   for (auto& d : dsegs)
@@ -1748,6 +1776,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   stamp("setup");
   if (!chunks.empty()) {
     DevSegment* d_segs = scratch.alloc<DevSegment>(dsegs.size());
+    DevSegment* d_segs_opt = dsegs_opt.empty() ? nullptr : scratch.alloc<DevSegment>(dsegs_opt.size());
     FilterInsn* d_prog = scratch.alloc<FilterInsn>(std::max<size_t>(1, all_insns.size()));
     std::vector<Chunk> all_chunks = chunks;  // + the numGroupsLimit pass's chunks (limit segments only)
     for (int k : limit_segs)
@@ -1755,14 +1784,16 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     const size_t n_limit_chunks = all_chunks.size() - chunks.size();
     Chunk* d_chunks = scratch.alloc<Chunk>(all_chunks.size());
     const size_t b1 = sizeof(DevSegment) * dsegs.size(), b2 = sizeof(FilterInsn) * all_insns.size(),
-                 b3 = sizeof(Chunk) * all_chunks.size();
-    uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(b1 + b2 + b3));
+                 b3 = sizeof(Chunk) * all_chunks.size(), b4 = sizeof(DevSegment) * dsegs_opt.size();
+    uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(b1 + b2 + b3 + b4));
     memcpy(stage, dsegs.data(), b1);
     memcpy(stage + b1, all_insns.data(), b2);
     memcpy(stage + b1 + b2, all_chunks.data(), b3);
+    if (b4) memcpy(stage + b1 + b2 + b3, dsegs_opt.data(), b4);
     PH_HIP_CHECK(hipMemcpyAsync(d_segs, stage, b1, hipMemcpyHostToDevice, st));
     if (b2) PH_HIP_CHECK(hipMemcpyAsync(d_prog, stage + b1, b2, hipMemcpyHostToDevice, st));
     PH_HIP_CHECK(hipMemcpyAsync(d_chunks, stage + b1 + b2, b3, hipMemcpyHostToDevice, st));
+    if (b4) PH_HIP_CHECK(hipMemcpyAsync(d_segs_opt, stage + b1 + b2 + b3, b4, hipMemcpyHostToDevice, st));
     kp.segs = d_segs;
     kp.prog = d_prog;
     kp.chunks = d_chunks;
@@ -1773,7 +1804,48 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       int blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1)));
       if (mode == MODE_GROUP_LDS) blocks_per_cu = std::min(blocks_per_cu, 4);
       const int grid = (int)std::min<int64_t>((int64_t)chunks.size(), (int64_t)ctx->num_cus * blocks_per_cu);
-      if (!limit_segs.empty()) {
+      // device_ms opens here: it covers the numGroupsLimit pass and (below) the bitmap build too
+      PH_HIP_CHECK(hipEventRecord(lane.lane->ev_start, st));
+      // an interruptible call scans in batches of kInterruptChunks chunks and checks between them
+      const int32_t nchunks = (int32_t)chunks.size();
+      int32_t step = interruptible ? kInterruptChunks : nchunks;
+      if (const char* e = getenv("PH_INTERRUPT_CHUNKS")) if (interruptible) step = std::max(1, atoi(e));  // tests
+      auto run_scan = [&](KParams kx) {
+        for (int32_t cb = 0; cb < nchunks; cb += step) {
+          kx.chunk_begin = cb;
+          kx.chunk_end = std::min(nchunks, cb + step);
+          launch_scan(kx, mode, q->num_group_by, 0, std::min(grid, kx.chunk_end - cb), lds, st);
+          if (interruptible && kx.chunk_end < nchunks) {
+            PH_HIP_CHECK(hipStreamSynchronize(st));
+            check_interrupt();
+          }
+        }
+      };
+      bool scanned = false;
+      if (!limit_segs.empty() && limit_opt) {
+        KParams ko = kp;
+        ko.segs = d_segs_opt;
+        ko.late_prefetch = base_late;
+        run_scan(ko);
+        unsigned long long* keys_dev = scratch.alloc<unsigned long long>(1);
+        launch_count_nonzero(kp.out_count, TR, keys_dev, st);
+        PinnedBlock keys_host(ctx, st, 8);
+        PH_HIP_CHECK(hipMemcpyAsync(keys_host.p, keys_dev, 8, hipMemcpyDeviceToHost, st));
+        PH_HIP_CHECK(hipStreamSynchronize(st));
+        const int64_t merged_keys = (int64_t)*keys_host.as<unsigned long long>();
+        keys_host.release();
+        if (merged_keys < group_limit) {
+          scanned = true;  // no segment can hold `limit` keys: the untruncated scan is the reference's result
+          stats.limit_pass = 1;
+        } else {
+          if (mode == MODE_GROUP_HASH)
+            fail(PH_ERR_UNSUPPORTED, "numGroupsLimit reached over a key space beyond the dense budget");
+          init_tables();  // truncation needed: first-seen pass, then the rescan with keep bitsets
+          PH_HIP_CHECK(hipMemsetAsync(kp.matched_total, 0, 8, st));
+        }
+      }
+      if (!scanned && !limit_segs.empty()) {
+        stats.limit_pass = 2;
         // first-seen pass over every limit segment in ONE launch (MODE_GROUP_GLOBAL records each key's first
         // matching doc in the segment's own table), then the kept keys of every segment in one select step; the
         // pass walks the limit segments' chunks, appended after the main chunk list
@@ -1796,20 +1868,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         launch_limit_select(limit_first, G, group_limit, (int)limit_segs.size(), dbw, docbits, limit_keep, limit_scal,
                             st);
       }
-      // an interruptible call scans in batches of kInterruptChunks chunks and checks between them
-      const int32_t nchunks = (int32_t)chunks.size();
-      int32_t step = interruptible ? kInterruptChunks : nchunks;
-      if (const char* e = getenv("PH_INTERRUPT_CHUNKS")) if (interruptible) step = std::max(1, atoi(e));  // tests
-      PH_HIP_CHECK(hipEventRecord(lane.lane->ev_start, st));
-      for (int32_t cb = 0; cb < nchunks; cb += step) {
-        kp.chunk_begin = cb;
-        kp.chunk_end = std::min(nchunks, cb + step);
-        launch_scan(kp, mode, q->num_group_by, 0, std::min(grid, kp.chunk_end - cb), lds, st);
-        if (interruptible && kp.chunk_end < nchunks) {
-          PH_HIP_CHECK(hipStreamSynchronize(st));
-          check_interrupt();
-        }
-      }
+      if (!scanned) run_scan(kp);
       PH_HIP_CHECK(hipEventRecord(lane.lane->ev_stop, st));
     } else {
       // ---- partitioned group-by: batches of chunks; kernel A (filter + decode + partition) on `st`,
@@ -1849,6 +1908,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       // restores the r1 order
       kp.part_load_first = getenv("PH_PART_FLUSH_FIRST") == nullptr;
       kp.part_dbg = getenv("PH_PART_DBG") ? atoi(getenv("PH_PART_DBG")) : 0;  // timing experiments only
+      kp.part_depth = 1;
+      if (const char* e = getenv("PH_PART_DEPTH")) kp.part_depth = atoi(e) == 2 ? 2 : 1;  // tuning knob
       kp.part_vbits = vbits;
       kp.num_parts = (int32_t)P;
       const size_t lds_a = partition_lds_bytes(kp);
@@ -1967,7 +2028,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if (!defer_sync || kp.dbg) {
       PH_HIP_CHECK(hipStreamSynchronize(st));  // staging buffer reuse + results
       stamp("kernels done");
-      PH_HIP_CHECK(hipEventElapsedTime(&dev_ms, lane.lane->ev_start, lane.lane->ev_stop));
+      dev_ms = device_elapsed();
     }
     if (kp.dbg) {  // PH_DEBUG_STAMPS: where wave 0 of each workgroup spent its cycles (last launch)
       std::vector<unsigned long long> h(4 * (size_t)ctx->num_cus * 8);
@@ -1980,25 +2041,27 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
   } else {
     PH_HIP_CHECK(hipStreamSynchronize(st));
+    dev_ms = device_elapsed();  // the bitmap build alone (no chunk to scan)
   }
   stats.device_ms = dev_ms;
   res->mode = mode;
   stats.plan_mode = mode;
   if (kp.matched_total && defer_sync) {
-    dsc_nlim = limit_segs.size();
-    dsc = static_cast<unsigned long long*>(ctx->pinned_acquire(8 * (1 + 3 * dsc_nlim), &dsc_cap));
-    PH_HIP_CHECK(hipMemcpyAsync(dsc, kp.matched_total, 8, hipMemcpyDeviceToHost, st));
-    if (dsc_nlim) PH_HIP_CHECK(hipMemcpyAsync(dsc + 1, limit_scal, 24 * dsc_nlim, hipMemcpyDeviceToHost, st));
+    dsc_nlim = limit_scal ? limit_segs.size() : 0;
+    dsc = std::make_unique<PinnedBlock>(ctx, st, 8 * (1 + 3 * dsc_nlim));
+    unsigned long long* dw = dsc->as<unsigned long long>();
+    PH_HIP_CHECK(hipMemcpyAsync(dw, kp.matched_total, 8, hipMemcpyDeviceToHost, st));
+    if (dsc_nlim) PH_HIP_CHECK(hipMemcpyAsync(dw + 1, limit_scal, 24 * dsc_nlim, hipMemcpyDeviceToHost, st));
   } else if (kp.matched_total) {
     // group-by: numDocsScanned = matched docs (docs of keys beyond numGroupsLimit included,
     // GroupByOperator.java:106-107) and numGroupsLimitReached of any segment
-    std::vector<unsigned long long> sc(1 + 3 * limit_segs.size());
+    const size_t nlim = limit_scal ? limit_segs.size() : 0;
+    std::vector<unsigned long long> sc(1 + 3 * nlim);
     PH_HIP_CHECK(hipMemcpyAsync(sc.data(), kp.matched_total, 8, hipMemcpyDeviceToHost, st));
-    if (!limit_segs.empty())
-      PH_HIP_CHECK(hipMemcpyAsync(sc.data() + 1, limit_scal, 24 * limit_segs.size(), hipMemcpyDeviceToHost, st));
+    if (nlim) PH_HIP_CHECK(hipMemcpyAsync(sc.data() + 1, limit_scal, 24 * nlim, hipMemcpyDeviceToHost, st));
     PH_HIP_CHECK(hipStreamSynchronize(st));
     stats.num_docs_scanned = (int64_t)sc[0];
-    for (size_t t = 0; t < limit_segs.size(); ++t) stats.num_groups_limit_reached |= sc[1 + 3 * t + 2] != 0;
+    for (size_t t = 0; t < nlim; ++t) stats.num_groups_limit_reached |= sc[1 + 3 * t + 2] != 0;
   }
   if (dop == DENSE_EXECUTE) {
     // partial tables stay on the device for the cross-GPU reduction
@@ -2039,14 +2102,14 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   auto resolve_deferred = [&]() {
     if (defer_sync && !kp.dbg && timed) {
       stamp("kernels done");
-      PH_HIP_CHECK(hipEventElapsedTime(&dev_ms, lane.lane->ev_start, lane.lane->ev_stop));
+      dev_ms = device_elapsed();
       stats.device_ms = dev_ms;
     }
     if (dsc) {
-      stats.num_docs_scanned = (int64_t)dsc[0];
-      for (size_t t = 0; t < dsc_nlim; ++t) stats.num_groups_limit_reached |= dsc[1 + 3 * t + 2] != 0;
-      ctx->pinned_release(dsc, dsc_cap);
-      dsc = nullptr;
+      const unsigned long long* dw = dsc->as<unsigned long long>();
+      stats.num_docs_scanned = (int64_t)dw[0];
+      for (size_t t = 0; t < dsc_nlim; ++t) stats.num_groups_limit_reached |= dw[1 + 3 * t + 2] != 0;
+      dsc.reset();
     }
   };
   if (q->num_group_by == 0) {
@@ -2059,8 +2122,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       const int t = q->aggregations[k].type;
       need += t == PH_AGG_COUNT ? 0 : (t == PH_AGG_DISTINCTCOUNTHLL ? 4 * (size_t)m : 8);
     }
-    size_t blk_cap = 0;
-    uint8_t* blk = static_cast<uint8_t*>(ctx->pinned_acquire(need, &blk_cap));
+    PinnedBlock blk_hold(ctx, st, need);
+    uint8_t* blk = blk_hold.as<uint8_t>();
     PH_HIP_CHECK(hipMemcpyAsync(blk, kp.out_count, 8, hipMemcpyDeviceToHost, st));
     for (int k = 0; k < nagg; ++k) {
       const int t = q->aggregations[k].type;
@@ -2090,7 +2153,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         memcpy(dst, &v, 8);
       }
     }
-    ctx->pinned_release(blk, blk_cap);
+
   } else if (num_hll == 0) {
     // device-side compaction: non-empty groups in key order, keys decoded, values converted to double,
     // copied straight into pinned result columns
@@ -2127,14 +2190,14 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     cp.blk = scratch.alloc<unsigned long long>(kCompactBlocks + 2);
     PH_HIP_CHECK(hipMemsetAsync(cp.blk + kCompactBlocks + 1, 0, 8, st));
     launch_compact(cp, st);
-    size_t tot_cap = 0;
-    unsigned long long* tot = static_cast<unsigned long long*>(ctx->pinned_acquire(16, &tot_cap));
+    PinnedBlock tot_hold(ctx, st, 16);
+    unsigned long long* tot = tot_hold.as<unsigned long long>();
     PH_HIP_CHECK(hipMemcpyAsync(tot, cp.blk + kCompactBlocks, 16, hipMemcpyDeviceToHost, st));
     PH_HIP_CHECK(hipStreamSynchronize(st));
     resolve_deferred();
     const int64_t R = (int64_t)tot[0];
     const int64_t docs = (int64_t)tot[1];
-    ctx->pinned_release(tot, tot_cap);
+    tot_hold.release();
     res->num_groups = R;
     res->ctx = ctx;
     res->aggs.resize(nagg);
@@ -2152,6 +2215,19 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     res->key_entry_size.resize(q->num_group_by);
     res->keys.resize(q->num_group_by);
     std::vector<ResultBuf> string_ids(q->num_group_by);
+    struct IdsGuard {  // STRING keys' id columns: pinned blocks returned on every exit (a throw drains the stream)
+      Context* c;
+      hipStream_t s;
+      std::vector<ResultBuf>& v;
+      ~IdsGuard() {
+        for (auto& b : v)
+          if (b.pinned) {
+            if (std::uncaught_exceptions() > 0) (void)hipStreamSynchronize(s);
+            c->pinned_release(b.pinned, b.cap);
+            b.pinned = nullptr;
+          }
+      }
+    } ids_guard{ctx, st, string_ids};
     for (int g = 0; g < q->num_group_by; ++g) {
       const Dictionary& d = gdicts[g]->dict;
       res->key_types[g] = d.type;
@@ -2184,6 +2260,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       const int32_t* ids = reinterpret_cast<const int32_t*>(string_ids[g].data());
       for (int64_t r = 0; r < R; ++r) put_key_value(d, ids[r], res->keys[g].data() + (size_t)es * r, es);
       ctx->pinned_release(string_ids[g].pinned, string_ids[g].cap);
+      string_ids[g].pinned = nullptr;
     }
   } else {
     // group-by with DISTINCTCOUNTHLL registers: host-side materialisation

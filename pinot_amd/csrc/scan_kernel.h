@@ -226,6 +226,49 @@ __device__ __forceinline__ void tile_store(SegPtr S, int32_t nvalid, uint8_t* ws
   __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
 }
 
+// Two-deep form of the tile pipeline (k_part_scan2): the loads of a tile are issued two tiles ahead, into one of
+// two register sets, so a wave keeps two tiles of HBM reads in flight.  Every tile issues exactly NL buffer loads
+// with every lane active; a piece the tile does not need (beyond the segment's pieces, or past the tile's bytes)
+// gets an offset outside its descriptor's range, which the hardware answers with zeros and no memory access.
+// So the waitcnt pass can keep the younger set in flight: the wait before a set is consumed is vmcnt(NL), not
+// vmcnt(0) (plain loads with a shared fallback address were merged by the compiler into register copies of one
+// load, which forced a vmcnt(0) per tile).
+template <int NL>
+__device__ __forceinline__ void tile_load_fixed(bool live, SegPtr S, int32_t w0, int32_t nvalid, int lane,
+                                                Prefetch<NL>& pf) {
+  const int np = live ? S->npieces : 0;  // no tile: NL loads that all answer zeros (the count stays fixed)
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const bool have = k < np;
+    const int32_t stride = have ? S->pieces[k].stride : 0, off = have ? S->pieces[k].off : 0;
+    const uint8_t* base = have ? S->pieces[k].fwd : nullptr;
+    const bool need = have && off < nvalid * stride + 8;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0,
+                                                                        need ? 0x7fffffff : 0, 0x00020000);
+    const uint32_t vo = need ? (uint32_t)(w0 * stride + lane * 16) : 0x80000000u;
+    pf.r[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 0));
+  }
+}
+
+template <int NL>
+__device__ __forceinline__ void tile_store_nowait(SegPtr S, int32_t nvalid, uint8_t* wst, int lane,
+                                                  const Prefetch<NL>& pf) {
+  // the waitcnt pass waits for this set's loads only (vmcnt(2 NL - 1) .. vmcnt(NL)): the other set stays in flight
+  const int np = S->npieces;
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const int32_t stride = S->pieces[k].stride, off = S->pieces[k].off, lds = S->pieces[k].lds;
+    if (k < np && off + lane * 16 < nvalid * stride + 8) {
+      u32x4 v = pf.r[k];
+      v.x = __builtin_bswap32(v.x);
+      v.y = __builtin_bswap32(v.y);
+      v.z = __builtin_bswap32(v.z);
+      v.w = __builtin_bswap32(v.w);
+      *reinterpret_cast<u32x4*>(wst + lds + lane * 16) = v;
+    }
+  }
+}
+
 // Per-lane decode cursor over a staged (byte-swapped) stream.  Doc `lane` of 64-doc word u ends at bit
 // e = (64u + lane + 1) * b - 1 of the span; word u+1 starts exactly 2b dwords later, so the dword index
 // advances by 2b per word and the in-dword position of the value's last bit never changes: the value is

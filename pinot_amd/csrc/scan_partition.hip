@@ -317,8 +317,117 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
   if (matched && p.matched_total) atomicAdd(p.matched_total, matched);
 }
 
+// Kernel A with a two-deep load pipeline (PH_PART_DEPTH=2): the same rounds, rings and flushes as k_part_scan, but
+// a wave's loads run two tiles ahead in two register sets (tile_load_fixed), so each wave keeps two tiles of HBM
+// reads in flight instead of one (r2: kernel A streamed at 2.6 TB/s with one 12-word tile in flight per wave, its
+// occupancy held at 16 waves per CU by the rings + staging LDS).  In a round the flush stores go out BEFORE the
+// prefetch loads, so the wait before a set is consumed (vmcnt(NL): the other set still in flight) covers them.
+template <int NG, int REC64, int HASV>
+__global__ void __launch_bounds__(kPartBlock) k_part_scan2(const KParams p) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NL = kPrefetchPartition;
+  constexpr int WAVES = kPartWaves;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  SegPtr segs = (SegPtr)p.segs;
+  const PH_CONST Chunk* chunks = (const PH_CONST Chunk*)p.chunks;
+  uint8_t* wst = smem + p.stage_off + (size_t)wave * p.stage_stride;
+  const uint32_t wst_off = lds_addr(wst);
+  uint32_t* words = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
+  uint32_t* gpos = reinterpret_cast<uint32_t*>(smem + p.pl_bcnt_off);
+  uint32_t* lists = reinterpret_cast<uint32_t*>(smem + p.pl_misc_off);  // [2][P] listed partitions
+  uint32_t* lcnt = lists + 2 * p.num_parts;                            // [2] list lengths
+  for (int i = threadIdx.x; i < p.num_parts + 64; i += kPartBlock) words[i] = 0;
+  for (int i = threadIdx.x; i < p.num_parts; i += kPartBlock) gpos[i] = 0;
+  if (threadIdx.x < 2) lcnt[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t par = 0;
+  unsigned long long matched = 0;
+  const int32_t tw = p.tile_words;
+  const int32_t round_words = WAVES * tw;
+  const int64_t nch = p.chunk_end - p.chunk_begin;
+  const int32_t c0 = p.chunk_begin + (int32_t)(nch * blockIdx.x / gridDim.x);
+  int32_t c = c0, r = 0;
+  const int32_t c_end = p.chunk_begin + (int32_t)(nch * (blockIdx.x + 1) / gridDim.x);
+  // the round iterator (c, r) names the NEXT tile to load; t0 / t1 are the two tiles in flight (t0 older)
+  struct Tile {
+    SegPtr S;
+    int32_t w0, nvalid;
+    bool live;
+  };
+  auto next_tile = [&]() {
+    Tile t{nullptr, 0, 0, false};
+    if (c < c_end) {
+      const int32_t cbeg = chunks[c].word_begin, cend = chunks[c].word_end;
+      t.S = segs + chunks[c].seg;
+      t.w0 = cbeg + r * round_words + wave * tw;
+      t.nvalid = min(tw, cend - t.w0);
+      t.live = true;
+      if (cbeg + (r + 1) * round_words < cend) {
+        ++r;
+      } else {
+        ++c;
+        r = 0;
+      }
+    }
+    return t;
+  };
+  Prefetch<NL> pa, pb;
+  Tile t0 = next_tile();
+  tile_load_fixed<NL>(t0.live && t0.nvalid > 0, t0.S, t0.w0, t0.nvalid, lane, pa);
+  Tile t1 = next_tile();
+  tile_load_fixed<NL>(t1.live && t1.nvalid > 0, t1.S, t1.w0, t1.nvalid, lane, pb);
+  // one round on the tile in `cur` (its loads the older set); the tile two ahead reloads `cur`
+  auto round = [&](Prefetch<NL>& cur) {
+    if (t0.live) tile_store_nowait<NL>(t0.S, t0.nvalid, wst, lane, cur);
+    {
+      const uint32_t prev = par ^ 1u;
+      const uint32_t nl = lcnt[prev];
+      if (threadIdx.x == 0) lcnt[par] = 0;
+      part_flush_listed<REC64, kPartBlock>(p, smem, lists + prev * p.num_parts, nl, matched);
+    }
+    lds_barrier();  // ring words are final before anyone appends again; this wave's staging is written
+    const Tile t2 = next_tile();
+    tile_load_fixed<NL>(t2.live && t2.nvalid > 0, t2.S, t2.w0, t2.nvalid, lane, cur);  // always NL loads
+    if (t0.live && t0.nvalid > 0) {
+      const int fk = t0.S->fkind;
+      uint32_t* fl = lists + par * p.num_parts;
+      uint32_t* fc = lcnt + par;
+      if (fk == FK_RANGE) part_tile<NG, REC64, HASV, FK_RANGE>(p, t0.S, smem, wst_off, lane, t0.w0, t0.nvalid, fl, fc);
+      else if (fk == FK_DOCRANGE) part_tile<NG, REC64, HASV, FK_DOCRANGE>(p, t0.S, smem, wst_off, lane, t0.w0, t0.nvalid, fl, fc);
+      else part_tile<NG, REC64, HASV, FK_ALL>(p, t0.S, smem, wst_off, lane, t0.w0, t0.nvalid, fl, fc);
+    }
+    lds_barrier();  // this round's appends are complete before the next round's flush; staging read
+    par ^= 1u;
+    t0 = t1;
+    t1 = t2;
+  };
+  // rounds are workgroup-uniform (every wave of a workgroup walks the same chunk range), so the barriers match.
+  // The round count is padded to even (a last round without a tile stages nothing and appends nothing): the loop
+  // body is then the unconditional pair round(pa); round(pb), whose load / consume order the waitcnt pass can
+  // follow (with a conditional exit between the two rounds it waited for the younger set as well: vmcnt(0))
+  int32_t nrounds = 0;
+  for (int32_t cc = c0; cc < c_end; ++cc) {
+    const int32_t words = chunks[cc].word_end - chunks[cc].word_begin;
+    nrounds += (words + round_words - 1) / round_words;
+  }
+  for (int32_t i = 0; i < nrounds; i += 2) {
+    round(pa);
+    round(pb);
+  }
+  part_flush_listed<REC64, kPartBlock>(p, smem, lists + (par ^ 1u) * p.num_parts, lcnt[par ^ 1u], matched);
+  lds_barrier();
+  part_flush_final<REC64, kPartBlock>(p, smem, matched);
+  if (matched && p.matched_total) atomicAdd(p.matched_total, matched);
+}
+
 template <int NG, int REC64, int HASV>
 static void launch_part_fast(const KParams& p, int grid, size_t lds, hipStream_t s) {
+  if (p.part_depth == 2) {
+    allow_lds(k_part_scan2<NG, REC64, HASV>, lds);
+    hipLaunchKernelGGL((k_part_scan2<NG, REC64, HASV>), dim3(grid), dim3(kPartBlock), lds, s, p);
+    return;
+  }
   allow_lds(k_part_scan<NG, REC64, HASV>, lds);
   hipLaunchKernelGGL((k_part_scan<NG, REC64, HASV>), dim3(grid), dim3(kPartBlock), lds, s, p);
 }

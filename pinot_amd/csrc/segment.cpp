@@ -85,6 +85,8 @@ Lane::Lane(int dev) : device(dev) {
   PH_HIP_CHECK(hipStreamCreateWithFlags(&stream_b, hipStreamNonBlocking));
   PH_HIP_CHECK(hipEventCreate(&ev_start));
   PH_HIP_CHECK(hipEventCreate(&ev_stop));
+  PH_HIP_CHECK(hipEventCreate(&ev_bm0));
+  PH_HIP_CHECK(hipEventCreate(&ev_bm1));
 }
 
 Lane::~Lane() {
@@ -93,6 +95,8 @@ Lane::~Lane() {
   if (stream_b) (void)hipStreamSynchronize(stream_b);
   if (ev_start) (void)hipEventDestroy(ev_start);
   if (ev_stop) (void)hipEventDestroy(ev_stop);
+  if (ev_bm0) (void)hipEventDestroy(ev_bm0);
+  if (ev_bm1) (void)hipEventDestroy(ev_bm1);
   for (auto e : ev_pool) (void)hipEventDestroy(e);
   if (stream) (void)hipStreamDestroy(stream);
   if (stream_b) (void)hipStreamDestroy(stream_b);

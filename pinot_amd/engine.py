@@ -41,6 +41,7 @@ class ExecutionStats:
     device_ms: float
     host_ms: float
     mode: int = 0
+    limit_pass: int = 0  # numGroupsLimit: 0 not needed, 1 optimistic scan sufficed, 2 first-seen pass + rescan
 
 
 @dataclass
@@ -311,7 +312,8 @@ class GpuContext:
         stats = ExecutionStats(st.num_docs_scanned, st.num_entries_scanned_in_filter,
                                st.num_entries_scanned_post_filter, st.num_total_docs, st.num_segments_processed,
                                st.num_segments_matched, bool(st.num_groups_limit_reached),
-                               bool(st.sum_precision_flag), st.device_ms, st.host_ms, st.plan_mode)
+                               bool(st.sum_precision_flag), st.device_ms, st.host_ms, st.plan_mode,
+                               st.limit_pass)
         return IntermediateResult(key_cols, agg_cols, n, [a.function for a in q.aggregations], stats)
 
     # ---------------------------------------------------------------- dense partials (multi-GPU combine)

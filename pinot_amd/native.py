@@ -111,7 +111,7 @@ class ExecStats(ctypes.Structure):
                 ("num_segments_processed", ctypes.c_int64), ("num_segments_matched", ctypes.c_int64),
                 ("num_groups_limit_reached", ctypes.c_int32), ("sum_precision_flag", ctypes.c_int32),
                 ("device_ms", ctypes.c_double), ("host_ms", ctypes.c_double), ("plan_mode", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("limit_pass", ctypes.c_int32)]
 
 
 # every symbol declared in include/pinot_hip.h

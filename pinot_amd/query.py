@@ -111,10 +111,11 @@ class FilterContext:
 
 # --------------------------------------------------------------------------- aggregations
 # 2-operand expressions inside aggregates (SSB Q1.x SUM(lo_extendedprice * lo_discount), Q4.x
-# SUM(lo_revenue - lo_supplycost)): MultiplicationTransformFunction "mult", SubtractionTransformFunction "sub",
-# AdditionTransformFunction "add" (pinot-core/.../operator/transform/function/*.java); the result is DOUBLE and
-# computed per row as double arithmetic (MultiplicationTransformFunction.java:89-104).
-EXPR_OPS = {"*": "mult", "-": "sub", "+": "add"}
+# SUM(lo_revenue - lo_supplycost)), computed per row as double arithmetic (MultiplicationTransformFunction.java:89-104).
+# Their names in result columns are the parser's canonical SqlKind names (CalciteSqlParser.java:798
+# canonicalizeFunctionNamePreservingSpecialKey(functionKind.name()): TIMES -> "times", MINUS -> "minus", PLUS -> "plus"),
+# so SUM(a*b) is reported as `sum(times(a,b))`, the same name datatable.cpp's agg_column_name writes.
+EXPR_OPS = {"*": "times", "-": "minus", "+": "plus"}
 
 
 @dataclass(frozen=True)

@@ -64,6 +64,9 @@ def test_datatable_broker_reduce(setup, sql):
     for name, a in zip(t.column_names[nk:], q.aggregations):  # AggregationFunction.getResultColumnName()
         arg = a.column if a.op is None else f"{ops[a.op]}({a.column},{a.column2})"
         assert name == ("count(*)" if a.function == "COUNT" else f"{a.function.lower()}({arg})")
+    # the Python broker's result columns carry the same names as the DataTable schema
+    names = {a.result_name() for a in q.aggregations}
+    assert set(t.column_names[nk:]) == names, (t.column_names, names)
     assert t.column_types[nk:] == [{"COUNT": "LONG", "DISTINCTCOUNTHLL": "OBJECT"}.get(a.function, "DOUBLE")
                                    for a in q.aggregations]
     r = ctx.execute(q, servers[1])

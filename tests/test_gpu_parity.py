@@ -13,6 +13,7 @@ from pinot_amd.query import parse_sql
 from pinot_amd.reduce import reduce_groups
 from pinot_amd.segment import create_segment
 from tests import kat_sv
+from tests.seeds import seed_of
 
 pytestmark = pytest.mark.gpu
 
@@ -128,7 +129,7 @@ FILTERS = [
 
 @pytest.mark.parametrize("where", FILTERS)
 def test_random_aggregation_only(ctx, where):
-    rng = np.random.default_rng(abs(hash(where)) % 2**32)
+    rng = np.random.default_rng(seed_of(where))
     tables = [_random_table(rng, n) for n in (20_000, 777, 64 * 300 + 1)]
     _both(ctx, tables, "SELECT COUNT(*), SUM(m), MIN(b), MAX(c), SUM(d), MIN(d), MAX(d) FROM t" + where,
           inverted=("a", "str"))
@@ -137,7 +138,7 @@ def test_random_aggregation_only(ctx, where):
 @pytest.mark.parametrize("where", FILTERS[:12])
 @pytest.mark.parametrize("group", ["a", "str", "s", "a, str", "s, a, str", "b", "c"])
 def test_random_group_by(ctx, where, group):
-    rng = np.random.default_rng((abs(hash(where + group))) % 2**32)
+    rng = np.random.default_rng(seed_of(where + group))
     tables = [_random_table(rng, n) for n in (9_999, 30_000)]
     _both(ctx, tables, f"SET numGroupsLimit=10000000; SELECT {group}, COUNT(*), SUM(m), MIN(d), MAX(b), SUM(d) "
                        f"FROM t{where} GROUP BY {group} ORDER BY {group} LIMIT 100000", inverted=("a", "str"))
@@ -334,7 +335,7 @@ def test_num_groups_limit_first_seen(ctx, case):
     # DictionaryBasedGroupKeyGenerator keeps the first numGroupsLimit keys of each segment in doc order and drops
     # the docs of later keys (IntGroupIdMap.getGroupId :992-1017); numGroupsLimitReached = numGroups >= limit
     # (GroupByOperator.java:111).  Default limit 100 000, 2-column keys with a 1M cardinality product.
-    rng = np.random.default_rng(hash(case) % 2**32)
+    rng = np.random.default_rng(seed_of(case))
     tables = []
     for n in (400_000, 250_003):
         if case == "few":  # 1 000 real groups (g2 follows g1) although the cardinality product is 1M
@@ -366,6 +367,57 @@ def test_num_groups_limit_first_seen(ctx, case):
     assert r.stats.num_groups_limit_reached == e.stats.num_groups_limit_reached
     if case in ("many", "filtered", "three_cols"):
         assert r.stats.num_groups_limit_reached
+        assert r.stats.limit_pass == 2  # truncation ran: the first-seen pass and the rescan
+    if case == "few":  # 1 000 real keys under a product of 1M >= limit: the optimistic scan suffices, no pass
+        assert not r.stats.num_groups_limit_reached and r.stats.limit_pass == 1
+
+
+@pytest.mark.parametrize("eager", [False, True])
+def test_num_groups_limit_product_above_real_keys(ctx, eager, monkeypatch):
+    # a cardinality product far above the limit but fewer real keys than the limit: numGroupsLimitReached stays
+    # false and the result is the untruncated group-by (optimistic form: no first-seen pass at all); the
+    # pass-first order (PH_LIMIT_EAGER) gives the same answer
+    if eager:
+        monkeypatch.setenv("PH_LIMIT_EAGER", "1")
+    rng = np.random.default_rng(seed_of("product_above_real_keys"))
+    tables = []
+    for n in (300_000, 200_001):
+        a = rng.integers(0, 2000, n).astype(np.int32)
+        b = ((a * 13 + rng.integers(0, 3, n)) % 1500).astype(np.int32)  # ~6000 real (a, b) keys of 3M
+        b[:1500] = np.arange(1500)  # every b value present: cardinality product 2000 x 1500 per segment
+        a[:2000] = np.arange(2000)
+        tables.append({"a": (a, "INT"), "b": (b, "INT"),
+                       "m": (rng.integers(-50, 1 << 18, n).astype(np.int32), "INT")})
+    sql = ("SET numGroupsLimit=20000; SELECT a, b, COUNT(*), SUM(m), MIN(m) FROM t GROUP BY a, b ORDER BY a, b "
+           "LIMIT 100000")
+    r, _ = _both(ctx, tables, sql)
+    q = parse_sql(sql)
+    e = O.execute(q, [O.build_segment(f"s{i}", t) for i, t in enumerate(tables)])
+    assert not r.stats.num_groups_limit_reached and not e.stats.num_groups_limit_reached
+    assert r.num_groups < 20000
+    assert r.stats.limit_pass == (2 if eager else 1)
+
+
+@pytest.mark.parametrize("shape", ["pruned", "empty"])
+def test_group_by_with_nothing_to_scan_fresh_context(shape):
+    # a plain group-by (deferred-sync result path) whose filter prunes every segment / whose segments are empty,
+    # on a fresh context (fresh lanes: no event was ever recorded): 0 groups, device_ms 0, no error
+    from pinot_amd.engine import GpuContext
+    c = GpuContext(0)
+    try:
+        n = 0 if shape == "empty" else 5000
+        rng = np.random.default_rng(seed_of(shape))
+        cols = {"g": (rng.integers(0, 50, n).astype(np.int32), "INT"),
+                "m": (rng.integers(0, 100, n).astype(np.int32), "INT")}
+        segs = [c.pin(create_segment(f"e{i}", cols)) for i in range(3)]
+        where = " WHERE m > 1000" if shape == "pruned" else ""
+        sql = f"SELECT g, COUNT(*), SUM(m) FROM t{where} GROUP BY g ORDER BY g LIMIT 100"
+        r = c.execute(parse_sql(sql), segs)
+        assert r.num_groups == 0 and r.stats.num_docs_scanned == 0 and r.stats.device_ms == 0.0
+        r2 = c.execute(parse_sql(sql), segs)  # the same lane again
+        assert r2.num_groups == 0 and r2.stats.device_ms == 0.0
+    finally:
+        c.close()
 
 
 def test_bad_query_is_reported(ctx, sv):
@@ -469,7 +521,7 @@ CONJ_FILTERS = [
 @pytest.mark.parametrize("where", CONJ_FILTERS)
 @pytest.mark.parametrize("group", ["", "a, str", "s", "b"])
 def test_conjunctive_scan_leaves(ctx, where, group):
-    rng = np.random.default_rng((abs(hash(where + group))) % 2**32)
+    rng = np.random.default_rng(seed_of(where + group))
     tables = [_random_table(rng, n) for n in (12_345, 64 * 500 + 3)]
     if group:
         sql = (f"SET numGroupsLimit=10000000; SELECT {group}, COUNT(*), SUM(m), MIN(d), MAX(b) FROM t{where} "
@@ -492,6 +544,6 @@ def test_conjunctive_scan_leaves(ctx, where, group):
     "ORDER BY b, c LIMIT 1000000",
 ])
 def test_group_cache_global_table(ctx, sql):
-    rng = np.random.default_rng(abs(hash(sql)) % 2**32)
+    rng = np.random.default_rng(seed_of(sql))
     tables = [_random_table(rng, n) for n in (40_000, 64 * 700 + 9)]
     _both(ctx, tables, sql, inverted=())

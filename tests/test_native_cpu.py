@@ -140,6 +140,13 @@ def test_sql_parser_shapes():
     assert q.filter.type == "AND" and q.filter.children[1].type == "OR"
 
 
+def test_expression_result_column_names():
+    # AggregationFunction.getResultColumnName over the parser's canonical expression names (CalciteSqlParser.java:798:
+    # SqlKind TIMES / MINUS / PLUS), the names datatable.cpp's agg_column_name writes into the DataTable schema
+    q = parse_sql("SELECT SUM(a * b), SUM(a - b), MAX(a + b), COUNT(*), SUM(a) FROM t")
+    assert q.result_columns() == ["sum(times(a,b))", "sum(minus(a,b))", "max(plus(a,b))", "count(*)", "sum(a)"]
+
+
 def test_segment_group_trim_gate():
     # minSegmentGroupTrimSize > 0 with ORDER BY: the reference trims per segment (an approximation), so the GPU
     # plan declines (UNSUPPORTED -> CPU plan); -1 (the default) and queries without ORDER BY stay on the GPU path

@@ -8,6 +8,7 @@ import pytest
 from pinot_amd import native as N
 from pinot_amd.segment import read_raw_forward_index, write_raw_forward_index
 from tests import raw_codecs as RC
+from tests.seeds import seed_of
 
 TYPES = {"INT": np.int32, "LONG": np.int64, "FLOAT": np.float32, "DOUBLE": np.float64}
 
@@ -27,7 +28,7 @@ def _values(dt, n, seed):
 @pytest.mark.parametrize("comp", ["PASS_THROUGH", "LZ4", "LZ4_LENGTH_PREFIXED", "SNAPPY"])
 @pytest.mark.parametrize("version", [2, 3, 4])
 def test_raw_reader_round_trip(dt, comp, version):
-    v = _values(dt, 4321, hash((dt, comp, version)) & 0xFFFF)
+    v = _values(dt, 4321, seed_of(f"{dt}/{comp}/{version}") & 0xFFFF)
     buf = write_raw_forward_index(v, dt, comp, version)
     got = read_raw_forward_index(buf, dt, len(v))
     ind = RC.read_raw(buf.tobytes(), dt, len(v))
