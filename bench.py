@@ -58,18 +58,32 @@ BUILT = {
     # BASELINE.json configs[0]: the README AdAnalytics query on one 10M-row segment (sorted daysSinceEpoch)
     "config1": ("ads", 1, 10_000_000, 10_000_000,
                 "config1: README AdAnalytics, sorted daysSinceEpoch range + accountId IN, GROUP BY day, one segment"),
-    # BASELINE.json configs[4] on one GPU: DISTINCTCOUNTHLL(u), u at b = 24, WHERE c IN (10 ids) on an inverted
-    # index (~1 % selectivity); 4 distinct 10M-row segments pinned 25 times each (segment build is ~6 s each)
-    "config5": ("hll", 4, 1_000_000_000, 10_000_000,
-                "config5: DISTINCTCOUNTHLL(u) (b=24) WHERE c IN (10 ids) via inverted bitmaps, 1 % selectivity"),
+    # BASELINE.json configs[4] on one GPU: the 4B-row table (400 x 10M-row segments, ~26 GB pinned), DISTINCTCOUNTHLL(u),
+    # u at b = 24, WHERE c IN (10 ids) on an inverted index (~1 % selectivity); 4 distinct 10M-row segments pinned 100
+    # times each (segment build is ~6 s each)
+    "config5": ("hll", 4, 4_000_000_000, 10_000_000,
+                "config5: DISTINCTCOUNTHLL(u) (b=24) WHERE c IN (10 ids) via inverted bitmaps, 1 % selectivity, 4B rows"),
 }
 # BASELINE.json configs[3]: the 13 SSB queries as one flight over a denormalised lineorder table (SF100 = 600M rows,
 # 60 x 10M-row segments: 4 distinct segments built in dictId form by tests/workloads.py, pinned 15 times each)
 FLIGHTS = {"config4": (4, 600_000_000, 10_000_000,
                        "config4: SSB lineorder SF100 flight Q1.1-Q4.3 (13 queries), string dimensions as dictId scans")}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
-KERNEL_NAMES = {0: "k_scan<MODE_COUNT>", 1: "k_scan<MODE_AGG>", 2: "k_scan<MODE_GROUP_LDS>",
-                3: "k_scan<MODE_GROUP_GLOBAL>", 4: "k_scan<MODE_PARTITION> + k_part_agg"}
+MODE_NAMES = {0: "MODE_COUNT", 1: "MODE_AGG", 2: "MODE_GROUP_LDS", 3: "MODE_GROUP_GLOBAL", 4: "MODE_PARTITION",
+              5: "MODE_GROUP_HASH"}
+CPU_NOTE = ("threads = this job's CPU share on the GPU box (OMP_NUM_THREADS; the pool gives one GPU job 16 CPUs and "
+            "asks GPU jobs to size worker pools to it), not the machine's host_cores; value_t1 is the one-thread rate")
+
+
+def kernel_name(mode, scan_kernel):
+    """The scan kernel that ran (ph_exec_stats.scan_kernel), with its plan mode for the generic k_scan."""
+    from pinot_amd.engine import SCAN_KERNEL_NAMES
+    name = SCAN_KERNEL_NAMES.get(scan_kernel, "k_scan")
+    if scan_kernel == 1:
+        name = f"k_scan<{MODE_NAMES.get(mode, mode)}>"
+    if scan_kernel == 3:
+        name += " (+ k_roaring_chunk bitmap build)"
+    return name
 
 
 def log(*a):
@@ -237,6 +251,7 @@ def flight_main(args, world, rank, dist, device):
         result["cpu_baseline"] = {
             "value": len(queries) * n * seg_rows / dt, "unit": "rows/s", "cores": threads, "kind": "port",
             "value_t1": len(queries) * seg_rows / dt1, "host_cores": os.cpu_count(), "cpu_model": cpu_model(),
+            "cores_note": CPU_NOTE,
             "sample": f"the 13 queries over {n} of {nseg} segments x {seg_rows} rows, oracle C restatement on "
                       f"{threads} host threads, {dt:.2f}s; value_t1 = one segment on one thread, {dt1:.2f}s"}
         if not args.no_parity:  # every query of the flight on one segment, bit-exact (SUM of integer expressions)
@@ -395,6 +410,7 @@ def main():
             return scan.device_ms, scan.plan_mode
         r = ctx.execute(q, pinned, copy=False)
         last["res"] = r
+        last["kernel"] = r.stats.scan_kernel
         return r.stats.device_ms, r.stats.mode
 
     for _ in range(args.warmup):
@@ -449,8 +465,10 @@ def main():
                                                                   else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                     "kernel": KERNEL_NAMES.get(mode, "k_scan"), "kernel_ms": kernel_ms,
-                     "algorithmic_bytes_per_launch": alg},
+                     "kernel": kernel_name(mode, last.get("kernel", 1)), "kernel_ms": kernel_ms,
+                     "algorithmic_bytes_per_launch": alg,
+                     # bytes the kernels actually moved (PMC FETCH + WRITE, profiles/) over the same device time
+                     "achieved_traffic_gbs": (traffic / (kernel_ms / 1000.0) / 1e9) if traffic and kernel_ms else None},
     }
     if phases:
         result["phases_ms"] = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
@@ -462,7 +480,7 @@ def main():
         rows = n * seg_rows
         result["cpu_baseline"] = {"value": rows / dt, "unit": "rows/s", "cores": threads, "kind": "port",
                                   "value_t1": seg_rows / dt1, "host_cores": os.cpu_count(),
-                                  "cpu_model": cpu_model(),
+                                  "cpu_model": cpu_model(), "cores_note": CPU_NOTE,
                                   "sample": f"{n} of {nseg} segments x {seg_rows} rows (same data and query), oracle "
                                             f"C restatement of the reference loop nest (one worker per segment, as "
                                             f"GroupByCombineOperator) on {threads} host threads, {dt:.2f}s; "

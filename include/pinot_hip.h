@@ -177,7 +177,21 @@ typedef struct {
   int32_t limit_pass;                      /* numGroupsLimit emulation: 0 no segment could reach the limit, 1 the
                                               untruncated scan's table held < limit keys (no pass needed), 2 the
                                               first-seen pass and the truncating scan ran */
+  int32_t scan_kernel;                     /* the scan's kernel (PH_KERNEL_*): which hand-written form ran */
+  int32_t reserved;
 } ph_exec_stats;
+
+/* ph_exec_stats.scan_kernel */
+enum {
+  PH_KERNEL_NONE = 0,          /* no scan (metadata / index-only answer, or nothing to scan) */
+  PH_KERNEL_SCAN = 1,          /* k_scan<MODE, ...>: the generic persistent scan */
+  PH_KERNEL_AGG_LEAN = 2,      /* k_agg_lean: one packed integer column, aggregation only */
+  PH_KERNEL_AGG_SPARSE = 3,    /* k_agg_sparse: gathers of the docs of selective inverted-index bitmaps */
+  PH_KERNEL_GROUP_LDS_LEAN = 4,/* k_group_lds_lean: LDS-private group tables */
+  PH_KERNEL_PART_LEAN = 5,     /* k_part_scan + k_part_agg: partitioned group-by, one tile of loads in flight */
+  PH_KERNEL_PART_LEAN2 = 6,    /* k_part_scan2 + k_part_agg: partitioned group-by, two tiles of loads in flight */
+  PH_KERNEL_PART_SCAN = 7      /* k_scan<MODE_PARTITION> + k_part_agg: partitioned group-by with gathers */
+};
 
 /* ------------------------------------------------------------------ context */
 int ph_ctx_create(int32_t device_ordinal, ph_ctx** out);
@@ -290,6 +304,13 @@ int ph_dense_finalize(ph_ctx* ctx, const ph_query* query, ph_segment* const* seg
  * (INT int32, LONG int64, FLOAT float, DOUBLE double) at `out`.  Host-only; what ph_segment_pin runs on a raw
  * column. */
 int ph_raw_forward_index_read(const void* buf, uint64_t size, int32_t data_type, int32_t num_docs, void* out);
+
+/* The V3 index_map reader the directory loader uses (SingleFileIndexDirectory.loadMap :213-247, keys split from the
+ * right as ColumnIndexUtils.parseIndexMapKeys :33-45): the startOffset and size (magic included) of `column`'s
+ * `index_id` buffer in columns.psf.  PH_ERR_BAD_QUERY when the map has no such entry; PH_ERR_INVALID_ARGUMENT when the
+ * file is missing or malformed.  Host-only. */
+int ph_index_map_lookup(const char* index_map_path, const char* column, const char* index_id, int64_t* start_offset,
+                        int64_t* size);
 
 /* FixedBitSVForwardIndexWriter: packs n dictIds with `bits` bits, MSB-first big-endian; out_size >=
  * (n*bits+7)/8 */

@@ -365,6 +365,19 @@ int ph_raw_forward_index_read(const void* buf, uint64_t size, int32_t data_type,
   });
 }
 
+int ph_index_map_lookup(const char* index_map_path, const char* column, const char* index_id, int64_t* start_offset,
+                        int64_t* size) {
+  return guarded([&] {
+    if (!index_map_path || !column || !index_id || !start_offset || !size)
+      ph::fail(PH_ERR_INVALID_ARGUMENT, "null argument");
+    const ph::IndexMap m = ph::read_index_map(index_map_path);
+    auto it = m.find({column, index_id});
+    if (it == m.end()) ph::fail(PH_ERR_BAD_QUERY, std::string("index_map has no ") + column + "." + index_id);
+    *start_offset = it->second.first;
+    *size = it->second.second;
+  });
+}
+
 int ph_fixed_bit_pack(const int32_t* dict_ids, int64_t n, int32_t bits, uint8_t* out, uint64_t out_size) {
   return guarded([&] {
     if (n < 0 || bits < 1 || bits > 31 || (n > 0 && (!dict_ids || !out)))

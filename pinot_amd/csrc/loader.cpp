@@ -37,7 +37,7 @@ std::map<std::string, std::string> read_properties(const std::string& path) {
   if (!in) fail(PH_ERR_INVALID_ARGUMENT, "cannot open " + path);
   std::map<std::string, std::string> kv;
   std::string line;
-  auto unescape = [](const std::string& s) {
+  auto unescape = [&path](const std::string& s) {
     std::string o;
     for (size_t i = 0; i < s.size(); ++i) {
       if (s[i] == '\\' && i + 1 < s.size()) {
@@ -45,7 +45,16 @@ std::map<std::string, std::string> read_properties(const std::string& path) {
         if (c == 't') o += '\t';
         else if (c == 'n') o += '\n';
         else if (c == 'u' && i + 4 < s.size()) {
-          const unsigned v = (unsigned)std::stoul(s.substr(i + 1, 4), nullptr, 16);
+          unsigned v = 0;
+          bool hex = true;
+          for (size_t k = i + 1; k <= i + 4; ++k) {
+            const char h = s[k];
+            const int d = (h >= '0' && h <= '9') ? h - '0' : (h >= 'a' && h <= 'f') ? h - 'a' + 10
+                          : (h >= 'A' && h <= 'F') ? h - 'A' + 10 : -1;
+            if (d < 0) hex = false;
+            v = (v << 4) | (unsigned)(d < 0 ? 0 : d);
+          }
+          if (!hex) fail(PH_ERR_INVALID_ARGUMENT, "malformed \\uxxxx escape in " + path);
           i += 4;
           if (v < 0x80) o += (char)v;
           else o += '?';
@@ -78,6 +87,19 @@ std::map<std::string, std::string> read_properties(const std::string& path) {
     kv[unescape(trim(t.substr(0, sep)))] = unescape(trim(t.substr(sep + 1)));
   }
   return kv;
+}
+
+// a whole decimal integer in [lo, hi] (metadata / index_map values are untrusted bytes)
+int64_t to_i64(const std::string& s, const std::string& what, int64_t lo = INT64_MIN, int64_t hi = INT64_MAX) {
+  size_t used = 0;
+  long long v = 0;
+  try {
+    v = std::stoll(s, &used);
+  } catch (...) {
+    used = 0;
+  }
+  if (used == 0 || used != s.size() || v < lo || v > hi) fail(PH_ERR_INVALID_ARGUMENT, "bad " + what + ": '" + s + "'");
+  return (int64_t)v;
 }
 
 struct Mapped {
@@ -118,6 +140,31 @@ bool file_exists(const std::string& p) {
   return stat(p.c_str(), &st) == 0;
 }
 
+}  // namespace
+
+// index_map of a V3 segment (SingleFileIndexDirectory.loadMap :213-247): `<col>.<indexId>.startOffset|size`
+// properties; the key is split from the right because a column name may contain dots
+// (ColumnIndexUtils.parseIndexMapKeys :33-45, whose Preconditions reject a key without both separators)
+IndexMap read_index_map(const std::string& path) {
+  IndexMap imap;
+  auto im = read_properties(path);
+  for (auto& kv : im) {
+    const std::string& k = kv.first;
+    const size_t a = k.rfind('.');
+    if (a == std::string::npos) fail(PH_ERR_INVALID_ARGUMENT, "index_map: key separator not found: " + k);
+    const size_t b = a == 0 ? std::string::npos : k.rfind('.', a - 1);
+    if (b == std::string::npos) fail(PH_ERR_INVALID_ARGUMENT, "index_map: index separator not found: " + k);
+    const std::string col = k.substr(0, b), idx = k.substr(b + 1, a - b - 1), what = k.substr(a + 1);
+    auto& e = imap[{col, idx}];
+    const int64_t v = to_i64(kv.second, "index_map value of " + k);
+    if (what == "startOffset") e.first = v;
+    else if (what == "size") e.second = v;
+  }
+  return imap;
+}
+
+namespace {
+
 int32_t data_type_of(const std::string& t, const std::string& col) {
   // stored types (FieldSpec.DataType.getStoredType): BOOLEAN -> INT, TIMESTAMP -> LONG
   if (t == "INT" || t == "BOOLEAN") return PH_INT;
@@ -143,8 +190,7 @@ ph_segment* segment_load_dir_impl(Context* ctx, const char* dir_c, const char* c
   const std::string* docs_s = get("segment.total.docs");
   if (!docs_s) fail(PH_ERR_INVALID_ARGUMENT, "metadata.properties without segment.total.docs");
   const std::string seg_name = get("segment.name") ? *get("segment.name") : dir;
-  const int64_t num_docs = std::stoll(*docs_s);
-  if (num_docs < 0 || num_docs > INT32_MAX) fail(PH_ERR_INVALID_ARGUMENT, "segment.total.docs out of range");
+  const int64_t num_docs = to_i64(*docs_s, "segment.total.docs", 0, INT32_MAX);
   // only zero padding loads (ColumnMetadataImpl.java:297-300: unescapeJava(segment.padding.character) must be
   // "\0"; a missing key -- pre-2016 '%'-padded segments -- fails the load)
   {
@@ -176,21 +222,10 @@ ph_segment* segment_load_dir_impl(Context* ctx, const char* dir_c, const char* c
   }
 
   // index_map (V3): <col>.<indexId>.<startOffset|size>, split from the right
-  std::map<std::pair<std::string, std::string>, std::pair<int64_t, int64_t>> imap;  // (col, index) -> (start, size)
+  IndexMap imap;  // (col, index) -> (start, size)
   std::unique_ptr<Mapped> psf;
   if (v3) {
-    auto im = read_properties(dir + "/index_map");
-    for (auto& kv : im) {
-      const std::string& k = kv.first;
-      const size_t a = k.rfind('.');
-      if (a == std::string::npos || a == 0) continue;
-      const size_t b = k.rfind('.', a - 1);
-      if (b == std::string::npos) continue;
-      const std::string col = k.substr(0, b), idx = k.substr(b + 1, a - b - 1), what = k.substr(a + 1);
-      auto& e = imap[{col, idx}];
-      if (what == "startOffset") e.first = std::stoll(kv.second);
-      else if (what == "size") e.second = std::stoll(kv.second);
-    }
+    imap = read_index_map(dir + "/index_map");
     psf = map_file(dir + "/columns.psf", true);
   }
   std::vector<std::unique_ptr<Mapped>> v1files;
@@ -199,7 +234,7 @@ ph_segment* segment_load_dir_impl(Context* ctx, const char* dir_c, const char* c
     auto it = imap.find({col, idx});
     if (it == imap.end()) return false;
     const int64_t start = it->second.first, sz = it->second.second;
-    if (start < 0 || sz < 8 || (uint64_t)(start + sz) > psf->n)
+    if (start < 0 || sz < 8 || (uint64_t)start > psf->n || (uint64_t)sz > psf->n - (uint64_t)start)
       fail(PH_ERR_INVALID_ARGUMENT, "index_map entry out of columns.psf: " + col + "." + idx);
     const uint8_t* base = static_cast<const uint8_t*>(psf->p) + start;
     uint64_t magic = 0;
@@ -246,12 +281,16 @@ ph_segment* segment_load_dir_impl(Context* ctx, const char* dir_c, const char* c
       descs.push_back(d);
       continue;
     }
-    d.cardinality = (int32_t)std::stol(*prop("cardinality"));
-    d.bits_per_element = prop("bitsPerElement") ? (int32_t)std::stol(*prop("bitsPerElement")) : 0;
+    auto iprop = [&](const char* p, int64_t lo, int64_t hi) -> int32_t {
+      const std::string* v = prop(p);
+      if (!v) fail(PH_ERR_INVALID_ARGUMENT, "column " + c + " without " + p);
+      return (int32_t)to_i64(*v, "column." + c + "." + p, lo, hi);
+    };
+    d.cardinality = iprop("cardinality", 0, INT32_MAX);
+    d.bits_per_element = prop("bitsPerElement") ? iprop("bitsPerElement", 0, 32) : 0;
     d.is_sorted = prop("isSorted") && *prop("isSorted") == "true";
-    d.dictionary_entry_size = d.data_type == PH_STRING
-                                  ? (int32_t)std::stol(*prop("lengthOfEachEntry"))
-                                  : ((d.data_type == PH_LONG || d.data_type == PH_DOUBLE) ? 8 : 4);
+    d.dictionary_entry_size = d.data_type == PH_STRING ? iprop("lengthOfEachEntry", 0, INT32_MAX)
+                                                       : ((d.data_type == PH_LONG || d.data_type == PH_DOUBLE) ? 8 : 4);
     bool ok_fwd, ok_dict;
     if (v3) {
       ok_fwd = v3_buffer(c, "forward_index", &d.forward_index, &d.forward_index_size);

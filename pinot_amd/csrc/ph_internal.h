@@ -550,6 +550,9 @@ void launch_fill_i64(int64_t* p, int64_t v, int64_t n, hipStream_t s);
 void launch_hll_table(const void* values, int32_t is_int, int64_t n, int log2m, uint32_t* out, hipStream_t s);
 
 void build_bitmap_directory(Column& c);  // at pin, from c.inverted
+// (column, index id) -> (startOffset, size) of a V3 index_map file (loader.cpp)
+typedef std::map<std::pair<std::string, std::string>, std::pair<int64_t, int64_t>> IndexMap;
+IndexMap read_index_map(const std::string& path);
 ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc);
 ph_segment* segment_load_dir_impl(Context* ctx, const char* dir, const char* const* columns, int32_t num_columns);
 // every container of every (leaf, dictId) work item of a query in one launch (one wave per container)

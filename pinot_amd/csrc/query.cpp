@@ -431,72 +431,6 @@ void emit(const PNode& n, SegProgram& p) {
   p.max_depth = std::max(p.max_depth, p.depth);
 }
 
-// ------------------------------------------------------------------ roaring container directory
-struct RoaringView {
-  std::vector<RoaringContainer> containers;
-};
-
-uint32_t le32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
-uint16_t le16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
-uint32_t be32u(const uint8_t* p) { return ((uint32_t)p[0] << 24) | (p[1] << 16) | (p[2] << 8) | p[3]; }
-
-// Parse one portable-format RoaringBitmap (RoaringFormatSpec; RoaringBitmap 0.9.38 serialize()).
-void parse_roaring(const uint8_t* blob, uint64_t len, uint64_t blob_offset, std::vector<RoaringContainer>& out) {
-  if (len < 4) fail(PH_ERR_INVALID_ARGUMENT, "inverted index: truncated bitmap");
-  const uint32_t cookie = le32(blob);
-  uint64_t pos = 4;
-  uint32_t size;
-  const uint8_t* run_flags = nullptr;
-  bool has_offsets;
-  if ((cookie & 0xFFFF) == 12347) {  // SERIAL_COOKIE: run containers present
-    size = (cookie >> 16) + 1;
-    run_flags = blob + pos;
-    pos += (size + 7) / 8;
-    has_offsets = size >= 4;  // NO_OFFSET_THRESHOLD
-  } else if (cookie == 12346) {  // SERIAL_COOKIE_NO_RUNCONTAINER
-    size = le32(blob + pos);
-    pos += 4;
-    has_offsets = true;
-  } else {
-    fail(PH_ERR_INVALID_ARGUMENT, "inverted index: bad roaring cookie");
-  }
-  const uint8_t* desc = blob + pos;
-  pos += 4ull * size;
-  const uint8_t* offs = nullptr;
-  if (has_offsets) {
-    offs = blob + pos;
-    pos += 4ull * size;
-  }
-  if (pos > len) fail(PH_ERR_INVALID_ARGUMENT, "inverted index: truncated roaring header");
-  uint64_t cur = pos;
-  for (uint32_t i = 0; i < size; ++i) {
-    RoaringContainer c{};
-    c.key = le16(desc + 4 * i);
-    const uint32_t card = (uint32_t)le16(desc + 4 * i + 2) + 1;
-    const bool is_run = run_flags && ((run_flags[i / 8] >> (i % 8)) & 1);
-    uint64_t at = has_offsets ? le32(offs + 4 * i) : cur;
-    uint64_t bytes;
-    if (is_run) {
-      c.type = 2;
-      if (at + 2 > len) fail(PH_ERR_INVALID_ARGUMENT, "inverted index: truncated run container");
-      c.card = le16(blob + at);
-      bytes = 2 + 4ull * c.card;
-    } else if (card <= 4096) {
-      c.type = 0;
-      c.card = (int32_t)card;
-      bytes = 2ull * card;
-    } else {
-      c.type = 1;
-      c.card = (int32_t)card;
-      bytes = 8192;
-    }
-    if (at + bytes > len) fail(PH_ERR_INVALID_ARGUMENT, "inverted index: truncated container");
-    c.offset = blob_offset + at;
-    cur = at + bytes;
-    out.push_back(c);
-  }
-}
-
 // docs of the dictIds' bitmaps: a single-value column's bitmaps are disjoint, so the OR's cardinality is the sum
 // (InvertedIndexFilterOperator.getNumMatchingDocs :101-127)
 int64_t bitmap_docs(const Column& c, const std::vector<int32_t>& ids) {
@@ -506,35 +440,6 @@ int64_t bitmap_docs(const Column& c, const std::vector<int32_t>& ids) {
 }
 
 }  // namespace
-
-void build_bitmap_directory(Column& c) {
-  // BitmapInvertedIndexReader.getDocIds: offsets are uint32 BE; normalise by the first offset
-  // (absolute or relative formats, BitmapInvertedIndexReader.java:40-61)
-  const uint8_t* b = c.inverted.data();
-  const uint64_t off_end = 4ull * (c.cardinality + 1);
-  const uint64_t first = be32u(b);
-  c.dir.clear();
-  c.dir_begin.assign(1, 0);
-  c.id_docs.assign(c.cardinality, 0);
-  for (int32_t id = 0; id < c.cardinality; ++id) {
-    uint64_t s = be32u(b + 4ull * id) - first, e = be32u(b + 4ull * (id + 1)) - first;
-    if (off_end + e > c.inverted.size() || e < s) fail(PH_ERR_INVALID_ARGUMENT, "inverted index: bad offsets");
-    const size_t k0 = c.dir.size();
-    parse_roaring(b + off_end + s, e - s, off_end + s, c.dir);
-    int64_t docs = 0;
-    for (size_t k = k0; k < c.dir.size(); ++k) {
-      const RoaringContainer& rc = c.dir[k];
-      if (rc.type != 2) {
-        docs += rc.card;
-      } else {  // run container: (start, length - 1) pairs after the run count
-        const uint8_t* r = b + rc.offset + 2;
-        for (int32_t j = 0; j < rc.card; ++j) docs += (int64_t)le16(r + 4 * j + 2) + 1;
-      }
-    }
-    c.id_docs[id] = docs;
-    c.dir_begin.push_back((int64_t)c.dir.size());
-  }
-}
 
 namespace {
 
@@ -1804,6 +1709,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       int blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1)));
       if (mode == MODE_GROUP_LDS) blocks_per_cu = std::min(blocks_per_cu, 4);
       const int grid = (int)std::min<int64_t>((int64_t)chunks.size(), (int64_t)ctx->num_cus * blocks_per_cu);
+      stats.scan_kernel = kp.agg_sparse ? PH_KERNEL_AGG_SPARSE
+                          : kp.agg_fast  ? PH_KERNEL_AGG_LEAN
+                          : kp.lds_fast  ? PH_KERNEL_GROUP_LDS_LEAN
+                                         : PH_KERNEL_SCAN;
       // device_ms opens here: it covers the numGroupsLimit pass and (below) the bitmap build too
       PH_HIP_CHECK(hipEventRecord(lane.lane->ev_start, st));
       // an interruptible call scans in batches of kInterruptChunks chunks and checks between them
@@ -1910,6 +1819,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       kp.part_dbg = getenv("PH_PART_DBG") ? atoi(getenv("PH_PART_DBG")) : 0;  // timing experiments only
       kp.part_depth = 1;
       if (const char* e = getenv("PH_PART_DEPTH")) kp.part_depth = atoi(e) == 2 ? 2 : 1;  // tuning knob
+      stats.scan_kernel = !kp.part_fast ? PH_KERNEL_PART_SCAN
+                          : kp.part_depth == 2 ? PH_KERNEL_PART_LEAN2 : PH_KERNEL_PART_LEAN;
       kp.part_vbits = vbits;
       kp.num_parts = (int32_t)P;
       const size_t lds_a = partition_lds_bytes(kp);

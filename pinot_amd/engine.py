@@ -42,6 +42,12 @@ class ExecutionStats:
     host_ms: float
     mode: int = 0
     limit_pass: int = 0  # numGroupsLimit: 0 not needed, 1 optimistic scan sufficed, 2 first-seen pass + rescan
+    scan_kernel: int = 0  # PH_KERNEL_*: the scan's kernel form (SCAN_KERNEL_NAMES)
+
+
+SCAN_KERNEL_NAMES = {0: "none", 1: "k_scan", 2: "k_agg_lean", 3: "k_agg_sparse", 4: "k_group_lds_lean",
+                     5: "k_part_scan + k_part_agg", 6: "k_part_scan2 + k_part_agg",
+                     7: "k_scan<MODE_PARTITION> + k_part_agg"}
 
 
 @dataclass
@@ -313,7 +319,7 @@ class GpuContext:
                                st.num_entries_scanned_post_filter, st.num_total_docs, st.num_segments_processed,
                                st.num_segments_matched, bool(st.num_groups_limit_reached),
                                bool(st.sum_precision_flag), st.device_ms, st.host_ms, st.plan_mode,
-                               st.limit_pass)
+                               st.limit_pass, st.scan_kernel)
         return IntermediateResult(key_cols, agg_cols, n, [a.function for a in q.aggregations], stats)
 
     # ---------------------------------------------------------------- dense partials (multi-GPU combine)

@@ -111,7 +111,8 @@ class ExecStats(ctypes.Structure):
                 ("num_segments_processed", ctypes.c_int64), ("num_segments_matched", ctypes.c_int64),
                 ("num_groups_limit_reached", ctypes.c_int32), ("sum_precision_flag", ctypes.c_int32),
                 ("device_ms", ctypes.c_double), ("host_ms", ctypes.c_double), ("plan_mode", ctypes.c_int32),
-                ("limit_pass", ctypes.c_int32)]
+                ("limit_pass", ctypes.c_int32),
+                ("scan_kernel", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 # every symbol declared in include/pinot_hip.h
@@ -121,7 +122,7 @@ EXPORTED_SYMBOLS = (
     "ph_result_destroy", "ph_result_stats", "ph_result_num_groups", "ph_result_key_entry_size", "ph_result_key_type",
     "ph_result_group_keys", "ph_result_aggregation", "ph_result_key_data", "ph_result_aggregation_data",
     "ph_query_dense_layout", "ph_query_execute_dense", "ph_dense_finalize", "ph_fixed_bit_pack",
-    "ph_raw_forward_index_read", "ph_result_datatable", "ph_selftest_unpack",
+    "ph_raw_forward_index_read", "ph_index_map_lookup", "ph_result_datatable", "ph_selftest_unpack",
     "ph_selftest_unpack_staged", "ph_last_error", "ph_version",
 )
 
@@ -185,6 +186,8 @@ def lib():
                                ctypes.POINTER(vp)], ctypes.c_int),
         "ph_fixed_bit_pack": ([vp, i64, i32, vp, ctypes.c_uint64], ctypes.c_int),
         "ph_raw_forward_index_read": ([vp, ctypes.c_uint64, i32, i32, vp], ctypes.c_int),
+        "ph_index_map_lookup": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(i64),
+                                 ctypes.POINTER(i64)], ctypes.c_int),
         "ph_result_datatable": ([vp, ctypes.POINTER(Query), ctypes.POINTER(MetadataEntry), i32, vp, ctypes.c_uint64,
                                  ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
         "ph_selftest_unpack": ([vp, vp, ctypes.c_uint64, i64, i32, vp], ctypes.c_int),

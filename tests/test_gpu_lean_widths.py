@@ -1,0 +1,94 @@
+"""GPU: the lean kernels' own decode (LaneStream / lds_value, scan_kernel.h) swept over every stream width 1..31
+against the oracle, each query asserting which kernel ran (ph_exec_stats.scan_kernel):
+
+  k_agg_lean          aggregation only, one packed integer column (value streams of 1..26 bits)
+  k_group_lds_lean    LDS-private group table (value streams of 1..31 bits)
+  k_part_scan(2)      partitioned group-by, 90 000 keys (value streams of 1..31 bits; 32- and 64-bit records)
+
+The aggregated column's frame-of-reference stream is `w` bits wide (values base + [0, 2^w - 1], both extremes
+present) and the filter column's dictId stream min(w, 24) bits wide (a dictionary of 2^(b-1) + 1 values of which
+the rows reference a subset), so both the value and the filter decode of every lean kernel see width w.  Segment
+lengths are not multiples of a tile.  Bar: bit-exact (COUNT, integer SUM, MIN, MAX, keys)."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from pinot_amd.engine import SCAN_KERNEL_NAMES
+from pinot_amd.query import parse_sql
+from pinot_amd.reduce import reduce_groups
+from pinot_amd.segment import SegmentBuffers, create_column, create_column_from_dict_ids
+from tests.seeds import seed_of
+
+pytestmark = pytest.mark.gpu
+
+PH_KERNEL_AGG_LEAN, PH_KERNEL_GROUP_LDS_LEAN, PH_KERNEL_PART_LEAN, PH_KERNEL_PART_LEAN2 = 2, 4, 5, 6
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from pinot_amd.engine import GpuContext
+    c = GpuContext(0)
+    yield c
+    c.close()
+
+
+def _tables(w):
+    rng = np.random.default_rng(seed_of(f"lean-width-{w}"))
+    bf = min(w, 24)
+    fcard = (1 << (bf - 1)) + 1 if bf > 1 else 2
+    out = []
+    for n in (70_001, 33_333):
+        off = rng.integers(0, 1 << w, n, dtype=np.int64)
+        off[:2] = [0, (1 << w) - 1]  # FOR width exactly w
+        m = (off - (1 << 30)).astype(np.int64)  # negative and positive values
+        fid = rng.integers(0, fcard, n).astype(np.int32)
+        fid[:2] = [0, fcard - 1]
+        out.append({"m": m, "fid": fid, "fcard": fcard,
+                    "g": rng.integers(0, 37, n).astype(np.int32),
+                    "g1": rng.integers(0, 300, n).astype(np.int32), "g2": rng.integers(0, 300, n).astype(np.int32)})
+    return out
+
+
+def _segments(ctx, w):
+    gpu, ora = [], []
+    for i, t in enumerate(_tables(w)):
+        n = len(t["m"])
+        seg = SegmentBuffers(f"lw{w}_{i}", n)
+        seg.columns["m"] = create_column("m", t["m"], "LONG")
+        fdict = np.arange(t["fcard"], dtype=np.int32)
+        seg.columns["f"] = create_column_from_dict_ids("f", fdict, t["fid"], "INT", allow_sorted=False)
+        for c in ("g", "g1", "g2"):
+            t[c][:300 if c != "g" else 37] = np.arange(300 if c != "g" else 37)  # complete dictionaries
+            seg.columns[c] = create_column(c, t[c], "INT")
+        gpu.append(ctx.pin(seg))
+        ora.append(O.build_segment(seg.name, {"m": (t["m"], "LONG"), "f": (fdict[t["fid"]], "INT"),
+                                              "g": (t["g"], "INT"), "g1": (t["g1"], "INT"),
+                                              "g2": (t["g2"], "INT")}))
+    return gpu, ora, _tables(w)[0]["fcard"]
+
+
+def _check(ctx, gpu, ora, sql, kernel):
+    q = parse_sql(sql)
+    r = ctx.execute(q, gpu)
+    e = O.execute(q, ora)
+    assert reduce_groups(q, r.keys, r.aggs).rows == reduce_groups(q, e.keys, e.aggs).rows, sql
+    assert r.stats.num_docs_scanned == e.stats.num_docs_scanned
+    assert r.stats.scan_kernel == kernel, (sql, SCAN_KERNEL_NAMES.get(r.stats.scan_kernel))
+
+
+@pytest.mark.parametrize("w", list(range(1, 32)))
+def test_lean_kernels_every_width(ctx, w, monkeypatch):
+    gpu, ora, fcard = _segments(ctx, w)
+    where = f" WHERE f BETWEEN {fcard // 5} AND {fcard - 1 - fcard // 7}" if fcard > 2 else " WHERE f = 1"
+    # k_agg_lean: 32-bit tile sums need value offsets below 2^26; wider streams run k_scan<MODE_AGG>
+    _check(ctx, gpu, ora, f"SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where}",
+           PH_KERNEL_AGG_LEAN if w <= 26 else 1)
+    _check(ctx, gpu, ora, f"SELECT g, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where} GROUP BY g ORDER BY g LIMIT 100",
+           PH_KERNEL_GROUP_LDS_LEAN)
+    part = (f"SET numGroupsLimit=2000000; SELECT g1, g2, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where} "
+            f"GROUP BY g1, g2 ORDER BY g1, g2 LIMIT 200000")
+    _check(ctx, gpu, ora, part, PH_KERNEL_PART_LEAN)
+    monkeypatch.setenv("PH_PART_DEPTH", "2")
+    _check(ctx, gpu, ora, part, PH_KERNEL_PART_LEAN2)
+    for s in gpu:
+        s.unpin()

@@ -45,3 +45,52 @@ def test_v3_and_v1_round_trip(tmp_path):
         seg, _ = SD.read_dir(str(tmp_path / d))
         e = O.execute(q, [seg])
         assert reduce_groups(q, e.keys, e.aggs).rows == exp_rows, d
+
+
+# ------------------------------------------------------------------ index_map pinned by the reference's own file
+REF_INDEX_MAP = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "startree_segment", "index_map")
+
+
+def _expected_index_map(path):
+    """ColumnIndexUtils.parseIndexMapKeys restated (split from the right) over java.util.Properties lines."""
+    out = {}
+    for line in open(path, encoding="utf-8"):
+        t = line.strip()
+        if not t or t[0] in "#!":
+            continue
+        k, v = [x.strip() for x in t.split("=", 1)]
+        a = k.rindex(".")
+        b = k.rindex(".", 0, a)
+        e = out.setdefault((k[:b], k[b + 1:a]), [0, 0])
+        e[0 if k[a + 1:] == "startOffset" else 1] = int(v)
+    return out
+
+
+def _lookup(path, col, idx):
+    import ctypes
+    from pinot_amd import native as N
+    start, size = ctypes.c_int64(-1), ctypes.c_int64(-1)
+    rc = N.lib().ph_index_map_lookup(path.encode(), col.encode(), idx.encode(), ctypes.byref(start), ctypes.byref(size))
+    return rc, start.value, size.value
+
+
+def test_index_map_reference_file():
+    # pinot-segment-local/src/test/resources/data/startree/segment/index_map (a reference-written V3 index_map,
+    # committed as tests/golden/startree_segment/index_map): every (column, index) entry the loader resolves
+    exp = _expected_index_map(REF_INDEX_MAP)
+    assert len(exp) == 172 and ("$ts$DAY", "range_index") in exp
+    for (col, idx), (start, size) in exp.items():
+        assert _lookup(REF_INDEX_MAP, col, idx) == (0, start, size), (col, idx)
+    assert _lookup(REF_INDEX_MAP, "$ts$DAY", "inverted_index")[0] == 2  # PH_ERR_BAD_QUERY: no such entry
+
+
+def test_index_map_dotted_column_and_malformed_keys(tmp_path):
+    p = tmp_path / "index_map"
+    p.write_text("# comment\ncol.with.dots.dictionary.startOffset = 8\ncol.with.dots.dictionary.size : 24\n"
+                 "plain.forward_index.startOffset=32\nplain.forward_index.size=100\n")
+    assert _lookup(str(p), "col.with.dots", "dictionary") == (0, 8, 24)
+    assert _lookup(str(p), "plain", "forward_index") == (0, 32, 100)
+    for bad in ("nodots = 3\n", "one.dot = 3\n", "c.i.startOffset = 12x\n"):
+        p.write_text(bad)
+        assert _lookup(str(p), "c", "i")[0] == 1  # PH_ERR_INVALID_ARGUMENT (Preconditions.checkState / bad number)
+    assert _lookup(str(tmp_path / "missing"), "c", "i")[0] == 1
