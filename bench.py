@@ -242,7 +242,9 @@ def flight_main(args, world, rank, dist, device):
         t1 = time.perf_counter()
         exp = [O.execute(q, osegs, 1) for q in queries]  # one segment, one thread, every query
         dt1 = time.perf_counter() - t1
-        n = int(max(1, min(len(bufs), args.cpu_seconds / max(dt1, 1e-3) * threads)))
+        # one segment per thread (the oracle's flight does not scale past one wave of segments: r3 measured 77 s
+        # for 39 segments on 16 threads against 2.0 s for one segment on one)
+        n = int(max(1, min(len(bufs), threads)))
         sample = oracle_segments(bufs[:n])
         t2 = time.perf_counter()
         for q in queries:
@@ -293,9 +295,12 @@ def cpu_baseline(bufs, q, threads, target_s=10.0, makers=None):
     from oracle import oracle as O
 
     def osegs(k):  # oracle segments of the first k (sorted columns / inverted indexes: from the values)
-        if makers:
+        if makers:  # one oracle segment per distinct maker (setdefault would build every one eagerly)
             built = {}
-            return [built.setdefault(id(mk), mk()) for mk in makers[:k]]
+            for mk in makers[:k]:
+                if id(mk) not in built:
+                    built[id(mk)] = mk()
+            return [built[id(mk)] for mk in makers[:k]]
         return oracle_segments(bufs[:k])
     dt1, _, _ = O.execute_timed(q, osegs(1), 1)  # one segment on one thread
     waves = max(1, int(target_s / max(dt1, 1e-3)))  # segments per thread in ~target_s
@@ -413,11 +418,13 @@ def main():
         last["kernel"] = r.stats.scan_kernel
         return r.stats.device_ms, r.stats.mode
 
+    log(f"[rank {rank}] pinned {len(pinned)} segments ({time.time() - t0:.1f}s); warmup")
     for _ in range(args.warmup):
         step()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    log(f"[rank {rank}] timing {args.steps} steps")
     dev_ms, phases = [], []
     mode = -1
     ts = time.perf_counter()
@@ -476,6 +483,7 @@ def main():
         result["groups"] = last["res"].num_groups
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = host_threads()
+        log(f"[rank {rank}] {ms_per_step:.3f} ms/step; CPU baseline on {threads} threads")
         n, dt, dt1, keys, aggs = cpu_baseline(bufs, q, threads, args.cpu_seconds, ora_makers or None)
         rows = n * seg_rows
         result["cpu_baseline"] = {"value": rows / dt, "unit": "rows/s", "cores": threads, "kind": "port",
@@ -492,7 +500,10 @@ def main():
             from pinot_amd.reduce import reduce_groups
             r = ctx.execute(q, pinned[:n])
             built_o = {}
-            e = O.execute(q, [built_o.setdefault(id(mk), mk()) for mk in ora_makers[:n]])
+            for mk in ora_makers[:n]:
+                if id(mk) not in built_o:
+                    built_o[id(mk)] = mk()
+            e = O.execute(q, [built_o[id(mk)] for mk in ora_makers[:n]])
             ok = reduce_groups(q, r.keys, r.aggs).rows == reduce_groups(q, e.keys, e.aggs).rows
             for k, a in enumerate(q.aggregations):
                 if a.function == "DISTINCTCOUNTHLL":

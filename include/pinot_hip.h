@@ -91,6 +91,15 @@ typedef struct {
    * ForwardIndexReaderFactory.createRawIndexReader (:75-82) reads it; cardinality, bits_per_element and the
    * dictionary are then ignored (the pin decodes the values once and dictionary-encodes them in HBM) */
   int32_t raw_forward_index;
+  /* optional range index (BitSlicedRangeIndexCreator.java:38-131: int32 BE version 2, int64 BE min, then the serialized
+   * RoaringBitmap RangeBitmap; V1 file <column>.bitmap.range, V3 index_map key range_index); NULL when the column has
+   * none.  A version-2 (exact) index makes RANGE, and EQ on a column without an inverted index, a
+   * RangeIndexBasedFilterOperator leaf (FilterOperatorUtils.java:97-120): index-based for the AND order and the
+   * statistics (no entries scanned in filter).  The kernels evaluate such a leaf from the packed dictIds -- the same
+   * doc set as the exact bit-sliced bitmaps, at b bits per doc, which is what reading every bit slice costs too --
+   * so the slices themselves are not read. */
+  const void* range_index;
+  uint64_t range_index_size;
 } ph_column_desc;
 
 typedef struct {
@@ -190,7 +199,8 @@ enum {
   PH_KERNEL_GROUP_LDS_LEAN = 4,/* k_group_lds_lean: LDS-private group tables */
   PH_KERNEL_PART_LEAN = 5,     /* k_part_scan + k_part_agg: partitioned group-by, one tile of loads in flight */
   PH_KERNEL_PART_LEAN2 = 6,    /* k_part_scan2 + k_part_agg: partitioned group-by, two tiles of loads in flight */
-  PH_KERNEL_PART_SCAN = 7      /* k_scan<MODE_PARTITION> + k_part_agg: partitioned group-by with gathers */
+  PH_KERNEL_PART_SCAN = 7,     /* k_scan<MODE_PARTITION> + k_part_agg: partitioned group-by with gathers */
+  PH_KERNEL_PART_REG = 8       /* k_part_reg + k_part_agg: partitioned group-by, register-direct decode */
 };
 
 /* ------------------------------------------------------------------ context */

@@ -162,6 +162,7 @@ class OracleColumn:
     bits: int
     is_sorted: bool
     has_inverted: bool = False
+    has_range_index: bool = False  # an exact bit-sliced range index (rangeIndexColumns)
     fwd: Optional[np.ndarray] = None      # packed big-endian fixed-bit bytes (unsorted)
     sorted_ranges: Optional[np.ndarray] = None  # int32 [card, 2]
 
@@ -201,12 +202,14 @@ def build_column(name: str, values: np.ndarray, data_type: str, inverted: bool =
     return col
 
 
-def build_segment(name: str, columns: Dict[str, tuple], inverted: Sequence[str] = ()) -> OracleSegment:
+def build_segment(name: str, columns: Dict[str, tuple], inverted: Sequence[str] = (),
+                  range_index: Sequence[str] = ()) -> OracleSegment:
     """columns: name -> (values, data_type)"""
     n = None
     seg = OracleSegment(name, 0)
     for c, (vals, dt) in columns.items():
         col = build_column(c, vals, dt, c in inverted)
+        col.has_range_index = c in range_index
         seg.columns[c] = col
         n = len(vals) if n is None else n
         assert n == len(vals)
@@ -315,9 +318,13 @@ def _plan_filter(f, seg: OracleSegment, col_index: Dict[str, int]):
         if always_true:
             return _Leaf("all")
         # FilterOperatorUtils.DefaultImplementation.getLeafFilterOperator
+        # (FilterOperatorUtils.java:97-120): RANGE -> sorted, else range index, else scan; others -> sorted, else
+        # inverted, else an exact range index for EQ (RangeIndexBasedFilterOperator.canEvaluate :56-61), else scan
         if col.is_sorted:
             is_scan = False
         elif p.TYPE != "RANGE" and col.has_inverted:
+            is_scan = False
+        elif col.has_range_index and p.TYPE in ("RANGE", "EQ"):
             is_scan = False
         else:
             is_scan = True

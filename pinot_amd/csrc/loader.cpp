@@ -278,6 +278,8 @@ ph_segment* segment_load_dir_impl(Context* ctx, const char* dir_c, const char* c
       const bool ok = v3 ? v3_buffer(c, "forward_index", &d.forward_index, &d.forward_index_size)
                          : v1_buffer(c + ".sv.raw.fwd", false, &d.forward_index, &d.forward_index_size);
       if (!ok) fail(PH_ERR_INVALID_ARGUMENT, "column " + c + ": raw forward index missing");
+      if (v3) v3_buffer(c, "range_index", &d.range_index, &d.range_index_size);
+      else v1_buffer(c + ".bitmap.range", false, &d.range_index, &d.range_index_size);
       descs.push_back(d);
       continue;
     }
@@ -296,11 +298,13 @@ ph_segment* segment_load_dir_impl(Context* ctx, const char* dir_c, const char* c
       ok_fwd = v3_buffer(c, "forward_index", &d.forward_index, &d.forward_index_size);
       ok_dict = v3_buffer(c, "dictionary", &d.dictionary, &d.dictionary_size);
       v3_buffer(c, "inverted_index", &d.inverted_index, &d.inverted_index_size);
+      v3_buffer(c, "range_index", &d.range_index, &d.range_index_size);  // StandardIndexes.RANGE_ID
     } else {
       ok_fwd = v1_buffer(c + (d.is_sorted ? ".sv.sorted.fwd" : ".sv.unsorted.fwd"), false, &d.forward_index,
                          &d.forward_index_size);
       ok_dict = v1_buffer(c + ".dict", false, &d.dictionary, &d.dictionary_size);
       v1_buffer(c + ".bitmap.inv", false, &d.inverted_index, &d.inverted_index_size);
+      v1_buffer(c + ".bitmap.range", false, &d.range_index, &d.range_index_size);  // BITMAP_RANGE_INDEX_FILE_EXTENSION
     }
     if (!ok_fwd || !ok_dict) fail(PH_ERR_INVALID_ARGUMENT, "column " + c + ": forward index or dictionary missing");
     descs.push_back(d);

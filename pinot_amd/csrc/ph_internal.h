@@ -114,6 +114,11 @@ constexpr int kWaves = kBlock / 64;
 // the big LDS item: 8 waves per ring set doubles the resident waves per CU at the same ring footprint)
 constexpr int kPartBlock = 512;
 constexpr int kPartWaves = kPartBlock / 64;
+// k_part_reg (kernel A, register-direct): 4-wave workgroups; a wave tile is 32 words = 2048 docs, lane l owning the
+// 32 consecutive docs [32 l, 32 l + 32) of it, whose b-bit values are exactly b dwords of every stream
+constexpr int kRegBlock = 256;
+constexpr int kRegWaves = kRegBlock / 64;
+constexpr int kRegTileWords = 32;
 constexpr int kSparseStepWords = 64;              // k_agg_sparse: bitmap words (4096 docs) per wave step
 constexpr int kChunkWords = 256;                     // 16384 docs per chunk (a multiple of every round)
 constexpr int kInterruptChunks = 8192;               // an interruptible scan checks every 8192 chunks (~134M docs)
@@ -239,6 +244,10 @@ struct KParams {
   uint32_t* first_doc;            // non-null: this launch is the numGroupsLimit first-seen pass (DevSegment.first_doc)
   unsigned long long* hkeys;      // MODE_GROUP_HASH: [num_groups] slot keys (kHashEmpty = free); out_* by slot
   int64_t hmask;                  // MODE_GROUP_HASH: slots - 1 (a power of two >= 2x the distinct keys possible)
+  // MODE_GROUP_HASH numGroupsLimit (one limit segment per launch): the segment's first-seen table -- raw key per slot
+  // (lkeys, lmask) -- whose slots the segment's keep bitset (DevSegment.keep) indexes
+  unsigned long long* lkeys;
+  int64_t lmask;
   uint32_t* out_hll;              // [num_groups][num_hll][2^log2m]
   // MODE_PARTITION (kernel A) -- records to per-partition buffers
   int32_t part_klo;               // key bits kept in a record (keys per partition = 1 << part_klo)
@@ -260,6 +269,9 @@ struct KParams {
   int32_t part_slot_log2;         // C = 1 << part_slot_log2 LDS ring slots per partition
   int32_t part_fast;              // kernel A may run the lean k_part_scan (no gathers; ALL / RANGE / DOCRANGE leaves)
   int32_t part_depth;             // lean kernel A: tiles of loads in flight per wave (1: k_part_scan, 2: k_part_scan2)
+  int32_t part_reg;               // kernel A = k_part_reg (register-direct decode; 0: the LDS-staged forms)
+  int32_t part_ck, part_cv;       // k_part_reg: 16-byte loads per lane of a filter / key stream, of the value stream
+  int32_t part_rounds;            // k_part_reg: append rounds (flush + barrier) per tile (1 or 2)
   unsigned long long* ovf_count;  // overflow table (same layout as out_*), merged at the end
   int64_t* ovf_sum;
   int64_t* ovf_min;
@@ -397,6 +409,7 @@ struct Column {
   int32_t bits = 1;
   bool is_sorted = false;
   bool is_raw = false;                // pinned from a raw forward index (dictionary-encoded at pin)
+  bool has_range_index = false;       // an exact (version 2) bit-sliced range index came with the column
   Dictionary dict;
   std::vector<int32_t> sorted_ranges;  // [card][2] (sorted columns)
   std::vector<uint8_t> inverted;       // host copy of the inverted index (offsets + roaring blobs)
@@ -532,6 +545,8 @@ void launch_scan(const KParams& p, int mode, int ngroup, int rec64, int grid, si
 void launch_part_agg(const PartAggParams& p, size_t lds, hipStream_t s);
 size_t part_agg_lds_bytes(const PartAggParams& p);
 size_t partition_lds_bytes(KParams& p);  // fills the pl_* offsets, returns the dynamic LDS size
+int part_reg_blocks_per_cu(const KParams& p, int ng, size_t lds);  // k_part_reg occupancy
+void launch_part_reg(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);  // scan_partition_reg.hip
 struct MergeParams {
   unsigned long long* out_count;
   int64_t* out_sum;

@@ -47,6 +47,7 @@ struct PNode {
   std::vector<int32_t> ranges;        // OP_DOCRANGES pairs
   int bitmap_leaf = -1;               // OP_BITMAP: index into the query's bitmap list
   bool scan = false;
+  bool range_index = false;  // a scan-evaluated RangeIndexBasedFilterOperator leaf: index-based for the statistics
   std::vector<PNode> kids;
 };
 
@@ -67,7 +68,80 @@ struct DictIdSet {
 
 std::string lit(const char* s) { return s ? std::string(s) : std::string(); }
 
+// Raw (no-dictionary) FLOAT / DOUBLE columns are dictionary-encoded at pin in Double.compare order (-0.0 before 0.0,
+// NaN last), but the reference evaluates their predicates on the primitive values: EQ / IN `value == literal`
+// (so 0 matches -0.0 and 0.0, NaN matches nothing), RANGE `value >= lo && value <= hi` with exclusive bounds moved
+// by Math.nextUp / nextDown (NaN never matches), NOT_EQ / NOT_IN their complements (NaN included)
+// (EqualsPredicateEvaluatorFactory / InPredicateEvaluatorFactory / RangePredicateEvaluatorFactory raw-value
+// evaluators, e.g. RangePredicateEvaluatorFactory.java:482-522).  The matching dictIds are computed value by value.
+DictIdSet evaluate_raw_real(const ph_predicate& p, const Column& c) {
+  DictIdSet r;
+  const Dictionary& d = c.dict;
+  const int64_t card = d.size;
+  const bool is_float = d.type == PH_FLOAT;
+  auto parse = [&](const std::string& s) -> double {
+    const char* b = s.c_str();
+    char* e = nullptr;
+    const double v = is_float ? (double)strtof(b, &e) : strtod(b, &e);
+    if (e == b) fail(PH_ERR_BAD_QUERY, "not a number: " + s);
+    return v;
+  };
+  std::vector<char> match((size_t)card, 0);
+  bool exclusive = false;
+  switch (p.type) {
+    case PH_PRED_EQ:
+    case PH_PRED_NOT_EQ:
+    case PH_PRED_IN:
+    case PH_PRED_NOT_IN: {
+      if ((p.type == PH_PRED_EQ || p.type == PH_PRED_NOT_EQ) && (p.num_values != 1 || !p.values))
+        fail(PH_ERR_BAD_QUERY, "EQ predicate needs one value");
+      for (int i = 0; i < p.num_values; ++i) {
+        const double x = parse(lit(p.values[i]));
+        for (int64_t k = 0; k < card; ++k) match[k] |= d.reals[k] == x;
+      }
+      exclusive = p.type == PH_PRED_NOT_EQ || p.type == PH_PRED_NOT_IN;
+      break;
+    }
+    case PH_PRED_RANGE: {
+      const std::string lo = lit(p.lower), hi = lit(p.upper);
+      double L = -INFINITY, U = INFINITY;
+      if (p.lower && lo != "*") {
+        L = parse(lo);
+        if (!p.lower_inclusive) L = is_float ? (double)nextafterf((float)L, INFINITY) : nextafter(L, INFINITY);
+      }
+      if (p.upper && hi != "*") {
+        U = parse(hi);
+        if (!p.upper_inclusive) U = is_float ? (double)nextafterf((float)U, -INFINITY) : nextafter(U, -INFINITY);
+      }
+      for (int64_t k = 0; k < card; ++k) match[k] = d.reals[k] >= L && d.reals[k] <= U;
+      break;
+    }
+    default:
+      fail(PH_ERR_UNSUPPORTED, "predicate type " + std::to_string(p.type) + " is not on the GPU path");
+  }
+  std::vector<int32_t> ids;
+  for (int64_t k = 0; k < card; ++k)
+    if (match[k]) ids.push_back((int32_t)k);
+  if (exclusive) {
+    if (ids.empty()) { r.always_true = true; return r; }
+    if ((int64_t)ids.size() == card) { r.always_false = true; return r; }
+    r.exclusive = true;
+    r.ids = std::move(ids);
+    return r;
+  }
+  if (ids.empty()) { r.always_false = true; return r; }
+  if ((int64_t)ids.size() == card) { r.always_true = true; return r; }
+  if (ids.back() - ids.front() + 1 == (int32_t)ids.size()) {
+    r.is_range = true;
+    r.start = ids.front();
+    r.end = ids.back() + 1;
+  }
+  r.ids = std::move(ids);
+  return r;
+}
+
 DictIdSet evaluate_predicate(const ph_predicate& p, const Column& c) {
+  if (c.is_raw && (c.dict.type == PH_FLOAT || c.dict.type == PH_DOUBLE)) return evaluate_raw_real(p, c);
   DictIdSet r;
   const Dictionary& d = c.dict;
   const int64_t card = d.size;
@@ -208,6 +282,10 @@ struct Planner {
     }
     n.scan = true;
     n.col = sl;
+    // RangeIndexBasedFilterOperator (FilterOperatorUtils.java:97-120; canEvaluate :56-61): RANGE on a column with an
+    // exact range index, or EQ on one without an inverted index.  Same doc set as a scan of the dictIds, which is
+    // how the kernels evaluate it; it scans no entries (BitmapDocIdSet)
+    n.range_index = c.has_range_index && (p.type == PH_PRED_RANGE || (p.type == PH_PRED_EQ && !c.has_inverted()));
     if (s.is_range) {
       n.op = OP_RANGE;
       n.lo = (uint32_t)s.start;
@@ -392,7 +470,7 @@ void merge_same_column_leaves(PNode& n, const CardOf& card_of) {
 
 int count_scan_leaves(const PNode& n) {
   if (n.kind != L_NODE) return 0;
-  int s = n.scan ? 1 : 0;
+  int s = (n.scan && !n.range_index) ? 1 : 0;
   for (auto& k : n.kids) s += count_scan_leaves(k);
   return s;
 }
@@ -1373,8 +1451,11 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       for (int k = 0; k < d.nconj; ++k) {
         const PNode& leaf = single_conj ? root : root.kids[k];
         d.cstream[k] = conj_stream.at(leaf.col);
-        d.clo[k] = leaf.lo;
-        d.clen[k] = leaf.len;
+        // a set leaf carries no range (clen 0 marks it until its device bitset is attached below: the prefetch
+        // order keys off it).  r3: a set merged from same-column EQ leaves kept the first leaf's [lo, lo + 1), so
+        // with no numGroupsLimit pass forcing the gathering kernel, SSB Q3.3 / Q3.4 matched only that dictId
+        d.clo[k] = leaf.op == OP_SET ? 0u : leaf.lo;
+        d.clen[k] = leaf.op == OP_SET ? 0u : leaf.len;
         if (leaf.op == OP_SET) conj_set_fix.push_back({si * kMaxConj + k, leaf.set});
       }
     } else if (conj_query && root.scan) {
@@ -1563,12 +1644,6 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   }
   // per-segment tile pieces: the 1 KiB wave-loads of a full tile, stream by stream
   for (auto& d : dsegs) fill_tile_pieces(d, kp.nstage, kp.stage_soff, kp.tile_words);
-  // the optimistic numGroupsLimit scan's segment table: no keep bitsets, no first-doc tables
-  std::vector<DevSegment> dsegs_opt;
-  if (!limit_segs.empty() && limit_opt) {
-    dsegs_opt = dsegs;
-    for (auto& d : dsegs_opt) d.keep = nullptr, d.first_doc = nullptr;
-  }
   // the lean kernel A (k_part_scan) covers gather-free tiles with ALL / RANGE / DOCRANGE filter leaves
   kp.part_fast = !kp.late_prefetch && getenv("PH_PART_GENERIC") == nullptr;
   for (auto& d : dsegs)
@@ -1676,6 +1751,13 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   }
   if (!payload_fix.empty() || !fset_fix.empty() || !conj_set_fix.empty())
     PH_HIP_CHECK(hipStreamSynchronize(st));  // pageable copies above
+  // the optimistic numGroupsLimit scan's segment table: no keep bitsets, no first-doc tables (copied after every
+  // device pointer above is fixed up: r3 copied it before, so FK_CONJ set leaves scanned with null bitsets)
+  std::vector<DevSegment> dsegs_opt;
+  if (!limit_segs.empty() && limit_opt) {
+    dsegs_opt = dsegs;
+    for (auto& d : dsegs_opt) d.keep = nullptr, d.first_doc = nullptr;
+  }
 
   check_interrupt();
   stamp("setup");
@@ -1746,9 +1828,81 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         if (merged_keys < group_limit) {
           scanned = true;  // no segment can hold `limit` keys: the untruncated scan is the reference's result
           stats.limit_pass = 1;
+        } else if (mode == MODE_GROUP_HASH) {
+          // truncation over a key space beyond the dense budget (LongMapBasedHolder / ArrayMapBasedHolder regime,
+          // DictionaryBasedGroupKeyGenerator.java:629-637,809-817): the segments that cannot reach the limit are
+          // rescanned in one launch; each limit segment then runs, one at a time, (1) a first-seen pass into its
+          // own hash table (slot -> first matching doc of the slot's key), (2) the selection of the slots whose
+          // keys are among the first `limit` (the dense path's k_limit_* kernels over slots instead of keys), and
+          // (3) its scan, which looks each key's slot up in that table and aggregates only kept keys
+          scanned = true;
+          stats.limit_pass = 2;
+          init_tables();
+          PH_HIP_CHECK(hipMemsetAsync(kp.matched_total, 0, 8, st));
+          std::vector<char> is_lim(dsegs.size(), 0);
+          int32_t maxdocs = 1;
+          for (int k : limit_segs) {
+            is_lim[k] = 1;
+            maxdocs = std::max(maxdocs, dsegs[k].num_docs);
+          }
+          int64_t H2 = 1024;
+          while (H2 < 2 * (int64_t)maxdocs) H2 <<= 1;
+          unsigned long long* hk2 = scratch.alloc<unsigned long long>((size_t)H2);
+          uint32_t* first2 = scratch.alloc<uint32_t>((size_t)H2);
+          uint32_t* keep2 = scratch.alloc<uint32_t>((size_t)(H2 + 31) / 32);
+          const int64_t dbw = (int64_t)maxdocs / 32 + 2;
+          uint32_t* docbits = scratch.alloc<uint32_t>((size_t)dbw);
+          limit_scal = scratch.alloc<unsigned long long>(3 * limit_segs.size());
+          PH_HIP_CHECK(hipMemsetAsync(limit_scal, 0, 24 * limit_segs.size(), st));
+          // segment table of the limit rescans: every limit segment's keep bitset is keep2 (one segment at a time)
+          std::vector<DevSegment> dl = dsegs_opt;
+          for (int k : limit_segs) dl[k].keep = keep2;
+          DevSegment* d_segs_lim = scratch.alloc<DevSegment>(dl.size());
+          PH_HIP_CHECK(hipMemcpy(d_segs_lim, dl.data(), sizeof(DevSegment) * dl.size(), hipMemcpyHostToDevice));
+          auto launch_range = [&](KParams kx, int32_t cb, int32_t ce) {
+            if (ce <= cb) return;
+            kx.chunk_begin = cb;
+            kx.chunk_end = ce;
+            launch_scan(kx, mode, q->num_group_by, 0, std::min(grid, ce - cb), lds, st);
+          };
+          // the segments that cannot reach the limit: contiguous chunk ranges of non-limit segments
+          {
+            KParams kn = kp;
+            kn.segs = d_segs_opt;
+            kn.late_prefetch = base_late;
+            int32_t cb = -1, ce = -1;
+            for (size_t k = 0; k < dsegs.size(); ++k) {
+              if (is_lim[k]) continue;
+              if (dseg_chunks[k].first != ce) {
+                launch_range(kn, cb, ce);
+                cb = dseg_chunks[k].first;
+              }
+              ce = dseg_chunks[k].second;
+            }
+            launch_range(kn, cb, ce);
+          }
+          for (size_t t = 0; t < limit_segs.size(); ++t) {
+            const int k = limit_segs[t];
+            PH_HIP_CHECK(hipMemsetAsync(hk2, 0xFF, 8 * (size_t)H2, st));
+            PH_HIP_CHECK(hipMemsetAsync(first2, 0xFF, 4 * (size_t)H2, st));
+            PH_HIP_CHECK(hipMemsetAsync(docbits, 0, 4 * (size_t)dbw, st));
+            KParams k1 = kp;  // (1) first-seen pass: no aggregation, no matched count
+            k1.segs = d_segs_opt;
+            k1.late_prefetch = 1;
+            k1.matched_total = nullptr;
+            k1.hkeys = hk2;
+            k1.hmask = H2 - 1;
+            k1.first_doc = first2;
+            launch_range(k1, dseg_chunks[k].first, dseg_chunks[k].second);
+            launch_limit_select(first2, H2, group_limit, 1, dbw, docbits, keep2, limit_scal + 3 * t, st);  // (2)
+            KParams k2 = kp;  // (3) the truncated scan
+            k2.segs = d_segs_lim;
+            k2.late_prefetch = 1;
+            k2.lkeys = hk2;
+            k2.lmask = H2 - 1;
+            launch_range(k2, dseg_chunks[k].first, dseg_chunks[k].second);
+          }
         } else {
-          if (mode == MODE_GROUP_HASH)
-            fail(PH_ERR_UNSUPPORTED, "numGroupsLimit reached over a key space beyond the dense budget");
           init_tables();  // truncation needed: first-seen pass, then the rescan with keep bitsets
           PH_HIP_CHECK(hipMemsetAsync(kp.matched_total, 0, 8, st));
         }
@@ -1819,13 +1973,34 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       kp.part_dbg = getenv("PH_PART_DBG") ? atoi(getenv("PH_PART_DBG")) : 0;  // timing experiments only
       kp.part_depth = 1;
       if (const char* e = getenv("PH_PART_DEPTH")) kp.part_depth = atoi(e) == 2 ? 2 : 1;  // tuning knob
+      // register-direct kernel A (k_part_reg): 32-bit records, <= 3 key columns, filter / key streams <= 16 bits
+      // and a value stream <= 32 bits (the lane's dwords of a stream are one register window of 4 * CK / 4 * CV)
+      kp.part_reg = 0;
+      if (kp.part_fast && !rec64 && q->num_group_by <= 3 && getenv("PH_PART_LDS") == nullptr && kp.part_depth == 1) {
+        int kb = 1, vb = 1;
+        for (auto& d : dsegs) {
+          if (d.fkind == FK_RANGE) kb = std::max(kb, (int)d.streams[kp.f_stream].bits);
+          for (int gi = 0; gi < q->num_group_by; ++gi) kb = std::max(kb, (int)d.streams[kp.g_stream[gi]].bits);
+          if (nvals) vb = std::max(vb, (int)d.streams[kp.v_stream[0]].bits);
+        }
+        if (kb <= 16 && vb <= 32) {
+          kp.part_reg = 1;
+          kp.part_ck = (kb <= 12 && vb <= 20) ? 3 : 4;
+          kp.part_cv = kp.part_ck == 3 ? 5 : 8;
+          kp.part_rounds = 2;  // two append rounds per 2048-doc tile: ~8 records per partition per round
+          if (const char* e = getenv("PH_PART_ROUNDS")) kp.part_rounds = atoi(e) == 1 ? 1 : 2;  // tuning knob
+          kp.stage_stride = 0;  // no staging
+        }
+      }
       stats.scan_kernel = !kp.part_fast ? PH_KERNEL_PART_SCAN
+                          : kp.part_reg ? PH_KERNEL_PART_REG
                           : kp.part_depth == 2 ? PH_KERNEL_PART_LEAN2 : PH_KERNEL_PART_LEAN;
       kp.part_vbits = vbits;
       kp.num_parts = (int32_t)P;
       const size_t lds_a = partition_lds_bytes(kp);
       int a_cap = 4;  // 8-wave workgroups: <= 4 per CU (32 waves)
-      if (const char* e = getenv("PH_PART_WG_PER_CU")) a_cap = std::max(1, std::min(4, atoi(e)));  // tuning knob
+      if (kp.part_reg) a_cap = part_reg_blocks_per_cu(kp, q->num_group_by, lds_a);  // 4-wave groups, VGPR-bound
+      if (const char* e = getenv("PH_PART_WG_PER_CU")) a_cap = std::max(1, std::min(8, atoi(e)));  // tuning knob
       const int a_per_cu = (int)std::max<size_t>(1, std::min<size_t>(a_cap, (160 * 1024) / lds_a));
       const int grid_a = ctx->num_cus * a_per_cu;
       int max_batch_chunks = 0;

@@ -621,8 +621,29 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
         atomicMin(&S->first_doc[g], doc);
         return;
       }
+      if (MODE == MODE_GROUP_HASH && LATE && p.first_doc) {  // the same over one segment's first-seen hash table
+        atomicMin(&p.first_doc[g], doc);
+        return;
+      }
       if (MODE != MODE_GROUP_HASH && LATE && S->keep && !((gld(S->keep + (g >> 5)) >> (g & 31)) & 1u))
         return;  // beyond numGroupsLimit
+      if (MODE == MODE_GROUP_HASH && LATE && S->keep) {
+        // beyond numGroupsLimit?  the key's slot in the segment's first-seen table (the pass placed every key this
+        // scan meets) indexes the keep bitset
+        unsigned long long h = (unsigned long long)key;
+        h ^= h >> 33;
+        h *= 0xff51afd7ed558ccdull;
+        h ^= h >> 33;
+        h *= 0xc4ceb9fe1a85ec53ull;
+        h ^= h >> 33;
+        int64_t ls = (int64_t)(h & (unsigned long long)p.lmask);
+        for (int64_t probe = 0; probe <= p.lmask; ++probe) {
+          const unsigned long long k = gld(p.lkeys + ls);
+          if (k == (unsigned long long)key || k == kHashEmpty) break;
+          ls = (ls + 1) & p.lmask;
+        }
+        if (!((gld(S->keep + (ls >> 5)) >> (ls & 31)) & 1u)) return;
+      }
       // MODE_GROUP_GLOBAL: the workgroup's LDS group cache first (slot found -> aggregate in LDS like MODE_GROUP_LDS)
       bool local = MODE == MODE_GROUP_LDS;
       if (MODE == MODE_GROUP_GLOBAL && p.gc_slots) {

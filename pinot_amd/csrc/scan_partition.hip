@@ -1,6 +1,6 @@
 // scan_partition.hip -- the partitioned group-by (MODE_PARTITION): kernel A (k_scan instantiations that append records
 // to per-(partition, workgroup) regions) and kernel B (k_part_agg), plus the overflow-table merge.
-#include "scan_kernel.h"
+#include "scan_partition.h"
 
 namespace ph {
 
@@ -123,89 +123,6 @@ __device__ __forceinline__ void part_tile(const KParams& p, SegPtr S, uint8_t* s
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         if (h[q] && w[q] >= C) part_overflow<REC64>(p, bk[q], rec[q]);
-    }
-  }
-}
-
-// Flush of the lean kernel's rings, listed partitions only: a partition enters the round's list when an append
-// completes its first whole 64-byte chunk, so the flush touches ~(round records / 16) partitions instead of all P.
-// Per listed partition (8 lanes of one wave) the whole chunks go to the partition's region at its flushed
-// position with 16-byte stores, and the < 16 leftovers move to the front of the ring.  Every lane reads before
-// any lane of its wave writes (LDS ops of a wave execute in order), so a leftover never overwrites a record still
-// to be stored.  `matched` gains the appends that went to the overflow table (a full ring).
-template <int REC64, int BLOCK>
-__device__ void part_flush_listed(const KParams& p, uint8_t* smem, const uint32_t* flist, uint32_t nlisted,
-                                  unsigned long long& matched) {
-  using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
-  constexpr uint32_t CH = 64 / sizeof(Rec);  // records per 64-byte chunk
-  constexpr uint32_t PQ = 16 / sizeof(Rec);  // records per 16-byte quarter
-  Rec* slots = reinterpret_cast<Rec*>(smem + p.pl_slot_off);
-  uint32_t* pend = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
-  uint32_t* gpos = reinterpret_cast<uint32_t*>(smem + p.pl_bcnt_off);
-  const int cl = p.part_slot_log2;
-  const uint32_t C = 1u << cl;
-  const uint32_t cap = (uint32_t)p.part_cap;
-  const uint32_t total = nlisted * 8u;
-  for (uint32_t t = threadIdx.x; t < total; t += BLOCK) {
-    const uint32_t b = flist[t >> 3], i = t & 7u;
-    const uint32_t raw = pend[b];
-    const uint32_t n = min(raw, C);  // records beyond C went to the overflow table
-    const uint32_t out = n & ~(CH - 1u), left = n - out;
-    const uint32_t g = gpos[b];
-    Rec* ring = slots + ((size_t)b << cl);
-    // reads: quarters i and i + 8 of the outgoing records (C / PQ <= 16), leftovers i and i + 8 (< CH <= 16)
-    u32x4 q0 = {0u, 0u, 0u, 0u}, q1 = {0u, 0u, 0u, 0u};
-    const uint32_t r0 = i * PQ, r1 = (i + 8u) * PQ;
-    if (r0 < out) q0 = *reinterpret_cast<const u32x4*>(ring + r0);
-    if (r1 < out) q1 = *reinterpret_cast<const u32x4*>(ring + r1);
-    Rec l0 = 0, l1 = 0;
-    if (i < left) l0 = ring[out + i];
-    if (i + 8u < left) l1 = ring[out + i + 8u];
-    // writes
-    Rec* region = reinterpret_cast<Rec*>(p.part_buf) + part_region(p, b, blockIdx.x) * (size_t)cap;
-    if (r0 < out) {
-      if (g + r0 + PQ <= cap) {
-        *reinterpret_cast<u32x4*>(region + g + r0) = q0;
-      } else {
-        const Rec* e = reinterpret_cast<const Rec*>(&q0);
-        for (uint32_t k = 0; k < PQ; ++k) part_store<REC64>(p, b, g + r0 + k, e[k]);
-      }
-    }
-    if (r1 < out) {
-      if (g + r1 + PQ <= cap) {
-        *reinterpret_cast<u32x4*>(region + g + r1) = q1;
-      } else {
-        const Rec* e = reinterpret_cast<const Rec*>(&q1);
-        for (uint32_t k = 0; k < PQ; ++k) part_store<REC64>(p, b, g + r1 + k, e[k]);
-      }
-    }
-    if (i < left) ring[i] = l0;
-    if (i + 8u < left) ring[i + 8u] = l1;
-    if (i == 0) {
-      pend[b] = left;
-      gpos[b] = g + out;
-      matched += raw - n;
-    }
-  }
-}
-
-// Final flush of the lean kernel (after the last listed flush): every partition's < 16 pending records, the
-// region record counts, and the matched docs = the regions' records (overflow appends counted already).
-template <int REC64, int BLOCK>
-__device__ void part_flush_final(const KParams& p, uint8_t* smem, unsigned long long& matched) {
-  using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
-  const Rec* slots = reinterpret_cast<const Rec*>(smem + p.pl_slot_off);
-  const uint32_t* pend = reinterpret_cast<const uint32_t*>(smem + p.pl_lcnt_off);
-  const uint32_t* gpos = reinterpret_cast<const uint32_t*>(smem + p.pl_bcnt_off);
-  const int cl = p.part_slot_log2;
-  const uint32_t total = (uint32_t)p.num_parts * 16u;
-  for (uint32_t t = threadIdx.x; t < total; t += BLOCK) {
-    const uint32_t b = t >> 4, i = t & 15u;
-    const uint32_t n = pend[b], g = gpos[b];  // n < 16 after the listed flushes
-    if (i < n) part_store<REC64>(p, b, g + i, slots[((size_t)b << cl) + i]);
-    if (i == 0) {
-      p.part_count[(size_t)b * gridDim.x + blockIdx.x] = g + n;  // records of region (b, blockIdx)
-      matched += g + n;
     }
   }
 }
@@ -445,6 +362,10 @@ static void launch_part_fast_ng(const KParams& p, int rec64, int grid, size_t ld
 }
 
 void launch_scan_partition(const KParams& p, int ng, int rec64, int grid, size_t lds, hipStream_t s) {
+  if (p.part_reg) {
+    launch_part_reg(p, ng, grid, lds, s);
+    return;
+  }
   if (!p.part_fast) {
     launch_mode<MODE_PARTITION>(p, ng, rec64, grid, lds, s);
     return;

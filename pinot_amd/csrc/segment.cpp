@@ -404,6 +404,15 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
     col->cardinality = d.cardinality;
     col->is_sorted = d.is_sorted != 0;
     col->is_raw = d.raw_forward_index != 0;
+    if (d.range_index) {
+      // BitSlicedRangeIndexReader header: int32 BE version, int64 BE min.  Version 2 (BitSlicedRangeIndexCreator) is
+      // exact; a legacy version-1 index (RangeIndexCreator: ranges + a partial scan) is ignored -- the leaf then
+      // scans, with the same doc set and that form's own entry count
+      if (d.range_index_size < 12) fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": truncated range index");
+      const uint8_t* h = static_cast<const uint8_t*>(d.range_index);
+      const uint32_t version = (uint32_t)h[0] << 24 | (uint32_t)h[1] << 16 | (uint32_t)h[2] << 8 | h[3];
+      col->has_range_index = version == 2;
+    }
     const uint8_t* fwd = static_cast<const uint8_t*>(d.forward_index);
     if (!fwd) fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": missing forward index");
     std::vector<uint8_t> packed;

@@ -119,6 +119,10 @@ class DistributedQuery:
     def __init__(self, ctx, group=None):
         self.ctx = ctx
         self.group = group
+        # (query, segment set) -> (layout, padded tables): planning the layout and allocating / filling the tables
+        # once per query shape, not per step (ph_query_execute_dense re-initialises the live rows every call; the
+        # padding rows keep their reduction identities through every reduction)
+        self._cache = {}
 
     def execute(self, q, segments: Sequence, copy: bool = True):
         """Returns (this rank's finalised key shard or None, (g0, g1), scan statistics of this rank).  The scan
@@ -133,8 +137,15 @@ class DistributedQuery:
         import torch.distributed as dist
         world = dist.get_world_size(self.group) if dist.is_initialized() else 1
         t0 = time.perf_counter()
-        layout = Layout.from_native(self.ctx.dense_layout(q, segments))
-        tables = alloc_tables(layout, world, dev)
+        key = (repr(q), tuple(id(s) for s in segments), world, self.ctx.device)
+        hit = self._cache.get(key)
+        if hit is None:
+            layout = Layout.from_native(self.ctx.dense_layout(q, segments))
+            hit = (layout, alloc_tables(layout, world, dev), list(segments))  # holds the segments: ids stay unique
+            if len(self._cache) >= 16:
+                self._cache.pop(next(iter(self._cache)))
+            self._cache[key] = hit
+        layout, tables = hit[0], hit[1]
         scan_stats = self.ctx.execute_dense(q, segments, [t.data_ptr() for t in tables])  # returns after the scan
         t1 = time.perf_counter()
         shards, g0, g1 = reduce_tables(tables, layout, self.group)

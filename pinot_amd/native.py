@@ -52,7 +52,8 @@ class ColumnDesc(ctypes.Structure):
                 ("dictionary", ctypes.c_void_p), ("dictionary_size", ctypes.c_uint64),
                 ("dictionary_entry_size", ctypes.c_int32),
                 ("inverted_index", ctypes.c_void_p), ("inverted_index_size", ctypes.c_uint64),
-                ("raw_forward_index", ctypes.c_int32)]
+                ("raw_forward_index", ctypes.c_int32),
+                ("range_index", ctypes.c_void_p), ("range_index_size", ctypes.c_uint64)]
 
 
 class MetadataEntry(ctypes.Structure):

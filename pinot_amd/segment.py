@@ -135,6 +135,15 @@ class ColumnBuffers:
     dictionary_values: np.ndarray   # native values (for tests / reduce)
     inverted_index: Optional[np.ndarray] = None
     raw: bool = False               # forward_index is a raw chunk forward index (no dictionary)
+    range_index: Optional[np.ndarray] = None  # bit-sliced range index bytes (header: version 2, min)
+
+
+def range_index_header(min_value: int = 0) -> np.ndarray:
+    """The BitSlicedRangeIndexCreator header (BitSlicedRangeIndexCreator.java:125-131: int32 BE version 2, int64 BE
+    min -- 0 for a dictionary column, whose index is built over dictIds).  The GPU path reads only this header: it
+    evaluates a range-indexed leaf from the packed dictIds (the same doc set as the exact index), so the serialized
+    RoaringBitmap RangeBitmap that follows in a reference-written file is not built here."""
+    return np.frombuffer(np.array([2], ">i4").tobytes() + np.array([min_value], ">i8").tobytes(), np.uint8).copy()
 
 
 @dataclass
@@ -321,9 +330,9 @@ def create_raw_column(name: str, values, data_type: str, compression: str = "PAS
 
 def create_segment(name: str, columns: Dict[str, tuple], inverted: Sequence[str] = (),
                    run_optimize: bool = False, raw: Sequence[str] = (), raw_compression: str = "PASS_THROUGH",
-                   raw_version: int = 2) -> SegmentBuffers:
+                   raw_version: int = 2, range_index: Sequence[str] = ()) -> SegmentBuffers:
     """columns: name -> (values, data_type) -- SegmentIndexCreationDriverImpl for SV columns (dictionary-encoded, or
-    raw for the names in ``raw``: noDictionaryColumns)."""
+    raw for the names in ``raw``: noDictionaryColumns; ``range_index``: rangeIndexColumns, see range_index_header)."""
     seg = SegmentBuffers(name, 0)
     n = None
     for c, (vals, dt) in columns.items():
@@ -331,6 +340,8 @@ def create_segment(name: str, columns: Dict[str, tuple], inverted: Sequence[str]
             seg.columns[c] = create_raw_column(c, vals, dt, raw_compression, raw_version)
         else:
             seg.columns[c] = create_column(c, vals, dt, c in inverted, run_optimize)
+        if c in range_index:
+            seg.columns[c].range_index = range_index_header()
         n = len(vals) if n is None else n
         if n != len(vals):
             raise ValueError("columns of different lengths")
@@ -389,6 +400,11 @@ class PinnedSegment:
                 keep.append(inv)
                 d.inverted_index = inv.ctypes.data
                 d.inverted_index_size = inv.nbytes
+            if cb.range_index is not None:
+                ri = np.ascontiguousarray(cb.range_index)
+                keep.append(ri)
+                d.range_index = ri.ctypes.data
+                d.range_index_size = ri.nbytes
         desc = N.SegmentDesc(buffers.name.encode(), buffers.num_docs, len(buffers.columns), cols)
         h = ctypes.c_void_p()
         N.check(N.lib().ph_segment_pin(ctx.handle, ctypes.byref(desc), ctypes.byref(h)))

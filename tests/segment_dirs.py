@@ -41,13 +41,14 @@ def _metadata(seg, extra=None):
 
 
 def _buffers(cb):
-    if cb.raw:  # no-dictionary column: the raw chunk forward index only
-        return [("forward_index", np.ascontiguousarray(cb.forward_index).tobytes())]
+    ri = [("range_index", np.ascontiguousarray(cb.range_index).tobytes())] if cb.range_index is not None else []
+    if cb.raw:  # no-dictionary column: the raw chunk forward index (+ a range index)
+        return [("forward_index", np.ascontiguousarray(cb.forward_index).tobytes())] + ri
     out = [("dictionary", np.ascontiguousarray(cb.dictionary).tobytes()),
            ("forward_index", np.ascontiguousarray(cb.forward_index).tobytes())]
     if cb.inverted_index is not None:
         out.append(("inverted_index", np.ascontiguousarray(cb.inverted_index).tobytes()))
-    return out
+    return out + ri
 
 
 def write_v3(seg, path, extra_meta=None):
@@ -71,7 +72,7 @@ def write_v1(seg, path):
     for c, cb in seg.columns.items():
         ext = {"dictionary": ".dict", "forward_index": ".sv.raw.fwd" if cb.raw else
                (".sv.sorted.fwd" if cb.is_sorted else ".sv.unsorted.fwd"),
-               "inverted_index": ".bitmap.inv"}
+               "inverted_index": ".bitmap.inv", "range_index": ".bitmap.range"}
         for idx, payload in _buffers(cb):
             open(os.path.join(path, c + ext[idx]), "wb").write(payload)
 
@@ -130,4 +131,12 @@ def read_dir(path):
             ids = np.repeat(np.arange(card, dtype=np.int32), np.maximum(r[:, 1] - r[:, 0] + 1, 0))
             fwd = O.fixed_bit_pack(ids, bits).tobytes()
         out[c] = dict(dictionary=values, fwd=np.frombuffer(fwd, np.uint8), bits=bits, data_type=dt, num_docs=n)
-    return O.segment_from_dict_ids(meta.get("segment.name", path), out), meta
+    seg = O.segment_from_dict_ids(meta.get("segment.name", path), out)
+    for c in cols:  # exact (version 2) range indexes: RangeIndexBasedFilterOperator leaves
+        if v3:
+            hdr = buf(c, "range_index")[:4] if f"{c}.range_index.startOffset" in imap else b""
+        else:
+            rp = os.path.join(d, c + ".bitmap.range")
+            hdr = open(rp, "rb").read(4) if os.path.exists(rp) else b""
+        seg.columns[c].has_range_index = hdr == b"\x00\x00\x00\x02"
+    return seg, meta

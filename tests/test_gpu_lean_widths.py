@@ -3,6 +3,7 @@ against the oracle, each query asserting which kernel ran (ph_exec_stats.scan_ke
 
   k_agg_lean          aggregation only, one packed integer column (value streams of 1..26 bits)
   k_group_lds_lean    LDS-private group table (value streams of 1..31 bits)
+  k_part_reg          partitioned group-by, register-direct decode (filter streams <= 16 bits; 32-bit records)
   k_part_scan(2)      partitioned group-by, 90 000 keys (value streams of 1..31 bits; 32- and 64-bit records)
 
 The aggregated column's frame-of-reference stream is `w` bits wide (values base + [0, 2^w - 1], both extremes
@@ -21,7 +22,7 @@ from tests.seeds import seed_of
 
 pytestmark = pytest.mark.gpu
 
-PH_KERNEL_AGG_LEAN, PH_KERNEL_GROUP_LDS_LEAN, PH_KERNEL_PART_LEAN, PH_KERNEL_PART_LEAN2 = 2, 4, 5, 6
+PH_KERNEL_AGG_LEAN, PH_KERNEL_GROUP_LDS_LEAN, PH_KERNEL_PART_LEAN, PH_KERNEL_PART_LEAN2, PH_KERNEL_PART_REG = 2, 4, 5, 6, 8
 
 
 @pytest.fixture(scope="module")
@@ -87,6 +88,14 @@ def test_lean_kernels_every_width(ctx, w, monkeypatch):
            PH_KERNEL_GROUP_LDS_LEAN)
     part = (f"SET numGroupsLimit=2000000; SELECT g1, g2, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where} "
             f"GROUP BY g1, g2 ORDER BY g1, g2 LIMIT 200000")
+    # k_part_reg decodes from registers (its own per-width switch): filter / key streams <= 16 bits
+    _check(ctx, gpu, ora, part, PH_KERNEL_PART_REG if min(w, 24) <= 16 else PH_KERNEL_PART_LEAN)
+    monkeypatch.setenv("PH_PART_ROUNDS", "1")  # one append round per tile (64-slot rings)
+    monkeypatch.setenv("PH_PART_RING_LOG2", "6")
+    _check(ctx, gpu, ora, part, PH_KERNEL_PART_REG if min(w, 24) <= 16 else PH_KERNEL_PART_LEAN)
+    monkeypatch.delenv("PH_PART_ROUNDS")
+    monkeypatch.delenv("PH_PART_RING_LOG2")
+    monkeypatch.setenv("PH_PART_LDS", "1")  # the LDS-staged forms
     _check(ctx, gpu, ora, part, PH_KERNEL_PART_LEAN)
     monkeypatch.setenv("PH_PART_DEPTH", "2")
     _check(ctx, gpu, ora, part, PH_KERNEL_PART_LEAN2)

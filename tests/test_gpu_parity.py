@@ -304,6 +304,33 @@ def test_hash_group_by_beyond_dense_budget(ctx, where):
     assert len(got.rows) > (300_000 if not where else 100_000)
 
 
+@pytest.mark.parametrize("where", ["", " WHERE f < 300", " WHERE f IN (1, 5, 9, 300, 301, 777) OR g1 < 9000"])
+def test_hash_group_by_num_groups_limit(ctx, where):
+    # numGroupsLimit over a key space beyond the dense budget (LongMapBasedHolder.getGroupId,
+    # DictionaryBasedGroupKeyGenerator.java:629-637): the reference's DEFAULT limit of 100 000 on a ~1.7e12 key
+    # space -- each segment keeps its first 100 000 keys in doc order and drops the docs of later keys; one small
+    # segment cannot reach the limit and aggregates everything.  Bit-exact vs the oracle's IntGroupIdMap emulation.
+    rng = np.random.default_rng(seed_of(f"hash-limit{where}"))
+    tables = []
+    for n in (500_000, 180_001, 40_000):  # the first segment matches > 100 000 keys under every filter
+        t = {c: (rng.integers(0, 12_000, n).astype(np.int32) * 3 + k, "INT") for k, c in enumerate(("g1", "g2", "g3"))}
+        t["m"] = (rng.integers(-1 << 20, 1 << 30, n).astype(np.int32), "INT")
+        t["f"] = (rng.integers(0, 1000, n).astype(np.int32), "INT")
+        t["g1"][0][: n // 10] = 5  # hot keys
+        t["g2"][0][: n // 10] = 7
+        tables.append(t)
+    sql = (f"SELECT g1, g2, g3, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where} "
+           f"GROUP BY g1, g2, g3 ORDER BY g1, g2, g3 LIMIT 10000000")
+    q = parse_sql(sql)
+    r, got = _both(ctx, tables, sql)
+    e = O.execute(q, [O.build_segment(f"s{i}", t) for i, t in enumerate(tables)])
+    assert r.stats.mode == 5  # MODE_GROUP_HASH
+    assert e.stats.num_groups_limit_reached  # the oracle truncated: the case tests what it means to
+    assert r.stats.num_groups_limit_reached
+    assert r.stats.limit_pass == 2
+    assert r.stats.num_docs_scanned == e.stats.num_docs_scanned
+
+
 def test_remap_cache_bounded_over_segment_subsets(ctx):
     # without a table dictionary every distinct segment set unions its own dictionary, and each segment gets a
     # device remap to it; the union cache is a bounded FIFO (64 entries) and a segment's remaps must be released
@@ -372,11 +399,15 @@ def test_num_groups_limit_first_seen(ctx, case):
         assert not r.stats.num_groups_limit_reached and r.stats.limit_pass == 1
 
 
+@pytest.mark.parametrize("where", ["", " WHERE a IN (3, 5, 7, 11, 400, 1999) AND m > 100", " WHERE b NOT IN (3, 4)",
+                                   " WHERE (a = 3 OR a = 1999) AND m > 100"])
 @pytest.mark.parametrize("eager", [False, True])
-def test_num_groups_limit_product_above_real_keys(ctx, eager, monkeypatch):
+def test_num_groups_limit_product_above_real_keys(ctx, eager, where, monkeypatch):
     # a cardinality product far above the limit but fewer real keys than the limit: numGroupsLimitReached stays
     # false and the result is the untruncated group-by (optimistic form: no first-seen pass at all); the
-    # pass-first order (PH_LIMIT_EAGER) gives the same answer
+    # pass-first order (PH_LIMIT_EAGER) gives the same answer.  The filtered forms put a bitset leaf in the scan
+    # (FK_CONJ set leaf, FK_SET): r3's optimistic scan read a segment table copied before those device bitsets
+    # were attached, and filtered SSB Q3.3 / Q3.4 returned a fraction of their groups
     if eager:
         monkeypatch.setenv("PH_LIMIT_EAGER", "1")
     rng = np.random.default_rng(seed_of("product_above_real_keys"))
@@ -388,8 +419,8 @@ def test_num_groups_limit_product_above_real_keys(ctx, eager, monkeypatch):
         a[:2000] = np.arange(2000)
         tables.append({"a": (a, "INT"), "b": (b, "INT"),
                        "m": (rng.integers(-50, 1 << 18, n).astype(np.int32), "INT")})
-    sql = ("SET numGroupsLimit=20000; SELECT a, b, COUNT(*), SUM(m), MIN(m) FROM t GROUP BY a, b ORDER BY a, b "
-           "LIMIT 100000")
+    sql = (f"SET numGroupsLimit=20000; SELECT a, b, COUNT(*), SUM(m), MIN(m) FROM t{where} GROUP BY a, b "
+           f"ORDER BY a, b LIMIT 100000")
     r, _ = _both(ctx, tables, sql)
     q = parse_sql(sql)
     e = O.execute(q, [O.build_segment(f"s{i}", t) for i, t in enumerate(tables)])
@@ -547,3 +578,15 @@ def test_group_cache_global_table(ctx, sql):
     rng = np.random.default_rng(seed_of(sql))
     tables = [_random_table(rng, n) for n in (40_000, 64 * 700 + 9)]
     _both(ctx, tables, sql, inverted=())
+
+
+@pytest.mark.parametrize("where", ["(a = 3 OR a = 17) AND (b = 5 OR b = 9) AND m > 0",
+                                   "a IN (3, 17, 30) AND b BETWEEN 2 AND 20 AND m > 0"])
+def test_conj_set_leaf_merged_from_equalities(ctx, where):
+    # FK_CONJ with a set leaf merged from same-column EQ leaves (SSB Q3.3 / Q3.4's `c_city = .. OR c_city = ..`),
+    # on a small key space (no numGroupsLimit pass): the set must be read as a bitset (r3: it kept the first EQ's
+    # single-id range and the gathering kernel was not selected -> only that id matched)
+    rng = np.random.default_rng(seed_of(where))
+    tables = [{"a": (rng.integers(0, 40, n).astype(np.int32), "INT"), "b": (rng.integers(0, 30, n).astype(np.int32), "INT"),
+               "m": (rng.integers(-100, 1000, n).astype(np.int32), "INT")} for n in (200_000, 77_777)]
+    _both(ctx, tables, f"SELECT a, b, COUNT(*), SUM(m) FROM t WHERE {where} GROUP BY a, b ORDER BY a, b LIMIT 1000")

@@ -90,3 +90,37 @@ def test_raw_columns_from_directories(ctx, tmp_path, layout):
     ora, _ = SD.read_dir(path)
     for sql in SQL:
         _check(ctx, [seg], [ora], sql)
+
+
+def test_raw_real_predicates_primitive_semantics(ctx):
+    # raw FLOAT / DOUBLE predicates compare primitives (EqualsPredicateEvaluatorFactory / RangePredicateEvaluatorFactory
+    # raw-value evaluators, RangePredicateEvaluatorFactory.java:482-522): 0 matches -0.0 and 0.0, NaN matches no EQ /
+    # IN / RANGE (not even an unbounded one) and every NOT_EQ / NOT_IN.  The pinned column is dictionary-encoded in
+    # Double.compare order (-0.0 < 0.0, NaN last), so the planner must not map these to plain dictId ranges
+    # (ADVICE r2).  Expected counts / sums from numpy's IEEE comparisons, which are the primitive semantics.
+    rng = np.random.default_rng(404)
+    n = 100_003
+    d = np.round(rng.normal(0, 4, n), 1)
+    d[rng.integers(0, n, 3000)] = -0.0
+    d[rng.integers(0, n, 3000)] = 0.0
+    d[rng.integers(0, n, 500)] = np.nan
+    f = d.astype(np.float32)
+    m = rng.integers(-1000, 1000, n).astype(np.int32)
+    cols = {"d": (d, "DOUBLE"), "f": (f, "FLOAT"), "m": (m, "INT")}
+    seg = ctx.pin(create_segment("rawnan", cols, raw=("d", "f"), raw_compression="LZ4"))
+    cases = {
+        "d = 0": d == 0, "d = -0.0": d == 0, "d <> 0": ~(d == 0), "d IN (0, 1.5)": (d == 0) | (d == 1.5),
+        "d NOT IN (0, 1.5)": ~((d == 0) | (d == 1.5)), "d > 1": d > 1, "d >= 0": d >= 0, "d < 0": d < 0,
+        "d <= 0": d <= 0, "d BETWEEN -1 AND 0": (d >= -1) & (d <= 0), "d = 'NaN'": np.zeros(n, bool), "d <> 'NaN'": np.ones(n, bool),
+        "f = 0": f == 0, "f > -0.5": f > np.float32(-0.5), "f < 0.3": f < np.float32(0.3), "f <> 0": ~(f == 0),
+    }
+    for where, mask in cases.items():
+        q = parse_sql(f"SELECT COUNT(*), SUM(m) FROM t WHERE {where}")
+        r = ctx.execute(q, [seg])
+        got = reduce_groups(q, r.keys, r.aggs).rows
+        cnt = int(np.count_nonzero(mask))
+        exp_sum = float(m[mask].astype(np.int64).sum()) if cnt else None
+        assert got[0][0] == cnt, (where, got, cnt)
+        if cnt:
+            assert got[0][1] == exp_sum, (where, got, exp_sum)
+    seg.unpin()
