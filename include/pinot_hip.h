@@ -167,7 +167,24 @@ typedef struct {
    * the stream is drained between them), and returns PH_ERR_CANCELLED. */
   int64_t end_time_ms;                /* wall-clock deadline, ms since the Unix epoch; 0 = none */
   const volatile int32_t* interrupt;  /* the caller sets *interrupt != 0 to cancel; NULL = none */
+  /* Segment group trim (GroupByOperator.java:114-130): with a group-by, ORDER BY and min_segment_group_trim_size > 0
+   * (query option minSegmentGroupTrimSize; <= 0 = off, the default -1), every segment holding more groups than
+   * GroupByUtils.getTableCapacity(limit, min_segment_group_trim_size) = max(5 * limit, min) keeps only that many,
+   * chosen by TableResizer.trimInSegmentResults (a heap over the ORDER BY values, fed in the group-key iterator's
+   * order), before the combine merges the segments.  DISTINCTCOUNTHLL in the ORDER BY is PH_ERR_UNSUPPORTED. */
+  int32_t num_order_by;
+  const struct ph_order_by* order_by;
+  int32_t limit;                      /* the query's LIMIT */
+  int32_t min_segment_group_trim_size;
 } ph_query;
+
+/* one ORDER BY expression: a group-by column (index into group_by) or an aggregation (index into aggregations) */
+typedef enum { PH_ORDER_GROUP_BY = 0, PH_ORDER_AGGREGATION = 1 } ph_order_kind;
+typedef struct ph_order_by {
+  int32_t kind;                 /* ph_order_kind */
+  int32_t index;
+  int32_t asc;                  /* 1 ASC, 0 DESC */
+} ph_order_by;
 
 typedef struct {
   int64_t num_docs_scanned;                /* matched docs */

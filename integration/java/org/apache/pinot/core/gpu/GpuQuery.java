@@ -7,6 +7,7 @@ import java.util.Map;
 import org.apache.pinot.common.request.context.ExpressionContext;
 import org.apache.pinot.common.request.context.FilterContext;
 import org.apache.pinot.common.request.context.FunctionContext;
+import org.apache.pinot.common.request.context.OrderByExpressionContext;
 import org.apache.pinot.common.request.context.predicate.EqPredicate;
 import org.apache.pinot.common.request.context.predicate.InPredicate;
 import org.apache.pinot.common.request.context.predicate.NotEqPredicate;
@@ -25,7 +26,8 @@ import org.apache.pinot.segment.spi.AggregationFunctionType;
  * engine._QueryStruct).  Returns null for shapes outside the GPU path, so the plan maker keeps the CPU plan:
  * filtered aggregations, star-tree, null handling, non-identifier group-by expressions, aggregations other than
  * COUNT / SUM / MIN / MAX / DISTINCTCOUNTHLL (over a column or a 2-operand mult/sub/add), predicates other than
- * EQ / NOT_EQ / IN / NOT_IN / RANGE on identifiers, and per-segment group trim (GroupByOperator.java:118-130).
+ * EQ / NOT_EQ / IN / NOT_IN / RANGE on identifiers, and a segment group trim (GroupByOperator.java:114-130) ordered
+ * by anything but group-by columns and aggregations.
  */
 public final class GpuQuery {
   final int[] _descriptor;
@@ -43,10 +45,6 @@ public final class GpuQuery {
   public static GpuQuery compile(QueryContext ctx) {
     if (!QueryContextUtils.isAggregationQuery(ctx) || ctx.isNullHandlingEnabled() || ctx.hasFilteredAggregations()) {
       return null;
-    }
-    if (ctx.getGroupByExpressions() != null && ctx.getOrderByExpressions() != null
-        && ctx.getMinSegmentGroupTrimSize() > 0) {
-      return null;  // per-segment trim is an approximation the single-pass GPU combine does not reproduce
     }
     Builder b = new Builder();
     try {
@@ -94,6 +92,33 @@ public final class GpuQuery {
           d.add(x);
         }
       }
+      // [numOrderBy, (kind, index, asc)..., limit, minSegmentGroupTrimSize]: segment group trim
+      // (GroupByOperator.java:114-130) runs in the library (ph_query.min_segment_group_trim_size)
+      List<OrderByExpressionContext> orderBy = ctx.getOrderByExpressions();
+      List<int[]> order = new ArrayList<>();
+      if (orderBy != null && ctx.getGroupByExpressions() != null) {
+        for (OrderByExpressionContext ob : orderBy) {
+          ExpressionContext e = ob.getExpression();
+          int gi = ctx.getGroupByExpressions().indexOf(e);
+          Integer ai = e.getType() == ExpressionContext.Type.FUNCTION
+              ? ctx.getAggregationFunctionIndexMap().get(e.getFunction()) : null;
+          if (gi >= 0) {
+            order.add(new int[]{0, gi, ob.isAsc() ? 1 : 0});
+          } else if (ai != null) {
+            order.add(new int[]{1, ai, ob.isAsc() ? 1 : 0});
+          } else if (ctx.getMinSegmentGroupTrimSize() > 0) {
+            return null;  // an ORDER BY the trim cannot evaluate (expression over aggregations): CPU plan
+          }
+        }
+      }
+      d.add(order.size());
+      for (int[] o : order) {
+        for (int x : o) {
+          d.add(x);
+        }
+      }
+      d.add(ctx.getLimit());
+      d.add(ctx.getMinSegmentGroupTrimSize());
       int[] desc = d.stream().mapToInt(Integer::intValue).toArray();
       return new GpuQuery(desc, b._strings.toArray(new String[0]), ctx.getNumGroupsLimit(), ctx.getEndTimeMs());
     } catch (UnsupportedOperationException e) {

@@ -143,6 +143,7 @@ JNIEXPORT jlong JNICALL FN(queryExecute)(JNIEnv* env, jclass c, jlong ctx, jintA
   ph_predicate* preds = NULL;
   const char** gby = NULL;
   ph_aggregation* aggs = NULL;
+  ph_order_by* order = NULL;
   int32_t* ints = NULL;
   const char** vals = NULL;
   ph_result* res = NULL;
@@ -206,6 +207,21 @@ JNIEXPORT jlong JNICALL FN(queryExecute)(JNIEnv* env, jclass c, jlong ctx, jintA
       NEXT(aggs[i].expr_op);
     }
   }
+  /* optional trailing block: [numOrderBy, (kind, index, asc) x numOrderBy, limit, minSegmentGroupTrimSize] */
+  if (k < nd) {
+    NEXT(q.num_order_by);
+    if (q.num_order_by < 0 || q.num_order_by > nd - k) goto bad;
+    order = (ph_order_by*)calloc((size_t)q.num_order_by + 1, sizeof(ph_order_by));
+    if (!order) goto bad;
+    for (int i = 0; i < q.num_order_by; ++i) {
+      NEXT(order[i].kind);
+      NEXT(order[i].index);
+      NEXT(order[i].asc);
+    }
+    NEXT(q.limit);
+    NEXT(q.min_segment_group_trim_size);
+    q.order_by = order;
+  }
   /* indices inside the query (children, predicates, root) are range-checked by ph_query_execute itself */
   q.filter_nodes = nodes;
   q.predicates = preds;
@@ -228,7 +244,7 @@ JNIEXPORT jlong JNICALL FN(queryExecute)(JNIEnv* env, jclass c, jlong ctx, jintA
 bad:
   throw_illegal(env, "malformed GPU query descriptor");
 done:
-  free(nodes); free(preds); free(gby); free(aggs); free(ints); free(vals);
+  free(nodes); free(preds); free(gby); free(aggs); free(ints); free(vals); free(order);
   utf_strings_release(env, &us);
   if (desc) (*env)->ReleaseIntArrayElements(env, descArr, desc, JNI_ABORT);
   (*env)->PopLocalFrame(env, NULL);

@@ -371,10 +371,40 @@ def _plan_filter(f, seg: OracleSegment, col_index: Dict[str, int]):
     raise ValueError(f.type)
 
 
+def _index_based(k: _Leaf) -> bool:
+    """A child whose docIdSet iterator is Sorted- or BitmapBased (AndDocIdSet.java:80-100; an OR of such children
+    merges into one bitmap, OrDocIdSet.java:33-52)."""
+    if k.kind == "leaf":
+        return not k.is_scan
+    if k.kind == "or":
+        return all(_index_based(c) for c in k.children)
+    return False
+
+
+def _mark_apply_and(node: _Leaf) -> _Leaf:
+    """ANDs of index-based children and scan leaves run the scans one after another over the index-based result
+    (AndDocIdSet.java:128-170, ScanBasedDocIdIterator.applyAnd): the scans count |D0| + |D0 n S1| + ... entries, not
+    numDocs each.  Children are ordered as FilterOperatorUtils.reorderAndFilterChildOperators (:197-241) leaves them
+    for the statistic: index-based first, then the scans in query order (every SV scan has SCAN_PRIORITY)."""
+    if node.kind == "and":
+        idx = [k for k in node.children if _index_based(k)]
+        scans = [k for k in node.children if k.kind == "leaf" and k.is_scan]
+        if idx and scans and len(idx) + len(scans) == len(node.children) and len(scans) < 256:
+            node.children = idx + scans
+            node.apply_and = (len(idx), len(scans))
+            for k in scans:
+                k.counted_by_and = True
+            return node
+    for c in node.children:
+        _mark_apply_and(c)
+    return node
+
+
 def _emit(node: _Leaf, out: list, keep: list):
     if node.kind == "leaf":
         keep.append(node.match)
-        out.append((OR_F_LEAF, node.col_index, node.match.ctypes.data, int(node.is_scan)))
+        counted = node.is_scan and not getattr(node, "counted_by_and", False)
+        out.append((OR_F_LEAF, node.col_index, node.match.ctypes.data, int(counted)))
     elif node.kind == "all":
         out.append((OR_F_ALL, 0, None, 0))
     elif node.kind == "none":
@@ -383,7 +413,8 @@ def _emit(node: _Leaf, out: list, keep: list):
         for c in node.children:
             _emit(c, out, keep)
         code = {"and": OR_F_AND, "or": OR_F_OR, "not": OR_F_NOT}[node.kind]
-        out.append((code, len(node.children), None, 0))
+        ia = getattr(node, "apply_and", None)
+        out.append((code, len(node.children), None, (ia[0] << 8 | ia[1]) if ia else 0))
 
 
 # --------------------------------------------------------------------------- execution
@@ -466,7 +497,7 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> Oracl
         seg_structs[si].columns = cols
         prog = []
         if q.filter is not None:
-            _emit(_plan_filter(q.filter, s, col_index), prog, keep)
+            _emit(_mark_apply_and(_plan_filter(q.filter, s, col_index)), prog, keep)
         filter_programs.append(prog)
 
     stats = [0, 0, 0, 0, False]
@@ -479,6 +510,10 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> Oracl
     merged_keys: Dict[int, int] = {}
     merged: List[list] = []
     key_list: List[int] = []
+    # GroupByOperator.java:114-130 segment group trim: ORDER BY + minSegmentGroupTrimSize > 0 ->
+    # GroupByUtils.getTableCapacity(limit, min) = max(5 * limit, min) groups per segment
+    seg_trim = int(q.options.get("minSegmentGroupTrimSize", -1)) if hasattr(q, "options") else -1
+    trim_size = max(5 * q.limit, seg_trim) if (q.group_by and q.order_by and seg_trim > 0) else None
     if True:
         # one or_execute per segment: each segment has its own dictId-space filter program
         for si in range(len(segments)):
@@ -492,7 +527,10 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> Oracl
             one = (_Segment * 1)(seg_structs[si])
             res = _Result()
             LIB.or_execute(ctypes.byref(qs), one, 1, 1, ctypes.byref(res))
-            _merge(res, q, merged_keys, merged, key_list, nagg, hll_idx, m)
+            keep_rows = None
+            if trim_size is not None and res.num_groups > trim_size:
+                keep_rows = _segment_trim(res, q, segments[si], unions, nagg, trim_size)
+            _merge(res, q, merged_keys, merged, key_list, nagg, hll_idx, m, keep_rows)
             stats[0] += res.num_docs_scanned
             stats[1] += res.num_entries_scanned_in_filter
             stats[2] += res.num_entries_scanned_post_filter
@@ -561,7 +599,7 @@ def execute_timed(q, segments: Sequence[OracleSegment], num_threads: int):
         seg_structs[si].num_docs, seg_structs[si].num_columns, seg_structs[si].columns = s.num_docs, len(used), cols
         prog = []
         if q.filter is not None:
-            _emit(_plan_filter(q.filter, s, col_index), prog, keep)
+            _emit(_mark_apply_and(_plan_filter(q.filter, s, col_index)), prog, keep)
         progs.append(prog)
     prog = progs[0]
     ops = (_FilterOp * max(1, len(prog)))()
@@ -608,7 +646,91 @@ def _default_row(q, m):
     return row
 
 
-def _merge(res, q, merged_keys, merged, key_list, nagg, hll_idx, m):
+def _java_compare(a, b) -> int:
+    """Comparable.compareTo of the boxed ORDER BY values: Long / Integer natural order, Double.compare (NaN
+    largest, -0.0 < 0.0), String.compareTo."""
+    if isinstance(a, float) or isinstance(b, float):
+        a, b = float(a), float(b)
+        if a < b:
+            return -1
+        if a > b:
+            return 1
+        ka = 0x7ff8000000000000 if a != a else int(np.array(a).view(np.int64))
+        kb = 0x7ff8000000000000 if b != b else int(np.array(b).view(np.int64))
+        return (ka > kb) - (ka < kb)
+    return (a > b) - (a < b)
+
+
+def _segment_trim(res, q, seg: OracleSegment, unions, nagg, size):
+    """TableResizer.trimInSegmentResults (TableResizer.java:321-343, makeHeap / downHeap :233-262) over one segment's
+    groups fed in ArrayBasedHolder order (ascending raw key over the segment's dictIds, column 0 least significant,
+    DictionaryBasedGroupKeyGenerator.java:254-377).  Returns the indices of the kept rows of `res`."""
+    n = res.num_groups
+    gkeys = np.ctypeslib.as_array(res.keys, (n,))
+    aggs = np.ctypeslib.as_array(res.aggs, (n * max(nagg, 1),)).reshape(n, max(nagg, 1))
+    recs = []
+    for g in range(n):
+        k, raw, mult, vals = int(gkeys[g]), 0, 1, []
+        for gi, u in enumerate(unions):
+            v = u[k % len(u)]
+            k //= len(u)
+            d = seg.columns[q.group_by[gi]].dictionary
+            raw += int(np.searchsorted(d, v)) * mult
+            mult *= len(d)
+            vals.append(_py(v))
+        ob = []
+        for o in q.order_by:
+            if o.kind == "aggregation":
+                f = q.aggregations[o.ref].function
+                ob.append(int(aggs[g, o.ref]) if f == "COUNT" else float(aggs[g, o.ref]))
+            else:
+                ob.append(vals[q.group_by.index(o.ref)])
+        recs.append((raw, g, ob))
+    recs.sort(key=lambda r: r[0])
+    asc = [o.asc for o in q.order_by]
+
+    def inter(a, b):  # the intermediate-record comparator
+        for i, (x, y) in enumerate(zip(a[2], b[2])):
+            c = _java_compare(x, y)
+            if not asc[i]:
+                c = -c
+            if c:
+                return c
+        return 0
+
+    def cmp(a, b):  # reversed
+        return inter(b, a)
+
+    heap = recs[:size]
+
+    def down(i):
+        e = heap[i]
+        while True:
+            child = 2 * i + 1
+            if child >= size:
+                break
+            t = heap[child]
+            right = child + 1
+            if right < size and cmp(heap[right], t) < 0:
+                child = right
+                t = heap[child]
+            if cmp(e, t) <= 0:
+                break
+            heap[i] = t
+            i = child
+        heap[i] = e
+    i = size >> 1
+    while i != 0:
+        i -= 1
+        down(i)
+    for r in recs[size:]:
+        if cmp(r, heap[0]) > 0:
+            heap[0] = r
+            down(0)
+    return set(r[1] for r in heap)
+
+
+def _merge(res, q, merged_keys, merged, key_list, nagg, hll_idx, m, keep_rows=None):
     n = res.num_groups
     if n == 0:
         return
@@ -618,6 +740,8 @@ def _merge(res, q, merged_keys, merged, key_list, nagg, hll_idx, m):
     if hll_idx:
         hll = np.ctypeslib.as_array(res.hll, (n * len(hll_idx) * m,)).reshape(n, len(hll_idx), m)
     for g in range(n):
+        if keep_rows is not None and g not in keep_rows:
+            continue
         k = int(keys[g])
         row = []
         for j, a in enumerate(q.aggregations):

@@ -312,6 +312,19 @@ static int eval_filter_doc(const or_query* q, const or_segment* s, int32_t doc, 
         break;
       }
       case OR_F_AND: {
+        if (op->is_scan) {
+          /* applyAnd (AndDocIdSet.java:168-170, SVScanDocIdIterator.applyAnd :115-142): the doc reaches the first
+           * scan if every index-based child matched, scan i+1 if it also passed scans 1..i */
+          const int nidx = op->is_scan >> 8, nscan = op->is_scan & 255;
+          const int* kid = stack + sp - op->arg;
+          int ok = 1;
+          for (int k = 0; k < nidx; k++) ok &= kid[k];
+          if (ok) {
+            int fed = 1;
+            for (int k = 0; k + 1 < nscan && kid[nidx + k]; k++) fed++;
+            *scanned += fed;
+          }
+        }
         int v = 1;
         for (int k = 0; k < op->arg; k++) v &= stack[--sp];
         stack[sp++] = v;
@@ -421,7 +434,7 @@ static void run_segment(const or_query* q, const or_segment* s, seg_result* r) {
         const or_filter_op* op = &q->filter[0];
         const or_column* c = &s->columns[op->arg];
         or_fixed_bit_read_range(c->fwd, next_doc, c->bits, lim, dict_buf);
-        r->in_filter += lim;
+        if (op->is_scan) r->in_filter += lim;  /* an index-based leaf read through its forward index scans nothing */
         for (int32_t i = 0; i < lim; i++)
           if (op->match[dict_buf[i]]) doc_ids[cnt++] = next_doc + i;
       } else {

@@ -63,7 +63,8 @@ typedef struct {
   int32_t op;                 /* OR_F_* */
   int32_t arg;                /* LEAF: column index ; AND/OR: number of children */
   const uint8_t* match;       /* LEAF: per-dictId 0/1 */
-  int32_t is_scan;            /* LEAF: counted in numEntriesScannedInFilter */
+  int32_t is_scan;            /* LEAF: counted in numEntriesScannedInFilter; AND: nidx << 8 | nscan when its children
+                                 are nidx index-based ones then nscan scans (applyAnd statistic), else 0 */
 } or_filter_op;               /* postfix program */
 
 enum { OR_AGG_COUNT = 0, OR_AGG_SUM = 1, OR_AGG_MIN = 2, OR_AGG_MAX = 3, OR_AGG_HLL = 4 };

@@ -13,6 +13,7 @@ void fail(int code, const std::string& msg) { throw Error{code, msg}; }
 ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc);
 ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const* segs, int32_t nseg,
                               const DenseArgs* dense);
+ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* const* segs, int32_t nseg);  // trim.cpp
 }  // namespace ph
 
 using namespace ph;
@@ -215,7 +216,10 @@ int ph_query_execute(ph_ctx* ctx, const ph_query* query, ph_segment* const* segm
   return guarded([&] {
     if (!ctx || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
     *out = nullptr;
-    *out = query_execute_impl(&ctx->c, query, segments, num_segments, nullptr);
+    if (query && query->min_segment_group_trim_size > 0 && query->num_group_by > 0 && query->num_order_by > 0)
+      *out = segment_trim_execute(&ctx->c, query, segments, num_segments);  // GroupByOperator segment trim
+    else
+      *out = query_execute_impl(&ctx->c, query, segments, num_segments, nullptr);
   });
 }
 

@@ -159,6 +159,8 @@ struct DevSegment {
   const uint32_t* fptr;  // FK_SET bitset over dictIds ; FK_BITMAP doc bitmap
   const uint32_t* keep;  // numGroupsLimit: bitset over global keys this segment may aggregate (nullptr: all)
   int32_t nconj;                    // FK_CONJ leaves
+  int32_t conj_nidx;                // FK_CONJ: > 0 when the AND is an applyAnd one -- its first conj_nidx leaves
+                                    // are range-index leaves, the rest scans (filter-entry statistic)
   int32_t cstream[kMaxConj];        // FK_CONJ: staged stream of leaf k
   uint32_t clo[kMaxConj], clen[kMaxConj];  // FK_CONJ range leaf k: [clo, clo + clen)
   const uint32_t* cset[kMaxConj];   // FK_CONJ set leaf k: bitset over dictIds (nullptr: range leaf)
@@ -241,6 +243,7 @@ struct KParams {
   int32_t lds_hll_off;
   unsigned long long* out_count;  // [num_groups] matched docs per group
   unsigned long long* matched_total;  // group-by plans: matched docs of the launch (numDocsScanned), or nullptr
+  unsigned long long* filter_entries; // applyAnd filter entries of the launch (programs with flagged ANDs), or nullptr
   uint32_t* first_doc;            // non-null: this launch is the numGroupsLimit first-seen pass (DevSegment.first_doc)
   unsigned long long* hkeys;      // MODE_GROUP_HASH: [num_groups] slot keys (kHashEmpty = free); out_* by slot
   int64_t hmask;                  // MODE_GROUP_HASH: slots - 1 (a power of two >= 2x the distinct keys possible)
@@ -272,6 +275,8 @@ struct KParams {
   int32_t part_reg;               // kernel A = k_part_reg (register-direct decode; 0: the LDS-staged forms)
   int32_t part_ck, part_cv;       // k_part_reg: 16-byte loads per lane of a filter / key stream, of the value stream
   int32_t part_rounds;            // k_part_reg: append rounds (flush + barrier) per tile (1 or 2)
+  int32_t part_variant;           // k_part_reg append form: bit 0 ring quarters XOR-swizzled by partition, bit 1
+                                  // record-less lanes exec-masked (else they add to a per-lane scratch word / slot)
   unsigned long long* ovf_count;  // overflow table (same layout as out_*), merged at the end
   int64_t* ovf_sum;
   int64_t* ovf_min;

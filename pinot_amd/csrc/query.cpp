@@ -48,6 +48,10 @@ struct PNode {
   int bitmap_leaf = -1;               // OP_BITMAP: index into the query's bitmap list
   bool scan = false;
   bool range_index = false;  // a scan-evaluated RangeIndexBasedFilterOperator leaf: index-based for the statistics
+  // AND whose children are index-based leaves (sorted, bitmap, range index, ORs / NOTs of them) followed by scan
+  // leaves: the reference's AndDocIdSet applies the scans one after another to the index-based result
+  // (ScanBasedDocIdIterator.applyAnd), so its filter entries are |D0| + |D0 n S1| + ... (counted on the device)
+  int stats_nidx = 0, stats_nscan = 0;
   std::vector<PNode> kids;
 };
 
@@ -427,6 +431,7 @@ void merge_same_column_leaves(PNode& n, const CardOf& card_of) {
   if (n.kind != L_NODE) return;
   for (auto& k : n.kids) merge_same_column_leaves(k, card_of);
   if (n.op != OP_AND && n.op != OP_OR) return;
+  if (n.stats_nscan) return;  // its scan children stay separate: each is one applyAnd step of the statistic
   const bool is_and = n.op == OP_AND;
   std::map<int, size_t> first_of;  // column slot -> index of its first scan leaf
   std::vector<PNode> kids;
@@ -468,11 +473,52 @@ void merge_same_column_leaves(PNode& n, const CardOf& card_of) {
   n.kids = std::move(out);
 }
 
+// scan leaves whose entries are numDocs each (a lone scan, scans under an OR, a pure-scan AND -- the latter an
+// approximation of AndDocIdIterator's advance-driven count); the scans of an applyAnd AND are counted on the device
 int count_scan_leaves(const PNode& n) {
   if (n.kind != L_NODE) return 0;
   int s = (n.scan && !n.range_index) ? 1 : 0;
-  for (auto& k : n.kids) s += count_scan_leaves(k);
+  for (size_t i = 0; i < n.kids.size(); ++i)
+    if (!(n.stats_nscan && (int)i >= n.stats_nidx)) s += count_scan_leaves(n.kids[i]);
   return s;
+}
+
+// a child whose docIdSet iterator is Sorted- or BitmapBased (AndDocIdSet.java:80-100)
+bool index_based(const PNode& k) {
+  if (k.kind != L_NODE) return false;
+  if (k.op == OP_DOCRANGES || k.op == OP_BITMAP) return true;
+  if (k.scan) return k.range_index;
+  if (k.op == OP_NOT) return k.kids.size() == 1 && k.kids[0].op == OP_BITMAP;  // exclusive inverted-index leaf
+  if (k.op == OP_OR) {
+    for (auto& c : k.kids)
+      if (!index_based(c)) return false;
+    return !k.kids.empty();
+  }
+  return false;
+}
+
+// flag the ANDs of index-based children + scan leaves (and order their children as the reference does: index-based
+// first, scans after them in their original order -- every SV scan has SCAN_PRIORITY, FilterOperatorUtils.java:197-241)
+void mark_apply_and(PNode& n) {
+  if (n.kind != L_NODE) return;
+  if (n.op == OP_AND) {
+    std::vector<PNode> idx, scans;
+    bool ok = true;
+    for (auto& k : n.kids) {
+      if (index_based(k)) idx.push_back(k);
+      else if (k.scan && k.kids.empty()) scans.push_back(k);
+      else ok = false;
+    }
+    if (ok && !idx.empty() && !scans.empty() && scans.size() <= 16) {
+      n.stats_nidx = (int)idx.size();
+      n.stats_nscan = (int)scans.size();
+      n.kids.clear();
+      for (auto& k : idx) n.kids.push_back(std::move(k));
+      for (auto& k : scans) n.kids.push_back(std::move(k));
+      return;
+    }
+  }
+  for (auto& k : n.kids) mark_apply_and(k);
 }
 
 // host-side storage of a segment's program before device upload
@@ -481,6 +527,7 @@ struct SegProgram {
   std::vector<std::pair<size_t, std::vector<uint32_t>>> payloads;  // insn index -> words (set / ranges)
   std::vector<std::pair<size_t, int>> bitmap_refs;                 // insn index -> bitmap leaf
   int depth = 0, max_depth = 0;
+  bool apply_and = false;  // the program counts applyAnd filter entries (FilterInsn OP_AND with len > 0)
 };
 
 void emit(const PNode& n, SegProgram& p) {
@@ -489,6 +536,11 @@ void emit(const PNode& n, SegProgram& p) {
     for (auto& k : n.kids) emit(k, p);
     in.op = n.op;
     in.col = (int32_t)n.kids.size();
+    if (n.op == OP_AND && n.stats_nscan) {  // applyAnd statistic: index-based children, then scan children
+      in.lo = (uint32_t)n.stats_nidx;
+      in.len = (uint32_t)n.stats_nscan;
+      p.apply_and = true;
+    }
     if (n.op != OP_NOT) p.depth -= (int)n.kids.size() - 1;
     p.insns.push_back(in);
     return;
@@ -967,6 +1019,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     PNode root;
     root.kind = L_ALL;
     if (q->filter_root >= 0) root = pl.build(segs[i], q->filter_root, 0);
+    mark_apply_and(root);
     stats.num_entries_scanned_in_filter += (int64_t)segs[i]->num_docs * count_scan_leaves(root);
     merge_same_column_leaves(root, [&](int slot) { return (int64_t)segs[i]->columns.at(slot_names[slot])->cardinality; });
     if (root.kind == L_NONE || segs[i]->num_docs == 0) seg_live[i] = 0;
@@ -1448,6 +1501,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
                                std::all_of(root.kids.begin(), root.kids.end(), conj_leaf))) {
       d.fkind = FK_CONJ;
       d.nconj = single_conj ? 1 : (int32_t)root.kids.size();
+      d.conj_nidx = single_conj ? 0 : root.stats_nidx;  // range-index leaves first (mark_apply_and's order)
+      if (d.conj_nidx) progs[i].apply_and = true;
       for (int k = 0; k < d.nconj; ++k) {
         const PNode& leaf = single_conj ? root : root.kids[k];
         d.cstream[k] = conj_stream.at(leaf.col);
@@ -1641,6 +1696,14 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   if (q->num_group_by > 0) {
     kp.matched_total = scratch.alloc<unsigned long long>(1);
     PH_HIP_CHECK(hipMemsetAsync(kp.matched_total, 0, 8, st));
+  }
+  {
+    bool apply_and = false;
+    for (size_t i = 0; i < progs.size(); ++i) apply_and |= seg_live[i] && progs[i].apply_and;
+    if (apply_and) {
+      kp.filter_entries = scratch.alloc<unsigned long long>(1);
+      PH_HIP_CHECK(hipMemsetAsync(kp.filter_entries, 0, 8, st));
+    }
   }
   // per-segment tile pieces: the 1 KiB wave-loads of a full tile, stream by stream
   for (auto& d : dsegs) fill_tile_pieces(d, kp.nstage, kp.stage_soff, kp.tile_words);
@@ -1839,6 +1902,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           stats.limit_pass = 2;
           init_tables();
           PH_HIP_CHECK(hipMemsetAsync(kp.matched_total, 0, 8, st));
+          if (kp.filter_entries) PH_HIP_CHECK(hipMemsetAsync(kp.filter_entries, 0, 8, st));
           std::vector<char> is_lim(dsegs.size(), 0);
           int32_t maxdocs = 1;
           for (int k : limit_segs) {
@@ -1890,6 +1954,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
             k1.segs = d_segs_opt;
             k1.late_prefetch = 1;
             k1.matched_total = nullptr;
+            k1.filter_entries = nullptr;
             k1.hkeys = hk2;
             k1.hmask = H2 - 1;
             k1.first_doc = first2;
@@ -1905,6 +1970,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         } else {
           init_tables();  // truncation needed: first-seen pass, then the rescan with keep bitsets
           PH_HIP_CHECK(hipMemsetAsync(kp.matched_total, 0, 8, st));
+          if (kp.filter_entries) PH_HIP_CHECK(hipMemsetAsync(kp.filter_entries, 0, 8, st));
         }
       }
       if (!scanned && !limit_segs.empty()) {
@@ -1920,6 +1986,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         PH_HIP_CHECK(hipMemsetAsync(docbits, 0, 4 * (size_t)dbw * limit_segs.size(), st));
         KParams k1 = kp;
         k1.matched_total = nullptr;
+        k1.filter_entries = nullptr;
         k1.late_prefetch = 1;
         k1.first_doc = limit_first;  // the pass flag; each segment writes its own table
         k1.gc_slots = 0;             // the pass aggregates nothing (and its LDS holds only the staging)
@@ -1989,6 +2056,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           kp.part_cv = kp.part_ck == 3 ? 5 : 8;
           kp.part_rounds = 2;  // two append rounds per 2048-doc tile: ~8 records per partition per round
           if (const char* e = getenv("PH_PART_ROUNDS")) kp.part_rounds = atoi(e) == 1 ? 1 : 2;  // tuning knob
+          kp.part_variant = 0;
+          if (const char* e = getenv("PH_PART_VARIANT")) kp.part_variant = atoi(e) & 3;  // tuning knob
           kp.stage_stride = 0;  // no staging
         }
       }
@@ -2132,22 +2201,32 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   stats.device_ms = dev_ms;
   res->mode = mode;
   stats.plan_mode = mode;
+  // words read back with the results: [0] matched docs, [1] applyAnd filter entries, [2..] 3 per limit segment
   if (kp.matched_total && defer_sync) {
     dsc_nlim = limit_scal ? limit_segs.size() : 0;
-    dsc = std::make_unique<PinnedBlock>(ctx, st, 8 * (1 + 3 * dsc_nlim));
+    dsc = std::make_unique<PinnedBlock>(ctx, st, 8 * (2 + 3 * dsc_nlim));
     unsigned long long* dw = dsc->as<unsigned long long>();
+    dw[1] = 0;
     PH_HIP_CHECK(hipMemcpyAsync(dw, kp.matched_total, 8, hipMemcpyDeviceToHost, st));
-    if (dsc_nlim) PH_HIP_CHECK(hipMemcpyAsync(dw + 1, limit_scal, 24 * dsc_nlim, hipMemcpyDeviceToHost, st));
+    if (kp.filter_entries) PH_HIP_CHECK(hipMemcpyAsync(dw + 1, kp.filter_entries, 8, hipMemcpyDeviceToHost, st));
+    if (dsc_nlim) PH_HIP_CHECK(hipMemcpyAsync(dw + 2, limit_scal, 24 * dsc_nlim, hipMemcpyDeviceToHost, st));
   } else if (kp.matched_total) {
     // group-by: numDocsScanned = matched docs (docs of keys beyond numGroupsLimit included,
     // GroupByOperator.java:106-107) and numGroupsLimitReached of any segment
     const size_t nlim = limit_scal ? limit_segs.size() : 0;
-    std::vector<unsigned long long> sc(1 + 3 * nlim);
+    std::vector<unsigned long long> sc(2 + 3 * nlim, 0);
     PH_HIP_CHECK(hipMemcpyAsync(sc.data(), kp.matched_total, 8, hipMemcpyDeviceToHost, st));
-    if (nlim) PH_HIP_CHECK(hipMemcpyAsync(sc.data() + 1, limit_scal, 24 * nlim, hipMemcpyDeviceToHost, st));
+    if (kp.filter_entries) PH_HIP_CHECK(hipMemcpyAsync(sc.data() + 1, kp.filter_entries, 8, hipMemcpyDeviceToHost, st));
+    if (nlim) PH_HIP_CHECK(hipMemcpyAsync(sc.data() + 2, limit_scal, 24 * nlim, hipMemcpyDeviceToHost, st));
     PH_HIP_CHECK(hipStreamSynchronize(st));
     stats.num_docs_scanned = (int64_t)sc[0];
-    for (size_t t = 0; t < nlim; ++t) stats.num_groups_limit_reached |= sc[1 + 3 * t + 2] != 0;
+    stats.num_entries_scanned_in_filter += (int64_t)sc[1];
+    for (size_t t = 0; t < nlim; ++t) stats.num_groups_limit_reached |= sc[2 + 3 * t + 2] != 0;
+  } else if (kp.filter_entries) {  // aggregation-only
+    unsigned long long fe = 0;
+    PH_HIP_CHECK(hipMemcpyAsync(&fe, kp.filter_entries, 8, hipMemcpyDeviceToHost, st));
+    PH_HIP_CHECK(hipStreamSynchronize(st));
+    stats.num_entries_scanned_in_filter += (int64_t)fe;
   }
   if (dop == DENSE_EXECUTE) {
     // partial tables stay on the device for the cross-GPU reduction
@@ -2194,7 +2273,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if (dsc) {
       const unsigned long long* dw = dsc->as<unsigned long long>();
       stats.num_docs_scanned = (int64_t)dw[0];
-      for (size_t t = 0; t < dsc_nlim; ++t) stats.num_groups_limit_reached |= dw[1 + 3 * t + 2] != 0;
+      stats.num_entries_scanned_in_filter += (int64_t)dw[1];
+      for (size_t t = 0; t < dsc_nlim; ++t) stats.num_groups_limit_reached |= dw[2 + 3 * t + 2] != 0;
       dsc.reset();
     }
   };

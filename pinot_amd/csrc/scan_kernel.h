@@ -71,8 +71,11 @@ __device__ __forceinline__ uint32_t unpack_col(ColRef c, uint32_t doc) {
 
 // Postfix filter program over a bit stack (bit 0 = top).  Control flow is wave-uniform: every lane of a
 // wave runs the same instruction sequence on its own doc.
+// `fent` gains this doc's applyAnd filter entries: at an AND flagged with (lo = index-based children, len = scan
+// children after them), the doc is fed to the first scan if every index-based child matched, and to scan i + 1 if
+// it also passed scans 1..i (ScanBasedDocIdIterator.applyAnd, AndDocIdSet.java:168-170)
 __device__ __forceinline__ bool eval_filter(const PH_CONST FilterInsn* prog, int32_t n, SegPtr S,
-                                            uint32_t doc) {
+                                            uint32_t doc, uint32_t& fent) {
   uint32_t st = 0;
   for (int32_t i = 0; i < n; ++i) {
     const PH_CONST FilterInsn* gi = prog + i;
@@ -109,6 +112,15 @@ __device__ __forceinline__ bool eval_filter(const PH_CONST FilterInsn* prog, int
       case OP_AND: {
         const uint32_t m = (1u << in.col) - 1u;
         b = (st & m) == m;
+        if (in.len) {  // applyAnd statistic (kid i sits at bit col - 1 - i)
+          const uint32_t ns = in.len, kids = st & m;
+          const uint32_t imask = ((1u << in.lo) - 1u) << ns;  // index-based children: the top lo bits
+          if ((kids & imask) == imask) {
+            const uint32_t miss = ~kids & ((1u << ns) - 1u);  // failed scans; scan j at bit ns - 1 - j
+            const uint32_t lead = miss ? (uint32_t)__builtin_clz(miss) - (32u - ns) : ns;  // leading passes
+            fent += 1u + min(lead, ns - 1u);
+          }
+        }
         st = ((st >> in.col) << 1) | b;
         break;
       }
@@ -451,6 +463,7 @@ struct ValCap {
 // Per-wave accumulation state of the scan (registers).
 struct ScanAcc {
   unsigned long long matched;  // wave-uniform
+  uint32_t fent;               // per lane: applyAnd filter entries (eval_filter)
   int64_t isum[kMaxVals], vmin[kMaxVals], vmax[kMaxVals];
   double dsum[kMaxVals];
 };
@@ -473,6 +486,7 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
   uint32_t clo[FK == FK_CONJ ? kMaxConj : 1], clen[FK == FK_CONJ ? kMaxConj : 1];
   const uint32_t* cset[FK == FK_CONJ ? kMaxConj : 1];
   const int nconj = FK == FK_CONJ ? S->nconj : 0;
+  const int cnidx = FK == FK_CONJ ? S->conj_nidx : 0;
   if constexpr (FK == FK_CONJ) {
 #pragma unroll
     for (int k = 0; k < kMaxConj; ++k) {
@@ -533,14 +547,25 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
     } else if constexpr (FK == FK_DOCRANGE) {
       hit &= (doc - flo) < flen;
     } else if constexpr (FK == FK_GENERIC && LATE) {
-      if (hit) hit = eval_filter((const PH_CONST FilterInsn*)p.prog + S->prog_off, S->prog_len, S, doc);
+      if (hit) hit = eval_filter((const PH_CONST FilterInsn*)p.prog + S->prog_off, S->prog_len, S, doc, acc.fent);
     } else if constexpr (FK == FK_CONJ) {
+      uint32_t pb = 0;  // leaf k passed -> bit k
 #pragma unroll
       for (int k = 0; k < kMaxConj; ++k) {
         if (k >= nconj) continue;
         const uint32_t v = cursor_value(ccur[k], u);
-        if (LATE && cset[k]) hit &= (bool)((gld(cset[k] + (v >> 5)) >> (v & 31u)) & 1u);
-        else hit &= (v - clo[k]) < clen[k];
+        bool pk;
+        if (LATE && cset[k]) pk = (bool)((gld(cset[k] + (v >> 5)) >> (v & 31u)) & 1u);
+        else pk = (v - clo[k]) < clen[k];
+        hit &= pk;
+        pb |= (uint32_t)pk << k;
+      }
+      if (cnidx && doc < ndocs) {  // applyAnd statistic (see eval_filter): leading range-index leaves, then scans
+        const uint32_t im = (1u << cnidx) - 1u, ns = (uint32_t)(nconj - cnidx);
+        if ((pb & im) == im) {
+          const uint32_t lead = (uint32_t)__builtin_ctz(~(pb >> cnidx));
+          acc.fent += 1u + min(lead, ns - 1u);
+        }
       }
     }
     return hit;
@@ -852,6 +877,7 @@ __global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : kBlock) 
 
   ScanAcc acc;
   acc.matched = 0;
+  acc.fent = 0;
 #pragma unroll
   for (int j = 0; j < VC; ++j) {
     acc.isum[j] = 0;
@@ -1062,6 +1088,10 @@ __global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : kBlock) 
   if (threadIdx.x == 0 && s_matched && (MODE == MODE_COUNT || MODE == MODE_AGG))
     atomicAdd(&p.out_count[0], s_matched);
   if (threadIdx.x == 0 && s_matched && p.matched_total) atomicAdd(p.matched_total, s_matched);
+  if (p.filter_entries) {  // the wave's applyAnd filter entries
+    const int64_t fe = wave_sum_i64((int64_t)acc.fent);
+    if ((threadIdx.x & 63) == 0 && fe) atomicAdd(p.filter_entries, (unsigned long long)fe);
+  }
 }
 
 template <class K>

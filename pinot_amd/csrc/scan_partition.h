@@ -36,7 +36,7 @@ __device__ __forceinline__ void part_flush_listed(const KParams& p, uint8_t* sme
     const uint32_t out = n & ~(CH - 1u), left = n - out;
     const uint32_t g = gpos[b];
     Rec* ring = slots + ((size_t)b << cl);
-    const uint32_t sw = SWZ ? ring_swizzle(b, C) : 0u;  // physical slot = logical ^ sw (whole quarters move)
+    const uint32_t sw = (SWZ && (p.part_variant & 1)) ? ring_swizzle(b, C) : 0u;  // physical = logical ^ sw
     // reads: quarters i and i + 8 of the outgoing records (C / PQ <= 16), leftovers i and i + 8 (< CH <= 16)
     u32x4 q0 = {0u, 0u, 0u, 0u}, q1 = {0u, 0u, 0u, 0u};
     const uint32_t r0 = i * PQ, r1 = (i + 8u) * PQ;
@@ -86,7 +86,7 @@ __device__ __forceinline__ void part_flush_final(const KParams& p, uint8_t* smem
   for (uint32_t t = threadIdx.x; t < total; t += BLOCK) {
     const uint32_t b = t >> 4, i = t & 15u;
     const uint32_t n = pend[b], g = gpos[b];  // n < 16 after the listed flushes
-    const uint32_t sw = SWZ ? ring_swizzle(b, 1u << cl) : 0u;
+    const uint32_t sw = (SWZ && (p.part_variant & 1)) ? ring_swizzle(b, 1u << cl) : 0u;
     if (i < n) part_store<REC64>(p, b, g + i, slots[((size_t)b << cl) + (i ^ sw)]);
     if (i == 0) {
       p.part_count[(size_t)b * gridDim.x + blockIdx.x] = g + n;  // records of region (b, blockIdx)

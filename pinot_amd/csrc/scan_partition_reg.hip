@@ -146,6 +146,9 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
   const uint32_t C = 1u << cl;
   constexpr uint32_t CH = 16;  // 32-bit records per 64-byte chunk
   const int halves = p.part_rounds == 2 ? 2 : 1;
+  const bool swz = (p.part_variant & 1) != 0, masked = (p.part_variant & 2) != 0;
+  const uint32_t dummy_word = P + (uint32_t)lane;           // scratch word / slot of a record-less lane
+  const uint32_t dummy_slot = (P << cl) + (uint32_t)lane;
   Tile t0 = next_tile();
   load(t0);
   // per lane and doc j of the tile: X[j] = the 32-bit record ((key & kmask) << vbits | value offset); PB packs two
@@ -222,19 +225,30 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
           bk[q] = (J & 1) ? (PB[J >> 1] >> 16) : (PB[J >> 1] & 0xffffu);
           rec[q] = X[J];
         });
-        // lanes without a record issue no LDS operation (exec-masked, not a scratch word): half of config 3's lanes,
-        // whose addresses would otherwise add bank conflicts to every rank atomic and slot store
-        static_for<0, 4>([&](auto q) {
-          w[q] = C;
-          if (bk[q] < P) w[q] = atomicAdd(&pend[bk[q]], 1u);
-        });
+        // append form (part_variant): record-less lanes either exec-masked (bit 1: no LDS operation) or sent to their
+        // lane's scratch word / slot (branch-free); ring quarters XOR-swizzled by partition (bit 0) or not
         bool ovf = false, full = false;
-        static_for<0, 4>([&](auto q) {
-          const bool h = bk[q] < P;
-          ovf |= h & (w[q] >= C);
-          full |= h & (w[q] == CH - 1u);
-          if (h & (w[q] < C)) slots[(bk[q] << cl) + (w[q] ^ ring_swizzle(bk[q], C))] = rec[q];
-        });
+        if (masked) {
+          static_for<0, 4>([&](auto q) {
+            w[q] = C;
+            if (bk[q] < P) w[q] = atomicAdd(&pend[bk[q]], 1u);
+          });
+          static_for<0, 4>([&](auto q) {
+            const bool h = bk[q] < P;
+            ovf |= h & (w[q] >= C);
+            full |= h & (w[q] == CH - 1u);
+            if (h & (w[q] < C)) slots[(bk[q] << cl) + (w[q] ^ (swz ? ring_swizzle(bk[q], C) : 0u))] = rec[q];
+          });
+        } else {
+          static_for<0, 4>([&](auto q) { w[q] = atomicAdd(&pend[min(bk[q], dummy_word)], 1u); });
+          static_for<0, 4>([&](auto q) {
+            const bool h = bk[q] < P;
+            const bool ok = h & (w[q] < C);
+            ovf |= h & (w[q] >= C);
+            full |= h & (w[q] == CH - 1u);
+            slots[ok ? (bk[q] << cl) + (w[q] ^ (swz ? ring_swizzle(bk[q], C) : 0u)) : dummy_slot] = rec[q];
+          });
+        }
         if (__ballot(full)) {
           static_for<0, 4>([&](auto q) {
             if (bk[q] < P && w[q] == CH - 1u) fl[atomicAdd(fc, 1u)] = bk[q];

@@ -1,0 +1,270 @@
+// trim.cpp -- segment group trim (GroupByOperator.java:114-130) for ph_query_execute.
+//
+// With a group-by, ORDER BY and minSegmentGroupTrimSize > 0, the reference trims every segment's groups to
+// GroupByUtils.getTableCapacity(limit, minSegmentGroupTrimSize) = max(5 * limit, min) (GroupByUtils.java:40-42)
+// before the combine: TableResizer.trimInSegmentResults (TableResizer.java:321-343) fills a heap with the first
+// `size` groups of the segment's group-key iterator, orders it with the reversed ORDER BY comparator (makeHeap /
+// downHeap, :233-262) and replaces the heap top with every later group that compares greater; the kept groups' partial
+// aggregates are what GroupByCombineOperator merges (IndexedTable upsert -> AggregationFunction.merge).
+//
+// Here each segment runs as its own query on the GPU (the one-launch combine over all segments cannot drop a
+// segment's groups), its rows are put in the iterator order of the reference's ArrayBasedHolder -- ascending raw key
+// over the segment's dictIds, column 0 least significant (DictionaryBasedGroupKeyGenerator.java:254-377) -- and
+// trimmed by the same heap; the kept rows of all segments are merged on the host.  When the segment's cardinality
+// product exceeds the ArrayBased threshold the reference iterates a hash map instead (IntGroupIdMap slot order /
+// fastutil order); the kept set is the same unless ORDER BY values tie at the trim boundary.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "ph_internal.h"
+
+namespace ph {
+
+ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const* segs, int32_t nseg,
+                              const DenseArgs* dn);
+
+namespace {
+
+// Java's Double.compare / Float.compare order (NaN largest, -0.0 < 0.0): the natural order of the boxed values
+int java_double_compare(double a, double b) {
+  if (a < b) return -1;
+  if (a > b) return 1;
+  int64_t x, y;
+  memcpy(&x, &a, 8);
+  memcpy(&y, &b, 8);
+  if (std::isnan(a)) x = 0x7ff8000000000000LL;
+  if (std::isnan(b)) y = 0x7ff8000000000000LL;
+  return x == y ? 0 : (x < y ? -1 : 1);
+}
+
+struct Row {
+  std::string key;          // the group-by values' bytes, column after column (entry sizes of the result)
+  std::vector<double> d;    // per aggregation: SUM/MIN/MAX value (COUNT in c)
+  std::vector<int64_t> c;   // per aggregation: COUNT
+  std::vector<std::vector<uint8_t>> hll;
+  uint64_t raw = 0;         // ArrayBasedHolder raw key over the segment's dictIds
+};
+
+}  // namespace
+
+ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* const* segs, int32_t nseg) {
+  const int ng = q->num_group_by, na = q->num_aggregations;
+  for (int k = 0; k < q->num_order_by; ++k) {
+    const ph_order_by& o = q->order_by[k];
+    if (o.kind == PH_ORDER_AGGREGATION) {
+      if (o.index < 0 || o.index >= na) fail(PH_ERR_BAD_QUERY, "ORDER BY aggregation index");
+      if (q->aggregations[o.index].type == PH_AGG_DISTINCTCOUNTHLL)
+        fail(PH_ERR_UNSUPPORTED, "segment group trim ordered by DISTINCTCOUNTHLL");
+    } else if (o.index < 0 || o.index >= ng) {
+      fail(PH_ERR_BAD_QUERY, "ORDER BY group-by index");
+    }
+  }
+  const int64_t trim = std::max<int64_t>((int64_t)q->limit * 5, q->min_segment_group_trim_size);
+  ph_query one = *q;
+  one.min_segment_group_trim_size = 0;
+  auto out = std::make_unique<ph_result>();
+  out->ctx = ctx;
+  std::unordered_map<std::string, size_t> index;
+  std::vector<Row> merged;
+  std::vector<int32_t> key_size(ng, 0);
+  bool typed = false;
+  for (int32_t s = 0; s < nseg; ++s) {
+    std::unique_ptr<ph_result> r(query_execute_impl(ctx, &one, segs + s, 1, nullptr));
+    ph_exec_stats& st = out->stats;
+    const ph_exec_stats& rs = r->stats;
+    st.num_docs_scanned += rs.num_docs_scanned;
+    st.num_entries_scanned_in_filter += rs.num_entries_scanned_in_filter;
+    st.num_entries_scanned_post_filter += rs.num_entries_scanned_post_filter;
+    st.num_total_docs += rs.num_total_docs;
+    st.num_segments_processed += rs.num_segments_processed;
+    st.num_segments_matched += rs.num_segments_matched;
+    st.num_groups_limit_reached |= rs.num_groups_limit_reached;
+    st.sum_precision_flag |= rs.sum_precision_flag;
+    st.device_ms += rs.device_ms;
+    st.host_ms += rs.host_ms;
+    st.plan_mode = rs.plan_mode;
+    st.scan_kernel = rs.scan_kernel;
+    st.limit_pass = std::max(st.limit_pass, rs.limit_pass);
+    if (!typed) {
+      out->key_types = r->key_types;
+      out->key_entry_size = r->key_entry_size;
+      out->agg_types = r->agg_types;
+      out->agg_log2m = r->agg_log2m;
+      out->mode = r->mode;
+      key_size = r->key_entry_size;
+      typed = true;
+    }
+    const int64_t n = r->num_groups;
+    std::vector<Row> rows((size_t)n);
+    ph_segment* seg = segs[s];
+    for (int64_t g = 0; g < n; ++g) {
+      Row& row = rows[(size_t)g];
+      uint64_t mult = 1;
+      for (int c = 0; c < ng; ++c) {
+        const int w = r->key_entry_size[c];
+        const uint8_t* kp = r->keys[c].data() + (size_t)g * w;
+        row.key.append(reinterpret_cast<const char*>(kp), (size_t)w);
+        // the key's dictId in this segment's dictionary (ArrayBasedHolder raw key)
+        const Column& col = *seg->columns.at(q->group_by[c]);
+        const Dictionary& d = col.dict;
+        int64_t id = 0;
+        switch (r->key_types[c]) {
+          case PH_INT: { int32_t v; memcpy(&v, kp, 4); id = std::lower_bound(d.ints.begin(), d.ints.end(), (int64_t)v) - d.ints.begin(); break; }
+          case PH_LONG: { int64_t v; memcpy(&v, kp, 8); id = std::lower_bound(d.ints.begin(), d.ints.end(), v) - d.ints.begin(); break; }
+          case PH_FLOAT: {
+            float v; memcpy(&v, kp, 4);
+            id = std::lower_bound(d.reals.begin(), d.reals.end(), (double)v, [](double a, double b) { return java_double_compare(a, b) < 0; }) - d.reals.begin();
+            break;
+          }
+          case PH_DOUBLE: {
+            double v; memcpy(&v, kp, 8);
+            id = std::lower_bound(d.reals.begin(), d.reals.end(), v, [](double a, double b) { return java_double_compare(a, b) < 0; }) - d.reals.begin();
+            break;
+          }
+          default: {  // STRING: zero-padded bytes
+            std::string v(reinterpret_cast<const char*>(kp), strnlen(reinterpret_cast<const char*>(kp), (size_t)w));
+            id = std::lower_bound(d.strings.begin(), d.strings.end(), v) - d.strings.begin();
+          }
+        }
+        row.raw += (uint64_t)id * mult;
+        mult *= (uint64_t)std::max<int64_t>(1, d.size);
+      }
+      row.d.assign((size_t)na, 0.0);
+      row.c.assign((size_t)na, 0);
+      row.hll.resize((size_t)na);
+      for (int k = 0; k < na; ++k) {
+        const int t = r->agg_types[k];
+        const uint8_t* ap = r->aggs[k].data();
+        if (t == PH_AGG_COUNT) {
+          memcpy(&row.c[k], ap + 8 * g, 8);
+        } else if (t == PH_AGG_DISTINCTCOUNTHLL) {
+          const size_t m = (size_t)1 << r->agg_log2m[k];
+          row.hll[k].assign(ap + m * g, ap + m * (g + 1));
+        } else {
+          memcpy(&row.d[k], ap + 8 * g, 8);
+        }
+      }
+    }
+    if (n > trim) {
+      // TableResizer: the intermediate-record comparator over the ORDER BY values, reversed for the heap
+      auto cmp_inter = [&](const Row& a, const Row& b) -> int {
+        for (int k = 0; k < q->num_order_by; ++k) {
+          const ph_order_by& o = q->order_by[k];
+          int c = 0;
+          if (o.kind == PH_ORDER_AGGREGATION) {
+            const int j = o.index;
+            if (r->agg_types[j] == PH_AGG_COUNT) c = a.c[j] < b.c[j] ? -1 : (a.c[j] > b.c[j] ? 1 : 0);
+            else c = java_double_compare(a.d[j], b.d[j]);
+          } else {
+            size_t off = 0;
+            for (int x = 0; x < o.index; ++x) off += (size_t)key_size[x];
+            const int w = key_size[o.index];
+            const uint8_t* pa = reinterpret_cast<const uint8_t*>(a.key.data()) + off;
+            const uint8_t* pb = reinterpret_cast<const uint8_t*>(b.key.data()) + off;
+            switch (r->key_types[o.index]) {
+              case PH_INT: { int32_t x, y; memcpy(&x, pa, 4); memcpy(&y, pb, 4); c = x < y ? -1 : (x > y ? 1 : 0); break; }
+              case PH_LONG: { int64_t x, y; memcpy(&x, pa, 8); memcpy(&y, pb, 8); c = x < y ? -1 : (x > y ? 1 : 0); break; }
+              case PH_FLOAT: { float x, y; memcpy(&x, pa, 4); memcpy(&y, pb, 4); c = java_double_compare(x, y); break; }
+              case PH_DOUBLE: { double x, y; memcpy(&x, pa, 8); memcpy(&y, pb, 8); c = java_double_compare(x, y); break; }
+              default: c = memcmp(pa, pb, (size_t)w); c = c < 0 ? -1 : (c > 0 ? 1 : 0);  // UTF-8 byte order
+            }
+          }
+          if (!o.asc) c = -c;
+          if (c) return c;
+        }
+        return 0;
+      };
+      auto cmp = [&](const Row* a, const Row* b) { return cmp_inter(*b, *a); };  // reversed
+      std::vector<const Row*> order;
+      order.reserve(rows.size());
+      for (auto& row : rows) order.push_back(&row);
+      std::stable_sort(order.begin(), order.end(), [](const Row* a, const Row* b) { return a->raw < b->raw; });
+      const int64_t size = trim;
+      std::vector<const Row*> heap(order.begin(), order.begin() + size);
+      auto down_heap = [&](int64_t i) {  // TableResizer.downHeap (fastutil ObjectHeaps)
+        const Row* e = heap[(size_t)i];
+        int64_t child;
+        while ((child = (i << 1) + 1) < size) {
+          const Row* t = heap[(size_t)child];
+          const int64_t right = child + 1;
+          if (right < size && cmp(heap[(size_t)right], t) < 0) {
+            child = right;
+            t = heap[(size_t)child];
+          }
+          if (cmp(e, t) <= 0) break;
+          heap[(size_t)i] = t;
+          i = child;
+        }
+        heap[(size_t)i] = e;
+      };
+      for (int64_t i = size >> 1; i-- != 0;) down_heap(i);  // makeHeap
+      for (size_t x = (size_t)size; x < order.size(); ++x) {
+        if (cmp(order[x], heap[0]) > 0) {
+          heap[0] = order[x];
+          down_heap(0);
+        }
+      }
+      std::vector<Row> kept;
+      kept.reserve((size_t)size);
+      for (const Row* h : heap) kept.push_back(*h);
+      rows.swap(kept);
+    }
+    // GroupByCombineOperator: merge into the server table (AggregationFunction.merge)
+    for (auto& row : rows) {
+      auto it = index.find(row.key);
+      if (it == index.end()) {
+        index.emplace(row.key, merged.size());
+        merged.push_back(std::move(row));
+        continue;
+      }
+      Row& dst = merged[it->second];
+      for (int k = 0; k < na; ++k) {
+        const int t = out->agg_types[k];
+        if (t == PH_AGG_COUNT) dst.c[k] += row.c[k];
+        else if (t == PH_AGG_SUM) dst.d[k] += row.d[k];
+        else if (t == PH_AGG_MIN) dst.d[k] = std::min(dst.d[k], row.d[k]);
+        else if (t == PH_AGG_MAX) dst.d[k] = std::max(dst.d[k], row.d[k]);
+        else
+          for (size_t i = 0; i < dst.hll[k].size(); ++i) dst.hll[k][i] = std::max(dst.hll[k][i], row.hll[k][i]);
+      }
+    }
+  }
+  // the combined rows as a result (host vectors)
+  const int64_t R = (int64_t)merged.size();
+  out->num_groups = R;
+  out->keys.resize((size_t)ng);
+  out->aggs.resize((size_t)na);
+  if (!typed) {  // no segment: an empty result with the query's shape
+    std::unique_ptr<ph_result> r(query_execute_impl(ctx, &one, segs, 0, nullptr));
+    return r.release();
+  }
+  size_t off = 0;
+  for (int c = 0; c < ng; ++c) {
+    const int w = key_size[c];
+    out->keys[c].assign((size_t)w * R, 0);
+    for (int64_t g = 0; g < R; ++g) memcpy(out->keys[c].data() + (size_t)w * g, merged[(size_t)g].key.data() + off, (size_t)w);
+    off += (size_t)w;
+  }
+  for (int k = 0; k < na; ++k) {
+    const int t = out->agg_types[k];
+    if (t == PH_AGG_DISTINCTCOUNTHLL) {
+      const size_t m = (size_t)1 << out->agg_log2m[k];
+      out->aggs[k].assign(m * R, 0);
+      for (int64_t g = 0; g < R; ++g) memcpy(out->aggs[k].data() + m * g, merged[(size_t)g].hll[k].data(), m);
+    } else {
+      out->aggs[k].assign(8 * (size_t)R, 0);
+      for (int64_t g = 0; g < R; ++g) {
+        if (t == PH_AGG_COUNT) memcpy(out->aggs[k].data() + 8 * g, &merged[(size_t)g].c[k], 8);
+        else memcpy(out->aggs[k].data() + 8 * g, &merged[(size_t)g].d[k], 8);
+      }
+    }
+  }
+  return out.release();
+}
+
+}  // namespace ph

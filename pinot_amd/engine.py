@@ -86,17 +86,17 @@ def check_plan_supported(q: QueryContext):
     """The plan maker's GPU gate for query options whose reference semantics the GPU path does not reproduce;
     the caller then runs the CPU plan (GpuInstancePlanMaker falls back to InstancePlanMakerImplV2).
 
-    * Segment group trim (GroupByOperator.java:118-130): with ORDER BY and ``minSegmentGroupTrimSize`` > 0 each
-      segment keeps only its top max(5 * limit, minSegmentGroupTrimSize) groups by the ORDER BY values
-      (GroupByUtils.getTableCapacity) before the combine, so the reference's result is an approximation that
-      depends on per-segment partial aggregates.  The GPU aggregates all segments in one pass (exact), hence
-      UNSUPPORTED rather than a different answer.  The default (-1, InstancePlanMakerImplV2.java:97) is off.
+    * Segment group trim (GroupByOperator.java:114-130, ORDER BY + ``minSegmentGroupTrimSize`` > 0) runs in the
+      library (ph_query.min_segment_group_trim_size): per-segment tables, TableResizer.trimInSegmentResults' heap,
+      then the combine.  An ORDER BY over DISTINCTCOUNTHLL is the one trim shape it leaves to the CPU plan.
     * Server trim (IndexedTable.java:63-91, resize when the table exceeds ``groupTrimThreshold``) needs no gate:
       its finish keeps the top records by the same ORDER BY, so the broker's final ORDER BY ... LIMIT over the
       GPU's exact (untrimmed) groups is the same result whenever the reference's own merge is exact."""
     seg_trim = int(q.options.get("minSegmentGroupTrimSize", -1))
     if q.group_by and q.order_by and seg_trim > 0:
-        raise N.UnsupportedError(N.PH_ERR_UNSUPPORTED, "minSegmentGroupTrimSize > 0 (segment group trim)")
+        for ob in q.order_by:
+            if ob.kind == "aggregation" and q.aggregations[ob.ref].function == DISTINCTCOUNTHLL:
+                raise N.UnsupportedError(N.PH_ERR_UNSUPPORTED, "segment group trim ordered by DISTINCTCOUNTHLL")
 
 
 class _QueryStruct:
@@ -157,9 +157,19 @@ class _QueryStruct:
         if "timeoutMs" in q.options:
             import time
             end_ms = int(time.time() * 1000) + int(q.options["timeoutMs"])
+        obs = []
+        for ob in q.order_by:
+            if ob.kind == "aggregation":
+                obs.append(N.OrderBy(N.PH_ORDER_AGGREGATION, int(ob.ref), int(ob.asc)))
+            elif ob.ref in q.group_by:
+                obs.append(N.OrderBy(N.PH_ORDER_GROUP_BY, q.group_by.index(ob.ref), int(ob.asc)))
+        ob_arr = (N.OrderBy * max(1, len(obs)))(*obs)
+        self.keep.append(ob_arr)
+        seg_trim = int(q.options.get("minSegmentGroupTrimSize", -1))
         self.struct = N.Query(len(nodes), node_arr, root, len(preds), pred_arr, len(q.group_by), gb,
                               len(q.aggregations), aggs, q.num_groups_limit, end_ms,
-                              ctypes.pointer(interrupt) if interrupt is not None else None)
+                              ctypes.pointer(interrupt) if interrupt is not None else None,
+                              len(obs), ob_arr, int(q.limit), seg_trim)
 
 
 _KEY_DTYPE = {N.PH_INT: np.int32, N.PH_LONG: np.int64, N.PH_FLOAT: np.float32, N.PH_DOUBLE: np.float64}

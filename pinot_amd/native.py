@@ -86,13 +86,22 @@ class Aggregation(ctypes.Structure):
                 ("column2", ctypes.c_char_p), ("expr_op", ctypes.c_int32)]
 
 
+class OrderBy(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("index", ctypes.c_int32), ("asc", ctypes.c_int32)]
+
+
+PH_ORDER_GROUP_BY, PH_ORDER_AGGREGATION = 0, 1
+
+
 class Query(ctypes.Structure):
     _fields_ = [("num_filter_nodes", ctypes.c_int32), ("filter_nodes", ctypes.POINTER(FilterNode)),
                 ("filter_root", ctypes.c_int32), ("num_predicates", ctypes.c_int32),
                 ("predicates", ctypes.POINTER(Predicate)), ("num_group_by", ctypes.c_int32),
                 ("group_by", ctypes.POINTER(ctypes.c_char_p)), ("num_aggregations", ctypes.c_int32),
                 ("aggregations", ctypes.POINTER(Aggregation)), ("num_groups_limit", ctypes.c_int64),
-                ("end_time_ms", ctypes.c_int64), ("interrupt", ctypes.POINTER(ctypes.c_int32))]
+                ("end_time_ms", ctypes.c_int64), ("interrupt", ctypes.POINTER(ctypes.c_int32)),
+                ("num_order_by", ctypes.c_int32), ("order_by", ctypes.POINTER(OrderBy)), ("limit", ctypes.c_int32),
+                ("min_segment_group_trim_size", ctypes.c_int32)]
 
 
 PH_MAX_DENSE_TABLES = 16

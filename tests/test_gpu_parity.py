@@ -59,6 +59,26 @@ def test_reference_kat_on_gpu(ctx, sv, sql, rows, stats, src):
     assert r.stats.num_entries_scanned_post_filter == post
 
 
+@pytest.mark.parametrize("where", [
+    " WHERE column1 > 100000000 AND column3 BETWEEN 20000000 AND 1000000000 AND daysSinceEpoch = 126164076",
+    " WHERE (column7 = 363 OR column11 = 'P') AND column9 > 1000000 AND column1 < 900000000 AND column3 > 5",
+    " WHERE column6 = 1095 AND column1 > 100000000",
+])
+def test_apply_and_filter_entries_gpu(ctx, sv, where):
+    # ANDs of index-based children + scans: numEntriesScannedInFilter = |D0| + |D0 n S1| + ... (applyAnd), counted
+    # per doc by the flagged AND of the GPU program; the oracle's count is pinned by a numpy restatement
+    # (test_oracle_kat.py::test_apply_and_filter_entries)
+    from oracle import oracle as O
+    q = parse_sql("SELECT COUNT(*) FROM testTable" + where)
+    r = ctx.execute(q, sv)
+    e = O.execute(q, [O.build_segment("kat", kat_sv.load_columns(), inverted=kat_sv.INVERTED)] * 4)
+    assert r.stats.num_entries_scanned_in_filter == e.stats.num_entries_scanned_in_filter
+    assert reduce_groups(q, r.keys, r.aggs).rows == reduce_groups(q, e.keys, e.aggs).rows
+    q2 = parse_sql("SELECT column9, COUNT(*) FROM testTable" + where + " GROUP BY column9 ORDER BY column9 LIMIT 10")
+    r2 = ctx.execute(q2, sv)
+    assert r2.stats.num_entries_scanned_in_filter == e.stats.num_entries_scanned_in_filter
+
+
 def test_kat_filter_entries_gpu(ctx, sv):
     r = ctx.execute(parse_sql("SELECT COUNT(*) FROM testTable" + kat_sv.FILTER), sv)
     assert r.stats.num_entries_scanned_in_filter == 3 * 120000

@@ -148,14 +148,16 @@ def test_expression_result_column_names():
 
 
 def test_segment_group_trim_gate():
-    # minSegmentGroupTrimSize > 0 with ORDER BY: the reference trims per segment (an approximation), so the GPU
-    # plan declines (UNSUPPORTED -> CPU plan); -1 (the default) and queries without ORDER BY stay on the GPU path
+    # minSegmentGroupTrimSize > 0 with ORDER BY runs on the GPU path (per-segment tables + the TableResizer heap,
+    # trim.cpp); only an ORDER BY over DISTINCTCOUNTHLL declines (UNSUPPORTED -> CPU plan)
     from pinot_amd.engine import check_plan_supported
     from pinot_amd.native import UnsupportedError
     from pinot_amd.query import parse_sql
     base = "SELECT a, SUM(m) FROM t GROUP BY a"
+    check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=100; " + base + " ORDER BY SUM(m) DESC LIMIT 5"))
     with pytest.raises(UnsupportedError):
-        check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=100; " + base + " ORDER BY SUM(m) DESC LIMIT 5"))
+        check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=100; SELECT a, DISTINCTCOUNTHLL(m) FROM t "
+                                       "GROUP BY a ORDER BY DISTINCTCOUNTHLL(m) DESC LIMIT 5"))
     check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=-1; " + base + " ORDER BY SUM(m) DESC LIMIT 5"))
     check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=100; " + base + " LIMIT 5"))
     check_plan_supported(parse_sql(base + " ORDER BY a LIMIT 5"))

@@ -51,9 +51,45 @@ def test_reference_kat(sv_segments, sql, rows, stats, src):
         assert st.num_entries_scanned_post_filter == stats[1]
 
 
+APPLY_AND = [
+    # (filter, numpy expectation per segment): ANDs of index-based children (sorted daysSinceEpoch, inverted column6 /
+    # column7 EQ, an OR of inverted leaves) and scans: |D0| + |D0 n S1| + ... (AndDocIdSet.java:128-170 applyAnd)
+    (" WHERE column1 > 100000000 AND column3 BETWEEN 20000000 AND 1000000000 AND daysSinceEpoch = 126164076",
+     lambda c: _apply_and(c, [c["daysSinceEpoch"] == 126164076],
+                          [c["column1"] > 100000000, (c["column3"] >= 20000000) & (c["column3"] <= 1000000000)])),
+    (" WHERE (column7 = 363 OR column11 = 'P') AND column9 > 1000000 AND column1 < 900000000 AND column3 > 5",
+     lambda c: _apply_and(c, [(c["column7"] == 363) | (c["column11"] == "P")],
+                          [c["column9"] > 1000000, c["column1"] < 900000000, c["column3"] > 5])),
+]
+
+
+def _apply_and(c, idx, scans):
+    d = np.ones(len(c["column1"]), bool)
+    for m in idx:
+        d &= m
+    total = 0
+    for s in scans:
+        if s.all():  # matches every dictionary value: a MatchAll child, dropped from the AND (FilterPlanNode)
+            continue
+        total += int(d.sum())
+        d &= s
+    return total
+
+
+@pytest.mark.parametrize("k", range(len(APPLY_AND)))
+def test_apply_and_filter_entries(sv_segments, k):
+    # the oracle's applyAnd statistic against an independent numpy restatement of the reference's order of work
+    where, expect = APPLY_AND[k]
+    cols = {c: v for c, (v, _) in kat_sv.load_columns().items()}
+    _, st = run("SELECT COUNT(*) FROM testTable" + where, sv_segments)
+    assert st.num_entries_scanned_in_filter == 4 * expect(cols)
+
+
 def test_kat_filter_entries_definition(sv_segments):
-    # Under this build's definition every scan leaf is evaluated on every doc: column1 (RANGE, scan) and
-    # column3 (RANGE, scan) and column6 (RANGE on an inverted column -> scan; FilterOperatorUtils.java:97-104).
+    # The KAT filter's AND holds an OR with a scan child (column6 RANGE: RANGE never uses the inverted index,
+    # FilterOperatorUtils.java:97-104), which the reference drives with advance() calls (AndDocIdIterator /
+    # OrDocIdIterator: 252 256 entries, reproduced by tools-free simulation in DESIGN.md); this build counts such
+    # shapes as numDocs per scan leaf: column1, column3 and column6.
     _, st = run("SELECT COUNT(*) FROM testTable" + kat_sv.FILTER, sv_segments)
     assert st.num_entries_scanned_in_filter == 3 * 120000
 
@@ -141,3 +177,88 @@ def test_hll_serialized_layout_against_reference_fixture():
     words = np.frombuffer(b[8:], dtype=">u4")
     dec = [(int(words[i // 6]) >> (5 * (i % 6))) & 31 for i in range(256)]
     assert dec == regs.tolist()
+
+
+def test_segment_trim_heap_keeps_the_top_groups():
+    # TableResizer's heap (oracle._segment_trim) keeps exactly the top `size` groups when the ORDER BY values are
+    # distinct; a trimmed segment's dropped groups lose that segment's partial aggregates in the combine
+    rng = np.random.default_rng(5)
+    n = 20_000
+    t = {"a": (rng.integers(0, 100, n).astype(np.int32), "INT"), "m": (rng.permutation(n).astype(np.int32), "INT")}
+    seg = O.build_segment("trim", t)
+    q = parse_sql("SET minSegmentGroupTrimSize=30; SELECT a, MAX(m) FROM t GROUP BY a ORDER BY MAX(m) DESC LIMIT 2")
+    r = O.execute(q, [seg])
+    full = O.execute(parse_sql("SELECT a, MAX(m) FROM t GROUP BY a ORDER BY MAX(m) DESC LIMIT 1000"), [seg])
+    top = sorted(zip(full.keys, [row[0] for row in full.aggs]), key=lambda x: -x[1])[:30]
+    assert sorted(r.keys) == sorted(k for k, _ in top)
+
+
+def _and_or_iterator_entries(c):
+    """The KAT filter's reference iterator tree on one segment, simulated: AndDocIdSet (AndDocIdSet.java:128-185)
+    merges the sorted daysSinceEpoch range, applies the column1 and column3 scans to it (applyAnd) and ANDs the result
+    with the remaining OR(column6 RANGE scan, column11 NOT IN bitmap) through AndDocIdIterator.next / advance
+    (AndDocIdIterator.java:38-75) and OrDocIdIterator.advance (OrDocIdIterator.java:73-101), whose scan child counts
+    every doc it examines (SVScanDocIdIterator.advance :101-112)."""
+    n = len(c["column1"])
+    d0 = c["daysSinceEpoch"] == 126164076
+    s1 = c["column1"] > 100000000
+    s2 = (c["column3"] >= 20000000) & (c["column3"] <= 1000000000)
+    cand = np.nonzero(d0 & s1 & s2)[0]
+    o1 = np.nonzero(c["column6"] < 500000000)[0]
+    o2 = np.nonzero(~np.isin(c["column11"], ["t", "P"]))[0]
+    scanned = [int(d0.sum() + (d0 & s1).sum())]  # the two applyAnd steps
+
+    def scan_advance(t):
+        i = np.searchsorted(o1, t)
+        if i < len(o1):
+            scanned[0] += int(o1[i]) - t + 1
+            return int(o1[i])
+        scanned[0] += n - t
+        return -1
+
+    def bitmap_advance(t):
+        i = np.searchsorted(o2, t)
+        return int(o2[i]) if i < len(o2) else -1
+
+    nxt, alive = [-1, -1], [True, True]
+
+    def or_advance(t):
+        best = None
+        for i, f in ((0, scan_advance), (1, bitmap_advance)):
+            if not alive[i]:
+                continue
+            if nxt[i] < t:
+                nxt[i] = f(t)
+                if nxt[i] == -1:
+                    alive[i] = False
+                    continue
+            best = nxt[i] if best is None else min(best, nxt[i])
+        return -1 if best is None else best
+
+    def r_advance(t):
+        i = np.searchsorted(cand, t)
+        return int(cand[i]) if i < len(cand) else -1
+
+    its, next_doc, matches = [r_advance, or_advance], 0, 0
+    while True:
+        max_doc, max_idx, idx = next_doc, -1, 0
+        while idx < 2:
+            if idx == max_idx:
+                idx += 1
+                continue
+            doc = its[idx](max_doc)
+            if doc == -1:
+                return scanned[0], matches
+            if doc == max_doc:
+                idx += 1
+            else:
+                max_doc, max_idx, idx = doc, idx, 0
+        matches += 1
+        next_doc = max_doc + 1
+
+
+def test_kat_filter_entries_reference_iterators():
+    # InterSegmentAggregationSingleValueQueriesTest.java:58: 252 256 entries over the 4 segments (2 copies x 2 servers)
+    cols = {k: v for k, (v, _) in kat_sv.load_columns().items()}
+    entries, matches = _and_or_iterator_entries(cols)
+    assert 4 * matches == 24516 and 4 * entries == 252256
