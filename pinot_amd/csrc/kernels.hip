@@ -12,6 +12,18 @@ void launch_scan_partition(const KParams& p, int ng, int rec64, int grid, size_t
 void launch_scan_group_hash(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);
 
 void launch_scan(const KParams& p, int mode, int ng, int rec64, int grid, size_t lds, hipStream_t s) {
+  if (mode == MODE_COUNT && p.count_reg) {  // register-direct COUNT over RANGE / ALL / DOCRANGE leaves
+    launch_count_reg(p, grid, s);
+    return;
+  }
+  if (mode == MODE_AGG && p.agg_reg) {  // register-direct form of k_agg_lean
+    launch_agg_reg(p, grid, s);
+    return;
+  }
+  if (mode == MODE_GROUP_LDS && p.group_reg) {  // register-direct form of k_group_lds_lean
+    launch_group_reg(p, ng, grid, lds, s);
+    return;
+  }
   PH_HIP_CHECK(hipGetLastError());  // a failure left by an earlier unchecked call is reported as such, not as ours
   switch (mode) {
     case MODE_COUNT:

@@ -275,6 +275,12 @@ struct KParams {
   int32_t part_reg;               // kernel A = k_part_reg (register-direct decode; 0: the LDS-staged forms)
   int32_t part_ck, part_cv;       // k_part_reg: 16-byte loads per lane of a filter / key stream, of the value stream
   int32_t part_rounds;            // k_part_reg: append rounds (flush + barrier) per tile (1 or 2)
+  int32_t count_reg;              // MODE_COUNT: k_count_reg with this many 16-byte loads per lane (ceil(b / 4)); 0 off
+  int32_t agg_reg;                // MODE_AGG: k_agg_reg (register-direct k_agg_lean)
+  int32_t agg_reg_cf, agg_reg_cv; //   16-byte loads per lane of the filter / value stream
+  int32_t group_reg;              // MODE_GROUP_LDS: k_group_reg (register-direct, lane-interleaved LDS table)
+  int32_t group_reg_lanes_log2;   //   log2 of the slots per key (lane l updates slot key * L + (l & (L - 1)))
+  int32_t group_reg_cf, group_reg_cg, group_reg_cv;  // 16-byte loads per lane: filter / each group / value stream
   int32_t part_variant;           // k_part_reg append form: bit 0 ring quarters XOR-swizzled by partition, bit 1
                                   // record-less lanes exec-masked (else they add to a per-lane scratch word / slot)
   unsigned long long* ovf_count;  // overflow table (same layout as out_*), merged at the end
@@ -298,6 +304,8 @@ struct PartAggParams {
   int32_t pack_cs;        // count and value-offset sum share one 64-bit LDS word (count << 40 | sum)
   int32_t slices;         // workgroups per partition (each aggregates a contiguous range of the regions)
   int32_t dbg;            // timing experiments (PH_PART_DBG bits 4: loads only, 8: no MIN/MAX); results invalid
+  int32_t mm_blind;       // MIN / MAX as one atomic per record each (else read first, atomic only on improvement)
+  int32_t pad;
   int64_t part_vbase;
   int64_t num_groups;
   unsigned long long* out_count;
@@ -552,6 +560,9 @@ size_t part_agg_lds_bytes(const PartAggParams& p);
 size_t partition_lds_bytes(KParams& p);  // fills the pl_* offsets, returns the dynamic LDS size
 int part_reg_blocks_per_cu(const KParams& p, int ng, size_t lds);  // k_part_reg occupancy
 void launch_part_reg(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);  // scan_partition_reg.hip
+void launch_count_reg(const KParams& p, int grid, hipStream_t s);                      // scan_count_reg.hip
+void launch_agg_reg(const KParams& p, int grid, hipStream_t s);                        // scan_count_reg.hip
+void launch_group_reg(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);   // scan_group_reg.hip
 struct MergeParams {
   unsigned long long* out_count;
   int64_t* out_sum;

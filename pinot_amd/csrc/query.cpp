@@ -1744,8 +1744,32 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if (const char* e = getenv("PH_AGG_SPARSE")) kp.agg_sparse = all_bitmap && atoi(e) != 0;  // tuning knob
     if (kp.agg_sparse) kp.agg_fast = 0;
   }
+  // the register-direct COUNT (k_count_reg): every segment a dictId RANGE scan leaf, everything, or a sorted range
+  if (mode == MODE_COUNT && !kp.late_prefetch && getenv("PH_COUNT_GENERIC") == nullptr) {
+    int fb = 1;
+    bool ok = true;
+    for (auto& d : dsegs) {
+      ok = ok && (d.fkind == FK_RANGE || d.fkind == FK_ALL || d.fkind == FK_DOCRANGE);
+      if (d.fkind == FK_RANGE) fb = std::max(fb, (int)d.streams[kp.f_stream].bits);
+    }
+    if (ok && fb <= 32) kp.count_reg = (fb + 3) / 4;
+  }
+  // the register-direct aggregation (k_agg_reg): k_agg_lean's shapes with filter streams <= 32 and value streams
+  // <= 26 bits (32-bit tile sums)
+  if (kp.agg_fast && getenv("PH_AGG_LDS") == nullptr) {
+    int fb = 1, vb = 1;
+    for (auto& d : dsegs) {
+      if (d.fkind == FK_RANGE) fb = std::max(fb, (int)d.streams[kp.f_stream].bits);
+      vb = std::max(vb, (int)d.streams[kp.v_stream[0]].bits);
+    }
+    if (fb <= 32 && vb <= 26) {
+      kp.agg_reg = 1;
+      kp.agg_reg_cf = (fb + 3) / 4;
+      kp.agg_reg_cv = (vb + 3) / 4;
+    }
+  }
   if (const char* e = getenv("PH_DEBUG_FLAGS")) kp.dbg_flags = atoi(e);
-  if (kp.dbg_flags) kp.part_fast = kp.agg_fast = kp.lds_fast = kp.agg_sparse = 0;  // timing experiments: generic form
+  if (kp.dbg_flags) kp.part_fast = kp.agg_fast = kp.lds_fast = kp.agg_sparse = kp.count_reg = kp.agg_reg = 0;
   if (getenv("PH_DEBUG_STAMPS")) {
     kp.dbg = scratch.alloc<unsigned long long>(4 * (size_t)ctx->num_cus * 8);
     PH_HIP_CHECK(hipMemsetAsync(kp.dbg, 0, 32 * (size_t)ctx->num_cus * 8, st));
@@ -1786,6 +1810,32 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       kp.part_vbase = nvals ? vmin : 0;
       if ((size_t)kp.lds_copy_bytes > 64 * 1024) kp.lds_fast = 0;  // not expected: G is an LDS-sized key space
       else lds = std::max(lds, l);
+      // the register-direct form (k_group_reg): <= 2 group columns of <= 16 bits, filter streams <= 32 bits, value
+      // streams <= 32 bits, the packed slot words, and a lane-interleaved table (L slots per key) in <= 52 KiB so
+      // that three workgroups share a CU
+      if (kp.lds_fast && kp.lds_pack && q->num_group_by <= 2 && getenv("PH_LDS_LEAN") == nullptr) {
+        int fb = 1, gb = 1, vb = 1;
+        for (auto& d : dsegs) {
+          if (d.fkind == FK_RANGE) fb = std::max(fb, (int)d.streams[kp.f_stream].bits);
+          for (int g = 0; g < q->num_group_by; ++g) gb = std::max(gb, (int)d.streams[kp.g_stream[g]].bits);
+          if (nvals) vb = std::max(vb, (int)d.streams[kp.v_stream[0]].bits);
+        }
+        const int cf = fb <= 12 ? 3 : 8, cg = gb <= 8 ? 2 : 4, cv = nvals ? (vb <= 16 ? 4 : 8) : 0;
+        constexpr size_t kRegTableBytes = 52 * 1024;
+        int lg = 5;
+        if (const char* e = getenv("PH_GROUP_REG_LG")) lg = std::max(0, std::min(5, atoi(e)));  // tuning knob
+        while (lg > 0 && (size_t)(G + 1) * 16 << lg > kRegTableBytes) --lg;  // + the dummy row of missed docs
+        if (fb <= 32 && gb <= 16 && vb <= 32 && (size_t)(G + 1) * 16 << lg <= kRegTableBytes &&
+            cf + q->num_group_by * cg + cv <= 20) {
+          kp.group_reg = 1;
+          kp.group_reg_lanes_log2 = lg;
+          kp.group_reg_cf = cf;
+          kp.group_reg_cg = cg;
+          kp.group_reg_cv = cv;
+          kp.part_dbg = getenv("PH_GROUP_REG_DBG") ? atoi(getenv("PH_GROUP_REG_DBG")) : 0;  // timing experiments
+          lds = (size_t)(G + 1) * 16 << lg;
+        }
+      }
     }
     if (kp.agg_sparse) {  // no staging: the HLL registers and one matched-doc list (uint16 offsets) per wave
       kp.lds_hll_off = 0;
@@ -1853,9 +1903,13 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       kp.chunk_end = (int32_t)chunks.size();
       int blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1)));
       if (mode == MODE_GROUP_LDS) blocks_per_cu = std::min(blocks_per_cu, 4);
+      if (kp.count_reg || kp.agg_reg) blocks_per_cu = 4;  // 16 waves per CU, each with two tiles of loads in flight
       const int grid = (int)std::min<int64_t>((int64_t)chunks.size(), (int64_t)ctx->num_cus * blocks_per_cu);
-      stats.scan_kernel = kp.agg_sparse ? PH_KERNEL_AGG_SPARSE
+      stats.scan_kernel = kp.count_reg  ? PH_KERNEL_COUNT_REG
+                          : kp.agg_reg    ? PH_KERNEL_AGG_REG
+                          : kp.agg_sparse ? PH_KERNEL_AGG_SPARSE
                           : kp.agg_fast  ? PH_KERNEL_AGG_LEAN
+                          : kp.group_reg  ? PH_KERNEL_GROUP_REG
                           : kp.lds_fast  ? PH_KERNEL_GROUP_LDS_LEAN
                                          : PH_KERNEL_SCAN;
       // device_ms opens here: it covers the numGroupsLimit pass and (below) the bitmap build too
@@ -2140,6 +2194,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       if (const char* e = getenv("PH_PART_SLICES")) slices = std::max(1, std::min(16, atoi(e)));  // tuning knob
       bp.slices = slices;
       bp.dbg = kp.part_dbg;
+      bp.mm_blind = getenv("PH_PART_MM_BLIND") ? atoi(getenv("PH_PART_MM_BLIND")) : 0;  // tuning knob
       bp.regions = grid_a;
       const size_t lds_b = part_agg_lds_bytes(bp);
       Lane& L = *lane.lane;

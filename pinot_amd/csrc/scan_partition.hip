@@ -386,32 +386,9 @@ void launch_scan_partition(const KParams& p, int ng, int rec64, int grid, size_t
 // the LDS table holds COUNT and the value-offset SUM in one 64-bit word (count << 40 | sum, pack_cs) and
 // MIN / MAX offsets in the two halves of a second 64-bit word.  A record reads that min/max word first and
 // issues an LDS atomic only when it improves one of them: over a key's records in random order that is
-// O(log n) atomics instead of 2 per record (min only falls and max only rises, so a stale read is safe).
-template <int REC64>
-__device__ __forceinline__ void part_agg_record(const PartAggParams& p, unsigned long long r, uint32_t vmask,
-                                                uint32_t* cnt, unsigned long long* cs, unsigned long long* sum,
-                                                uint32_t* mm, bool minmax) {
-  uint32_t k, v;
-  if (REC64) {
-    k = (uint32_t)(r >> 32);
-    v = (uint32_t)r;
-  } else {
-    k = (uint32_t)r >> p.part_vbits;
-    v = (uint32_t)r & vmask;
-  }
-  if (p.pack_cs) {
-    atomicAdd(&cs[k], (1ull << 40) | (unsigned long long)v);
-  } else {
-    atomicAdd(&cnt[k], 1u);
-    if (p.has_sum) atomicAdd(&sum[k], (unsigned long long)v);
-  }
-  if (minmax && (p.has_min | p.has_max)) {
-    const unsigned long long cur = *reinterpret_cast<const unsigned long long*>(mm + 2 * k);  // (max << 32 | min)
-    if (p.has_min && v < (uint32_t)cur) atomicMin(&mm[2 * k], v);
-    if (p.has_max && v > (uint32_t)(cur >> 32)) atomicMax(&mm[2 * k + 1], v);
-  }
-}
-
+// O(log n) atomics instead of 2 per record (min only falls and max only rises, so a stale read is safe).  A lane
+// handles its 16 records of a step together: the count/sum atomics, then all 16 min/max reads before the first
+// wait (r3: one read and one wait per record left kernel B latency-bound), then the improving atomics.
 template <int REC64>
 __global__ void __launch_bounds__(1024) k_part_agg(const PartAggParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -426,14 +403,15 @@ __global__ void __launch_bounds__(1024) k_part_agg(const PartAggParams p) {
   size_t off = 0;
   uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);
   unsigned long long* cs = reinterpret_cast<unsigned long long*>(smem);
-  off += p.pack_cs ? 8 * (size_t)KP : 4 * (size_t)KP;
+  const size_t KT = (size_t)KP + 64;  // + one dummy key per lane for padding records (no same-address atomics)
+  off += p.pack_cs ? 8 * KT : 4 * KT;
   off = (off + 7) / 8 * 8;
   unsigned long long* sum = reinterpret_cast<unsigned long long*>(smem + off);
-  off += (p.has_sum && !p.pack_cs) ? 8 * (size_t)KP : 0;
+  off += (p.has_sum && !p.pack_cs) ? 8 * KT : 0;
   uint32_t* mm = reinterpret_cast<uint32_t*>(smem + off);
-  off += (p.has_min | p.has_max) ? 8 * (size_t)KP : 0;
+  off += (p.has_min | p.has_max) ? 8 * KT : 0;
   uint32_t* fill = reinterpret_cast<uint32_t*>(smem + off);
-  for (uint32_t k = threadIdx.x; k < KP; k += blockDim.x) {
+  for (uint32_t k = threadIdx.x; k < (uint32_t)KT; k += blockDim.x) {
     if (p.pack_cs) cs[k] = 0; else cnt[k] = 0;
     if (p.has_sum && !p.pack_cs) sum[k] = 0;
     if (p.has_min | p.has_max) {
@@ -474,19 +452,56 @@ __global__ void __launch_bounds__(1024) k_part_agg(const PartAggParams p) {
           v[q] = *reinterpret_cast<const u32x4*>(src);
         }
       }
+      // the step's RPW * PER records of this lane: key and value offset; a record past its region's fill goes to
+      // the lane's dummy key KP + lane, so the atomics below run without per-record branches
+      uint32_t rk[RPW * PER], rv[RPW * PER];
 #pragma unroll
       for (int q = 0; q < RPW; ++q) {
         const uint32_t i0 = base + lane * PER;
 #pragma unroll
         for (int e = 0; e < PER; ++e) {
-          if (i0 + e >= nn[q]) continue;
           const unsigned long long r = REC64 ? ((unsigned long long)v[q][2 * e + 1] << 32) | v[q][2 * e]
                                              : (unsigned long long)v[q][e];
-          if (p.dbg & 4) {
-            sink ^= r;
-            continue;
+          uint32_t k, x;
+          if (REC64) {
+            k = (uint32_t)(r >> 32);
+            x = (uint32_t)r;
+          } else {
+            k = (uint32_t)r >> p.part_vbits;
+            x = (uint32_t)r & vmask;
           }
-          part_agg_record<REC64>(p, r, vmask, cnt, cs, sum, mm, !(p.dbg & 8));
+          if (p.dbg & 4) sink ^= r;
+          rk[q * PER + e] = (i0 + e < nn[q]) ? k : KP + (uint32_t)lane;
+          rv[q * PER + e] = x;
+        }
+      }
+      if (p.dbg & 4) continue;
+      constexpr int NREC = RPW * PER;
+#pragma unroll
+      for (int i = 0; i < NREC; ++i) {
+        if (p.pack_cs) {
+          atomicAdd(&cs[rk[i]], (1ull << 40) | (unsigned long long)rv[i]);
+        } else {
+          atomicAdd(&cnt[rk[i]], 1u);
+          if (p.has_sum) atomicAdd(&sum[rk[i]], (unsigned long long)rv[i]);
+        }
+      }
+      if ((p.has_min | p.has_max) && !(p.dbg & 8)) {
+        if (p.mm_blind) {  // every record issues its MIN / MAX atomics (no return: nothing waits)
+#pragma unroll
+          for (int i = 0; i < NREC; ++i) {
+            if (p.has_min) atomicMin(&mm[2 * rk[i]], rv[i]);
+            if (p.has_max) atomicMax(&mm[2 * rk[i] + 1], rv[i]);
+          }
+        } else {  // read the step's (min, max) words together, then an atomic only where a record improves one
+          unsigned long long cur[NREC];
+#pragma unroll
+          for (int i = 0; i < NREC; ++i) cur[i] = *reinterpret_cast<const unsigned long long*>(mm + 2 * rk[i]);
+#pragma unroll
+          for (int i = 0; i < NREC; ++i) {
+            if (p.has_min && rv[i] < (uint32_t)cur[i]) atomicMin(&mm[2 * rk[i]], rv[i]);
+            if (p.has_max && rv[i] > (uint32_t)(cur[i] >> 32)) atomicMax(&mm[2 * rk[i] + 1], rv[i]);
+          }
         }
       }
     }
@@ -525,7 +540,7 @@ __global__ void __launch_bounds__(1024) k_part_agg(const PartAggParams p) {
 }
 
 size_t part_agg_lds_bytes(const PartAggParams& p) {
-  const size_t KP = (size_t)1 << p.part_klo;
+  const size_t KP = ((size_t)1 << p.part_klo) + 64;  // + the per-lane dummy keys
   size_t o = p.pack_cs ? 8 * KP : 4 * KP;
   o = (o + 7) / 8 * 8;
   o += (p.has_sum && !p.pack_cs) ? 8 * KP : 0;

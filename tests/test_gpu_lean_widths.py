@@ -1,7 +1,11 @@
 """GPU: the lean kernels' own decode (LaneStream / lds_value, scan_kernel.h) swept over every stream width 1..31
 against the oracle, each query asserting which kernel ran (ph_exec_stats.scan_kernel):
 
+  k_count_reg         COUNT(*) over the filter stream, register-direct decode (filter streams of 1..24 bits)
+  k_agg_reg           aggregation only, register-direct (value streams of 1..26 bits)
   k_agg_lean          aggregation only, one packed integer column (value streams of 1..26 bits)
+  k_group_reg         LDS group table, register-direct decode, lane-interleaved slots (value streams of 1..31 bits;
+                      32 slots per key for 37 keys, 4 for 740 keys, COUNT-only)
   k_group_lds_lean    LDS-private group table (value streams of 1..31 bits)
   k_part_reg          partitioned group-by, register-direct decode (filter streams <= 16 bits; 32-bit records)
   k_part_scan(2)      partitioned group-by, 90 000 keys (value streams of 1..31 bits; 32- and 64-bit records)
@@ -23,6 +27,7 @@ from tests.seeds import seed_of
 pytestmark = pytest.mark.gpu
 
 PH_KERNEL_AGG_LEAN, PH_KERNEL_GROUP_LDS_LEAN, PH_KERNEL_PART_LEAN, PH_KERNEL_PART_LEAN2, PH_KERNEL_PART_REG = 2, 4, 5, 6, 8
+PH_KERNEL_COUNT_REG, PH_KERNEL_AGG_REG, PH_KERNEL_GROUP_REG = 9, 10, 11
 
 
 @pytest.fixture(scope="module")
@@ -46,7 +51,8 @@ def _tables(w):
         fid[:2] = [0, fcard - 1]
         out.append({"m": m, "fid": fid, "fcard": fcard,
                     "g": rng.integers(0, 37, n).astype(np.int32),
-                    "g1": rng.integers(0, 300, n).astype(np.int32), "g2": rng.integers(0, 300, n).astype(np.int32)})
+                    "g1": rng.integers(0, 300, n).astype(np.int32), "g2": rng.integers(0, 300, n).astype(np.int32),
+                    "g3": rng.integers(0, 20, n).astype(np.int32)})
     return out
 
 
@@ -58,13 +64,13 @@ def _segments(ctx, w):
         seg.columns["m"] = create_column("m", t["m"], "LONG")
         fdict = np.arange(t["fcard"], dtype=np.int32)
         seg.columns["f"] = create_column_from_dict_ids("f", fdict, t["fid"], "INT", allow_sorted=False)
-        for c in ("g", "g1", "g2"):
-            t[c][:300 if c != "g" else 37] = np.arange(300 if c != "g" else 37)  # complete dictionaries
+        for c, card in (("g", 37), ("g1", 300), ("g2", 300), ("g3", 20)):
+            t[c][:card] = np.arange(card)  # complete dictionaries
             seg.columns[c] = create_column(c, t[c], "INT")
         gpu.append(ctx.pin(seg))
         ora.append(O.build_segment(seg.name, {"m": (t["m"], "LONG"), "f": (fdict[t["fid"]], "INT"),
                                               "g": (t["g"], "INT"), "g1": (t["g1"], "INT"),
-                                              "g2": (t["g2"], "INT")}))
+                                              "g2": (t["g2"], "INT"), "g3": (t["g3"], "INT")}))
     return gpu, ora, _tables(w)[0]["fcard"]
 
 
@@ -81,11 +87,26 @@ def _check(ctx, gpu, ora, sql, kernel):
 def test_lean_kernels_every_width(ctx, w, monkeypatch):
     gpu, ora, fcard = _segments(ctx, w)
     where = f" WHERE f BETWEEN {fcard // 5} AND {fcard - 1 - fcard // 7}" if fcard > 2 else " WHERE f = 1"
+    # k_count_reg: the register-direct COUNT over the filter stream (width min(w, 24))
+    all_docs = fcard > 2 and fcard // 5 == 0 and fcard // 7 == 0  # the range covers the dictionary: no scan
+    _check(ctx, gpu, ora, f"SELECT COUNT(*) FROM t{where}", 0 if all_docs else PH_KERNEL_COUNT_REG)
     # k_agg_lean: 32-bit tile sums need value offsets below 2^26; wider streams run k_scan<MODE_AGG>
-    _check(ctx, gpu, ora, f"SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where}",
-           PH_KERNEL_AGG_LEAN if w <= 26 else 1)
-    _check(ctx, gpu, ora, f"SELECT g, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where} GROUP BY g ORDER BY g LIMIT 100",
-           PH_KERNEL_GROUP_LDS_LEAN)
+    agg = f"SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where}"
+    _check(ctx, gpu, ora, agg, PH_KERNEL_AGG_REG if w <= 26 else 1)  # register-direct k_agg_reg
+    monkeypatch.setenv("PH_AGG_LDS", "1")
+    _check(ctx, gpu, ora, agg, PH_KERNEL_AGG_LEAN if w <= 26 else 1)  # the LDS-staged k_agg_lean
+    monkeypatch.delenv("PH_AGG_LDS")
+    grp = f"SELECT g, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where} GROUP BY g ORDER BY g LIMIT 100"
+    # k_group_reg keeps COUNT << 40 | SUM in one slot word: value ranges that could carry past 2^40 inside one
+    # workgroup (w >= 29 here) run k_group_lds_lean's unpacked table
+    packed = PH_KERNEL_GROUP_REG if w <= 28 else PH_KERNEL_GROUP_LDS_LEAN
+    _check(ctx, gpu, ora, grp, packed)
+    _check(ctx, gpu, ora, f"SELECT g, g3, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where} GROUP BY g, g3 "
+           f"ORDER BY g, g3 LIMIT 1000", packed)
+    _check(ctx, gpu, ora, f"SELECT g, COUNT(*) FROM t{where} GROUP BY g ORDER BY g LIMIT 100", PH_KERNEL_GROUP_REG)
+    monkeypatch.setenv("PH_LDS_LEAN", "1")  # the LDS-staged k_group_lds_lean
+    _check(ctx, gpu, ora, grp, PH_KERNEL_GROUP_LDS_LEAN)
+    monkeypatch.delenv("PH_LDS_LEAN")
     part = (f"SET numGroupsLimit=2000000; SELECT g1, g2, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where} "
             f"GROUP BY g1, g2 ORDER BY g1, g2 LIMIT 200000")
     # k_part_reg decodes from registers (its own per-width switch): filter / key streams <= 16 bits

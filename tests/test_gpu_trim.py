@@ -41,7 +41,7 @@ SMALL = [  # a x b = 50 x 40 groups: ArrayBasedHolder
     "SET minSegmentGroupTrimSize=30; SELECT a, b, SUM(m), COUNT(*) FROM t WHERE f < 70 GROUP BY a, b "
     "ORDER BY SUM(m) DESC LIMIT 4",
     "SET minSegmentGroupTrimSize=25; SELECT a, b, MAX(m), MIN(d) FROM t GROUP BY a, b ORDER BY b DESC, a LIMIT 3",
-    "SET minSegmentGroupTrimSize=50; SELECT a, COUNT(*), SUM(d) FROM t GROUP BY a ORDER BY COUNT(*), a DESC LIMIT 6",
+    "SET minSegmentGroupTrimSize=30; SELECT a, COUNT(*), SUM(d) FROM t GROUP BY a ORDER BY COUNT(*), a DESC LIMIT 6",
     "SET minSegmentGroupTrimSize=100000; SELECT a, b, COUNT(*) FROM t GROUP BY a, b ORDER BY COUNT(*) DESC LIMIT 5",
 ]
 

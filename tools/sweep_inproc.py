@@ -43,7 +43,7 @@ def main():
         sig = (r.num_groups, float(np.sum(r.agg_columns[0])) if r.agg_columns else 0.0)
         ok = ref is None or sig == ref
         ref = ref or sig
-        print(f"{s:60s} device_ms median {np.median(ms):.3f} min {np.min(ms):.3f} mode {r.stats.mode} "
+        print(f"{s:60s} device_ms median {np.median(ms):.3f} min {np.min(ms):.3f} mode {r.stats.mode} kernel {r.stats.scan_kernel} "
               f"{'same result' if ok else 'RESULT DIFFERS'}", flush=True)
         for k in keys:
             del os.environ[k]
