@@ -1755,8 +1755,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if (ok && fb <= 32) kp.count_reg = (fb + 3) / 4;
   }
   // the register-direct aggregation (k_agg_reg): k_agg_lean's shapes with filter streams <= 32 and value streams
-  // <= 26 bits (32-bit tile sums)
-  if (kp.agg_fast && getenv("PH_AGG_LDS") == nullptr) {
+  // <= 26 bits (32-bit tile sums).  Opt-in (PH_AGG_REG=1): r3 measured it slower than the LDS-staged k_agg_lean on
+  // config3-agg (0.90 vs 0.78 ms: 131 VGPRs hold it at 3 waves per SIMD with one tile of loads in flight)
+  if (kp.agg_fast && getenv("PH_AGG_REG") != nullptr) {
     int fb = 1, vb = 1;
     for (auto& d : dsegs) {
       if (d.fkind == FK_RANGE) fb = std::max(fb, (int)d.streams[kp.f_stream].bits);
@@ -1811,8 +1812,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       if ((size_t)kp.lds_copy_bytes > 64 * 1024) kp.lds_fast = 0;  // not expected: G is an LDS-sized key space
       else lds = std::max(lds, l);
       // the register-direct form (k_group_reg): <= 2 group columns of <= 16 bits, filter streams <= 32 bits, value
-      // streams <= 32 bits, the packed slot words, and a lane-interleaved table (L slots per key) in <= 52 KiB so
-      // that three workgroups share a CU
+      // streams <= 32 bits, the packed slot words, and a lane-interleaved table (L slots per key) in <= 40 KiB so
+      // that four workgroups share a CU (r3, config3-lds: L = 16 at four workgroups per CU 1.08 ms, L = 32 at
+      // three 1.18-1.24 ms -- occupancy beats the 2-way bank sharing of L = 16)
       if (kp.lds_fast && kp.lds_pack && q->num_group_by <= 2 && getenv("PH_LDS_LEAN") == nullptr) {
         int fb = 1, gb = 1, vb = 1;
         for (auto& d : dsegs) {
@@ -1821,7 +1823,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           if (nvals) vb = std::max(vb, (int)d.streams[kp.v_stream[0]].bits);
         }
         const int cf = fb <= 12 ? 3 : 8, cg = gb <= 8 ? 2 : 4, cv = nvals ? (vb <= 16 ? 4 : 8) : 0;
-        constexpr size_t kRegTableBytes = 52 * 1024;
+        constexpr size_t kRegTableBytes = 40 * 1024;
         int lg = 5;
         if (const char* e = getenv("PH_GROUP_REG_LG")) lg = std::max(0, std::min(5, atoi(e)));  // tuning knob
         while (lg > 0 && (size_t)(G + 1) * 16 << lg > kRegTableBytes) --lg;  // + the dummy row of missed docs

@@ -219,7 +219,7 @@ static void launch_group_reg_f(const KParams& p, int grid, size_t lds, hipStream
 }
 
 void launch_group_reg(const KParams& p, int ng, int grid, size_t lds, hipStream_t s) {
-  // the host picks lds <= 52 KiB (three workgroups per CU): no dynamic-LDS attribute needed
+  // the host picks lds <= 40 KiB (four workgroups per CU): no dynamic-LDS attribute needed
   if (ng == 1) launch_group_reg_f<1>(p, grid, lds, s);
   else launch_group_reg_f<2>(p, grid, lds, s);
   PH_HIP_CHECK(hipGetLastError());

@@ -3,6 +3,10 @@
 #include "scan_partition.h"
 #include "reg_decode.h"
 
+#ifndef PH_PART_AB
+#define PH_PART_AB 4
+#endif
+
 namespace ph {
 
 // ------------------------------------------------------------------ kernel A, register-direct form (k_part_reg)
@@ -93,6 +97,7 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
   const int cl = p.part_slot_log2;
   const uint32_t C = 1u << cl;
   constexpr uint32_t CH = 16;  // 32-bit records per 64-byte chunk
+  constexpr int kAB = PH_PART_AB;  // records per lane whose rank atomics are in flight together
   const int halves = p.part_rounds == 2 ? 2 : 1;
   const bool swz = (p.part_variant & 1) != 0, masked = (p.part_variant & 2) != 0;
   const uint32_t dummy_word = P + (uint32_t)lane;           // scratch word / slot of a record-less lane
@@ -165,10 +170,10 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
       lds_barrier();
       uint32_t* fl = lists + par * P;
       uint32_t* fc = lcnt + par;
-      static_for<decltype(jb)::value / 4, decltype(je)::value / 4>([&](auto u) {
-        constexpr int j0 = decltype(u)::value * 4;
-        uint32_t bk[4], w[4], rec[4];
-        static_for<0, 4>([&](auto q) {
+      static_for<decltype(jb)::value / kAB, decltype(je)::value / kAB>([&](auto u) {
+        constexpr int j0 = decltype(u)::value * kAB;
+        uint32_t bk[kAB], w[kAB], rec[kAB];
+        static_for<0, kAB>([&](auto q) {
           constexpr int J = j0 + decltype(q)::value;
           bk[q] = (J & 1) ? (PB[J >> 1] >> 16) : (PB[J >> 1] & 0xffffu);
           rec[q] = X[J];
@@ -177,19 +182,19 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
         // lane's scratch word / slot (branch-free); ring quarters XOR-swizzled by partition (bit 0) or not
         bool ovf = false, full = false;
         if (masked) {
-          static_for<0, 4>([&](auto q) {
+          static_for<0, kAB>([&](auto q) {
             w[q] = C;
             if (bk[q] < P) w[q] = atomicAdd(&pend[bk[q]], 1u);
           });
-          static_for<0, 4>([&](auto q) {
+          static_for<0, kAB>([&](auto q) {
             const bool h = bk[q] < P;
             ovf |= h & (w[q] >= C);
             full |= h & (w[q] == CH - 1u);
             if (h & (w[q] < C)) slots[(bk[q] << cl) + (w[q] ^ (swz ? ring_swizzle(bk[q], C) : 0u))] = rec[q];
           });
         } else {
-          static_for<0, 4>([&](auto q) { w[q] = atomicAdd(&pend[min(bk[q], dummy_word)], 1u); });
-          static_for<0, 4>([&](auto q) {
+          static_for<0, kAB>([&](auto q) { w[q] = atomicAdd(&pend[min(bk[q], dummy_word)], 1u); });
+          static_for<0, kAB>([&](auto q) {
             const bool h = bk[q] < P;
             const bool ok = h & (w[q] < C);
             ovf |= h & (w[q] >= C);
@@ -198,12 +203,12 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
           });
         }
         if (__ballot(full)) {
-          static_for<0, 4>([&](auto q) {
+          static_for<0, kAB>([&](auto q) {
             if (bk[q] < P && w[q] == CH - 1u) fl[atomicAdd(fc, 1u)] = bk[q];
           });
         }
         if (__ballot(ovf)) {
-          static_for<0, 4>([&](auto q) {
+          static_for<0, kAB>([&](auto q) {
             if (bk[q] < P && w[q] >= C) part_overflow<0>(p, bk[q], rec[q]);
           });
         }

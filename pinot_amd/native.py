@@ -9,7 +9,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpinot_hip.so")
+LIB_PATH = os.environ.get("PH_LIB_PATH") or os.path.join(HERE, "libpinot_hip.so")  # override: kernel experiments
 
 PH_OK = 0
 PH_ERR_INVALID_ARGUMENT = 1

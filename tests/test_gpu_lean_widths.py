@@ -92,10 +92,10 @@ def test_lean_kernels_every_width(ctx, w, monkeypatch):
     _check(ctx, gpu, ora, f"SELECT COUNT(*) FROM t{where}", 0 if all_docs else PH_KERNEL_COUNT_REG)
     # k_agg_lean: 32-bit tile sums need value offsets below 2^26; wider streams run k_scan<MODE_AGG>
     agg = f"SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where}"
-    _check(ctx, gpu, ora, agg, PH_KERNEL_AGG_REG if w <= 26 else 1)  # register-direct k_agg_reg
-    monkeypatch.setenv("PH_AGG_LDS", "1")
-    _check(ctx, gpu, ora, agg, PH_KERNEL_AGG_LEAN if w <= 26 else 1)  # the LDS-staged k_agg_lean
-    monkeypatch.delenv("PH_AGG_LDS")
+    _check(ctx, gpu, ora, agg, PH_KERNEL_AGG_LEAN if w <= 26 else 1)  # the LDS-staged k_agg_lean (default)
+    monkeypatch.setenv("PH_AGG_REG", "1")
+    _check(ctx, gpu, ora, agg, PH_KERNEL_AGG_REG if w <= 26 else 1)  # register-direct k_agg_reg (opt-in)
+    monkeypatch.delenv("PH_AGG_REG")
     grp = f"SELECT g, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where} GROUP BY g ORDER BY g LIMIT 100"
     # k_group_reg keeps COUNT << 40 | SUM in one slot word: value ranges that could carry past 2^40 inside one
     # workgroup (w >= 29 here) run k_group_lds_lean's unpacked table
