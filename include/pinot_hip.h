@@ -220,7 +220,8 @@ enum {
   PH_KERNEL_PART_REG = 8,      /* k_part_reg + k_part_agg: partitioned group-by, register-direct decode */
   PH_KERNEL_COUNT_REG = 9,     /* k_count_reg: COUNT(*) over RANGE / ALL / sorted leaves, register-direct decode */
   PH_KERNEL_AGG_REG = 10,      /* k_agg_reg: k_agg_lean's aggregation in the register-direct form */
-  PH_KERNEL_GROUP_REG = 11     /* k_group_reg: k_group_lds_lean's group-by in the register-direct form */
+  PH_KERNEL_GROUP_REG = 11,    /* k_group_reg: k_group_lds_lean's group-by in the register-direct form */
+  PH_KERNEL_GROUP_SPARSE = 12  /* k_group_sparse: group-by over selective inverted-index ANDs, matched-doc gathers */
 };
 
 /* ------------------------------------------------------------------ context */

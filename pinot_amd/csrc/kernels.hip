@@ -20,6 +20,10 @@ void launch_scan(const KParams& p, int mode, int ng, int rec64, int grid, size_t
     launch_agg_reg(p, grid, s);
     return;
   }
+  if ((mode == MODE_GROUP_LDS || mode == MODE_GROUP_GLOBAL) && p.group_sparse && !p.first_doc) {
+    launch_group_sparse(p, mode, grid, lds, s);  // selective bitmap ANDs: gathers of the matched docs
+    return;
+  }
   if (mode == MODE_GROUP_LDS && p.group_reg) {  // register-direct form of k_group_lds_lean
     launch_group_reg(p, ng, grid, lds, s);
     return;

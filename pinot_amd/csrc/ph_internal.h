@@ -84,6 +84,7 @@ enum : int32_t { FK_ALL = 0, FK_RANGE = 1, FK_SET = 2, FK_BITMAP = 3, FK_DOCRANG
 // FilterPlanNode shape of multi-predicate WHERE clauses (AndFilterOperator over ScanBasedFilterOperators), decoded
 // from the staged tile like a single leaf instead of gathered per doc by the generic program
 constexpr int kMaxConj = 4;
+constexpr int kSparseBitmaps = 6;  // k_group_sparse: inverted-index doc bitmaps per segment filter
 
 // How an aggregated numeric column is read:
 //   VK_PACKED   frame-of-reference stream (value - base) in `bits`, built once per column in HBM from the
@@ -165,6 +166,17 @@ struct DevSegment {
   uint32_t clo[kMaxConj], clen[kMaxConj];  // FK_CONJ range leaf k: [clo, clo + clen)
   const uint32_t* cset[kMaxConj];   // FK_CONJ set leaf k: bitset over dictIds (nullptr: range leaf)
   uint32_t* first_doc;              // numGroupsLimit pass: this segment's [num_groups] first matching doc per key
+  // k_group_sparse (KParams::group_sparse): the filter as an AND of sp_nbm inverted-index doc bitmaps (ORs of
+  // consecutive ones where sp_or is set), then sp_nscan
+  // scan leaves (dictId range [sp_lo, sp_lo + sp_len) or bitset sp_set) on column slot sp_slot, evaluated per
+  // matched doc by gathers; sp_stats: the AND is an applyAnd one (numEntriesScannedInFilter).  The segment keeps
+  // its generic program (fkind) for the numGroupsLimit passes.
+  int32_t sp_nbm, sp_nscan, sp_stats, sp_pad;
+  const uint32_t* sp_bm[kSparseBitmaps];
+  int32_t sp_or[kSparseBitmaps];     // bitmap k ORs into bitmap k - 1's group (an OR of inverted leaves)
+  int32_t sp_slot[kMaxConj];
+  uint32_t sp_lo[kMaxConj], sp_len[kMaxConj];
+  const uint32_t* sp_set[kMaxConj];
   DevColumn cols[kMaxCols];
   DevValCol vals[kMaxVals];
   DevValCol vals2[kMaxVals];       // second operand of a 2-operand expression term (KParams::val_op)
@@ -279,6 +291,7 @@ struct KParams {
   int32_t agg_reg;                // MODE_AGG: k_agg_reg (register-direct k_agg_lean)
   int32_t agg_reg_cf, agg_reg_cv; //   16-byte loads per lane of the filter / value stream
   int32_t group_reg;              // MODE_GROUP_LDS: k_group_reg (register-direct, lane-interleaved LDS table)
+  int32_t group_sparse;           // MODE_GROUP_LDS / GLOBAL: k_group_sparse (selective bitmap ANDs, DevSegment sp_*)
   int32_t group_reg_lanes_log2;   //   log2 of the slots per key (lane l updates slot key * L + (l & (L - 1)))
   int32_t group_reg_cf, group_reg_cg, group_reg_cv;  // 16-byte loads per lane: filter / each group / value stream
   int32_t part_variant;           // k_part_reg append form: bit 0 ring quarters XOR-swizzled by partition, bit 1
@@ -563,6 +576,7 @@ void launch_part_reg(const KParams& p, int ng, int grid, size_t lds, hipStream_t
 void launch_count_reg(const KParams& p, int grid, hipStream_t s);                      // scan_count_reg.hip
 void launch_agg_reg(const KParams& p, int grid, hipStream_t s);                        // scan_count_reg.hip
 void launch_group_reg(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);   // scan_group_reg.hip
+void launch_group_sparse(const KParams& p, int mode, int grid, size_t lds, hipStream_t s);  // scan_group_sparse.hip
 struct MergeParams {
   unsigned long long* out_count;
   int64_t* out_sum;

@@ -521,6 +521,50 @@ void mark_apply_and(PNode& n) {
   for (auto& k : n.kids) mark_apply_and(k);
 }
 
+// k_group_sparse's filter shape: one inverted-index leaf, or an AND of 1..kMaxConj of them and <= kMaxConj plain
+// scan leaves (dictId range / set; the applyAnd order of mark_apply_and: index-based kids first)
+struct SparseShape {
+  bool ok = false;
+  std::vector<std::vector<int>> groups;  // AND of ORs of bitmap leaves
+  std::vector<const PNode*> scans;       // scan leaves, in order
+};
+SparseShape sparse_shape(const PNode& r) {
+  SparseShape sh;
+  auto is_bitmap = [](const PNode& k) { return k.kind == L_NODE && k.op == OP_BITMAP; };
+  auto bitmap_or = [&](const PNode& k) {
+    if (k.kind != L_NODE || k.op != OP_OR || k.kids.empty()) return false;
+    for (auto& c : k.kids)
+      if (!is_bitmap(c)) return false;
+    return true;
+  };
+  auto is_scan = [](const PNode& k) {
+    return k.kind == L_NODE && k.scan && !k.range_index && k.kids.empty() && (k.op == OP_RANGE || k.op == OP_SET);
+  };
+  auto add_index = [&](const PNode& k) {
+    if (is_bitmap(k)) {
+      sh.groups.push_back({k.bitmap_leaf});
+      return true;
+    }
+    if (!bitmap_or(k)) return false;
+    sh.groups.emplace_back();
+    for (auto& c : k.kids) sh.groups.back().push_back(c.bitmap_leaf);
+    return true;
+  };
+  if (r.kind == L_NODE && r.op == OP_AND) {
+    for (auto& k : r.kids) {
+      if (add_index(k)) continue;
+      if (!is_scan(k)) return sh;
+      sh.scans.push_back(&k);
+    }
+  } else if (!add_index(r)) {
+    return sh;
+  }
+  size_t nbm = 0;
+  for (auto& g : sh.groups) nbm += g.size();
+  sh.ok = !sh.groups.empty() && nbm <= (size_t)kSparseBitmaps && (int)sh.scans.size() <= kMaxConj;
+  return sh;
+}
+
 // host-side storage of a segment's program before device upload
 struct SegProgram {
   std::vector<FilterInsn> insns;
@@ -1481,6 +1525,39 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<std::pair<size_t, std::vector<uint32_t>>> fset_fix;     // segment index -> FK_SET bitset
   std::vector<std::pair<size_t, int>> fbitmap_fix;                    // segment index -> bitmap leaf
   std::vector<std::pair<size_t, std::vector<uint32_t>>> conj_set_fix; // segment index * kMaxConj + leaf -> bitset
+  std::vector<std::pair<size_t, int>> sbm_fix;                         // segment index * kSparseBitmaps + k -> bitmap leaf
+  std::vector<std::pair<size_t, std::vector<uint32_t>>> sset_fix;     // segment index * kMaxConj + k -> bitset
+  // k_group_sparse: every live segment's filter is a sparse_shape AND whose bitmaps keep < 1/8 of the docs (the
+  // leaves' densities multiplied: an independence estimate) -> gather the matched docs instead of streaming every
+  // referenced column
+  bool sparse_plan = false;
+  if ((mode == MODE_GROUP_LDS || mode == MODE_GROUP_GLOBAL) && num_hll == 0 && nvals <= 1 && q->num_group_by > 0) {
+    bool ok = true;
+    double docs = 0, hits = 0;
+    for (int i = 0; i < nseg && ok; ++i) {
+      if (!seg_live[i]) continue;
+      const SparseShape sh = sparse_shape(roots[i]);
+      ok = sh.ok;
+      const double n = (double)std::max<int64_t>(1, segs[i]->num_docs);
+      double est = n;
+      for (auto& g : sh.groups) {
+        double d = 0;
+        for (int b : g) d += (double)bitmap_docs(*pl.bitmaps[b].col, pl.bitmaps[b].dict_ids) / n;
+        est *= std::min(1.0, d);
+      }
+      for (const PNode* k : sh.scans) {  // uniform dictIds: matched ids / cardinality
+        const double card = (double)std::max<int64_t>(1, segs[i]->columns.at(slot_names[k->col])->cardinality);
+        double ids = k->op == OP_RANGE ? (double)k->len : 0.0;
+        if (k->op == OP_SET)
+          for (uint32_t w : k->set) ids += (double)__builtin_popcount(w);
+        est *= std::min(1.0, ids / card);
+      }
+      hits += sh.ok ? est : 0;
+      docs += (double)segs[i]->num_docs;
+    }
+    sparse_plan = ok && docs > 0 && hits * 8 < docs;
+    if (const char* e = getenv("PH_GROUP_SPARSE")) sparse_plan = ok && docs > 0 && atoi(e) != 0;  // tuning knob
+  }
   std::vector<std::pair<int32_t, int32_t>> dseg_chunks;                // device segment -> its chunk range
   std::vector<int> dseg_src;                                           // device segment -> query segment index
   std::vector<std::pair<int32_t, int32_t>> seg_words;                  // device segment -> [first, end) words to scan
@@ -1543,6 +1620,25 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       for (auto& pp : progs[i].payloads) payload_fix.push_back({d.prog_off + pp.first, pp.second});
       for (auto& bb : progs[i].bitmap_refs) bitmap_fix.push_back({d.prog_off + bb.first, bb.second});
       all_insns.insert(all_insns.end(), progs[i].insns.begin(), progs[i].insns.end());
+    }
+    if (sparse_plan) {
+      const SparseShape sh = sparse_shape(root);
+      d.sp_nbm = 0;
+      for (auto& g : sh.groups)
+        for (size_t j = 0; j < g.size(); ++j) {
+          d.sp_or[d.sp_nbm] = j > 0;
+          sbm_fix.push_back({si * kSparseBitmaps + d.sp_nbm, g[j]});
+          ++d.sp_nbm;
+        }
+      d.sp_nscan = (int32_t)sh.scans.size();
+      d.sp_stats = root.op == OP_AND && root.stats_nscan > 0;
+      for (int k = 0; k < d.sp_nscan; ++k) {
+        const PNode& leaf = *sh.scans[k];
+        d.sp_slot[k] = leaf.col;
+        d.sp_lo[k] = leaf.op == OP_SET ? 0u : leaf.lo;
+        d.sp_len[k] = leaf.op == OP_SET ? 0u : leaf.len;
+        if (leaf.op == OP_SET) sset_fix.push_back({si * kMaxConj + k, leaf.set});
+      }
     }
     for (size_t sl = 0; sl < slot_names.size(); ++sl) {
       Column& c = *s->columns.at(slot_names[sl]);
@@ -1713,12 +1809,19 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if (d.fkind != FK_ALL && d.fkind != FK_RANGE && d.fkind != FK_DOCRANGE) kp.part_fast = 0;
   // the lean aggregation kernel (k_agg_lean) covers one packed integer value column with ALL / RANGE / DOCRANGE
   // leaves; its 32-bit tile sums need value offsets below 2^26
-  kp.agg_fast = mode == MODE_AGG && nvals == 1 && !val_exprs[0] && num_hll == 0 && val_is_int[0] &&
-                !kp.late_prefetch && getenv("PH_AGG_GENERIC") == nullptr;
-  for (auto& d : dsegs)
-    if ((d.fkind != FK_ALL && d.fkind != FK_RANGE && d.fkind != FK_DOCRANGE) || d.vals[0].kind != VK_PACKED ||
-        d.streams[kp.v_stream[0]].bits > 26)
+  //   r3: also FK_CONJ ANDs of range leaves (no applyAnd statistic to count) and integer 2-operand value terms of
+  //   two packed columns (per-doc int64 fold; SSB Q1.x)
+  kp.agg_fast = mode == MODE_AGG && nvals == 1 && num_hll == 0 && val_is_int[0] && !kp.late_prefetch &&
+                getenv("PH_AGG_GENERIC") == nullptr;
+  for (auto& d : dsegs) {
+    if (!kp.agg_fast) break;  // (val_exprs is empty without value columns)
+    bool conj_ok = d.fkind == FK_CONJ && d.conj_nidx == 0;
+    for (int k = 0; conj_ok && k < d.nconj; ++k) conj_ok = d.cset[k] == nullptr && d.clen[k] > 0;
+    if ((d.fkind != FK_ALL && d.fkind != FK_RANGE && d.fkind != FK_DOCRANGE && !conj_ok) ||
+        d.vals[0].kind != VK_PACKED || (!val_exprs[0] && d.streams[kp.v_stream[0]].bits > 26) ||
+        (val_exprs[0] && d.vals2[0].kind != VK_PACKED))
       kp.agg_fast = 0;
+  }
   // the lean LDS group-by (k_group_lds_lean): identity remaps, at most one packed integer value column whose
   // offsets from the table-wide minimum fit 32 bits, ALL / RANGE / DOCRANGE leaves
   kp.lds_fast = mode == MODE_GROUP_LDS && num_hll == 0 && nvals <= 1 && !kp.late_prefetch &&
@@ -1757,9 +1860,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // the register-direct aggregation (k_agg_reg): k_agg_lean's shapes with filter streams <= 32 and value streams
   // <= 26 bits (32-bit tile sums).  Opt-in (PH_AGG_REG=1): r3 measured it slower than the LDS-staged k_agg_lean on
   // config3-agg (0.90 vs 0.78 ms: 131 VGPRs hold it at 3 waves per SIMD with one tile of loads in flight)
-  if (kp.agg_fast && getenv("PH_AGG_REG") != nullptr) {
+  if (kp.agg_fast && !val_exprs[0] && getenv("PH_AGG_REG") != nullptr) {
     int fb = 1, vb = 1;
     for (auto& d : dsegs) {
+      if (d.fkind == FK_CONJ) fb = 64;  // k_agg_reg reads one filter stream
       if (d.fkind == FK_RANGE) fb = std::max(fb, (int)d.streams[kp.f_stream].bits);
       vb = std::max(vb, (int)d.streams[kp.v_stream[0]].bits);
     }
@@ -1839,6 +1943,15 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         }
       }
     }
+    if (sparse_plan) {  // the generic tables (LDS table or group cache) + one matched-doc list per wave
+      kp.pl_misc_off = (int32_t)((stage_bytes + lds_tables + 15) / 16 * 16);  // after the generic layout
+      const size_t l2 = (size_t)kp.pl_misc_off + (size_t)kWaves * kSparseStepWords * 64 * sizeof(uint16_t);
+      if (l2 <= 160 * 1024) {
+        kp.group_sparse = 1;
+        kp.group_reg = 0;
+        lds = l2;
+      }
+    }
     if (kp.agg_sparse) {  // no staging: the HLL registers and one matched-doc list (uint16 offsets) per wave
       kp.lds_hll_off = 0;
       kp.pl_misc_off = (int32_t)(((size_t)num_hll * (m ? m : 1) * 4 + 16 + 15) / 16 * 16);
@@ -1859,12 +1972,18 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     dsegs[ff.first].fptr = dp;
   }
   for (auto& fb : fbitmap_fix) dsegs[fb.first].fptr = bitmap_dev[fb.second];
+  for (auto& sb : sbm_fix) dsegs[sb.first / kSparseBitmaps].sp_bm[sb.first % kSparseBitmaps] = bitmap_dev[sb.second];
+  for (auto& sf : sset_fix) {
+    uint32_t* dp = scratch.alloc<uint32_t>(sf.second.size() + 1);
+    PH_HIP_CHECK(hipMemcpyAsync(dp, sf.second.data(), 4 * sf.second.size(), hipMemcpyHostToDevice, st));
+    dsegs[sf.first / kMaxConj].sp_set[sf.first % kMaxConj] = dp;
+  }
   for (auto& cf : conj_set_fix) {
     uint32_t* dp = scratch.alloc<uint32_t>(cf.second.size() + 1);
     PH_HIP_CHECK(hipMemcpyAsync(dp, cf.second.data(), 4 * cf.second.size(), hipMemcpyHostToDevice, st));
     dsegs[cf.first / kMaxConj].cset[cf.first % kMaxConj] = dp;
   }
-  if (!payload_fix.empty() || !fset_fix.empty() || !conj_set_fix.empty())
+  if (!payload_fix.empty() || !fset_fix.empty() || !conj_set_fix.empty() || !sset_fix.empty())
     PH_HIP_CHECK(hipStreamSynchronize(st));  // pageable copies above
   // the optimistic numGroupsLimit scan's segment table: no keep bitsets, no first-doc tables (copied after every
   // device pointer above is fixed up: r3 copied it before, so FK_CONJ set leaves scanned with null bitsets)
@@ -1911,6 +2030,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
                           : kp.agg_reg    ? PH_KERNEL_AGG_REG
                           : kp.agg_sparse ? PH_KERNEL_AGG_SPARSE
                           : kp.agg_fast  ? PH_KERNEL_AGG_LEAN
+                          : kp.group_sparse ? PH_KERNEL_GROUP_SPARSE
                           : kp.group_reg  ? PH_KERNEL_GROUP_REG
                           : kp.lds_fast  ? PH_KERNEL_GROUP_LDS_LEAN
                                          : PH_KERNEL_SCAN;

@@ -12,7 +12,11 @@ namespace ph {
 // tile, so the 32-bit sum cannot wrap), and the 64-bit absolute values are formed once per tile: SUM =
 // sum(offsets) + matches * base (the match count from the wave's ballots), MIN / MAX = base + min / max offset.
 // No LDS traffic beyond the wave's own staging, no barriers: every wave streams independently.
-template <int FK>
+//
+// Also FK_CONJ filters of range leaves only (an AND of dictId ranges on <= kMaxConj scan streams, no applyAnd
+// statistic) and integer 2-operand value terms `a <op> b` of two packed columns (EX = PH_EXPR_MULT / SUB / ADD: SSB
+// Q1.x's SUM(lo_extendedprice * lo_discount)), which fold per doc in exact int64 like k_scan's value-term path.
+template <int FK, int EX>
 __device__ __forceinline__ void agg_tile(const KParams& p, SegPtr S, uint32_t wst_off, int lane, int32_t w0,
                                          int32_t nvalid, int64_t& asum, int64_t& amin, int64_t& amax,
                                          unsigned long long& matched) {
@@ -20,7 +24,22 @@ __device__ __forceinline__ void agg_tile(const KParams& p, SegPtr S, uint32_t ws
   LaneStream fs = lane_stream(wst_off + (uint32_t)p.stage_soff[p.f_stream],
                               FK == FK_RANGE ? S->streams[p.f_stream].bits : 1, lane);
   LaneStream vs = lane_stream(wst_off + (uint32_t)p.stage_soff[p.v_stream[0]], S->streams[p.v_stream[0]].bits, lane);
+  LaneStream vs2 = vs;
+  if constexpr (EX != 0)
+    vs2 = lane_stream(wst_off + (uint32_t)p.stage_soff[p.v2_stream[0]], S->streams[p.v2_stream[0]].bits, lane);
   const uint32_t flo = S->flo, flen = S->flen;
+  constexpr int NC = FK == FK_CONJ ? kMaxConj : 1;
+  LaneStream cs[NC];
+  uint32_t clo[NC], clen[NC];
+  const int nconj = FK == FK_CONJ ? S->nconj : 0;
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    if (k >= nconj) continue;
+    cs[k] = lane_stream(wst_off + (uint32_t)p.stage_soff[S->cstream[k]], S->streams[S->cstream[k]].bits, lane);
+    clo[k] = S->clo[k];
+    clen[k] = S->clen[k];
+  }
+  const int64_t base = S->vals[0].base, base2 = EX != 0 ? S->vals2[0].base : 0;
   uint32_t doc = (uint32_t)w0 * 64u + (uint32_t)lane;
   uint32_t tsum = 0, tmin = 0xffffffffu, tmax = 0;
   uint32_t tcnt = 0;  // wave-uniform
@@ -30,24 +49,54 @@ __device__ __forceinline__ void agg_tile(const KParams& p, SegPtr S, uint32_t ws
       bool hh = (u + q < nvalid) & (doc < ndocs);
       if constexpr (FK == FK_RANGE) hh &= (lds_value(fs.off, fs.rsh, fs.mask) - flo) < flen;
       if constexpr (FK == FK_DOCRANGE) hh &= (doc - flo) < flen;
+      if constexpr (FK == FK_CONJ) {
+#pragma unroll
+        for (int k = 0; k < NC; ++k) {
+          if (k >= nconj) continue;
+          hh &= (lds_value(cs[k].off, cs[k].rsh, cs[k].mask) - clo[k]) < clen[k];
+          cs[k].off += cs[k].step;
+        }
+      }
       const uint32_t v = lds_value(vs.off, vs.rsh, vs.mask);
-      const uint32_t m0 = hh ? v : 0u;
-      tsum += m0;
-      tmax = max(tmax, m0);
-      tmin = min(tmin, hh ? v : 0xffffffffu);
+      if constexpr (EX == 0) {
+        const uint32_t m0 = hh ? v : 0u;
+        tsum += m0;
+        tmax = max(tmax, m0);
+        tmin = min(tmin, hh ? v : 0xffffffffu);
+      } else {
+        const int64_t x = base + (int64_t)v, y = base2 + (int64_t)lds_value(vs2.off, vs2.rsh, vs2.mask);
+        const int64_t e = EX == PH_EXPR_MULT ? x * y : (EX == PH_EXPR_SUB ? x - y : x + y);
+        asum += hh ? e : 0;
+        amin = min(amin, hh ? e : INT64_MAX);
+        amax = max(amax, hh ? e : INT64_MIN);
+        vs2.off += vs2.step;
+      }
       tcnt += (uint32_t)__popcll(__ballot(hh));
       vs.off += vs.step;
       if (FK == FK_RANGE) fs.off += fs.step;
       doc += 64u;
     }
   }
-  const int64_t base = S->vals[0].base;
   matched += tcnt;
-  asum += (int64_t)tsum;
-  if (lane == 0) asum += base * (int64_t)tcnt;  // the matches' common base, once per wave
-  if (tmin != 0xffffffffu) {                     // this lane matched in the tile
-    amin = min(amin, base + (int64_t)tmin);
-    amax = max(amax, base + (int64_t)tmax);
+  if constexpr (EX == 0) {
+    asum += (int64_t)tsum;
+    if (lane == 0) asum += base * (int64_t)tcnt;  // the matches' common base, once per wave
+    if (tmin != 0xffffffffu) {                     // this lane matched in the tile
+      amin = min(amin, base + (int64_t)tmin);
+      amax = max(amax, base + (int64_t)tmax);
+    }
+  }
+}
+
+template <int EX>
+__device__ __forceinline__ void agg_tile_any(const KParams& p, SegPtr S, uint32_t wst_off, int lane, int32_t w0,
+                                             int32_t nvalid, int64_t& asum, int64_t& amin, int64_t& amax,
+                                             unsigned long long& matched) {
+  switch (S->fkind) {
+    case FK_RANGE: agg_tile<FK_RANGE, EX>(p, S, wst_off, lane, w0, nvalid, asum, amin, amax, matched); break;
+    case FK_DOCRANGE: agg_tile<FK_DOCRANGE, EX>(p, S, wst_off, lane, w0, nvalid, asum, amin, amax, matched); break;
+    case FK_CONJ: agg_tile<FK_CONJ, EX>(p, S, wst_off, lane, w0, nvalid, asum, amin, amax, matched); break;
+    default: agg_tile<FK_ALL, EX>(p, S, wst_off, lane, w0, nvalid, asum, amin, amax, matched); break;
   }
 }
 
@@ -101,10 +150,12 @@ __global__ void __launch_bounds__(kBlock) k_agg_lean(const KParams p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     if (cnvalid > 0) {
-      const int fk = cs->fkind;
-      if (fk == FK_RANGE) agg_tile<FK_RANGE>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched);
-      else if (fk == FK_DOCRANGE) agg_tile<FK_DOCRANGE>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched);
-      else agg_tile<FK_ALL>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched);
+      switch (p.val_op[0]) {  // wave-uniform
+        case PH_EXPR_MULT: agg_tile_any<PH_EXPR_MULT>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched); break;
+        case PH_EXPR_SUB: agg_tile_any<PH_EXPR_SUB>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched); break;
+        case PH_EXPR_ADD: agg_tile_any<PH_EXPR_ADD>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched); break;
+        default: agg_tile_any<0>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched); break;
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();  // the staging area is rewritten by the next tile_store

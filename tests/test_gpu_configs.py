@@ -145,6 +145,62 @@ def test_config4_ssb(ctx, ssb, qid):
     # Q3.2-Q3.4 / Q4.3 have cardinality products of 0.4-1.75M keys (>= the default numGroupsLimit) over a few hundred
     # real groups: the optimistic scan answers them, no first-seen pass (k_limit_*) runs
     assert r.stats.limit_pass != 2 and not r.stats.num_groups_limit_reached
+    if qid.startswith("Q1."):  # AND of range leaves + SUM(a * b): the lean aggregation kernel's FK_CONJ / term form
+        assert r.stats.scan_kernel == 2, r.stats.scan_kernel
+
+
+SPARSE_SSB = ("Q2.1", "Q2.2", "Q2.3", "Q3.1", "Q3.2", "Q3.3", "Q3.4", "Q4.1", "Q4.2", "Q4.3")
+
+
+@pytest.mark.parametrize("qid", SPARSE_SSB)
+def test_group_sparse_matches_streaming(ctx, ssb, qid, monkeypatch):
+    # the selective inverted-index ANDs run k_group_sparse (matched-doc gathers); the same query on the streaming
+    # k_scan (PH_GROUP_SPARSE=0) and the oracle agree on rows, numDocsScanned and numEntriesScannedInFilter
+    gpu, ora = ssb
+    r, got = _check(ctx, gpu, ora, W.SSB_QUERIES[qid])
+    assert r.stats.scan_kernel == 12, r.stats.scan_kernel
+    monkeypatch.setenv("PH_GROUP_SPARSE", "0")
+    r2, got2 = _check(ctx, gpu, ora, W.SSB_QUERIES[qid])
+    assert r2.stats.scan_kernel != 12
+    assert got.rows == got2.rows
+    assert r.stats.num_entries_scanned_in_filter == r2.stats.num_entries_scanned_in_filter
+    e = O.execute(parse_sql(W.SSB_QUERIES[qid]), ora)
+    assert r.stats.num_entries_scanned_in_filter == e.stats.num_entries_scanned_in_filter
+
+
+def test_group_sparse_shapes(ctx, ssb, monkeypatch):
+    # forced onto k_group_sparse: MIN / MAX / COUNT-only, a set scan leaf, a plain-bitmap filter, a numGroupsLimit
+    # that truncates (the keep bitsets of the rescan), DOUBLE-free integer terms
+    gpu, ora = ssb
+    monkeypatch.setenv("PH_GROUP_SPARSE", "1")
+    for sql in ("SELECT d_year, MIN(lo_revenue), MAX(lo_revenue), COUNT(*) FROM lineorder WHERE s_region = 'ASIA' "
+                "AND lo_quantity IN (3, 7, 11, 40) GROUP BY d_year ORDER BY d_year LIMIT 100",
+                "SELECT c_nation, COUNT(*) FROM lineorder WHERE c_region = 'EUROPE' GROUP BY c_nation "
+                "ORDER BY c_nation LIMIT 100",
+                "SELECT p_brand1, s_city, SUM(lo_revenue - lo_supplycost) FROM lineorder WHERE p_mfgr = 'MFGR#3' "
+                "AND s_region = 'AFRICA' AND lo_discount < 4 AND d_year > 1993 GROUP BY p_brand1, s_city "
+                "ORDER BY p_brand1, s_city LIMIT 100000",
+                "SET numGroupsLimit=50; SELECT p_brand1, d_year, SUM(lo_revenue) FROM lineorder WHERE "
+                "p_category = 'MFGR#22' GROUP BY p_brand1, d_year ORDER BY p_brand1, d_year LIMIT 1000"):
+        r, _ = _check(ctx, gpu, ora, sql)
+        e = O.execute(parse_sql(sql), ora)
+        assert r.stats.num_entries_scanned_in_filter == e.stats.num_entries_scanned_in_filter, sql
+        assert r.stats.num_groups_limit_reached == e.stats.num_groups_limit_reached, sql
+
+
+def test_lean_agg_conj_terms(ctx, ssb):
+    # k_agg_lean's FK_CONJ + integer-term path against the oracle: MIN / MAX / SUM of a - b and a + b, COUNT, over
+    # 1..4 range leaves (exact int64)
+    gpu, ora = ssb
+    for sql in ("SELECT SUM(lo_revenue - lo_supplycost), MIN(lo_revenue - lo_supplycost), "
+                "MAX(lo_revenue - lo_supplycost), COUNT(*) FROM lineorder WHERE lo_discount BETWEEN 2 AND 8 "
+                "AND lo_quantity > 10 AND d_year <= 1996 AND d_weeknuminyear BETWEEN 3 AND 40",
+                "SELECT SUM(lo_quantity + lo_discount), MIN(lo_extendedprice * lo_discount) FROM lineorder "
+                "WHERE lo_quantity < 30",
+                "SELECT MAX(lo_extendedprice * lo_quantity), COUNT(*) FROM lineorder WHERE d_year = 1995 "
+                "AND lo_discount < 5"):
+        r, _ = _check(ctx, gpu, ora, sql)
+        assert r.stats.scan_kernel == 2, (sql, r.stats.scan_kernel)
 
 
 # ------------------------------------------------------------------ config 5
