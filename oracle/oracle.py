@@ -400,6 +400,106 @@ def _mark_apply_and(node: _Leaf) -> _Leaf:
     return node
 
 
+def _and_or_shape(node: _Leaf):
+    """An AND whose children are index-based, scan leaves and exactly ONE remaining OR of index-based / scan leaves,
+    with >= 1 index-based and >= 1 scan child or >= 2 index-based ones: AndDocIdSet.iterator (:128-185) merges the
+    index-based children, applies the scans (applyAnd) and returns AndDocIdIterator(merged, OR), whose scan
+    children count the docs their advance() examines.  -> (index kids, scan kids, the OR) or None."""
+    if node.kind != "and" or getattr(node, "apply_and", None):
+        return None
+    idx, scans, ors = [], [], []
+    for k in node.children:
+        if _index_based(k):
+            idx.append(k)
+        elif k.kind == "leaf" and k.is_scan:
+            scans.append(k)
+        elif k.kind == "or" and all(_index_based(c) or (c.kind == "leaf" and c.is_scan) for c in k.children):
+            ors.append(k)
+        else:
+            return None
+    if len(ors) != 1 or not ((idx and scans) or len(idx) > 1):
+        return None
+    return idx, scans, ors[0]
+
+
+def _doc_ids(col: OracleColumn, n: int) -> np.ndarray:
+    if col.fwd is not None:
+        return fixed_bit_unpack(col.fwd, n, col.bits)
+    sr = col.sorted_ranges
+    return np.repeat(np.arange(len(sr), dtype=np.int32), (sr[:, 1] - sr[:, 0] + 1).astype(np.int64))
+
+
+def _eval_docs(node: _Leaf, seg: OracleSegment, used: list) -> np.ndarray:
+    n = seg.num_docs
+    if node.kind == "leaf":
+        return node.match[_doc_ids(seg.columns[used[node.col_index]], n)].astype(bool)
+    if node.kind == "all":
+        return np.ones(n, bool)
+    if node.kind == "none":
+        return np.zeros(n, bool)
+    kids = [_eval_docs(c, seg, used) for c in node.children]
+    if node.kind == "and":
+        return np.logical_and.reduce(kids)
+    if node.kind == "or":
+        return np.logical_or.reduce(kids)
+    return ~kids[0]
+
+
+def and_or_entries(d0: np.ndarray, scans: list, b: np.ndarray, ors: list) -> int:
+    """numEntriesScannedInFilter of AndDocIdIterator(RangelessBitmapDocIdIterator(A), OrDocIdIterator(...)) over one
+    segment (AndDocIdIterator.java:38-75, OrDocIdIterator.java:73-101, SVScanDocIdIterator.advance :101-112), from
+    per-doc booleans: d0 = the merged index-based children, scans = the AND's scan children in order (applyAnd:
+    |D0| + |D0 n S1| + ...), b = the OR child, ors = the OR's scan children.  The leapfrog touches the OR at the
+    candidates a_i of A with B n [a_(i-1), a_i] non-empty (and a_0); a scan child advances there when it holds no
+    doc in [a_(i-1), a_i), examining [a_i, next match] (to the segment end when none, after which it is done)."""
+    n = len(d0)
+    ent, cur = 0, d0.copy()
+    for sc in scans:
+        ent += int(cur.sum())
+        cur &= sc
+    a = np.nonzero(cur)[0]
+    if len(a) == 0:
+        return ent
+    cb = np.concatenate([[0], np.cumsum(b, dtype=np.int64)])  # cb[x] = B docs in [0, x)
+    prev = np.concatenate([[a[0]], a[:-1]])
+    visited = np.ones(len(a), bool)
+    visited[1:] = cb[a[1:] + 1] - cb[prev[1:]] > 0
+    for o in ors:
+        co = np.concatenate([[0], np.cumsum(o, dtype=np.int64)])
+        adv = visited.copy()
+        adv[1:] &= co[a[1:]] - co[prev[1:]] > 0
+        pos = np.nonzero(o)[0]
+        t = a[adv]
+        j = np.searchsorted(pos, t)
+        hit = j < len(pos)
+        ent += int((pos[j[hit]] - t[hit] + 1).sum())
+        if not hit.all():
+            ent += int(n - t[~hit][0])  # the first advance past the last match scans to the end; the child is done
+    return ent
+
+
+def _uncount(node: _Leaf):
+    if node.kind == "leaf":
+        node.counted_by_and = True
+    for c in node.children:
+        _uncount(c)
+
+
+def _filter_plan(f, seg: OracleSegment, col_index: Dict[str, int], used: list):
+    """The segment's filter tree (applyAnd marked) and its exact AND-with-a-remaining-OR filter entries (or 0; its
+    scan leaves then count nothing in the C program)."""
+    root = _mark_apply_and(_plan_filter(f, seg, col_index))
+    sh = _and_or_shape(root)
+    if sh is None:
+        return root, 0
+    idx, scans, orn = sh
+    d0 = np.logical_and.reduce([_eval_docs(k, seg, used) for k in idx])
+    ent = and_or_entries(d0, [_eval_docs(k, seg, used) for k in scans], _eval_docs(orn, seg, used),
+                         [_eval_docs(k, seg, used) for k in orn.children if k.kind == "leaf" and k.is_scan])
+    _uncount(root)
+    return root, ent
+
+
 def _emit(node: _Leaf, out: list, keep: list):
     if node.kind == "leaf":
         keep.append(node.match)
@@ -460,6 +560,7 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> Oracl
 
     seg_structs = (_Segment * max(1, len(segments)))()
     filter_programs = []
+    extra_entries = []  # per segment: AND-with-a-remaining-OR filter entries (_filter_plan)
     for si, s in enumerate(segments):
         cols = (_Column * len(used))()
         keep.append(cols)
@@ -496,9 +597,12 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> Oracl
         seg_structs[si].num_columns = len(used)
         seg_structs[si].columns = cols
         prog = []
+        extra = 0
         if q.filter is not None:
-            _emit(_mark_apply_and(_plan_filter(q.filter, s, col_index)), prog, keep)
+            root, extra = _filter_plan(q.filter, s, col_index, used)
+            _emit(root, prog, keep)
         filter_programs.append(prog)
+        extra_entries.append(extra)
 
     stats = [0, 0, 0, 0, False]
     group_cols = np.array([col_index[g] for g in q.group_by], dtype=np.int32)
@@ -532,7 +636,7 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> Oracl
                 keep_rows = _segment_trim(res, q, segments[si], unions, nagg, trim_size)
             _merge(res, q, merged_keys, merged, key_list, nagg, hll_idx, m, keep_rows)
             stats[0] += res.num_docs_scanned
-            stats[1] += res.num_entries_scanned_in_filter
+            stats[1] += res.num_entries_scanned_in_filter + extra_entries[si]
             stats[2] += res.num_entries_scanned_post_filter
             stats[3] += res.num_total_docs
             stats[4] |= bool(res.num_groups_limit_reached)

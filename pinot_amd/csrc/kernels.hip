@@ -381,6 +381,36 @@ void launch_selftest_unpack(const uint32_t* fwd, int64_t n, int bits, int32_t* o
   PH_HIP_CHECK(hipGetLastError());
 }
 
+// ------------------------------------------------------------------ filter-entry statistic (AndDocIdIterator)
+// Doc bitmaps of up to kMaxFbProgs sub-programs of one segment's filter (the merged index-based children, the
+// AND's scans, the remaining OR and its scan children), one wave per 64-doc word: the host turns them into the
+// reference's advance()-driven numEntriesScannedInFilter (and_or_entries).  A statistics pass, run only for that
+// filter shape.
+__global__ void __launch_bounds__(256) k_filter_bitmaps(const FilterInsn* __restrict__ prog, const DevSegment* segs,
+                                                        const FbJob job) {
+  SegPtr S = (SegPtr)(segs + job.seg);
+  const int lane = threadIdx.x & 63;
+  const uint32_t ndocs = (uint32_t)S->num_docs;
+  for (int64_t w = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; w < job.nwords;
+       w += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    const uint32_t doc = (uint32_t)w * 64u + (uint32_t)lane;
+    for (int k = 0; k < job.nprog; ++k) {
+      uint32_t fent = 0;
+      const bool b = doc < ndocs && eval_filter((const PH_CONST FilterInsn*)prog + job.off[k], job.len[k], S, doc, fent);
+      const unsigned long long bal = __ballot(b);
+      if (lane == 0) job.out[(int64_t)k * job.nwords + w] = bal;
+    }
+  }
+}
+
+void launch_filter_bitmaps(const FilterInsn* prog, const DevSegment* segs, const FbJob& job, hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>((job.nwords + 3) / 4, 4096);
+  if (blocks <= 0) return;
+  PH_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_filter_bitmaps, dim3((unsigned)blocks), dim3(256), 0, s, prog, segs, job);
+  PH_HIP_CHECK(hipGetLastError());
+}
+
 __global__ void k_fill_i64(int64_t* __restrict__ p, int64_t v, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     p[i] = v;

@@ -612,6 +612,16 @@ void launch_limit_select(const uint32_t* first, int64_t G, int64_t limit, int ns
                          uint32_t* keep, unsigned long long* scal, hipStream_t s);
 // number of non-zero entries of cnt[0, n) into *out (zeroed by the call)
 void launch_count_nonzero(const unsigned long long* cnt, int64_t n, unsigned long long* out, hipStream_t s);
+// filter-entry statistic of an AND with a remaining OR (AndDocIdIterator + OrDocIdIterator advance() semantics)
+constexpr int kMaxFbProgs = 12;
+struct FbJob {
+  int32_t seg;                 // device segment
+  int32_t nprog;
+  int32_t off[kMaxFbProgs], len[kMaxFbProgs];  // sub-programs inside the query's program array
+  int64_t nwords;              // 64-doc words of the segment
+  unsigned long long* out;     // [nprog][nwords] doc bitmaps
+};
+void launch_filter_bitmaps(const FilterInsn* prog, const DevSegment* segs, const FbJob& job, hipStream_t s);
 void launch_selftest_staged(const DevSegment* seg, int32_t tile_words, int32_t stage_stride, int64_t n, int32_t* out,
                             hipStream_t s);
 // the 1 KiB wave-loads of a full tile of every staged stream of `d` (stage offsets per stream)

@@ -521,6 +521,107 @@ void mark_apply_and(PNode& n) {
   for (auto& k : n.kids) mark_apply_and(k);
 }
 
+// An AND of index-based children, scan leaves and exactly ONE remaining OR of index-based / scan leaves, with >= 1
+// index-based and >= 1 scan child or >= 2 index-based ones: AndDocIdSet.iterator (:128-185) merges the index-based
+// children, applies the scans (applyAnd) and returns AndDocIdIterator(merged, OR) -- the OR's scan children then
+// count the docs their advance() examines (SVScanDocIdIterator.advance :101-112), which the per-doc program cannot
+// see.  The statistic comes from doc bitmaps of the parts (k_filter_bitmaps) and and_or_entries below.
+struct AndOrShape {
+  bool ok = false;
+  PNode d0;                   // the merged index-based children (an AND of them, or the one)
+  std::vector<PNode> scans;   // the AND's scan children, in order (applyAnd)
+  PNode orn;                  // the remaining OR
+  std::vector<PNode> oscans;  // the OR's scan children
+};
+AndOrShape and_or_shape(const PNode& r) {
+  AndOrShape sh;
+  if (r.kind != L_NODE || r.op != OP_AND || r.stats_nscan) return sh;
+  auto plain_scan = [](const PNode& k) { return k.kind == L_NODE && k.scan && !k.range_index && k.kids.empty(); };
+  std::vector<PNode> idx, ors;
+  for (auto& k : r.kids) {
+    if (index_based(k)) {
+      idx.push_back(k);
+    } else if (plain_scan(k)) {
+      sh.scans.push_back(k);
+    } else if (k.kind == L_NODE && k.op == OP_OR) {
+      for (auto& c : k.kids)
+        if (!index_based(c) && !plain_scan(c)) return sh;
+      ors.push_back(k);
+    } else {
+      return sh;
+    }
+  }
+  if (ors.size() != 1 || !((!idx.empty() && !sh.scans.empty()) || idx.size() > 1)) return sh;
+  if (2 + sh.scans.size() + ors[0].kids.size() > (size_t)kMaxFbProgs) return sh;
+  if (idx.size() == 1) {
+    sh.d0 = idx[0];
+  } else {
+    sh.d0.op = OP_AND;
+    sh.d0.kids = idx;
+  }
+  sh.orn = ors[0];
+  for (auto& c : sh.orn.kids)
+    if (plain_scan(c)) sh.oscans.push_back(c);
+  sh.ok = true;
+  return sh;
+}
+
+// The statistic over one segment from its part bitmaps (64 docs per word, doc d at bit d & 63 of word d >> 6):
+// applyAnd gives |D0| + |D0 n S1| + ...; then the leapfrog of AndDocIdIterator(A, OR) touches the OR at the
+// candidates a_i of A with B n [a_(i-1), a_i] non-empty (and at a_0), and an OR scan child advances there when it
+// holds no doc in [a_(i-1), a_i), examining [a_i, its next match] -- to the segment end when there is none, after
+// which it is done (the closed form is checked against a literal iterator simulation in test_oracle_kat.py).
+int64_t and_or_entries(const uint64_t* d0, const std::vector<const uint64_t*>& scans, const uint64_t* b,
+                       const std::vector<const uint64_t*>& ors, int64_t nw, int64_t ndocs) {
+  std::vector<uint64_t> cur(d0, d0 + nw);
+  int64_t ent = 0;
+  for (const uint64_t* sc : scans)
+    for (int64_t w = 0; w < nw; ++w) {
+      ent += __builtin_popcountll(cur[w]);
+      cur[w] &= sc[w];
+    }
+  auto ranks = [&](const uint64_t* m) {  // docs of m before word w
+    std::vector<int64_t> r(nw + 1, 0);
+    for (int64_t w = 0; w < nw; ++w) r[w + 1] = r[w] + __builtin_popcountll(m[w]);
+    return r;
+  };
+  auto rank = [](const uint64_t* m, const std::vector<int64_t>& r, int64_t x) {  // docs of m in [0, x)
+    const int64_t w = x >> 6, o = x & 63;
+    return r[w] + (o ? __builtin_popcountll(m[w] & ((1ull << o) - 1ull)) : 0);
+  };
+  auto next = [&](const uint64_t* m, int64_t x) -> int64_t {  // first doc of m >= x, or -1
+    for (int64_t w = x >> 6; w < nw; ++w) {
+      const uint64_t v = w == (x >> 6) ? m[w] & (~0ull << (x & 63)) : m[w];
+      if (v) return w * 64 + __builtin_ctzll(v);
+    }
+    return -1;
+  };
+  const std::vector<int64_t> rb = ranks(b);
+  std::vector<std::vector<int64_t>> ro;
+  for (const uint64_t* o : ors) ro.push_back(ranks(o));
+  std::vector<char> done(ors.size(), 0);
+  int64_t prev = -1;
+  for (int64_t w = 0; w < nw; ++w)
+    for (uint64_t v = cur[w]; v; v &= v - 1) {
+      const int64_t a = w * 64 + __builtin_ctzll(v);
+      const bool visited = prev < 0 || rank(b, rb, a + 1) - rank(b, rb, prev) > 0;
+      if (visited) {
+        for (size_t c = 0; c < ors.size(); ++c) {
+          if (done[c] || (prev >= 0 && rank(ors[c], ro[c], a) - rank(ors[c], ro[c], prev) == 0)) continue;
+          const int64_t nx = next(ors[c], a);
+          if (nx >= 0) {
+            ent += nx - a + 1;
+          } else {
+            ent += ndocs - a;
+            done[c] = 1;
+          }
+        }
+      }
+      prev = a;
+    }
+  return ent;
+}
+
 // k_group_sparse's filter shape: one inverted-index leaf, or an AND of 1..kMaxConj of them and <= kMaxConj plain
 // scan leaves (dictId range / set; the applyAnd order of mark_apply_and: index-based kids first)
 struct SparseShape {
@@ -1059,12 +1160,14 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<SegProgram> progs(nseg);
   std::vector<PNode> roots(nseg);
   std::vector<char> seg_live(nseg, 1);
+  std::vector<AndOrShape> andor(nseg);  // segments whose filter statistic needs the advance() pass
   for (int i = 0; i < nseg && dop != DENSE_LAYOUT && !fin; ++i) {
     PNode root;
     root.kind = L_ALL;
     if (q->filter_root >= 0) root = pl.build(segs[i], q->filter_root, 0);
     mark_apply_and(root);
-    stats.num_entries_scanned_in_filter += (int64_t)segs[i]->num_docs * count_scan_leaves(root);
+    andor[i] = and_or_shape(root);
+    if (!andor[i].ok) stats.num_entries_scanned_in_filter += (int64_t)segs[i]->num_docs * count_scan_leaves(root);
     merge_same_column_leaves(root, [&](int slot) { return (int64_t)segs[i]->columns.at(slot_names[slot])->cardinality; });
     if (root.kind == L_NONE || segs[i]->num_docs == 0) seg_live[i] = 0;
     roots[i] = std::move(root);
@@ -1525,6 +1628,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<std::pair<size_t, std::vector<uint32_t>>> fset_fix;     // segment index -> FK_SET bitset
   std::vector<std::pair<size_t, int>> fbitmap_fix;                    // segment index -> bitmap leaf
   std::vector<std::pair<size_t, std::vector<uint32_t>>> conj_set_fix; // segment index * kMaxConj + leaf -> bitset
+  std::vector<std::pair<FbJob, int>> fb_jobs;                          // statistic passes (job, AND scan count)
   std::vector<std::pair<size_t, int>> sbm_fix;                         // segment index * kSparseBitmaps + k -> bitmap leaf
   std::vector<std::pair<size_t, std::vector<uint32_t>>> sset_fix;     // segment index * kMaxConj + k -> bitset
   // k_group_sparse: every live segment's filter is a sparse_shape AND whose bitmaps keep < 1/8 of the docs (the
@@ -1620,6 +1724,27 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       for (auto& pp : progs[i].payloads) payload_fix.push_back({d.prog_off + pp.first, pp.second});
       for (auto& bb : progs[i].bitmap_refs) bitmap_fix.push_back({d.prog_off + bb.first, bb.second});
       all_insns.insert(all_insns.end(), progs[i].insns.begin(), progs[i].insns.end());
+    }
+    if (andor[i].ok) {  // the statistic's part programs (k_filter_bitmaps)
+      FbJob job{};
+      job.seg = (int32_t)si;
+      job.nwords = ((int64_t)s->num_docs + 63) / 64;
+      std::vector<const PNode*> parts{&andor[i].d0};
+      for (auto& k : andor[i].scans) parts.push_back(&k);
+      parts.push_back(&andor[i].orn);
+      for (auto& k : andor[i].oscans) parts.push_back(&k);
+      for (const PNode* n : parts) {
+        SegProgram sp;
+        emit(*n, sp);
+        if (sp.max_depth > kMaxStack || (int)sp.insns.size() > kMaxProg) fail(PH_ERR_UNSUPPORTED, "filter too large");
+        job.off[job.nprog] = (int32_t)all_insns.size();
+        job.len[job.nprog] = (int32_t)sp.insns.size();
+        ++job.nprog;
+        for (auto& pp : sp.payloads) payload_fix.push_back({all_insns.size() + pp.first, pp.second});
+        for (auto& bb : sp.bitmap_refs) bitmap_fix.push_back({all_insns.size() + bb.first, bb.second});
+        all_insns.insert(all_insns.end(), sp.insns.begin(), sp.insns.end());
+      }
+      fb_jobs.push_back({job, (int)andor[i].scans.size()});
     }
     if (sparse_plan) {
       const SparseShape sh = sparse_shape(root);
@@ -2354,6 +2479,23 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       PH_HIP_CHECK(hipEventRecord(L.event(2 * batches.size() + 1), sb));
       PH_HIP_CHECK(hipStreamWaitEvent(st, L.event(2 * batches.size() + 1), 0));
       PH_HIP_CHECK(hipEventRecord(L.ev_stop, st));
+    }
+    // numEntriesScannedInFilter of ANDs with a remaining OR: the parts' doc bitmaps, then the host's closed form
+    // (a statistics pass, after the scan's device-time window)
+    for (auto& fj : fb_jobs) {
+      FbJob job = fj.first;
+      const int ns = fj.second;
+      const int64_t nw = job.nwords;
+      job.out = scratch.alloc<unsigned long long>((size_t)job.nprog * nw);
+      launch_filter_bitmaps(d_prog, d_segs, job, st);
+      std::vector<uint64_t> h((size_t)job.nprog * nw);
+      PH_HIP_CHECK(hipMemcpyAsync(h.data(), job.out, 8 * h.size(), hipMemcpyDeviceToHost, st));
+      PH_HIP_CHECK(hipStreamSynchronize(st));
+      std::vector<const uint64_t*> sc, oc;
+      for (int k = 0; k < ns; ++k) sc.push_back(h.data() + (size_t)(1 + k) * nw);
+      for (int k = ns + 2; k < job.nprog; ++k) oc.push_back(h.data() + (size_t)k * nw);
+      stats.num_entries_scanned_in_filter +=
+          and_or_entries(h.data(), sc, h.data() + (size_t)(1 + ns) * nw, oc, nw, dsegs[job.seg].num_docs);
     }
     stamp("launched");
     timed = true;

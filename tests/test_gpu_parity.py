@@ -80,8 +80,28 @@ def test_apply_and_filter_entries_gpu(ctx, sv, where):
 
 
 def test_kat_filter_entries_gpu(ctx, sv):
+    # InterSegmentAggregationSingleValueQueriesTest.java:58: the AND's remaining OR (column6 scan, column11 NOT IN
+    # bitmap) is driven by advance() -- k_filter_bitmaps + the host closed form
     r = ctx.execute(parse_sql("SELECT COUNT(*) FROM testTable" + kat_sv.FILTER), sv)
-    assert r.stats.num_entries_scanned_in_filter == 3 * 120000
+    assert r.stats.num_entries_scanned_in_filter == 252256
+    assert r.stats.num_docs_scanned == 24516
+
+
+@pytest.mark.parametrize("where", [
+    " WHERE daysSinceEpoch = 126164076 AND column1 > 100000000 AND (column6 < 500000000 OR column9 > 1000000)",
+    " WHERE column5 = 'gFuH' AND column11 = 'P' AND (column3 > 20000000 OR column11 = 'o' OR column1 < 5000000)",
+    " WHERE column7 = 788414092 AND column3 < 1500000000 "
+    "AND (column6 BETWEEN 3000 AND 900000000 OR column9 < 50000000)",
+])
+def test_and_or_filter_entries_gpu(ctx, sv, where):
+    # ANDs with one remaining OR of scans / index leaves: the reference's advance()-driven statistic on the GPU path
+    # equals the oracle's (whose closed form is checked against a literal iterator simulation)
+    from oracle import oracle as O
+    q = parse_sql("SELECT COUNT(*) FROM testTable" + where)
+    r = ctx.execute(q, sv)
+    e = O.execute(q, [O.build_segment("kat", kat_sv.load_columns(), inverted=kat_sv.INVERTED)] * 4)
+    assert r.stats.num_entries_scanned_in_filter == e.stats.num_entries_scanned_in_filter
+    assert reduce_groups(q, r.keys, r.aggs).rows == reduce_groups(q, e.keys, e.aggs).rows
 
 
 # ------------------------------------------------------------------ randomized parity vs the oracle

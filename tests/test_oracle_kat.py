@@ -14,6 +14,7 @@ from oracle import oracle as O
 from pinot_amd.query import parse_sql
 from pinot_amd.reduce import reduce_groups
 from tests import kat_sv
+from tests.seeds import seed_of
 
 
 @pytest.fixture(scope="module")
@@ -88,10 +89,10 @@ def test_apply_and_filter_entries(sv_segments, k):
 def test_kat_filter_entries_definition(sv_segments):
     # The KAT filter's AND holds an OR with a scan child (column6 RANGE: RANGE never uses the inverted index,
     # FilterOperatorUtils.java:97-104), which the reference drives with advance() calls (AndDocIdIterator /
-    # OrDocIdIterator: 252 256 entries, reproduced by tools-free simulation in DESIGN.md); this build counts such
-    # shapes as numDocs per scan leaf: column1, column3 and column6.
+    # OrDocIdIterator) after applyAnd of column1 / column3 over the sorted daysSinceEpoch range:
+    # InterSegmentAggregationSingleValueQueriesTest.java:58 pins 252 256 entries
     _, st = run("SELECT COUNT(*) FROM testTable" + kat_sv.FILTER, sv_segments)
-    assert st.num_entries_scanned_in_filter == 3 * 120000
+    assert st.num_entries_scanned_in_filter == 252256
 
 
 # ------------------------------------------------------------------ FastFilteredCountTest
@@ -255,6 +256,82 @@ def _and_or_iterator_entries(c):
                 max_doc, max_idx, idx = doc, idx, 0
         matches += 1
         next_doc = max_doc + 1
+
+
+def _iterator_entries(d0, scans, b_kids, n):
+    """Literal simulation of AndDocIdIterator(RangelessBitmapDocIdIterator(applyAnd(D0, scans)), OrDocIdIterator(
+    kids)): b_kids = [(is_scan, bool array)]; scan kids count every doc their advance() examines."""
+    cur = d0.copy()
+    scanned = 0
+    for sc in scans:
+        scanned += int(cur.sum())
+        cur &= sc
+    cand = np.nonzero(cur)[0]
+    kids = [(is_scan, np.nonzero(m)[0]) for is_scan, m in b_kids]
+    nxt, alive = [-1] * len(kids), [True] * len(kids)
+
+    def kid_advance(i, t):
+        nonlocal scanned
+        is_scan, pos = kids[i]
+        j = np.searchsorted(pos, t)
+        if is_scan:
+            scanned += (int(pos[j]) - t + 1) if j < len(pos) else n - t
+        return int(pos[j]) if j < len(pos) else -1
+
+    def or_advance(t):
+        best = None
+        for i in range(len(kids)):
+            if not alive[i]:
+                continue
+            if nxt[i] < t:
+                nxt[i] = kid_advance(i, t)
+                if nxt[i] == -1:
+                    alive[i] = False
+                    continue
+            best = nxt[i] if best is None else min(best, nxt[i])
+        return -1 if best is None else best
+
+    def r_advance(t):
+        i = np.searchsorted(cand, t)
+        return int(cand[i]) if i < len(cand) else -1
+
+    its, next_doc = [r_advance, or_advance], 0
+    while True:
+        max_doc, max_idx, idx = next_doc, -1, 0
+        while idx < 2:
+            if idx == max_idx:
+                idx += 1
+                continue
+            doc = its[idx](max_doc)
+            if doc == -1:
+                return scanned
+            if doc == max_doc:
+                idx += 1
+            else:
+                max_doc, max_idx, idx = doc, idx, 0
+        next_doc = max_doc + 1
+
+
+@pytest.mark.parametrize("case", range(60))
+def test_and_or_entries_closed_form_vs_iterators(case):
+    # oracle.and_or_entries (the per-candidate closed form the GPU path's host pass also uses) against the literal
+    # iterator simulation, on random densities
+    rng = np.random.default_rng(seed_of(f"and-or-{case}"))
+    n = int(rng.integers(1, 3000))
+    dens = rng.uniform(0.001, 0.9, 8)
+    d0 = rng.random(n) < dens[0]
+    scans = [rng.random(n) < dens[1 + k] for k in range(int(rng.integers(0, 3)))]
+    b_kids = [(bool(rng.integers(0, 2)), rng.random(n) < dens[4 + k]) for k in range(int(rng.integers(1, 4)))]
+    b = np.logical_or.reduce([m for _, m in b_kids])
+    ors = [m for is_scan, m in b_kids if is_scan]
+    assert O.and_or_entries(d0, scans, b, ors) == _iterator_entries(d0, scans, b_kids, n)
+
+
+def test_kat_filter_entries_oracle():
+    # the oracle's exact AND-with-a-remaining-OR statistic on the KAT filter: 252 256 over the 4 segments
+    e = O.execute(parse_sql("SELECT COUNT(*) FROM testTable" + kat_sv.FILTER),
+                  [O.build_segment("kat", kat_sv.load_columns(), inverted=kat_sv.INVERTED)] * 4)
+    assert e.stats.num_entries_scanned_in_filter == 252256
 
 
 def test_kat_filter_entries_reference_iterators():
