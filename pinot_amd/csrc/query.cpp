@@ -1166,9 +1166,12 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     root.kind = L_ALL;
     if (q->filter_root >= 0) root = pl.build(segs[i], q->filter_root, 0);
     mark_apply_and(root);
-    andor[i] = and_or_shape(root);
-    if (!andor[i].ok) stats.num_entries_scanned_in_filter += (int64_t)segs[i]->num_docs * count_scan_leaves(root);
+    const int64_t scan_leaves = count_scan_leaves(root);
     merge_same_column_leaves(root, [&](int slot) { return (int64_t)segs[i]->columns.at(slot_names[slot])->cardinality; });
+    // on the merged tree: an OR of same-column scan predicates is one IN leaf there (the reference's
+    // MergeEqInFilterOptimizer), not a remaining OR -- SSB Q4.2's `d_year = 1997 OR d_year = 1998`
+    andor[i] = and_or_shape(root);
+    if (!andor[i].ok) stats.num_entries_scanned_in_filter += (int64_t)segs[i]->num_docs * scan_leaves;
     if (root.kind == L_NONE || segs[i]->num_docs == 0) seg_live[i] = 0;
     roots[i] = std::move(root);
   }

@@ -100,6 +100,7 @@ __device__ __forceinline__ void agg_tile_any(const KParams& p, SegPtr S, uint32_
   }
 }
 
+template <int EX>
 __global__ void __launch_bounds__(kBlock) k_agg_lean(const KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NL = kPrefetchOther;
@@ -149,14 +150,7 @@ __global__ void __launch_bounds__(kBlock) k_agg_lean(const KParams p) {
     if (c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (cnvalid > 0) {
-      switch (p.val_op[0]) {  // wave-uniform
-        case PH_EXPR_MULT: agg_tile_any<PH_EXPR_MULT>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched); break;
-        case PH_EXPR_SUB: agg_tile_any<PH_EXPR_SUB>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched); break;
-        case PH_EXPR_ADD: agg_tile_any<PH_EXPR_ADD>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched); break;
-        default: agg_tile_any<0>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched); break;
-      }
-    }
+    if (cnvalid > 0) agg_tile_any<EX>(p, cs, wst_off, lane, cw0, cnvalid, asum, amin, amax, matched);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();  // the staging area is rewritten by the next tile_store
   }
@@ -298,9 +292,17 @@ void launch_scan_agg(const KParams& p, int mode, int grid, size_t lds, hipStream
   }
   if (mode == MODE_COUNT) {
     launch_late<MODE_COUNT, 0, 0>(p, grid, lds, s);
-  } else if (p.agg_fast) {
-    allow_lds(k_agg_lean, lds);
-    hipLaunchKernelGGL(k_agg_lean, dim3(grid), dim3(kBlock), lds, s, p);
+  } else if (p.agg_fast) {  // one kernel per value-term form (the plain column keeps k_agg_lean's r2 code size)
+    switch (p.val_op[0]) {
+#define PH_LEAN_CASE(e)                                                       \
+  case e:                                                                     \
+    allow_lds(k_agg_lean<e>, lds);                                            \
+    hipLaunchKernelGGL((k_agg_lean<e>), dim3(grid), dim3(kBlock), lds, s, p); \
+    break;
+      PH_LEAN_CASE(PH_EXPR_MULT) PH_LEAN_CASE(PH_EXPR_SUB) PH_LEAN_CASE(PH_EXPR_ADD)
+      default: PH_LEAN_CASE(0)
+#undef PH_LEAN_CASE
+    }
   } else if (p.num_vals <= 1 && !p.val_op[0]) {
     launch_late<MODE_AGG, 0, 1>(p, grid, lds, s);  // ValCap 1
   } else if (p.num_vals <= 1) {

@@ -152,11 +152,11 @@ SSB_INVERTED = ("c_region", "s_region", "c_nation", "s_nation", "c_city", "s_cit
                 "p_brand1")
 
 
-def ssb_segment_buffers(name: str, n: int, seed: int = 0xC004):
+def ssb_segment_buffers(name: str, n: int, seed: int = 0xC004, inverted=()):
     """A denormalised lineorder segment of n rows built straight in dictionary-id form (no string arrays of n
     entries): the same column set, value domains and dictionaries as ``ssb_columns`` (sorted distinct values),
-    drawn from its own seeded PCG64 stream.  For bench-sized segments (10M rows in seconds); no inverted indexes, so
-    the string predicates run as dictId scans."""
+    drawn from its own seeded PCG64 stream.  For bench-sized segments (10M rows in seconds; ~2 s more per inverted
+    column); columns not in `inverted` have no inverted index, so their predicates run as dictId scans."""
     from pinot_amd.segment import SegmentBuffers, create_column, create_column_from_dict_ids
     rng = np.random.default_rng(seed)
     seg = SegmentBuffers(name, n)
@@ -167,7 +167,7 @@ def ssb_segment_buffers(name: str, n: int, seed: int = 0xC004):
         used[np.unique(ids)] = True  # dictionary = values present (sorted), ids renumbered
         remap = np.cumsum(used) - 1
         seg.columns[col] = create_column_from_dict_ids(col, dictionary[used], remap[ids].astype(np.int32), dt,
-                                                       allow_sorted=False)
+                                                       inverted=col in inverted, allow_sorted=False)
     day = rng.integers(0, 2557, n)
     base = np.datetime64("1992-01-01")
     all_days = base + np.arange(2557).astype("timedelta64[D]")

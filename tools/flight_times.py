@@ -15,7 +15,8 @@ def main():
     from tests import workloads as W
     nseg = int(sys.argv[1]) if len(sys.argv) > 1 else 60
     distinct = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-    built = [W.ssb_segment_buffers(f"ssb_{j}", 10_000_000, seed=0xC004 + j) for j in range(distinct)]
+    inv = () if os.environ.get("FLIGHT_NO_INVERTED") else W.SSB_INVERTED
+    built = [W.ssb_segment_buffers(f"ssb_{j}", 10_000_000, seed=0xC004 + j, inverted=inv) for j in range(distinct)]
     ctx = GpuContext(0)
     pinned = [ctx.pin(built[i % distinct]) for i in range(nseg)]
     only = os.environ.get("FLIGHT_ONLY")
