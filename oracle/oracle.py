@@ -371,6 +371,42 @@ def _plan_filter(f, seg: OracleSegment, col_index: Dict[str, int]):
     raise ValueError(f.type)
 
 
+def _merge_same_column(node: _Leaf) -> _Leaf:
+    """Same-column scan leaves under one AND / OR become one leaf (their match arrays ANDed / ORed), as the
+    reference's query optimizer merges them before planning (MergeEqInFilterOptimizer, MergeRangeFilterOptimizer:
+    QueryOptimizer.java:47-49); the statistics then follow the merged tree.  Results are unchanged."""
+    if node.kind not in ("and", "or"):
+        return node
+    is_and = node.kind == "and"
+    out, first = [], {}
+    for k in (_merge_same_column(c) for c in node.children):
+        if k.kind == "leaf" and k.is_scan:
+            j = first.get(k.col_index)
+            if j is not None:
+                a = out[j]
+                m = (a.match & k.match) if is_and else (a.match | k.match)
+                out[j] = _Leaf("leaf", a.col_index, m.astype(a.match.dtype), True)
+                continue
+            first[k.col_index] = len(out)
+        out.append(k)
+    kids = []
+    for k in out:
+        if k.kind == "leaf" and k.is_scan and not k.match.any():
+            k = _Leaf("none")
+        elif k.kind == "leaf" and k.is_scan and k.match.all():
+            k = _Leaf("all")
+        if k.kind == ("none" if is_and else "all"):
+            return _Leaf(k.kind)
+        if k.kind != ("all" if is_and else "none"):
+            kids.append(k)
+    if not kids:
+        return _Leaf("all" if is_and else "none")
+    if len(kids) == 1:
+        return kids[0]
+    node.children = kids
+    return node
+
+
 def _index_based(k: _Leaf) -> bool:
     """A child whose docIdSet iterator is Sorted- or BitmapBased (AndDocIdSet.java:80-100; an OR of such children
     merges into one bitmap, OrDocIdSet.java:33-52)."""
@@ -488,7 +524,7 @@ def _uncount(node: _Leaf):
 def _filter_plan(f, seg: OracleSegment, col_index: Dict[str, int], used: list):
     """The segment's filter tree (applyAnd marked) and its exact AND-with-a-remaining-OR filter entries (or 0; its
     scan leaves then count nothing in the C program)."""
-    root = _mark_apply_and(_plan_filter(f, seg, col_index))
+    root = _mark_apply_and(_merge_same_column(_plan_filter(f, seg, col_index)))
     sh = _and_or_shape(root)
     if sh is None:
         return root, 0
@@ -703,7 +739,7 @@ def execute_timed(q, segments: Sequence[OracleSegment], num_threads: int):
         seg_structs[si].num_docs, seg_structs[si].num_columns, seg_structs[si].columns = s.num_docs, len(used), cols
         prog = []
         if q.filter is not None:
-            _emit(_mark_apply_and(_plan_filter(q.filter, s, col_index)), prog, keep)
+            _emit(_mark_apply_and(_merge_same_column(_plan_filter(q.filter, s, col_index))), prog, keep)
         progs.append(prog)
     prog = progs[0]
     ops = (_FilterOp * max(1, len(prog)))()

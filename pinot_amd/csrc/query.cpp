@@ -1165,13 +1165,13 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     PNode root;
     root.kind = L_ALL;
     if (q->filter_root >= 0) root = pl.build(segs[i], q->filter_root, 0);
-    mark_apply_and(root);
-    const int64_t scan_leaves = count_scan_leaves(root);
+    // same-column scan predicates merge first, as the reference's query optimizer merges them before planning
+    // (MergeEqInFilterOptimizer: `d_year = 1997 OR d_year = 1998` -> one IN; MergeRangeFilterOptimizer: ranges of
+    // one column under an AND), so the statistics below see the reference's operator tree
     merge_same_column_leaves(root, [&](int slot) { return (int64_t)segs[i]->columns.at(slot_names[slot])->cardinality; });
-    // on the merged tree: an OR of same-column scan predicates is one IN leaf there (the reference's
-    // MergeEqInFilterOptimizer), not a remaining OR -- SSB Q4.2's `d_year = 1997 OR d_year = 1998`
+    mark_apply_and(root);
     andor[i] = and_or_shape(root);
-    if (!andor[i].ok) stats.num_entries_scanned_in_filter += (int64_t)segs[i]->num_docs * scan_leaves;
+    if (!andor[i].ok) stats.num_entries_scanned_in_filter += (int64_t)segs[i]->num_docs * count_scan_leaves(root);
     if (root.kind == L_NONE || segs[i]->num_docs == 0) seg_live[i] = 0;
     roots[i] = std::move(root);
   }
