@@ -19,6 +19,8 @@
 //     values-keyed merge (GroupByCombineOperator.java:169-178 keys by Object[] values; the global id is a
 //     bijection with the value).
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -2485,20 +2487,43 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     // numEntriesScannedInFilter of ANDs with a remaining OR: the parts' doc bitmaps, then the host's closed form
     // (a statistics pass, after the scan's device-time window)
-    for (auto& fj : fb_jobs) {
-      FbJob job = fj.first;
-      const int ns = fj.second;
-      const int64_t nw = job.nwords;
-      job.out = scratch.alloc<unsigned long long>((size_t)job.nprog * nw);
-      launch_filter_bitmaps(d_prog, d_segs, job, st);
-      std::vector<uint64_t> h((size_t)job.nprog * nw);
-      PH_HIP_CHECK(hipMemcpyAsync(h.data(), job.out, 8 * h.size(), hipMemcpyDeviceToHost, st));
+    if (!fb_jobs.empty()) {
+      // every segment's part bitmaps in one launch set and one copy, then the segments' closed forms in parallel
+      size_t total = 0;
+      for (auto& fj : fb_jobs) total += (size_t)fj.first.nprog * (size_t)fj.first.nwords;
+      unsigned long long* dev = scratch.alloc<unsigned long long>(std::max<size_t>(1, total));
+      std::vector<uint64_t> h(std::max<size_t>(1, total));
+      std::vector<size_t> base(fb_jobs.size());
+      size_t off = 0;
+      for (size_t t = 0; t < fb_jobs.size(); ++t) {
+        FbJob job = fb_jobs[t].first;
+        job.out = dev + off;
+        base[t] = off;
+        off += (size_t)job.nprog * (size_t)job.nwords;
+        launch_filter_bitmaps(d_prog, d_segs, job, st);
+      }
+      PH_HIP_CHECK(hipMemcpyAsync(h.data(), dev, 8 * total, hipMemcpyDeviceToHost, st));
       PH_HIP_CHECK(hipStreamSynchronize(st));
-      std::vector<const uint64_t*> sc, oc;
-      for (int k = 0; k < ns; ++k) sc.push_back(h.data() + (size_t)(1 + k) * nw);
-      for (int k = ns + 2; k < job.nprog; ++k) oc.push_back(h.data() + (size_t)k * nw);
-      stats.num_entries_scanned_in_filter +=
-          and_or_entries(h.data(), sc, h.data() + (size_t)(1 + ns) * nw, oc, nw, dsegs[job.seg].num_docs);
+      std::vector<int64_t> ent(fb_jobs.size(), 0);
+      std::atomic<size_t> next_job{0};
+      auto work = [&]() {
+        for (size_t t; (t = next_job.fetch_add(1)) < fb_jobs.size();) {
+          const FbJob& job = fb_jobs[t].first;
+          const int ns = fb_jobs[t].second;
+          const int64_t nw = job.nwords;
+          const uint64_t* hb = h.data() + base[t];
+          std::vector<const uint64_t*> sc, oc;
+          for (int k = 0; k < ns; ++k) sc.push_back(hb + (size_t)(1 + k) * nw);
+          for (int k = ns + 2; k < job.nprog; ++k) oc.push_back(hb + (size_t)k * nw);
+          ent[t] = and_or_entries(hb, sc, hb + (size_t)(1 + ns) * nw, oc, nw, dsegs[job.seg].num_docs);
+        }
+      };
+      const size_t nthr = std::min<size_t>(fb_jobs.size(), std::max(1u, std::min(8u, std::thread::hardware_concurrency())));
+      std::vector<std::thread> pool;
+      for (size_t k = 1; k < nthr; ++k) pool.emplace_back(work);
+      work();
+      for (auto& th : pool) th.join();
+      for (int64_t e : ent) stats.num_entries_scanned_in_filter += e;
     }
     stamp("launched");
     timed = true;
