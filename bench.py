@@ -391,7 +391,8 @@ def main():
             ora_makers.append(mk)
         else:
             b = make_segment_buffers(i, seg_rows, seed=1000, cols=cols)
-        pinned.append(ctx.pin(b))
+        # DISTINCTCOUNTHLL columns get their HLL tables at pin (ph_column_desc.hll_log2m), not in the first query
+        pinned.append(ctx.pin(b, hll_columns=[a.column for a in q.aggregations if a.function == "DISTINCTCOUNTHLL"]))
         bufs.append(b)
         if k % 20 == 19:
             log(f"[rank {rank}] pinned {k + 1}/{len(mine)} segments ({time.time() - t0:.1f}s)")

@@ -100,6 +100,10 @@ typedef struct {
    * so the slices themselves are not read. */
   const void* range_index;
   uint64_t range_index_size;
+  /* > 0: build the column's DISTINCTCOUNTHLL table for this log2m at pin -- the per-dictId (register, rank) pairs of
+   * clearspring HyperLogLog.offer(dictionary value) (DistinctCountHLLAggregationFunction.java:438-447) -- so no
+   * query pays for it; 0: the first query that needs it builds it */
+  int32_t hll_log2m;
 } ph_column_desc;
 
 typedef struct {
@@ -221,7 +225,8 @@ enum {
   PH_KERNEL_COUNT_REG = 9,     /* k_count_reg: COUNT(*) over RANGE / ALL / sorted leaves, register-direct decode */
   PH_KERNEL_AGG_REG = 10,      /* k_agg_reg: k_agg_lean's aggregation in the register-direct form */
   PH_KERNEL_GROUP_REG = 11,    /* k_group_reg: k_group_lds_lean's group-by in the register-direct form */
-  PH_KERNEL_GROUP_SPARSE = 12  /* k_group_sparse: group-by over selective inverted-index ANDs, matched-doc gathers */
+  PH_KERNEL_GROUP_SPARSE = 12, /* k_group_sparse: group-by over selective inverted-index ANDs, matched-doc gathers */
+  PH_KERNEL_PART_WAVE = 13     /* k_part_wave + k_part_agg: partitioned group-by, wave-private rings, no barriers */
 };
 
 /* ------------------------------------------------------------------ context */
@@ -231,7 +236,16 @@ int ph_ctx_destroy(ph_ctx* ctx);
 int ph_ctx_set_stream(ph_ctx* ctx, void* hip_stream);
 
 /* ------------------------------------------------------------------ segments */
+/* Copies the column buffers into HBM and derives, on the pin stream, what queries read besides them: the
+ * frame-of-reference value stream of every INT / LONG column (value - min in bits(max - min), read instead of a
+ * dictionary gather per row) and the requested DISTINCTCOUNTHLL tables (hll_log2m).  The caller's buffers may be
+ * released when it returns. */
 int ph_segment_pin(ph_ctx* ctx, const ph_segment_desc* desc, ph_segment** out);
+/* Validates a segment descriptor without a device: what ph_segment_pin would refuse, and why (ph_last_error).
+ * PH_ERR_INVALID_ARGUMENT for a malformed descriptor; PH_ERR_UNSUPPORTED for a segment the GPU path does not serve:
+ * a packed stream (forward index, or the value stream derived from it) of 2 GiB or more, past the kernels' 32-bit
+ * buffer offsets -- the plan maker then keeps the segment on the CPU plan (GpuSegmentRegistry). */
+int ph_segment_check(const ph_segment_desc* desc);
 /* Pin a segment straight from its on-disk directory (replaces ImmutableSegmentLoader.load's index-buffer path,
  * ImmutableSegmentLoader.java / SingleFileIndexDirectory.java:72,213-305): V3 (<dir>/v3/: metadata.properties,
  * index_map, columns.psf) or V1 (one file per index).  `columns`

@@ -321,14 +321,16 @@ def _plan_filter(f, seg: OracleSegment, col_index: Dict[str, int]):
         # (FilterOperatorUtils.java:97-120): RANGE -> sorted, else range index, else scan; others -> sorted, else
         # inverted, else an exact range index for EQ (RangeIndexBasedFilterOperator.canEvaluate :56-61), else scan
         if col.is_sorted:
-            is_scan = False
+            is_scan, ikind = False, "sorted"
         elif p.TYPE != "RANGE" and col.has_inverted:
-            is_scan = False
+            is_scan, ikind = False, "inverted"
         elif col.has_range_index and p.TYPE in ("RANGE", "EQ"):
-            is_scan = False
+            is_scan, ikind = False, "range"
         else:
-            is_scan = True
-        return _Leaf("leaf", col_index[p.column], match, is_scan)
+            is_scan, ikind = True, "scan"
+        leaf = _Leaf("leaf", col_index[p.column], match, is_scan)
+        leaf.ikind = ikind
+        return leaf
     if f.type == "AND":
         kids = []
         for c in f.children:
@@ -386,6 +388,7 @@ def _merge_same_column(node: _Leaf) -> _Leaf:
                 a = out[j]
                 m = (a.match & k.match) if is_and else (a.match | k.match)
                 out[j] = _Leaf("leaf", a.col_index, m.astype(a.match.dtype), True)
+                out[j].ikind = "scan"
                 continue
             first[k.col_index] = len(out)
         out.append(k)
@@ -434,28 +437,6 @@ def _mark_apply_and(node: _Leaf) -> _Leaf:
     for c in node.children:
         _mark_apply_and(c)
     return node
-
-
-def _and_or_shape(node: _Leaf):
-    """An AND whose children are index-based, scan leaves and exactly ONE remaining OR of index-based / scan leaves,
-    with >= 1 index-based and >= 1 scan child or >= 2 index-based ones: AndDocIdSet.iterator (:128-185) merges the
-    index-based children, applies the scans (applyAnd) and returns AndDocIdIterator(merged, OR), whose scan
-    children count the docs their advance() examines.  -> (index kids, scan kids, the OR) or None."""
-    if node.kind != "and" or getattr(node, "apply_and", None):
-        return None
-    idx, scans, ors = [], [], []
-    for k in node.children:
-        if _index_based(k):
-            idx.append(k)
-        elif k.kind == "leaf" and k.is_scan:
-            scans.append(k)
-        elif k.kind == "or" and all(_index_based(c) or (c.kind == "leaf" and c.is_scan) for c in k.children):
-            ors.append(k)
-        else:
-            return None
-    if len(ors) != 1 or not ((idx and scans) or len(idx) > 1):
-        return None
-    return idx, scans, ors[0]
 
 
 def _doc_ids(col: OracleColumn, n: int) -> np.ndarray:
@@ -514,26 +495,10 @@ def and_or_entries(d0: np.ndarray, scans: list, b: np.ndarray, ors: list) -> int
     return ent
 
 
-def _uncount(node: _Leaf):
-    if node.kind == "leaf":
-        node.counted_by_and = True
-    for c in node.children:
-        _uncount(c)
-
-
 def _filter_plan(f, seg: OracleSegment, col_index: Dict[str, int], used: list):
-    """The segment's filter tree (applyAnd marked) and its exact AND-with-a-remaining-OR filter entries (or 0; its
-    scan leaves then count nothing in the C program)."""
-    root = _mark_apply_and(_merge_same_column(_plan_filter(f, seg, col_index)))
-    sh = _and_or_shape(root)
-    if sh is None:
-        return root, 0
-    idx, scans, orn = sh
-    d0 = np.logical_and.reduce([_eval_docs(k, seg, used) for k in idx])
-    ent = and_or_entries(d0, [_eval_docs(k, seg, used) for k in scans], _eval_docs(orn, seg, used),
-                         [_eval_docs(k, seg, used) for k in orn.children if k.kind == "leaf" and k.is_scan])
-    _uncount(root)
-    return root, ent
+    """The segment's filter tree for the C program (applyAnd marked; the statistic itself comes from
+    filter_entries)."""
+    return _mark_apply_and(_merge_same_column(_plan_filter(f, seg, col_index)))
 
 
 def _emit(node: _Leaf, out: list, keep: list):
@@ -551,6 +516,304 @@ def _emit(node: _Leaf, out: list, keep: list):
         code = {"and": OR_F_AND, "or": OR_F_OR, "not": OR_F_NOT}[node.kind]
         ia = getattr(node, "apply_and", None)
         out.append((code, len(node.children), None, (ia[0] << 8 | ia[1]) if ia else 0))
+
+
+# --------------------------------------------------------------------------- numEntriesScannedInFilter
+# A literal simulation of the reference's doc-id iterator tree over one segment, from per-doc booleans: the statistic
+# is the sum of the docs every SVScanDocIdIterator examines (SVScanDocIdIterator.java:76-142), which depends on how
+# the tree drives it -- next() in 256-doc batches, advance(t) doc by doc from t, applyAnd over the docs it is given.
+EOF_DOC = -(1 << 31)  # Constants.EOF (Integer.MIN_VALUE)
+
+
+class _ScanIt:
+    """SVScanDocIdIterator (:54-142)."""
+    kind = "scan"
+
+    def __init__(self, match: np.ndarray):
+        self.match = match
+        self.n = len(match)
+        self.pos = np.flatnonzero(match)
+        self.next_doc = 0
+        self.batch = self.pos[:0]
+        self.cursor = 0
+        self.first_mismatch = 0
+        self.entries = 0
+
+    def next(self):
+        if self.cursor >= self.first_mismatch:
+            # batches of 256 docs from next_doc until one holds a match (each batch counted whole)
+            j = int(np.searchsorted(self.pos, self.next_doc))
+            if self.next_doc >= self.n or j == len(self.pos):
+                self.entries += max(0, self.n - self.next_doc)
+                self.next_doc = max(self.next_doc, self.n)
+                self.batch, self.cursor, self.first_mismatch = self.pos[:0], 0, 0
+                return EOF_DOC
+            d = int(self.pos[j])
+            start = self.next_doc + ((d - self.next_doc) // 256) * 256
+            end = min(start + 256, self.n)
+            self.entries += end - self.next_doc
+            self.batch = self.pos[j:int(np.searchsorted(self.pos, end))]
+            self.next_doc = end
+            self.cursor, self.first_mismatch = 0, len(self.batch)
+        d = int(self.batch[self.cursor])
+        self.cursor += 1
+        return d
+
+    def advance(self, t):
+        self.next_doc = t
+        self.first_mismatch = 0
+        if t >= self.n:
+            return EOF_DOC
+        j = int(np.searchsorted(self.pos, t))
+        if j < len(self.pos):
+            d = int(self.pos[j])
+            self.entries += d - t + 1
+            self.next_doc = d + 1
+            return d
+        self.entries += self.n - t
+        self.next_doc = self.n
+        return EOF_DOC
+
+    def apply_and(self, docs: np.ndarray) -> np.ndarray:
+        self.entries += int(docs.sum())
+        return docs & self.match
+
+    def drain(self):  # next() until EOF: the rest of the batch costs nothing, every later doc is scanned
+        self.entries += max(0, self.n - self.next_doc)
+        self.next_doc = max(self.next_doc, self.n)
+        self.cursor = self.first_mismatch
+
+
+class _IndexIt:
+    """SortedDocIdIterator / BitmapDocIdIterator / RangelessBitmapDocIdIterator: no entries scanned."""
+
+    def __init__(self, docs: np.ndarray, kind: str):
+        self.docs = docs
+        self.kind = kind  # "sorted" | "bitmap"
+        self.pos = np.flatnonzero(docs)
+        self.cursor = 0
+
+    def next(self):
+        if self.cursor < len(self.pos):
+            self.cursor += 1
+            return int(self.pos[self.cursor - 1])
+        return EOF_DOC
+
+    def advance(self, t):
+        self.cursor = max(self.cursor, int(np.searchsorted(self.pos, t)))
+        return self.next()
+
+    def drain(self):
+        self.cursor = len(self.pos)
+
+
+class _AndIt:
+    """AndDocIdIterator (:38-75)."""
+    kind = "and"
+
+    def __init__(self, its):
+        self.its = its
+        self.next_doc = 0
+
+    def next(self):
+        max_doc, max_idx, i, k = self.next_doc, -1, 0, len(self.its)
+        while i < k:
+            if i == max_idx:
+                i += 1
+                continue
+            d = self.its[i].advance(max_doc)
+            if d == EOF_DOC:
+                return EOF_DOC
+            if d == max_doc:
+                i += 1
+            else:
+                max_doc, max_idx, i = d, i, 0
+        self.next_doc = max_doc + 1
+        return max_doc
+
+    def advance(self, t):
+        self.next_doc = t
+        return self.next()
+
+    def drain(self):
+        while self.next() != EOF_DOC:
+            pass
+
+
+class _OrIt:
+    """OrDocIdIterator (:41-126)."""
+    kind = "or"
+
+    def __init__(self, its):
+        self.its = list(its)
+        self.cur = [-1] * len(its)
+        self.live = len(its)
+        self.prev = -1
+
+    def _prune(self):
+        i = 0
+        while i < self.live:
+            if self.cur[i] == EOF_DOC:
+                self.live -= 1
+                self.its[i], self.cur[i] = self.its[self.live], self.cur[self.live]
+            else:
+                i += 1
+
+    def _step(self, t):
+        best, ex = None, False
+        for i in range(self.live):
+            d = self.cur[i]
+            if (t is None and d == self.prev) or (t is not None and d < t):
+                d = self.its[i].next() if t is None else self.its[i].advance(t)
+                self.cur[i] = d
+                if d == EOF_DOC:
+                    ex = True
+                    continue
+            best = d if best is None else min(best, d)
+        if ex:
+            self._prune()
+        if best is None:
+            return EOF_DOC
+        self.prev = best
+        return best
+
+    def next(self):
+        return self._step(None)
+
+    def advance(self, t):
+        return self._step(t)
+
+    def drain(self):  # every child is driven to EOF by next()
+        for i in range(self.live):
+            self.its[i].drain()
+        self.live = 0
+
+
+class _NotIt:
+    """NotDocIdIterator (:29-70); its constructor already calls the child's next()."""
+    kind = "not"
+
+    def __init__(self, child, n):
+        self.child, self.n = child, n
+        self.next_doc = 0
+        c = child.next()
+        self.next_non = n if c == EOF_DOC else c
+
+    def next(self):
+        while self.next_doc == self.next_non:
+            self.next_doc += 1
+            c = self.child.next()
+            self.next_non = self.n if c == EOF_DOC else c
+        if self.next_doc >= self.n:
+            return EOF_DOC
+        self.next_doc += 1
+        return self.next_doc - 1
+
+    def advance(self, t):
+        self.next_doc = t
+        if t > self.next_non:
+            c = self.child.advance(t)
+            self.next_non = self.n if c == EOF_DOC else c
+        return self.next()
+
+    def drain(self):
+        self.child.drain()
+        self.next_doc = self.n
+
+
+def _and_set(makers, n):
+    """AndDocIdSet.iterator (AndDocIdSet.java:71-185)."""
+    def make():
+        its = [m() for m in makers]
+        idx = [it for it in its if it.kind in ("sorted", "bitmap")]
+        scans = [it for it in its if it.kind == "scan"]
+        rest = [it for it in its if it.kind not in ("sorted", "bitmap", "scan")]
+        if (idx and scans) or len(idx) > 1:
+            docs = np.logical_and.reduce([it.docs for it in idx]) if len(idx) > 1 else idx[0].docs.copy()
+            for sc in scans:  # ScanBasedDocIdIterator.applyAnd, in the AND's child order
+                docs = sc.apply_and(docs)
+            merged = _IndexIt(docs, "bitmap")  # RangelessBitmapDocIdIterator
+            return merged if not rest else _AndIt([merged] + rest)
+        return _AndIt(its)
+    return make
+
+
+def _or_set(makers, n):
+    """OrDocIdSet.iterator (OrDocIdSet.java:61-126)."""
+    def make():
+        its = [m() for m in makers]
+        idx = [it for it in its if it.kind in ("sorted", "bitmap")]
+        rest = [it for it in its if it.kind not in ("sorted", "bitmap")]
+        if len(idx) > 1:
+            merged = _IndexIt(np.logical_or.reduce([it.docs for it in idx]), "bitmap")  # BitmapDocIdIterator
+            return merged if not rest else _OrIt([merged] + rest)
+        return _OrIt(its)
+    return make
+
+
+_PRIORITY = {"sorted": 0, "range": 200, "and": 300, "or": 400, "scan": 500, "inverted": 10000}
+
+
+def _priority(node: _Leaf) -> int:
+    """FilterOperatorUtils.reorderAndFilterChildOperators' priorities (:197-241, PrioritizedFilterOperator): sorted
+    0, range index 200, AND 300, OR 400, SV scan 500, NOT its child's; an InvertedIndexFilterOperator is none of the
+    listed classes, so UNKNOWN_FILTER_PRIORITY (10000)."""
+    if node.kind == "leaf":
+        return _PRIORITY[node.ikind]
+    if node.kind == "not":
+        return _priority(node.children[0])
+    return _PRIORITY[node.kind]
+
+
+def filter_entries(root: _Leaf, seg: OracleSegment, used: list) -> int:
+    """numEntriesScannedInFilter of one segment (see filter_entries_of)."""
+    return filter_entries_of(root, seg.num_docs, lambda node: _eval_docs(node, seg, used))
+
+
+def filter_entries_of(root: _Leaf, n: int, docs_of) -> int:
+    """numEntriesScannedInFilter of one segment of n docs: the planned tree's DocIdSets (BaseFilterOperator.getTrues /
+    getFalses: NOT swaps them, AND.getFalses = OR of the children's falses, OR.getFalses = AND of them, a leaf's falses
+    = NotDocIdSet), the iterator DocIdSetOperator draws from it (:59-86) drained to EOF, summed over the scans.
+    docs_of(leaf) = the leaf's per-doc match booleans."""
+    scans = []
+    if root.kind in ("all", "none"):
+        return 0
+
+    def leaf_maker(node):
+        docs = docs_of(node)
+        if node.ikind == "scan":
+            def mk():
+                it = _ScanIt(docs)
+                scans.append(it)
+                return it
+            return mk
+        kind = "sorted" if node.ikind == "sorted" else "bitmap"
+        return lambda: _IndexIt(docs, kind)
+
+    def trues(node):
+        if node.kind == "leaf":
+            return leaf_maker(node)
+        if node.kind == "and":
+            kids = sorted(node.children, key=_priority)  # stable, as List.sort
+            return _and_set([trues(c) for c in kids], n)
+        if node.kind == "or":
+            return _or_set([trues(c) for c in node.children], n)
+        return falses(node.children[0])
+
+    def falses(node):
+        if node.kind == "leaf":
+            t = trues(node)
+            return lambda: _NotIt(t(), n)
+        if node.kind == "and":
+            kids = sorted(node.children, key=_priority)
+            return _or_set([falses(c) for c in kids], n)
+        if node.kind == "or":
+            return _and_set([falses(c) for c in node.children], n)
+        return trues(node.children[0])
+
+    it = trues(root)()
+    it.drain()
+    return sum(sc.entries for sc in scans)
 
 
 # --------------------------------------------------------------------------- execution
@@ -596,7 +859,7 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> Oracl
 
     seg_structs = (_Segment * max(1, len(segments)))()
     filter_programs = []
-    extra_entries = []  # per segment: AND-with-a-remaining-OR filter entries (_filter_plan)
+    extra_entries = []  # per segment: numEntriesScannedInFilter (filter_entries: the iterator simulation)
     for si, s in enumerate(segments):
         cols = (_Column * len(used))()
         keep.append(cols)
@@ -635,8 +898,10 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> Oracl
         prog = []
         extra = 0
         if q.filter is not None:
-            root, extra = _filter_plan(q.filter, s, col_index, used)
+            root = _filter_plan(q.filter, s, col_index, used)
             _emit(root, prog, keep)
+            # the statistic from the iterator simulation (the C program's own count is not used)
+            extra = filter_entries(_merge_same_column(_plan_filter(q.filter, s, col_index)), s, used)
         filter_programs.append(prog)
         extra_entries.append(extra)
 
@@ -672,7 +937,7 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> Oracl
                 keep_rows = _segment_trim(res, q, segments[si], unions, nagg, trim_size)
             _merge(res, q, merged_keys, merged, key_list, nagg, hll_idx, m, keep_rows)
             stats[0] += res.num_docs_scanned
-            stats[1] += res.num_entries_scanned_in_filter + extra_entries[si]
+            stats[1] += extra_entries[si]
             stats[2] += res.num_entries_scanned_post_filter
             stats[3] += res.num_total_docs
             stats[4] |= bool(res.num_groups_limit_reached)
@@ -788,7 +1053,10 @@ def _default_row(q, m):
 
 def _java_compare(a, b) -> int:
     """Comparable.compareTo of the boxed ORDER BY values: Long / Integer natural order, Double.compare (NaN
-    largest, -0.0 < 0.0), String.compareTo."""
+    largest, -0.0 < 0.0), String.compareTo (UTF-16 code-unit order: big-endian UTF-16 bytes compare the same)."""
+    if isinstance(a, str) and isinstance(b, str):
+        x, y = a.encode("utf-16-be", "surrogatepass"), b.encode("utf-16-be", "surrogatepass")
+        return (x > y) - (x < y)
     if isinstance(a, float) or isinstance(b, float):
         a, b = float(a), float(b)
         if a < b:
@@ -838,10 +1106,20 @@ def _segment_trim(res, q, seg: OracleSegment, unions, nagg, size):
                 return c
         return 0
 
+    return set(r[1] for r in table_resizer_heap(recs, inter, size))
+
+
+def table_resizer_heap(recs, inter, size):
+    """TableResizer.trimInSegmentResults' heap (TableResizer.java:233-262,321-343): the first `size` records in
+    iterator order heapified under the REVERSED intermediate-record comparator `inter` (makeHeap / downHeap), then
+    every later record that compares greater than the top replaces it.  Returns the heap array (index 0 = the
+    kept record nearest the trim boundary), as the reference's returned list."""
     def cmp(a, b):  # reversed
         return inter(b, a)
 
-    heap = recs[:size]
+    if len(recs) <= size:
+        return list(recs)
+    heap = list(recs[:size])
 
     def down(i):
         e = heap[i]
@@ -867,7 +1145,7 @@ def _segment_trim(res, q, seg: OracleSegment, unions, nagg, size):
         if cmp(r, heap[0]) > 0:
             heap[0] = r
             down(0)
-    return set(r[1] for r in heap)
+    return heap
 
 
 def _merge(res, q, merged_keys, merged, key_list, nagg, hll_idx, m, keep_rows=None):

@@ -103,6 +103,10 @@ int ph_segment_load_dir(ph_ctx* ctx, const char* segment_dir, const char* const*
   });
 }
 
+int ph_segment_check(const ph_segment_desc* desc) {
+  return guarded([&] { segment_check_impl(desc); });
+}
+
 int ph_segment_unpin(ph_segment* seg) {
   return guarded([&] {
     if (!seg) return;
@@ -132,6 +136,7 @@ int ph_segment_unpin(ph_segment* seg) {
         }
       }
     }
+    c.pinned_rows -= seg->num_docs;
     delete seg;  // hipFree waits for work in flight on the buffers
   });
 }
@@ -196,7 +201,7 @@ int ph_table_set_dictionary(ph_ctx* ctx, const char* column, int32_t data_type, 
     }
     for (int64_t i = 1; i < count; ++i)
       if (d.compare(i - 1, d, i) >= 0) fail(PH_ERR_INVALID_ARGUMENT, "table dictionary must be sorted and unique");
-    g->id = ctx->c.next_id++;
+    g->id = next_object_id();
     std::lock_guard<std::mutex> lk(ctx->c.mu);
     ctx->c.table_dicts[column] = g;
   });
@@ -223,10 +228,19 @@ int ph_query_execute(ph_ctx* ctx, const ph_query* query, ph_segment* const* segm
   });
 }
 
+// Dense partials merge whole per-device tables, so GroupByOperator's per-segment trim (ORDER BY +
+// minSegmentGroupTrimSize > 0, GroupByOperator.java:114-130) cannot apply: such queries are not served here (the caller
+// takes ph_query_execute, which trims, or the CPU plan).
+static void reject_segment_trim(const ph_query* q) {
+  if (q && q->min_segment_group_trim_size > 0 && q->num_group_by > 0 && q->num_order_by > 0)
+    fail(PH_ERR_UNSUPPORTED, "segment group trim (minSegmentGroupTrimSize) on dense partials");
+}
+
 int ph_query_dense_layout(ph_ctx* ctx, const ph_query* query, ph_segment* const* segments, int32_t num_segments,
                           ph_dense_layout* out) {
   return guarded([&] {
     if (!ctx || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
+    reject_segment_trim(query);
     DenseArgs d{DENSE_LAYOUT, nullptr, 0, 0, out};
     query_execute_impl(&ctx->c, query, segments, num_segments, &d);
   });
@@ -236,6 +250,7 @@ int ph_query_execute_dense(ph_ctx* ctx, const ph_query* query, ph_segment* const
                            void* const* device_tables, ph_exec_stats* stats) {
   return guarded([&] {
     if (!ctx || !device_tables) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
+    reject_segment_trim(query);
     DenseArgs d{DENSE_EXECUTE, device_tables, 0, 0, nullptr};
     std::unique_ptr<ph_result> r(query_execute_impl(&ctx->c, query, segments, num_segments, &d));
     if (stats && r) *stats = r->stats;
@@ -247,6 +262,7 @@ int ph_dense_finalize(ph_ctx* ctx, const ph_query* query, ph_segment* const* seg
   return guarded([&] {
     if (!ctx || !device_tables || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
     *out = nullptr;
+    reject_segment_trim(query);
     DenseArgs d{DENSE_FINALIZE, const_cast<void* const*>(device_tables), group_begin, group_end, nullptr};
     *out = query_execute_impl(&ctx->c, query, segments, num_segments, &d);
   });

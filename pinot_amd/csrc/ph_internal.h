@@ -285,6 +285,7 @@ struct KParams {
   int32_t part_fast;              // kernel A may run the lean k_part_scan (no gathers; ALL / RANGE / DOCRANGE leaves)
   int32_t part_depth;             // lean kernel A: tiles of loads in flight per wave (1: k_part_scan, 2: k_part_scan2)
   int32_t part_reg;               // kernel A = k_part_reg (register-direct decode; 0: the LDS-staged forms)
+  int32_t part_wave;              // with part_reg: k_part_wave (wave-private rings, no workgroup barriers)
   int32_t part_ck, part_cv;       // k_part_reg: 16-byte loads per lane of a filter / key stream, of the value stream
   int32_t part_rounds;            // k_part_reg: append rounds (flush + barrier) per tile (1 or 2)
   int32_t count_reg;              // MODE_COUNT: k_count_reg with this many 16-byte loads per lane (ceil(b / 4)); 0 off
@@ -436,6 +437,7 @@ struct Column {
   bool is_sorted = false;
   bool is_raw = false;                // pinned from a raw forward index (dictionary-encoded at pin)
   bool has_range_index = false;       // an exact (version 2) bit-sliced range index came with the column
+  bool has_inexact_range_index = false;  // a legacy version-1 range index (ranges + a partial scan)
   Dictionary dict;
   std::vector<int32_t> sorted_ranges;  // [card][2] (sorted columns)
   std::vector<uint8_t> inverted;       // host copy of the inverted index (offsets + roaring blobs)
@@ -510,7 +512,10 @@ struct Context {
   std::map<std::string, int32_t> column_types;                      // ph_table_set_column_type (schema)
   std::map<std::string, std::shared_ptr<GlobalDict>> union_cache;   // column + segment-set -> union
   std::deque<std::string> union_order;                              // union_cache keys, oldest first
-  std::atomic<uint64_t> next_id{1};
+  // segment / dictionary ids come from one process-wide counter (next_object_id): a multi-device ph_ctx holds one
+  // Context per device, and union-cache keys and remaps must not confuse segments of different devices
+  std::atomic<int64_t> pinned_rows{0};  // docs of the segments pinned here (multi-device placement: greedy by rows)
+  int32_t device_index = 0;             // position in its ph_ctx's device list
   // execution lanes
   std::mutex lane_mu;
   std::vector<std::unique_ptr<Lane>> lanes_free;
@@ -573,6 +578,9 @@ size_t part_agg_lds_bytes(const PartAggParams& p);
 size_t partition_lds_bytes(KParams& p);  // fills the pl_* offsets, returns the dynamic LDS size
 int part_reg_blocks_per_cu(const KParams& p, int ng, size_t lds);  // k_part_reg occupancy
 void launch_part_reg(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);  // scan_partition_reg.hip
+size_t part_wave_lds_bytes(int32_t num_parts);                                        // scan_partition_wave.hip
+int part_wave_blocks_per_cu(const KParams& p, int ng, size_t lds);
+void launch_part_wave(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);
 void launch_count_reg(const KParams& p, int grid, hipStream_t s);                      // scan_count_reg.hip
 void launch_agg_reg(const KParams& p, int grid, hipStream_t s);                        // scan_count_reg.hip
 void launch_group_reg(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);   // scan_group_reg.hip
@@ -622,6 +630,31 @@ struct FbJob {
   unsigned long long* out;     // [nprog][nwords] doc bitmaps
 };
 void launch_filter_bitmaps(const FilterInsn* prog, const DevSegment* segs, const FbJob& job, hipStream_t s);
+// numEntriesScannedInFilter of AndDocIdIterator(scan_1 .. scan_k) drained by next() (every child an SV scan): the
+// scans' match bitmaps ([k][nwords] words at `bits`), per segment job; gaps longer than `step_cap` word steps go to
+// the fallback list (job << 40 | gap start) for the host
+struct ScanAndJob {
+  const unsigned long long* bits;
+  int64_t nwords, ndocs;
+  int32_t k, slot;  // scans; entries accumulate into out[slot]
+};
+void launch_scan_and_entries(const ScanAndJob* jobs, int32_t njobs, int64_t max_words, unsigned long long* out,
+                             unsigned long long* fb, uint32_t* fb_n, uint32_t fb_cap, int32_t step_cap, hipStream_t s);
+// host iterator simulation of the statistic (filter_sim.cpp): the planned filter tree over per-leaf doc bitmaps
+enum SimOp { SIM_LEAF = 0, SIM_AND = 1, SIM_OR = 2, SIM_NOT = 3 };
+enum SimLeafKind { SIM_SCAN = 0, SIM_SORTED = 1, SIM_BITMAP = 2 };
+struct SimLeaf {
+  int32_t kind;          // SimLeafKind: which iterator the reference builds for the leaf
+  const uint64_t* bits;  // the leaf's doc bitmap (ceil(num_docs / 64) words)
+};
+struct SimNode {
+  int32_t op = SIM_LEAF;
+  int32_t priority = 0;  // FilterOperatorUtils.reorderAndFilterChildOperators priority (AND children, stable order)
+  int32_t leaf = -1;
+  std::vector<SimNode> kids;
+};
+int64_t simulate_filter_entries(const SimNode& root, const std::vector<SimLeaf>& leaves, int64_t num_docs);
+int64_t scan_and_gap_entries(const uint64_t* const* scans, int k, int64_t num_docs, int64_t t);
 void launch_selftest_staged(const DevSegment* seg, int32_t tile_words, int32_t stage_stride, int64_t n, int32_t* out,
                             hipStream_t s);
 // the 1 KiB wave-loads of a full tile of every staged stream of `d` (stage offsets per stream)
@@ -657,6 +690,9 @@ void launch_compact(const CompactParams& p, hipStream_t s);
 int32_t murmur_hash_long(int64_t v);
 int32_t murmur_hash_bytes(const uint8_t* data, int32_t len, int32_t seed);
 uint32_t hll_entry(int32_t hash, int log2m);
+void segment_check_impl(const ph_segment_desc* desc);                    // segment.cpp
+uint64_t next_object_id();                                               // segment.cpp
+void build_hll_table(Context* ctx, Column& c, int log2m, hipStream_t st);  // into c.hll_tables (async on st)
 void fixed_bit_pack_host(const int32_t* ids, int64_t n, int bits, uint8_t* out);
 // raw (no-dictionary) forward indexes (rawfwd.cpp): decode a chunk forward index to native values, and
 // dictionary-encode native values (sorted distinct values + per-doc ids)

@@ -49,6 +49,8 @@ struct PNode {
   std::vector<int32_t> ranges;        // OP_DOCRANGES pairs
   int bitmap_leaf = -1;               // OP_BITMAP: index into the query's bitmap list
   bool scan = false;
+  bool exclusive = false;    // OP_NOT over OP_BITMAP built for an exclusive predicate (InvertedIndexFilterOperator's
+                             // flipped bitmap: a BitmapDocIdSet, not a user NOT)
   bool range_index = false;  // a scan-evaluated RangeIndexBasedFilterOperator leaf: index-based for the statistics
   // AND whose children are index-based leaves (sorted, bitmap, range index, ORs / NOTs of them) followed by scan
   // leaves: the reference's AndDocIdSet applies the scans one after another to the index-based result
@@ -281,6 +283,7 @@ struct Planner {
       if (s.exclusive) {
         PNode inv;
         inv.op = OP_NOT;
+        inv.exclusive = true;
         inv.kids.push_back(std::move(n));
         return inv;
       }
@@ -292,6 +295,10 @@ struct Planner {
     // exact range index, or EQ on one without an inverted index.  Same doc set as a scan of the dictIds, which is
     // how the kernels evaluate it; it scans no entries (BitmapDocIdSet)
     n.range_index = c.has_range_index && (p.type == PH_PRED_RANGE || (p.type == PH_PRED_EQ && !c.has_inverted()));
+    // a legacy version-1 range index is a RangeIndexBasedFilterOperator too (RangeIndexBasedFilterOperator.java:59-60),
+    // whose partial scan of the boundary ranges the statistics here do not model: such leaves take the CPU plan
+    if (c.has_inexact_range_index && (p.type == PH_PRED_RANGE || (p.type == PH_PRED_EQ && !c.has_inverted())))
+      fail(PH_ERR_UNSUPPORTED, "column " + c.name + ": a version-1 (inexact) range index leaf");
     if (s.is_range) {
       n.op = OP_RANGE;
       n.lo = (uint32_t)s.start;
@@ -490,7 +497,7 @@ bool index_based(const PNode& k) {
   if (k.kind != L_NODE) return false;
   if (k.op == OP_DOCRANGES || k.op == OP_BITMAP) return true;
   if (k.scan) return k.range_index;
-  if (k.op == OP_NOT) return k.kids.size() == 1 && k.kids[0].op == OP_BITMAP;  // exclusive inverted-index leaf
+  if (k.op == OP_NOT) return k.exclusive;  // exclusive inverted-index leaf (a user NOT is a NotDocIdSet)
   if (k.op == OP_OR) {
     for (auto& c : k.kids)
       if (!index_based(c)) return false;
@@ -523,105 +530,62 @@ void mark_apply_and(PNode& n) {
   for (auto& k : n.kids) mark_apply_and(k);
 }
 
-// An AND of index-based children, scan leaves and exactly ONE remaining OR of index-based / scan leaves, with >= 1
-// index-based and >= 1 scan child or >= 2 index-based ones: AndDocIdSet.iterator (:128-185) merges the index-based
-// children, applies the scans (applyAnd) and returns AndDocIdIterator(merged, OR) -- the OR's scan children then
-// count the docs their advance() examines (SVScanDocIdIterator.advance :101-112), which the per-doc program cannot
-// see.  The statistic comes from doc bitmaps of the parts (k_filter_bitmaps) and and_or_entries below.
-struct AndOrShape {
-  bool ok = false;
-  PNode d0;                   // the merged index-based children (an AND of them, or the one)
-  std::vector<PNode> scans;   // the AND's scan children, in order (applyAnd)
-  PNode orn;                  // the remaining OR
-  std::vector<PNode> oscans;  // the OR's scan children
-};
-AndOrShape and_or_shape(const PNode& r) {
-  AndOrShape sh;
-  if (r.kind != L_NODE || r.op != OP_AND || r.stats_nscan) return sh;
-  auto plain_scan = [](const PNode& k) { return k.kind == L_NODE && k.scan && !k.range_index && k.kids.empty(); };
-  std::vector<PNode> idx, ors;
+// How a segment's numEntriesScannedInFilter is computed (the reference counts the docs its scan iterators examine,
+// which depends on how its iterator tree drives them: filter_sim.cpp):
+//  ST_DEVICE  -- every scan is either drained by next() (a lone scan, scans under an OR / a NOT of a leaf: numDocs
+//                each) or applied by an AndDocIdSet to its merged index-based children (applyAnd: |D0| + |D0 n S1| +
+//                ..., counted per doc by the flagged AND of the device program / FK_CONJ / k_group_sparse);
+//  ST_SCANAND -- an AND of SV scans only: AndDocIdIterator leap-frogs their advance() (k_scan_and_entries);
+//  ST_SIM     -- anything else: the host runs the iterator tree over the leaves' doc bitmaps (k_filter_bitmaps).
+enum StatKind { ST_DEVICE = 0, ST_SCANAND = 1, ST_SIM = 2 };
+
+bool plain_scan(const PNode& k) { return k.kind == L_NODE && k.scan && !k.range_index && k.kids.empty(); }
+// a leaf of the reference's operator tree: a predicate leaf, or an exclusive inverted leaf (its flipped bitmap)
+bool stat_leaf(const PNode& k) { return k.kind == L_NODE && (k.kids.empty() || (k.op == OP_NOT && k.exclusive)); }
+
+int stat_kind(const PNode& r) {
+  if (r.kind != L_NODE || stat_leaf(r)) return ST_DEVICE;
+  auto leafish = [](const PNode& k) { return stat_leaf(k) || (k.op == OP_NOT && stat_leaf(k.kids[0])); };
+  if (r.op == OP_NOT) return leafish(r) ? ST_DEVICE : ST_SIM;
+  if (r.op == OP_OR) {
+    for (auto& k : r.kids)
+      if (!leafish(k)) return ST_SIM;
+    return ST_DEVICE;
+  }
+  int nidx = 0, nscan = 0;
   for (auto& k : r.kids) {
-    if (index_based(k)) {
-      idx.push_back(k);
-    } else if (plain_scan(k)) {
-      sh.scans.push_back(k);
-    } else if (k.kind == L_NODE && k.op == OP_OR) {
-      for (auto& c : k.kids)
-        if (!index_based(c) && !plain_scan(c)) return sh;
-      ors.push_back(k);
-    } else {
-      return sh;
-    }
+    if (index_based(k)) ++nidx;
+    else if (plain_scan(k)) ++nscan;
+    else return ST_SIM;
   }
-  if (ors.size() != 1 || !((!idx.empty() && !sh.scans.empty()) || idx.size() > 1)) return sh;
-  if (2 + sh.scans.size() + ors[0].kids.size() > (size_t)kMaxFbProgs) return sh;
-  if (idx.size() == 1) {
-    sh.d0 = idx[0];
-  } else {
-    sh.d0.op = OP_AND;
-    sh.d0.kids = idx;
-  }
-  sh.orn = ors[0];
-  for (auto& c : sh.orn.kids)
-    if (plain_scan(c)) sh.oscans.push_back(c);
-  sh.ok = true;
-  return sh;
+  if (nidx > 0) return nscan <= 16 ? ST_DEVICE : ST_SIM;  // mark_apply_and flags up to 16 scans
+  return nscan <= kMaxFbProgs ? ST_SCANAND : ST_SIM;
 }
 
-// The statistic over one segment from its part bitmaps (64 docs per word, doc d at bit d & 63 of word d >> 6):
-// applyAnd gives |D0| + |D0 n S1| + ...; then the leapfrog of AndDocIdIterator(A, OR) touches the OR at the
-// candidates a_i of A with B n [a_(i-1), a_i] non-empty (and at a_0), and an OR scan child advances there when it
-// holds no doc in [a_(i-1), a_i), examining [a_i, its next match] -- to the segment end when there is none, after
-// which it is done (the closed form is checked against a literal iterator simulation in test_oracle_kat.py).
-int64_t and_or_entries(const uint64_t* d0, const std::vector<const uint64_t*>& scans, const uint64_t* b,
-                       const std::vector<const uint64_t*>& ors, int64_t nw, int64_t ndocs) {
-  std::vector<uint64_t> cur(d0, d0 + nw);
-  int64_t ent = 0;
-  for (const uint64_t* sc : scans)
-    for (int64_t w = 0; w < nw; ++w) {
-      ent += __builtin_popcountll(cur[w]);
-      cur[w] &= sc[w];
-    }
-  auto ranks = [&](const uint64_t* m) {  // docs of m before word w
-    std::vector<int64_t> r(nw + 1, 0);
-    for (int64_t w = 0; w < nw; ++w) r[w + 1] = r[w] + __builtin_popcountll(m[w]);
-    return r;
-  };
-  auto rank = [](const uint64_t* m, const std::vector<int64_t>& r, int64_t x) {  // docs of m in [0, x)
-    const int64_t w = x >> 6, o = x & 63;
-    return r[w] + (o ? __builtin_popcountll(m[w] & ((1ull << o) - 1ull)) : 0);
-  };
-  auto next = [&](const uint64_t* m, int64_t x) -> int64_t {  // first doc of m >= x, or -1
-    for (int64_t w = x >> 6; w < nw; ++w) {
-      const uint64_t v = w == (x >> 6) ? m[w] & (~0ull << (x & 63)) : m[w];
-      if (v) return w * 64 + __builtin_ctzll(v);
-    }
-    return -1;
-  };
-  const std::vector<int64_t> rb = ranks(b);
-  std::vector<std::vector<int64_t>> ro;
-  for (const uint64_t* o : ors) ro.push_back(ranks(o));
-  std::vector<char> done(ors.size(), 0);
-  int64_t prev = -1;
-  for (int64_t w = 0; w < nw; ++w)
-    for (uint64_t v = cur[w]; v; v &= v - 1) {
-      const int64_t a = w * 64 + __builtin_ctzll(v);
-      const bool visited = prev < 0 || rank(b, rb, a + 1) - rank(b, rb, prev) > 0;
-      if (visited) {
-        for (size_t c = 0; c < ors.size(); ++c) {
-          if (done[c] || (prev >= 0 && rank(ors[c], ro[c], a) - rank(ors[c], ro[c], prev) == 0)) continue;
-          const int64_t nx = next(ors[c], a);
-          if (nx >= 0) {
-            ent += nx - a + 1;
-          } else {
-            ent += ndocs - a;
-            done[c] = 1;
-          }
-        }
-      }
-      prev = a;
-    }
-  return ent;
+// the statistic's tree of a segment for the host simulation: leaves collected in order (one doc bitmap each)
+SimNode to_sim(const PNode& n, std::vector<PNode>& leaves, std::vector<int32_t>& kinds) {
+  SimNode x;
+  if (stat_leaf(n)) {
+    x.op = SIM_LEAF;
+    x.leaf = (int32_t)leaves.size();
+    leaves.push_back(n);
+    // FilterOperatorUtils priorities (:197-241): SortedIndexBasedFilterOperator 0, RangeIndexBasedFilterOperator 200,
+    // ScanBasedFilterOperator 500; InvertedIndexFilterOperator is none of the listed classes (10000)
+    if (n.op == OP_DOCRANGES) { kinds.push_back(SIM_SORTED); x.priority = 0; }
+    else if (n.scan && n.range_index) { kinds.push_back(SIM_BITMAP); x.priority = 200; }
+    else if (n.scan) { kinds.push_back(SIM_SCAN); x.priority = 500; }
+    else { kinds.push_back(SIM_BITMAP); x.priority = 10000; }
+    return x;
+  }
+  x.op = n.op == OP_AND ? SIM_AND : (n.op == OP_OR ? SIM_OR : SIM_NOT);
+  x.priority = n.op == OP_AND ? 300 : 400;
+  for (auto& k : n.kids) x.kids.push_back(to_sim(k, leaves, kinds));
+  return x;
+}
+
+void clear_apply_and(PNode& n) {
+  n.stats_nidx = n.stats_nscan = 0;
+  for (auto& k : n.kids) clear_apply_and(k);
 }
 
 // k_group_sparse's filter shape: one inverted-index leaf, or an AND of 1..kMaxConj of them and <= kMaxConj plain
@@ -766,7 +730,7 @@ std::shared_ptr<GlobalDict> build_union(Context* ctx, const std::string& col, co
   }
   auto g = std::make_shared<GlobalDict>();
   g->dict = std::move(u);
-  g->id = ctx->next_id++;
+  g->id = next_object_id();
   return g;
 }
 
@@ -812,30 +776,16 @@ const void* global_dict_device_values(Context* ctx, GlobalDict& g) {
 }
 
 const uint32_t* segment_hll_table(Context* ctx, Column& c, int log2m, hipStream_t st) {
-  std::lock_guard<std::mutex> lk(c.cache_mu);
-  auto it = c.hll_tables.find(log2m);
-  if (it != c.hll_tables.end()) return it->second.buf->as<uint32_t>();
-  HllTable t;
-  t.buf = std::make_unique<DeviceBuffer>();
-  t.buf->alloc(sizeof(uint32_t) * std::max(1, c.cardinality), ctx->device);
-  if (c.data_type == PH_STRING) {
-    // MurmurHash.hash(String.getBytes()) = hash(bytes, len, -1)
-    std::vector<uint32_t> h(c.cardinality);
-    for (int32_t i = 0; i < c.cardinality; ++i) {
-      const std::string& s = c.dict.strings[i];
-      h[i] = hll_entry(murmur_hash_bytes(reinterpret_cast<const uint8_t*>(s.data()), (int32_t)s.size(), -1), log2m);
-    }
-    PH_HIP_CHECK(hipMemcpy(t.buf->ptr, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice));
-  } else if (c.data_type == PH_FLOAT) {
-    fail(PH_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL on FLOAT columns is not on the GPU path");
-  } else {
-    // INT / LONG -> hashLong((long) value); DOUBLE -> hashLong(doubleToRawLongBits)
-    launch_hll_table(c.d_values.ptr, c.data_type != PH_DOUBLE, c.cardinality, log2m, t.buf->as<uint32_t>(), st);
-    PH_HIP_CHECK(hipStreamSynchronize(st));
+  {
+    std::lock_guard<std::mutex> lk(c.cache_mu);
+    auto it = c.hll_tables.find(log2m);
+    if (it != c.hll_tables.end()) return it->second.buf->as<uint32_t>();
   }
-  const uint32_t* p = t.buf->as<uint32_t>();
-  c.hll_tables[log2m] = std::move(t);
-  return p;
+  // not built at pin (ph_column_desc.hll_log2m): the first query that needs it does
+  std::lock_guard<std::mutex> lk(c.cache_mu);
+  build_hll_table(ctx, c, log2m, st);
+  PH_HIP_CHECK(hipStreamSynchronize(st));
+  return c.hll_tables.at(log2m).buf->as<uint32_t>();
 }
 
 void put_key_value(const Dictionary& d, int64_t id, uint8_t* dst, int32_t entry) {
@@ -896,31 +846,8 @@ int bits_for_range(uint64_t range) {
 }
 
 // Frame-of-reference value stream of an INT/LONG column (VK_PACKED), built once per pinned column.
-bool ensure_value_stream(Context* ctx, ph_segment* seg, Column& c, hipStream_t st) {
-  std::lock_guard<std::mutex> lk(c.cache_mu);
-  if (c.vpacked_ready) return c.d_vpacked != nullptr;
-  c.vpacked_ready = true;
-  if (c.data_type != PH_INT && c.data_type != PH_LONG) return false;
-  if (c.cardinality <= 0 || seg->num_docs == 0) return false;
-  const int64_t lo = c.dict.ints.front(), hi = c.dict.ints.back();
-  const uint64_t range = (uint64_t)hi - (uint64_t)lo;
-  const int vb = std::max(1, bits_for_range(range));
-  if (vb > 31) return false;
-  // only worth it when it avoids a dictionary gather of meaningful size
-  const int64_t n = seg->num_docs;
-  const size_t bytes = (size_t)((n * vb + 7) / 8);
-  const size_t alloc = ((bytes + kFwdPadBytes + 255) / 256) * 256;
-  auto buf = std::make_unique<DeviceBuffer>();
-  buf->alloc(alloc, ctx->device);
-  PH_HIP_CHECK(hipMemsetAsync(buf->ptr, 0, alloc, st));
-  launch_encode_values(c.d_fwd.as<uint32_t>(), c.bits, c.d_values.as<int64_t>(), lo, vb, n, buf->as<uint32_t>(), st);
-  PH_HIP_CHECK(hipStreamSynchronize(st));
-  c.vbase = lo;
-  c.vbits = vb;
-  seg->device_bytes += (int64_t)alloc;
-  c.d_vpacked = std::move(buf);
-  return true;
-}
+// the frame-of-reference value stream of an INT / LONG column (VK_PACKED), built at pin (build_value_stream)
+bool ensure_value_stream(Context*, ph_segment*, Column& c, hipStream_t) { return c.d_vpacked != nullptr; }
 
 }  // namespace
 
@@ -1162,7 +1089,17 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<SegProgram> progs(nseg);
   std::vector<PNode> roots(nseg);
   std::vector<char> seg_live(nseg, 1);
-  std::vector<AndOrShape> andor(nseg);  // segments whose filter statistic needs the advance() pass
+  // segments whose filter statistic runs a pass of its own (ST_SCANAND / ST_SIM): the reference's tree over the
+  // leaves, the leaves themselves (one doc bitmap each) and their iterator kinds
+  struct StatSeg {
+    int qi, kind;
+    SimNode root;
+    std::vector<PNode> leaves;
+    std::vector<int32_t> leaf_kinds;
+    int32_t dseg = -1;
+    std::vector<size_t> jobs;  // its FbJobs (<= kMaxFbProgs leaves each, in leaf order)
+  };
+  std::vector<StatSeg> stat_segs;
   for (int i = 0; i < nseg && dop != DENSE_LAYOUT && !fin; ++i) {
     PNode root;
     root.kind = L_ALL;
@@ -1171,9 +1108,17 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     // (MergeEqInFilterOptimizer: `d_year = 1997 OR d_year = 1998` -> one IN; MergeRangeFilterOptimizer: ranges of
     // one column under an AND), so the statistics below see the reference's operator tree
     merge_same_column_leaves(root, [&](int slot) { return (int64_t)segs[i]->columns.at(slot_names[slot])->cardinality; });
+    const int sk = stat_kind(root);
+    if (sk != ST_DEVICE && segs[i]->num_docs > 0) {
+      StatSeg ss;
+      ss.qi = i;
+      ss.kind = sk;
+      ss.root = to_sim(root, ss.leaves, ss.leaf_kinds);
+      stat_segs.push_back(std::move(ss));
+    }
     mark_apply_and(root);
-    andor[i] = and_or_shape(root);
-    if (!andor[i].ok) stats.num_entries_scanned_in_filter += (int64_t)segs[i]->num_docs * count_scan_leaves(root);
+    if (sk != ST_DEVICE) clear_apply_and(root);  // the pass counts this segment, not the device program
+    else stats.num_entries_scanned_in_filter += (int64_t)segs[i]->num_docs * count_scan_leaves(root);
     if (root.kind == L_NONE || segs[i]->num_docs == 0) seg_live[i] = 0;
     roots[i] = std::move(root);
   }
@@ -1633,7 +1578,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<std::pair<size_t, std::vector<uint32_t>>> fset_fix;     // segment index -> FK_SET bitset
   std::vector<std::pair<size_t, int>> fbitmap_fix;                    // segment index -> bitmap leaf
   std::vector<std::pair<size_t, std::vector<uint32_t>>> conj_set_fix; // segment index * kMaxConj + leaf -> bitset
-  std::vector<std::pair<FbJob, int>> fb_jobs;                          // statistic passes (job, AND scan count)
+  std::vector<FbJob> fb_jobs;                                          // statistic passes: leaf doc bitmaps
   std::vector<std::pair<size_t, int>> sbm_fix;                         // segment index * kSparseBitmaps + k -> bitmap leaf
   std::vector<std::pair<size_t, std::vector<uint32_t>>> sset_fix;     // segment index * kMaxConj + k -> bitset
   // k_group_sparse: every live segment's filter is a sparse_shape AND whose bitmaps keep < 1/8 of the docs (the
@@ -1730,17 +1675,20 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       for (auto& bb : progs[i].bitmap_refs) bitmap_fix.push_back({d.prog_off + bb.first, bb.second});
       all_insns.insert(all_insns.end(), progs[i].insns.begin(), progs[i].insns.end());
     }
-    if (andor[i].ok) {  // the statistic's part programs (k_filter_bitmaps)
-      FbJob job{};
-      job.seg = (int32_t)si;
-      job.nwords = ((int64_t)s->num_docs + 63) / 64;
-      std::vector<const PNode*> parts{&andor[i].d0};
-      for (auto& k : andor[i].scans) parts.push_back(&k);
-      parts.push_back(&andor[i].orn);
-      for (auto& k : andor[i].oscans) parts.push_back(&k);
-      for (const PNode* n : parts) {
+    for (auto& ss : stat_segs) {  // the statistic's leaf programs (k_filter_bitmaps), <= kMaxFbProgs per job
+      if (ss.qi != i) continue;
+      ss.dseg = (int32_t)si;
+      for (size_t l = 0; l < ss.leaves.size(); ++l) {
+        if (l % kMaxFbProgs == 0) {
+          FbJob job{};
+          job.seg = (int32_t)si;
+          job.nwords = ((int64_t)s->num_docs + 63) / 64;
+          ss.jobs.push_back(fb_jobs.size());
+          fb_jobs.push_back(job);
+        }
+        FbJob& job = fb_jobs[ss.jobs.back()];
         SegProgram sp;
-        emit(*n, sp);
+        emit(ss.leaves[l], sp);
         if (sp.max_depth > kMaxStack || (int)sp.insns.size() > kMaxProg) fail(PH_ERR_UNSUPPORTED, "filter too large");
         job.off[job.nprog] = (int32_t)all_insns.size();
         job.len[job.nprog] = (int32_t)sp.insns.size();
@@ -1749,7 +1697,6 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         for (auto& bb : sp.bitmap_refs) bitmap_fix.push_back({all_insns.size() + bb.first, bb.second});
         all_insns.insert(all_insns.end(), sp.insns.begin(), sp.insns.end());
       }
-      fb_jobs.push_back({job, (int)andor[i].scans.size()});
     }
     if (sparse_plan) {
       const SparseShape sh = sparse_shape(root);
@@ -2372,9 +2319,16 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
                           : kp.part_depth == 2 ? PH_KERNEL_PART_LEAN2 : PH_KERNEL_PART_LEAN;
       kp.part_vbits = vbits;
       kp.num_parts = (int32_t)P;
-      const size_t lds_a = partition_lds_bytes(kp);
+      // k_part_wave: the register-direct kernel A with wave-private rings (no workgroup barriers); opt-in
+      // (PH_PART_WAVE=1): measured on config 3 it runs 4.6 ms against k_part_reg's 3.6 (8 waves per CU, LDS-bound)
+      kp.part_wave = 0;
+      if (const char* e = getenv("PH_PART_WAVE")) kp.part_wave = kp.part_reg && atoi(e) != 0 &&
+                                                                 part_wave_lds_bytes((int32_t)P) <= 160 * 1024;
+      if (kp.part_wave) stats.scan_kernel = PH_KERNEL_PART_WAVE;
+      const size_t lds_a = kp.part_wave ? part_wave_lds_bytes((int32_t)P) : partition_lds_bytes(kp);
       int a_cap = 4;  // 8-wave workgroups: <= 4 per CU (32 waves)
-      if (kp.part_reg) a_cap = part_reg_blocks_per_cu(kp, q->num_group_by, lds_a);  // 4-wave groups, VGPR-bound
+      if (kp.part_wave) a_cap = part_wave_blocks_per_cu(kp, q->num_group_by, lds_a);
+      else if (kp.part_reg) a_cap = part_reg_blocks_per_cu(kp, q->num_group_by, lds_a);  // 4-wave groups, VGPR-bound
       if (const char* e = getenv("PH_PART_WG_PER_CU")) a_cap = std::max(1, std::min(8, atoi(e)));  // tuning knob
       const int a_per_cu = (int)std::max<size_t>(1, std::min<size_t>(a_cap, (160 * 1024) / lds_a));
       const int grid_a = ctx->num_cus * a_per_cu;
@@ -2485,44 +2439,144 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       PH_HIP_CHECK(hipStreamWaitEvent(st, L.event(2 * batches.size() + 1), 0));
       PH_HIP_CHECK(hipEventRecord(L.ev_stop, st));
     }
-    // numEntriesScannedInFilter of ANDs with a remaining OR: the parts' doc bitmaps, then the host's closed form
-    // (a statistics pass, after the scan's device-time window)
-    if (!fb_jobs.empty()) {
-      // every segment's part bitmaps in one launch set and one copy, then the segments' closed forms in parallel
-      size_t total = 0;
-      for (auto& fj : fb_jobs) total += (size_t)fj.first.nprog * (size_t)fj.first.nwords;
-      unsigned long long* dev = scratch.alloc<unsigned long long>(std::max<size_t>(1, total));
-      std::vector<uint64_t> h(std::max<size_t>(1, total));
-      std::vector<size_t> base(fb_jobs.size());
-      size_t off = 0;
-      for (size_t t = 0; t < fb_jobs.size(); ++t) {
-        FbJob job = fb_jobs[t].first;
-        job.out = dev + off;
-        base[t] = off;
-        off += (size_t)job.nprog * (size_t)job.nwords;
-        launch_filter_bitmaps(d_prog, d_segs, job, st);
-      }
-      PH_HIP_CHECK(hipMemcpyAsync(h.data(), dev, 8 * total, hipMemcpyDeviceToHost, st));
-      PH_HIP_CHECK(hipStreamSynchronize(st));
-      std::vector<int64_t> ent(fb_jobs.size(), 0);
-      std::atomic<size_t> next_job{0};
-      auto work = [&]() {
-        for (size_t t; (t = next_job.fetch_add(1)) < fb_jobs.size();) {
-          const FbJob& job = fb_jobs[t].first;
-          const int ns = fb_jobs[t].second;
-          const int64_t nw = job.nwords;
-          const uint64_t* hb = h.data() + base[t];
-          std::vector<const uint64_t*> sc, oc;
-          for (int k = 0; k < ns; ++k) sc.push_back(hb + (size_t)(1 + k) * nw);
-          for (int k = ns + 2; k < job.nprog; ++k) oc.push_back(hb + (size_t)k * nw);
-          ent[t] = and_or_entries(hb, sc, hb + (size_t)(1 + ns) * nw, oc, nw, dsegs[job.seg].num_docs);
-        }
+    // numEntriesScannedInFilter of the ST_SCANAND / ST_SIM segments (a statistics pass after the scan's device-time
+    // window): the leaves' doc bitmaps (k_filter_bitmaps), then the AND-of-scans gap pass on the device or the
+    // iterator simulation on the host, in batches of segments bounded to kStatBatchWords words of bitmaps
+    if (!stat_segs.empty()) {
+      constexpr size_t kStatBatchWords = (size_t)32 << 20;  // 256 MiB
+      auto seg_words = [&](const StatSeg& ss) {
+        return ss.leaves.size() * (size_t)((dsegs[ss.dseg].num_docs + 63) / 64);
       };
-      const size_t nthr = std::min<size_t>(fb_jobs.size(), std::max(1u, std::min(8u, std::thread::hardware_concurrency())));
-      std::vector<std::thread> pool;
-      for (size_t k = 1; k < nthr; ++k) pool.emplace_back(work);
-      work();
-      for (auto& th : pool) th.join();
+      size_t total = 0, biggest = 0, n_scanand = 0;
+      for (auto& ss : stat_segs) {
+        if (ss.dseg < 0) continue;
+        total += seg_words(ss);
+        biggest = std::max(biggest, seg_words(ss));
+        n_scanand += ss.kind == ST_SCANAND;
+      }
+      const size_t cap_words = std::max<size_t>(1, std::min(total, std::max(kStatBatchWords, biggest)));
+      unsigned long long* dev = scratch.alloc<unsigned long long>(cap_words);
+      constexpr uint32_t kFbCap = 4096;
+      ScanAndJob* d_jobs = n_scanand ? scratch.alloc<ScanAndJob>(n_scanand) : nullptr;
+      unsigned long long* d_out = n_scanand ? scratch.alloc<unsigned long long>(n_scanand) : nullptr;
+      unsigned long long* d_fb = n_scanand ? scratch.alloc<unsigned long long>(kFbCap) : nullptr;
+      uint32_t* d_fbn = n_scanand ? scratch.alloc<uint32_t>(1) : nullptr;
+      std::vector<int64_t> ent(stat_segs.size(), 0);
+      size_t next = 0;
+      while (next < stat_segs.size()) {
+        // the batch: whole segments up to cap_words words of bitmaps
+        std::vector<size_t> batch, base;
+        size_t used = 0;
+        for (; next < stat_segs.size(); ++next) {
+          const StatSeg& ss = stat_segs[next];
+          if (ss.dseg < 0) continue;
+          if (!batch.empty() && used + seg_words(ss) > cap_words) break;
+          batch.push_back(next);
+          base.push_back(used);
+          used += seg_words(ss);
+        }
+        if (batch.empty()) break;
+        std::vector<ScanAndJob> sj;
+        std::vector<size_t> sj_seg;  // batch position of each scan-AND job
+        int64_t max_words = 0;
+        for (size_t b = 0; b < batch.size(); ++b) {
+          const StatSeg& ss = stat_segs[batch[b]];
+          const int64_t nw = (dsegs[ss.dseg].num_docs + 63) / 64;
+          for (size_t j = 0; j < ss.jobs.size(); ++j) {
+            FbJob job = fb_jobs[ss.jobs[j]];
+            job.out = dev + base[b] + j * kMaxFbProgs * (size_t)nw;
+            launch_filter_bitmaps(d_prog, d_segs, job, st);
+          }
+          if (ss.kind == ST_SCANAND) {
+            ScanAndJob J{};
+            J.bits = dev + base[b];
+            J.nwords = nw;
+            J.ndocs = dsegs[ss.dseg].num_docs;
+            J.k = (int32_t)ss.leaves.size();
+            J.slot = (int32_t)sj.size();
+            sj.push_back(J);
+            sj_seg.push_back(b);
+            max_words = std::max(max_words, nw);
+          }
+        }
+        std::vector<unsigned long long> out(sj.size(), 0);
+        uint32_t fbn = 0;
+        if (!sj.empty()) {
+          PH_HIP_CHECK(hipMemcpyAsync(d_jobs, sj.data(), sizeof(ScanAndJob) * sj.size(), hipMemcpyHostToDevice, st));
+          PH_HIP_CHECK(hipMemsetAsync(d_out, 0, 8 * sj.size(), st));
+          PH_HIP_CHECK(hipMemsetAsync(d_fbn, 0, 4, st));
+          launch_scan_and_entries(d_jobs, (int32_t)sj.size(), max_words, d_out, d_fb, d_fbn, kFbCap, 1 << 14, st);
+          PH_HIP_CHECK(hipMemcpyAsync(out.data(), d_out, 8 * sj.size(), hipMemcpyDeviceToHost, st));
+          PH_HIP_CHECK(hipMemcpyAsync(&fbn, d_fbn, 4, hipMemcpyDeviceToHost, st));
+        }
+        // the host side needs the simulated segments' bitmaps (and the fallback ones', below)
+        std::vector<uint64_t> h(used);
+        std::vector<char> on_host(batch.size(), 0);
+        auto fetch = [&](size_t b) {
+          const StatSeg& ss = stat_segs[batch[b]];
+          PH_HIP_CHECK(hipMemcpyAsync(h.data() + base[b], dev + base[b], 8 * seg_words(ss), hipMemcpyDeviceToHost, st));
+          on_host[b] = 1;
+        };
+        for (size_t b = 0; b < batch.size(); ++b)
+          if (stat_segs[batch[b]].kind == ST_SIM) fetch(b);
+        PH_HIP_CHECK(hipStreamSynchronize(st));
+        for (size_t j = 0; j < sj.size(); ++j) ent[batch[sj_seg[j]]] = (int64_t)out[j];
+        // gaps the device left (longer than its step cap): exact on the host from their start; a full list means
+        // those segments are simulated whole
+        std::vector<char> redo(batch.size(), 0);
+        std::vector<unsigned long long> fb(std::min(fbn, kFbCap));
+        if (fbn) {
+          PH_HIP_CHECK(hipMemcpy(fb.data(), d_fb, 8 * fb.size(), hipMemcpyDeviceToHost));
+          for (size_t j = 0; j < sj.size(); ++j)
+            if (fbn > kFbCap) redo[sj_seg[j]] = 1;
+          for (unsigned long long e : fb) {
+            const size_t b = sj_seg[(size_t)(e >> 40)];
+            if (!on_host[b]) fetch(b);
+          }
+          for (size_t b = 0; b < batch.size(); ++b)
+            if (redo[b] && !on_host[b]) fetch(b);
+          PH_HIP_CHECK(hipStreamSynchronize(st));
+          if (fbn <= kFbCap) {
+            for (unsigned long long e : fb) {
+              const size_t b = sj_seg[(size_t)(e >> 40)];
+              const StatSeg& ss = stat_segs[batch[b]];
+              const int64_t n = dsegs[ss.dseg].num_docs, nw = (n + 63) / 64;
+              std::vector<const uint64_t*> sc;
+              for (size_t l = 0; l < ss.leaves.size(); ++l) sc.push_back(h.data() + base[b] + l * (size_t)nw);
+              ent[batch[b]] += scan_and_gap_entries(sc.data(), (int)sc.size(), n, (int64_t)(e & ((1ull << 40) - 1ull)));
+            }
+          }
+        }
+        // host simulations (ST_SIM segments, and scan-AND segments to redo), on a small pool; an exception in a
+        // worker is rethrown here after the join
+        std::vector<size_t> work_items;
+        for (size_t b = 0; b < batch.size(); ++b)
+          if (stat_segs[batch[b]].kind == ST_SIM || redo[b]) work_items.push_back(b);
+        std::atomic<size_t> next_item{0};
+        std::vector<std::exception_ptr> errs;
+        std::mutex err_mu;
+        auto work = [&]() {
+          try {
+            for (size_t t; (t = next_item.fetch_add(1)) < work_items.size();) {
+              const size_t b = work_items[t];
+              const StatSeg& ss = stat_segs[batch[b]];
+              const int64_t n = dsegs[ss.dseg].num_docs, nw = (n + 63) / 64;
+              std::vector<SimLeaf> lv(ss.leaves.size());
+              for (size_t l = 0; l < lv.size(); ++l) lv[l] = {ss.leaf_kinds[l], h.data() + base[b] + l * (size_t)nw};
+              ent[batch[b]] = simulate_filter_entries(ss.root, lv, n);
+            }
+          } catch (...) {
+            std::lock_guard<std::mutex> lk(err_mu);
+            errs.push_back(std::current_exception());
+          }
+        };
+        const size_t nthr = std::min<size_t>(work_items.size(), std::max(1u, std::min(8u, std::thread::hardware_concurrency())));
+        std::vector<std::thread> pool;
+        for (size_t k = 1; k < nthr; ++k) pool.emplace_back(work);
+        if (!work_items.empty()) work();
+        for (auto& th : pool) th.join();
+        if (!errs.empty()) std::rethrow_exception(errs.front());
+      }
       for (int64_t e : ent) stats.num_entries_scanned_in_filter += e;
     }
     stamp("launched");

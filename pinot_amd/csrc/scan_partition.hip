@@ -363,7 +363,8 @@ static void launch_part_fast_ng(const KParams& p, int rec64, int grid, size_t ld
 
 void launch_scan_partition(const KParams& p, int ng, int rec64, int grid, size_t lds, hipStream_t s) {
   if (p.part_reg) {
-    launch_part_reg(p, ng, grid, lds, s);
+    if (p.part_wave) launch_part_wave(p, ng, grid, lds, s);
+    else launch_part_reg(p, ng, grid, lds, s);
     return;
   }
   if (!p.part_fast) {

@@ -383,9 +383,97 @@ static void parse_dictionary(const ph_column_desc& d, Dictionary* out) {
 }
 
 // ------------------------------------------------------------------ pin
-ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
+uint64_t next_object_id() {
+  static std::atomic<uint64_t> next{1};
+  return next++;
+}
+
+// The kernels address a packed stream with 32-bit buffer offsets (reg_decode.h reg_load, scan_kernel.h tile loads):
+// a stream plus its pad must stay below 2 GiB, else loads past it would read zeros and answer wrongly.
+constexpr uint64_t kMaxStreamBytes = 0x7fffffffull - kFwdPadBytes - 4096;
+
+static int bits_for_card(int64_t card) {  // PinotDataBitSet.getNumBitsPerValue(cardinality - 1)
+  int bits = 1;
+  while (bits < 31 && ((int64_t)1 << bits) < card) bits++;
+  return bits;
+}
+
+// what ph_segment_pin refuses before touching the device (sizes only: no buffer is read beyond its declared size)
+void segment_check_impl(const ph_segment_desc* desc) {
   if (!desc || desc->num_docs < 0 || desc->num_columns < 0 || (desc->num_columns && !desc->columns))
     fail(PH_ERR_INVALID_ARGUMENT, "bad segment descriptor");
+  const int64_t n = desc->num_docs;
+  for (int ci = 0; ci < desc->num_columns; ++ci) {
+    const ph_column_desc& d = desc->columns[ci];
+    if (!d.name) fail(PH_ERR_INVALID_ARGUMENT, "column without a name");
+    const std::string name = d.name;
+    if (!d.forward_index) fail(PH_ERR_INVALID_ARGUMENT, "column " + name + ": missing forward index");
+    if (d.hll_log2m < 0 || d.hll_log2m > 16) fail(PH_ERR_INVALID_ARGUMENT, "column " + name + ": hll_log2m");
+    // a raw column is dictionary-encoded at pin: at most n distinct values
+    const int64_t card = d.raw_forward_index ? std::max<int64_t>(1, n) : d.cardinality;
+    if (!d.raw_forward_index && d.cardinality <= 0 && n > 0) fail(PH_ERR_INVALID_ARGUMENT, "column " + name + ": cardinality <= 0");
+    const int bits = bits_for_card(card);
+    const uint64_t packed = ((uint64_t)n * (uint64_t)bits + 7) / 8;
+    if (packed > kMaxStreamBytes)
+      fail(PH_ERR_UNSUPPORTED, "column " + name + ": packed stream of " + std::to_string(packed) +
+                                   " bytes is past the 2 GiB range of the kernels' buffer offsets");
+    if (!d.raw_forward_index && !d.is_sorted && d.forward_index_size < packed)
+      fail(PH_ERR_INVALID_ARGUMENT, "column " + name + ": forward index too small");
+  }
+}
+
+// The frame-of-reference value stream of an INT / LONG column (VK_PACKED: value - min in bits(max - min) per doc),
+// encoded from the packed dictIds on the pin stream; not built when the range needs 32 bits or more, or when the
+// stream would pass the buffer-offset limit (the kernels then gather from the dictionary)
+static void build_value_stream(Context* ctx, ph_segment* seg, Column& c, hipStream_t st) {
+  c.vpacked_ready = true;
+  if (c.data_type != PH_INT && c.data_type != PH_LONG) return;
+  if (c.cardinality <= 0 || seg->num_docs == 0) return;
+  const int64_t lo = c.dict.ints.front(), hi = c.dict.ints.back();
+  const uint64_t range = (uint64_t)hi - (uint64_t)lo;
+  int vb = 1;
+  while (vb < 64 && (range >> vb) != 0) ++vb;
+  if (vb > 31) return;
+  const int64_t n = seg->num_docs;
+  const size_t bytes = (size_t)((n * vb + 7) / 8);
+  if (bytes > kMaxStreamBytes) return;
+  const size_t alloc = ((bytes + kFwdPadBytes + 255) / 256) * 256;
+  auto buf = std::make_unique<DeviceBuffer>();
+  buf->alloc(alloc, ctx->device);
+  PH_HIP_CHECK(hipMemsetAsync(buf->ptr, 0, alloc, st));
+  launch_encode_values(c.d_fwd.as<uint32_t>(), c.bits, c.d_values.as<int64_t>(), lo, vb, n, buf->as<uint32_t>(), st);
+  c.vbase = lo;
+  c.vbits = vb;
+  seg->device_bytes += (int64_t)alloc;
+  c.d_vpacked = std::move(buf);
+}
+
+// The column's DISTINCTCOUNTHLL table for log2m: per dictId the (register << 8 | rank) pair clearspring
+// HyperLogLog.offer would update for the dictionary value (DistinctCountHLLAggregationFunction.java:438-447), on `st`
+// (the caller synchronises)
+void build_hll_table(Context* ctx, Column& c, int log2m, hipStream_t st) {
+  if (c.hll_tables.count(log2m)) return;
+  if (c.data_type == PH_FLOAT) fail(PH_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL on FLOAT columns is not on the GPU path");
+  HllTable t;
+  t.buf = std::make_unique<DeviceBuffer>();
+  t.buf->alloc(sizeof(uint32_t) * std::max(1, c.cardinality), ctx->device);
+  if (c.data_type == PH_STRING) {
+    // MurmurHash.hash(String.getBytes()) = hash(bytes, len, -1)
+    std::vector<uint32_t> h(c.cardinality);
+    for (int32_t i = 0; i < c.cardinality; ++i) {
+      const std::string& s = c.dict.strings[i];
+      h[i] = hll_entry(murmur_hash_bytes(reinterpret_cast<const uint8_t*>(s.data()), (int32_t)s.size(), -1), log2m);
+    }
+    PH_HIP_CHECK(hipMemcpy(t.buf->ptr, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice));
+  } else {
+    // INT / LONG -> hashLong((long) value); DOUBLE -> hashLong(doubleToRawLongBits)
+    launch_hll_table(c.d_values.ptr, c.data_type != PH_DOUBLE, c.cardinality, log2m, t.buf->as<uint32_t>(), st);
+  }
+  c.hll_tables[log2m] = std::move(t);
+}
+
+ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
+  segment_check_impl(desc);
   PH_HIP_CHECK(hipSetDevice(ctx->device));
   LaneGuard lg(ctx);
   const hipStream_t st = lg.lane->stream;  // a pin never runs on the caller's external stream
@@ -412,6 +500,7 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
       const uint8_t* h = static_cast<const uint8_t*>(d.range_index);
       const uint32_t version = (uint32_t)h[0] << 24 | (uint32_t)h[1] << 16 | (uint32_t)h[2] << 8 | h[3];
       col->has_range_index = version == 2;
+      col->has_inexact_range_index = version != 2;
     }
     const uint8_t* fwd = static_cast<const uint8_t*>(d.forward_index);
     if (!fwd) fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": missing forward index");
@@ -434,9 +523,7 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
       if (!d.dictionary) fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": no dictionary and not marked raw");
       parse_dictionary(d, &col->dict);
     }
-    // PinotDataBitSet.getNumBitsPerValue(cardinality - 1)
-    int bits = 1;
-    while (bits < 31 && ((int64_t)1 << bits) < card) bits++;
+    const int bits = bits_for_card(card);  // PinotDataBitSet.getNumBitsPerValue(cardinality - 1)
     if (col->is_raw) {
       packed.assign((size_t)((n * bits + 7) / 8), 0);
       fixed_bit_pack_host(ids.data(), n, bits, packed.data());
@@ -497,11 +584,15 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
                                     hipMemcpyHostToDevice, st));
       seg->device_bytes += col->d_dir.bytes;
     }
+    // derived streams, on the pin stream: no query builds them (nor waits for one another doing so)
+    build_value_stream(ctx, seg.get(), *col, st);
+    if (d.hll_log2m > 0) build_hll_table(ctx, *col, d.hll_log2m, st);
     // the caller's buffers may be released after pin returns
     PH_HIP_CHECK(hipStreamSynchronize(st));
     seg->columns[col->name] = std::move(col);
   }
-  seg->id = ctx->next_id++;
+  seg->id = next_object_id();
+  ctx->pinned_rows += seg->num_docs;
   return seg.release();
 }
 

@@ -42,8 +42,40 @@ int java_double_compare(double a, double b) {
   return x == y ? 0 : (x < y ? -1 : 1);
 }
 
+// Java String.compareTo: UTF-16 code-unit order (UTF-8 byte order differs for supplementary-plane characters
+// against U+E000..U+FFFF)
+std::u16string utf16_of(const std::string& s) {
+  std::u16string out;
+  out.reserve(s.size());
+  for (size_t i = 0; i < s.size();) {
+    const uint8_t c = (uint8_t)s[i];
+    uint32_t cp = c, n = 0;
+    if (c >= 0xf0) { cp = c & 0x07; n = 3; }
+    else if (c >= 0xe0) { cp = c & 0x0f; n = 2; }
+    else if (c >= 0xc0) { cp = c & 0x1f; n = 1; }
+    ++i;
+    for (uint32_t k = 0; k < n && i < s.size(); ++k, ++i) cp = (cp << 6) | ((uint8_t)s[i] & 0x3f);
+    if (cp >= 0x10000) {
+      cp -= 0x10000;
+      out.push_back((char16_t)(0xd800 + (cp >> 10)));
+      out.push_back((char16_t)(0xdc00 + (cp & 0x3ff)));
+    } else {
+      out.push_back((char16_t)cp);
+    }
+  }
+  return out;
+}
+
+int java_string_compare(const std::string& a, const std::string& b) {
+  const std::u16string x = utf16_of(a), y = utf16_of(b);
+  return x < y ? -1 : (x > y ? 1 : 0);
+}
+
 struct Row {
-  std::string key;          // the group-by values' bytes, column after column (entry sizes of the result)
+  // per group-by column the value's bytes: numeric types at their fixed width, STRING without its zero padding (a
+  // segment-local query pads to its own max_string_len, so widths differ between segments)
+  std::vector<std::string> kv;
+  std::string key;          // merge key: the values, each length-prefixed
   std::vector<double> d;    // per aggregation: SUM/MIN/MAX value (COUNT in c)
   std::vector<int64_t> c;   // per aggregation: COUNT
   std::vector<std::vector<uint8_t>> hll;
@@ -92,13 +124,12 @@ ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* con
     st.limit_pass = std::max(st.limit_pass, rs.limit_pass);
     if (!typed) {
       out->key_types = r->key_types;
-      out->key_entry_size = r->key_entry_size;
       out->agg_types = r->agg_types;
       out->agg_log2m = r->agg_log2m;
       out->mode = r->mode;
-      key_size = r->key_entry_size;
       typed = true;
     }
+    for (int c = 0; c < ng && c < (int)r->key_entry_size.size(); ++c) key_size[c] = std::max(key_size[c], r->key_entry_size[c]);
     const int64_t n = r->num_groups;
     std::vector<Row> rows((size_t)n);
     ph_segment* seg = segs[s];
@@ -108,7 +139,11 @@ ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* con
       for (int c = 0; c < ng; ++c) {
         const int w = r->key_entry_size[c];
         const uint8_t* kp = r->keys[c].data() + (size_t)g * w;
-        row.key.append(reinterpret_cast<const char*>(kp), (size_t)w);
+        const size_t len = r->key_types[c] == PH_STRING ? strnlen(reinterpret_cast<const char*>(kp), (size_t)w) : (size_t)w;
+        row.kv.emplace_back(reinterpret_cast<const char*>(kp), len);
+        const uint32_t l32 = (uint32_t)len;
+        row.key.append(reinterpret_cast<const char*>(&l32), 4);
+        row.key.append(row.kv.back());
         // the key's dictId in this segment's dictionary (ArrayBasedHolder raw key)
         const Column& col = *seg->columns.at(q->group_by[c]);
         const Dictionary& d = col.dict;
@@ -161,17 +196,14 @@ ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* con
             if (r->agg_types[j] == PH_AGG_COUNT) c = a.c[j] < b.c[j] ? -1 : (a.c[j] > b.c[j] ? 1 : 0);
             else c = java_double_compare(a.d[j], b.d[j]);
           } else {
-            size_t off = 0;
-            for (int x = 0; x < o.index; ++x) off += (size_t)key_size[x];
-            const int w = key_size[o.index];
-            const uint8_t* pa = reinterpret_cast<const uint8_t*>(a.key.data()) + off;
-            const uint8_t* pb = reinterpret_cast<const uint8_t*>(b.key.data()) + off;
+            const uint8_t* pa = reinterpret_cast<const uint8_t*>(a.kv[o.index].data());
+            const uint8_t* pb = reinterpret_cast<const uint8_t*>(b.kv[o.index].data());
             switch (r->key_types[o.index]) {
               case PH_INT: { int32_t x, y; memcpy(&x, pa, 4); memcpy(&y, pb, 4); c = x < y ? -1 : (x > y ? 1 : 0); break; }
               case PH_LONG: { int64_t x, y; memcpy(&x, pa, 8); memcpy(&y, pb, 8); c = x < y ? -1 : (x > y ? 1 : 0); break; }
               case PH_FLOAT: { float x, y; memcpy(&x, pa, 4); memcpy(&y, pb, 4); c = java_double_compare(x, y); break; }
               case PH_DOUBLE: { double x, y; memcpy(&x, pa, 8); memcpy(&y, pb, 8); c = java_double_compare(x, y); break; }
-              default: c = memcmp(pa, pb, (size_t)w); c = c < 0 ? -1 : (c > 0 ? 1 : 0);  // UTF-8 byte order
+              default: c = java_string_compare(a.kv[o.index], b.kv[o.index]);
             }
           }
           if (!o.asc) c = -c;
@@ -243,12 +275,14 @@ ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* con
     std::unique_ptr<ph_result> r(query_execute_impl(ctx, &one, segs, 0, nullptr));
     return r.release();
   }
-  size_t off = 0;
+  out->key_entry_size = key_size;
   for (int c = 0; c < ng; ++c) {
-    const int w = key_size[c];
-    out->keys[c].assign((size_t)w * R, 0);
-    for (int64_t g = 0; g < R; ++g) memcpy(out->keys[c].data() + (size_t)w * g, merged[(size_t)g].key.data() + off, (size_t)w);
-    off += (size_t)w;
+    const size_t w = (size_t)key_size[c];
+    out->keys[c].assign(w * R, 0);
+    for (int64_t g = 0; g < R; ++g) {
+      const std::string& v = merged[(size_t)g].kv[c];
+      memcpy(out->keys[c].data() + w * g, v.data(), std::min(w, v.size()));
+    }
   }
   for (int k = 0; k < na; ++k) {
     const int t = out->agg_types[k];

@@ -49,7 +49,7 @@ SCAN_KERNEL_NAMES = {0: "none", 1: "k_scan", 2: "k_agg_lean", 3: "k_agg_sparse",
                      5: "k_part_scan + k_part_agg", 6: "k_part_scan2 + k_part_agg",
                      7: "k_scan<MODE_PARTITION> + k_part_agg", 8: "k_part_reg + k_part_agg",
                      9: "k_count_reg", 10: "k_agg_reg",
-                     11: "k_group_reg", 12: "k_group_sparse"}
+                     11: "k_group_reg", 12: "k_group_sparse", 13: "k_part_wave + k_part_agg"}
 
 
 @dataclass
@@ -227,8 +227,9 @@ class GpuContext:
     def set_stream(self, stream_ptr: int):
         N.check(N.lib().ph_ctx_set_stream(self.handle, ctypes.c_void_p(stream_ptr)))
 
-    def pin(self, buffers: SegmentBuffers) -> PinnedSegment:
-        seg = PinnedSegment(self, buffers)
+    def pin(self, buffers: SegmentBuffers, hll_columns=(), log2m: int = 8) -> PinnedSegment:
+        """ph_segment_pin; hll_columns get their DISTINCTCOUNTHLL table (log2m) built at pin."""
+        seg = PinnedSegment(self, buffers, hll_columns, log2m)
         self._segments.add(seg)
         return seg
 

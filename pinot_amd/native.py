@@ -53,7 +53,8 @@ class ColumnDesc(ctypes.Structure):
                 ("dictionary_entry_size", ctypes.c_int32),
                 ("inverted_index", ctypes.c_void_p), ("inverted_index_size", ctypes.c_uint64),
                 ("raw_forward_index", ctypes.c_int32),
-                ("range_index", ctypes.c_void_p), ("range_index_size", ctypes.c_uint64)]
+                ("range_index", ctypes.c_void_p), ("range_index_size", ctypes.c_uint64),
+                ("hll_log2m", ctypes.c_int32)]
 
 
 class MetadataEntry(ctypes.Structure):
@@ -127,7 +128,8 @@ class ExecStats(ctypes.Structure):
 
 # every symbol declared in include/pinot_hip.h
 EXPORTED_SYMBOLS = (
-    "ph_ctx_create", "ph_ctx_destroy", "ph_ctx_set_stream", "ph_segment_pin", "ph_segment_load_dir", "ph_segment_unpin",
+    "ph_ctx_create", "ph_ctx_destroy", "ph_ctx_set_stream", "ph_segment_pin", "ph_segment_check", "ph_segment_load_dir",
+    "ph_segment_unpin",
     "ph_segment_device_bytes", "ph_segment_num_docs", "ph_table_set_dictionary", "ph_table_set_column_type", "ph_query_execute",
     "ph_result_destroy", "ph_result_stats", "ph_result_num_groups", "ph_result_key_entry_size", "ph_result_key_type",
     "ph_result_group_keys", "ph_result_aggregation", "ph_result_key_data", "ph_result_aggregation_data",
@@ -171,6 +173,7 @@ def lib():
         "ph_ctx_destroy": ([vp], ctypes.c_int),
         "ph_ctx_set_stream": ([vp, vp], ctypes.c_int),
         "ph_segment_pin": ([vp, ctypes.POINTER(SegmentDesc), ctypes.POINTER(vp)], ctypes.c_int),
+        "ph_segment_check": ([ctypes.POINTER(SegmentDesc)], ctypes.c_int),
         "ph_segment_unpin": ([vp], ctypes.c_int),
         "ph_segment_load_dir": ([vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), i32, ctypes.POINTER(vp)],
                                 ctypes.c_int),

@@ -86,13 +86,16 @@ class FilterContext:
     def pred(p: Predicate) -> "FilterContext":
         return FilterContext("PREDICATE", (), p)
 
+    # FlattenAndOrFilterOptimizer (QueryOptimizer.java:47): an AND child of an AND (an OR child of an OR) is spliced
+    # into its parent, as the reference's query optimizer does before planning
+
     @staticmethod
     def and_(*c: "FilterContext") -> "FilterContext":
-        return FilterContext("AND", tuple(c))
+        return FilterContext("AND", tuple(x for k in c for x in (k.children if k.type == "AND" else (k,))))
 
     @staticmethod
     def or_(*c: "FilterContext") -> "FilterContext":
-        return FilterContext("OR", tuple(c))
+        return FilterContext("OR", tuple(x for k in c for x in (k.children if k.type == "OR" else (k,))))
 
     @staticmethod
     def not_(c: "FilterContext") -> "FilterContext":

@@ -370,7 +370,8 @@ class PinnedSegment:
         self.name = path
         return self
 
-    def __init__(self, ctx, buffers: SegmentBuffers):
+    def __init__(self, ctx, buffers: SegmentBuffers, hll_columns=(), log2m: int = 8):
+        """hll_columns: columns whose DISTINCTCOUNTHLL table (for log2m) is built at pin (ph_column_desc.hll_log2m)."""
         self.ctx = ctx
         self.name = buffers.name
         self.num_docs = buffers.num_docs
@@ -395,6 +396,7 @@ class PinnedSegment:
             d.dictionary_size = dic.nbytes
             d.dictionary_entry_size = cb.entry_size
             d.raw_forward_index = int(cb.raw)
+            d.hll_log2m = log2m if cb.name in hll_columns else 0
             if cb.inverted_index is not None:
                 inv = np.ascontiguousarray(cb.inverted_index)
                 keep.append(inv)

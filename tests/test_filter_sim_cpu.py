@@ -1,0 +1,146 @@
+"""CPU: numEntriesScannedInFilter by iterator simulation.  The library's host simulator (filter_sim.cpp, reached
+through the test hook phx_filter_entries_sim; the product calls it for filter shapes without a device pass) is checked
+against the oracle's restatement of the reference iterators (oracle.filter_entries_of) on random filter trees and doc
+sets, and the oracle's restatement against a fully literal variant (every next() batch by batch, no drain shortcut).
+The device-side pass for ANDs of scans (k_scan_and_entries) is checked on the GPU (test_gpu_parity.py)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from pinot_amd import native as N
+
+KINDS = {"scan": 0, "sorted": 1, "inverted": 2, "range": 2}
+PRIO = {"sorted": 0, "range": 200, "scan": 500, "inverted": 10000}
+
+
+def _random_tree(rng, depth, leaves):
+    if depth == 0 or rng.random() < 0.35:
+        kind = rng.choice(["scan", "scan", "scan", "sorted", "inverted", "range"])
+        node = O._Leaf("leaf", len(leaves), None, kind == "scan")
+        node.ikind = kind
+        leaves.append(node)
+        return node
+    op = rng.choice(["and", "and", "or", "not"])
+    node = O._Leaf(op)
+    if op == "not":
+        node.children = [_random_tree(rng, depth - 1, leaves)]
+    else:
+        node.children = [_random_tree(rng, depth - 1, leaves) for _ in range(int(rng.integers(2, 4)))]
+    return node
+
+
+def _docs(rng, n, kind):
+    if kind == "sorted":  # a doc range
+        a = int(rng.integers(0, n))
+        b = int(rng.integers(a, n + 1))
+        d = np.zeros(n, bool)
+        d[a:b] = True
+        return d
+    return rng.random(n) < rng.choice([0.02, 0.2, 0.5, 0.9])
+
+
+def _flatten(root):
+    """The test hook's flat tree: rows (op, priority, leaf, first child, child count); a node's children are
+    consecutive rows (a child's own subtree lives further on)."""
+    out = []
+
+    def rec(x, pos):
+        if x.kind == "leaf":
+            out[pos] = [0, PRIO[x.ikind], x.col_index, 0, 0]
+            return
+        op = {"and": 1, "or": 2, "not": 3}[x.kind]
+        first = len(out)
+        out.extend([None] * len(x.children))
+        out[pos] = [op, 300 if op == 1 else 400, -1, first, len(x.children)]
+        for j, c in enumerate(x.children):
+            rec(c, first + j)
+
+    out.append(None)
+    rec(root, 0)
+    return np.array(out, dtype=np.int32).ravel()
+
+
+def _native_sim(root, leaves, docs, n):
+    L = N.lib()
+    f = L.phx_filter_entries_sim
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64]
+    flat = _flatten(root)
+    kinds = np.array([KINDS[l.ikind] for l in leaves], dtype=np.int32)
+    nw = (n + 63) // 64
+    bits = []
+    for d in docs:
+        padded = np.zeros(nw * 64, bool)
+        padded[:n] = d
+        bits.append(np.packbits(padded.reshape(-1, 8)[:, ::-1], axis=1).ravel().view(np.uint64).copy())
+    ptrs = (ctypes.c_void_p * len(bits))(*[b.ctypes.data for b in bits])
+    return f(flat.ctypes.data, len(flat) // 5, kinds.ctypes.data, ptrs, len(bits), n)
+
+
+class _LiteralScan(O._ScanIt):
+    """SVScanDocIdIterator.next() batch by batch (no jump over empty batches), drained by next() calls."""
+
+    def next(self):
+        if self.cursor >= self.first_mismatch:
+            while True:
+                limit = min(self.n - self.next_doc, 256)
+                if limit <= 0:
+                    self.batch, self.cursor, self.first_mismatch = self.pos[:0], 0, 0
+                    return O.EOF_DOC
+                lo, hi = self.next_doc, self.next_doc + limit
+                b = self.pos[np.searchsorted(self.pos, lo):np.searchsorted(self.pos, hi)]
+                self.next_doc += limit
+                self.entries += limit
+                if len(b):
+                    break
+            self.batch, self.cursor, self.first_mismatch = b, 0, len(b)
+        self.cursor += 1
+        return int(self.batch[self.cursor - 1])
+
+    def drain(self):
+        while self.next() != O.EOF_DOC:
+            pass
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_native_filter_sim_matches_oracle(seed):
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.choice([1, 63, 64, 257, 3000, 20_011]))
+    leaves = []
+    root = _random_tree(rng, 3, leaves)
+    docs = [_docs(rng, n, l.ikind) for l in leaves]
+    exp = O.filter_entries_of(root, n, lambda node: docs[node.col_index])
+    got = _native_sim(root, leaves, docs, n)
+    assert got == exp, (seed, n)
+
+
+@pytest.mark.parametrize("seed", range(15))
+def test_oracle_sim_matches_literal_batches(seed, monkeypatch):
+    rng = np.random.default_rng(2000 + seed)
+    n = int(rng.choice([300, 5000]))
+    leaves = []
+    root = _random_tree(rng, 3, leaves)
+    docs = [_docs(rng, n, l.ikind) for l in leaves]
+    exp = O.filter_entries_of(root, n, lambda node: docs[node.col_index])
+    monkeypatch.setattr(O, "_ScanIt", _LiteralScan)
+    assert O.filter_entries_of(root, n, lambda node: docs[node.col_index]) == exp
+
+
+def test_scan_and_closed_cases():
+    # AND of scans only (AndDocIdIterator): hand-checked small cases
+    n = 10
+    a = np.zeros(n, bool)
+    b = np.zeros(n, bool)
+    a[[2, 5, 7]] = True
+    b[[5, 7, 9]] = True
+    la, lb = O._Leaf("leaf", 0, None, True), O._Leaf("leaf", 1, None, True)
+    la.ikind = lb.ikind = "scan"
+    root = O._Leaf("and")
+    root.children = [la, lb]
+    # next() #1 from 0: a.adv(0) -> 2 [3 docs]; b.adv(2) -> 5 [4]; a.adv(5) -> 5 [1]; output 5
+    # next() #2 from 6: a.adv(6) -> 7 [2]; b.adv(7) -> 7 [1]; output 7
+    # next() #3 from 8: a.adv(8) -> EOF [2 docs: 8, 9]
+    assert O.filter_entries_of(root, n, lambda x: [a, b][x.col_index]) == 3 + 4 + 1 + 2 + 1 + 2
+    assert _native_sim(root, [la, lb], [a, b], n) == 13

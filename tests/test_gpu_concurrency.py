@@ -116,3 +116,39 @@ def test_interrupt_during_long_scan(setup, monkeypatch):
         ctx.execute(q, big, interrupt=flag)
     timer.join()
     assert time.perf_counter() - t0 < 30
+
+
+def test_first_queries_after_pin_run_concurrently(setup):
+    # the derived streams are built at pin (ph_segment_pin: the INT value streams, and the HLL table requested by
+    # hll_columns), so the first queries on fresh segments share nothing to build: four threads start their first
+    # query together on newly pinned segments, each result equals the oracle's, and the segments' device bytes
+    # already include the value streams and the HLL table before any query ran
+    ctx, _, expected = setup
+    tables = _tables()
+    fresh = [ctx.pin(create_segment(f"f{i}", t, inverted=("a",)), hll_columns=("m",)) for i, t in enumerate(tables)]
+    plain = [ctx.pin(create_segment(f"p{i}", t, inverted=("a",))) for i, t in enumerate(tables)]
+    for f, p in zip(fresh, plain):
+        assert f.device_bytes > p.device_bytes  # + the HLL table (4 B per dictId), built at pin
+    before = [f.device_bytes for f in fresh]
+    errors = []
+    start = threading.Barrier(4)
+
+    def worker(k):
+        try:
+            start.wait()
+            sql = QUERIES[[0, 3, 4, 3][k]]
+            q = parse_sql(sql)
+            r = ctx.execute(q, fresh)
+            if reduce_groups(q, r.keys, r.aggs).rows != expected[sql]:
+                errors.append((k, sql))
+        except Exception as e:  # noqa: BLE001 -- surfaced below
+            errors.append((k, repr(e)))
+
+    threads = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in threads), "a query thread did not finish"
+    assert errors == []
+    assert [f.device_bytes for f in fresh] == before  # no query derived anything more for these columns' aggregates

@@ -62,6 +62,8 @@ def _check(ctx, gpu_segs, ora_segs, sql, hll_raw=True):
     assert r.stats.num_docs_scanned == e.stats.num_docs_scanned
     assert r.stats.num_total_docs == e.stats.num_total_docs
     assert r.stats.num_entries_scanned_post_filter == e.stats.num_entries_scanned_post_filter
+    # numEntriesScannedInFilter: the reference's iterator counts, for every filter shape (oracle.filter_entries)
+    assert r.stats.num_entries_scanned_in_filter == e.stats.num_entries_scanned_in_filter, sql
     return r, got
 
 

@@ -133,3 +133,20 @@ def test_distributed_query_world1(ctx):
     finally:
         dist.destroy_process_group()
         ctx.set_stream(0)
+
+
+def test_dense_partials_reject_segment_trim(ctx):
+    # GroupByOperator's segment trim (ORDER BY + minSegmentGroupTrimSize > 0) cannot run on whole dense partials: the
+    # dense entry points refuse it (PH_ERR_UNSUPPORTED) instead of returning untrimmed groups; DistributedQuery too
+    from pinot_amd import native as N
+    from pinot_amd.distributed import DistributedQuery
+    segs = _segs(ctx, 41, n=50_000, nseg=2)
+    q = parse_sql("SET minSegmentGroupTrimSize=10; SELECT a, b, SUM(m) FROM t GROUP BY a, b ORDER BY SUM(m) DESC "
+                  "LIMIT 5")
+    with pytest.raises(N.UnsupportedError):
+        ctx.dense_layout(q, segs)
+    with pytest.raises(N.UnsupportedError):
+        DistributedQuery(ctx).execute(q, segs)
+    # without the ORDER BY the option does not apply (GroupByOperator trims only ordered group-bys)
+    ctx.dense_layout(parse_sql("SET minSegmentGroupTrimSize=10; SELECT a, b, SUM(m) FROM t GROUP BY a, b LIMIT 5"),
+                     segs)

@@ -77,3 +77,20 @@ def test_range_index_from_directories(ctx, tmp_path, layout):
         if " s " in sql:
             continue  # the directory oracle (segment_dirs.read_dir) models no inverted index
         _check(ctx, [seg], [ora], sql, entries)
+
+
+def test_inexact_range_index_takes_the_cpu_plan(ctx):
+    # a legacy version-1 range index (ranges + a partial scan of the boundary ranges) is still a
+    # RangeIndexBasedFilterOperator leaf in the reference (RangeIndexBasedFilterOperator.java:59-60), whose entries
+    # the GPU statistics do not model: its RANGE / EQ leaves are PH_ERR_UNSUPPORTED (the plan maker's CPU fallback);
+    # other predicates on the column still run on the GPU
+    from pinot_amd import native as N
+    buf = create_segment("riv1", _cols(20_000, 9), range_index=("r",))
+    hdr = buf.columns["r"].range_index.copy()
+    hdr[:4] = np.frombuffer(np.array([1], ">i4").tobytes(), np.uint8)  # version 1
+    buf.columns["r"].range_index = hdr
+    seg = ctx.pin(buf)
+    with pytest.raises(N.UnsupportedError):
+        ctx.execute(parse_sql("SELECT COUNT(*) FROM t WHERE r BETWEEN 100 AND 700"), [seg])
+    r = ctx.execute(parse_sql("SELECT COUNT(*) FROM t WHERE r IN (3, 5, 9)"), [seg])
+    assert r.stats.num_entries_scanned_in_filter == 20_000

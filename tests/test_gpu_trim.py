@@ -78,3 +78,25 @@ def test_segment_trim_large_key_space(ctx):
     osegs = [O.build_segment(f"tl{i}", t) for i, t in enumerate(tables)]
     _check(ctx, segs, osegs, "SET minSegmentGroupTrimSize=500; SELECT a, b, SUM(m), COUNT(*) FROM t GROUP BY a, b "
                              "ORDER BY SUM(m) DESC LIMIT 10")
+
+
+def test_segment_trim_string_keys_of_differing_widths(ctx):
+    # no table dictionary: each segment's own query pads its STRING keys to that segment's max_string_len, so the
+    # merge must key on the unpadded values (the same string from two segments is ONE group) and the output must
+    # take the widest width; ORDER BY the string column itself and a two-column key exercise the comparator offsets
+    rng = np.random.default_rng(seed_of("trim-strings"))
+    words = [["s%d" % i for i in range(40)],                                  # width 3
+             ["s%d" % i for i in range(20, 60)] + ["long-%02d-" % i + "x" * i for i in range(30)],  # width up to 38
+             ["s%d" % i for i in range(0, 60, 3)]]
+    tables = []
+    for w, n in zip(words, (40_000, 35_003, 20_011)):
+        s = np.array(w, dtype=object)[rng.integers(0, len(w), n)]
+        tables.append({"s": (s, "STRING"), "b": (rng.integers(0, 7, n).astype(np.int32), "INT"),
+                       "m": (rng.integers(0, 1 << 20, n).astype(np.int32), "INT")})
+    segs = [ctx.pin(create_segment(f"ts{i}", t)) for i, t in enumerate(tables)]
+    osegs = [O.build_segment(f"ts{i}", t) for i, t in enumerate(tables)]
+    for sql in ("SET minSegmentGroupTrimSize=12; SELECT s, COUNT(*), SUM(m) FROM t GROUP BY s ORDER BY s DESC LIMIT 3",
+                "SET minSegmentGroupTrimSize=15; SELECT b, s, MAX(m) FROM t GROUP BY b, s ORDER BY s, b DESC LIMIT 4",
+                "SET minSegmentGroupTrimSize=20; SELECT s, b, SUM(m) FROM t GROUP BY s, b ORDER BY SUM(m) DESC LIMIT 5"):
+        r, _ = _check(ctx, segs, osegs, sql)
+        assert len(r.keys) == len(set(r.keys)), sql  # no group twice

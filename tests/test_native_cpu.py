@@ -161,3 +161,46 @@ def test_segment_group_trim_gate():
     check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=-1; " + base + " ORDER BY SUM(m) DESC LIMIT 5"))
     check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=100; " + base + " LIMIT 5"))
     check_plan_supported(parse_sql(base + " ORDER BY a LIMIT 5"))
+
+
+def _desc(num_docs, card, fwd_size, raw=0, name=b"v"):
+    import ctypes
+    fwd = np.zeros(16, np.uint8)
+    dic = np.arange(max(1, min(card, 1 << 16)), dtype=">i4")
+    cols = (N.ColumnDesc * 1)()
+    d = cols[0]
+    d.name = name
+    d.data_type = 0
+    d.cardinality = card
+    d.bits_per_element = num_bits_per_value(card - 1)
+    d.forward_index = fwd.ctypes.data
+    d.forward_index_size = fwd_size
+    d.dictionary = dic.ctypes.data
+    d.dictionary_size = dic.nbytes
+    d.dictionary_entry_size = 4
+    d.raw_forward_index = raw
+    desc = N.SegmentDesc(b"big", num_docs, 1, cols)
+    return desc, (fwd, dic, cols)
+
+
+def test_segment_check_refuses_streams_past_2gib():
+    # the kernels address a packed stream with 32-bit buffer offsets: a forward index of >= 2 GiB (here 2^31 - 1
+    # docs at b = 20: 5.4 GB, declared with a fake length -- the check reads no buffer) is PH_ERR_UNSUPPORTED, so
+    # the plan maker keeps the segment on the CPU plan instead of answering from zeros past 2 GiB
+    import ctypes
+    n = (1 << 31) - 1
+    desc, keep = _desc(n, 1 << 20, (n * 20 + 7) // 8)
+    assert N.lib().ph_segment_check(ctypes.byref(desc)) == N.PH_ERR_UNSUPPORTED
+    assert b"2 GiB" in N.lib().ph_last_error()
+    # ... also a raw column (dictionary-encoded at pin: up to n distinct values -> 31 bits per doc)
+    desc, keep = _desc(n, 0, 1 << 40, raw=1)
+    assert N.lib().ph_segment_check(ctypes.byref(desc)) == N.PH_ERR_UNSUPPORTED
+    # just below the limit: 858 993 000 docs at 20 bits = 2 147 482 500 bytes - accepted up to the pad
+    ok_docs = ((0x7fffffff - 1024 - 4096) * 8) // 20
+    desc, keep = _desc(ok_docs, 1 << 20, (ok_docs * 20 + 7) // 8)
+    assert N.lib().ph_segment_check(ctypes.byref(desc)) == N.PH_OK
+    desc, keep = _desc(ok_docs + 64, 1 << 20, ((ok_docs + 64) * 20 + 7) // 8)
+    assert N.lib().ph_segment_check(ctypes.byref(desc)) == N.PH_ERR_UNSUPPORTED
+    # malformed: a forward index shorter than its packed size
+    desc, keep = _desc(1000, 100, 10)
+    assert N.lib().ph_segment_check(ctypes.byref(desc)) == N.PH_ERR_INVALID_ARGUMENT

@@ -194,6 +194,40 @@ def test_segment_trim_heap_keeps_the_top_groups():
     assert sorted(r.keys) == sorted(k for k, _ in top)
 
 
+def test_table_resizer_in_segment_trim_kat():
+    # TableResizerTest.testInSegmentTrim (TableResizerTest.java:336-377): five groups (d1, d2, d3 | SUM(m1), MAX(m2),
+    # DISTINCTCOUNT(m3)) in group-id order, trimmed to 3; the returned list is the heap array (index 0 first)
+    recs = [("a", 10, 1.0, 10.0, 100.0, 1), ("b", 10, 2.0, 20.0, 200.0, 2), ("c", 200, 3.0, 30.0, 300.0, 2),
+            ("c", 50, 4.0, 30.0, 200.0, 3), ("c", 300, 5.0, 20.0, 100.0, 4)]
+
+    def by(cols):  # the intermediate-record comparator over (column index, ascending) pairs
+        def inter(a, b):
+            for ci, asc in cols:
+                c = O._java_compare(a[ci], b[ci])
+                if c:
+                    return c if asc else -c
+            return 0
+        return inter
+
+    def kept(cols):
+        return [recs.index(r) for r in O.table_resizer_heap(recs, by(cols), 3)]
+
+    h = kept([(2, False)])  # ORDER BY d3 DESC -> records 2, {3, 4}
+    assert h[0] == 2 and sorted(h[1:]) == [3, 4]
+    h = kept([(3, False), (4, False), (5, False)])  # SUM(m1) DESC, MAX(m2) DESC, DISTINCTCOUNT(m3) DESC
+    assert h[0] == 1 and sorted(h[1:]) == [2, 3]
+    h = kept([(5, False)] + [(0, True)])  # DISTINCTCOUNT(m3) DESC, then a tie-free key (the KAT's AVG(m4) ASC tie-break)
+    assert h[0] == 1 and sorted(h[1:]) == [3, 4]
+
+
+def test_java_string_order_is_utf16():
+    # String.compareTo compares UTF-16 code units: a supplementary character (surrogates D800-DBFF) sorts BEFORE
+    # U+E000..U+FFFF, where code-point / UTF-8 byte order puts it after
+    assert O._java_compare("\U0001F600", "") == -1
+    assert O._java_compare("", "\U0001F600") == 1
+    assert O._java_compare("ab", "abc") == -1 and O._java_compare("b", "abc") == 1
+
+
 def _and_or_iterator_entries(c):
     """The KAT filter's reference iterator tree on one segment, simulated: AndDocIdSet (AndDocIdSet.java:128-185)
     merges the sorted daysSinceEpoch range, applies the column1 and column3 scans to it (applyAnd) and ANDs the result
