@@ -192,7 +192,7 @@ typedef struct ph_order_by {
 
 typedef struct {
   int64_t num_docs_scanned;                /* matched docs */
-  int64_t num_entries_scanned_in_filter;   /* full-column entries per scan leaf */
+  int64_t num_entries_scanned_in_filter;   /* the docs the reference's scan iterators examine */
   int64_t num_entries_scanned_post_filter; /* numDocsScanned x projected columns */
   int64_t num_total_docs;
   int64_t num_segments_processed;
@@ -208,7 +208,9 @@ typedef struct {
                                               untruncated scan's table held < limit keys (no pass needed), 2 the
                                               first-seen pass and the truncating scan ran */
   int32_t scan_kernel;                     /* the scan's kernel (PH_KERNEL_*): which hand-written form ran */
-  int32_t reserved;
+  int32_t num_devices;                     /* devices whose segments the query scanned (multi-device contexts) */
+  double merge_ms;                         /* multi-device: combining the devices' partial tables (RCCL / local) */
+  double finalize_ms;                      /* multi-device: turning the merged key shards into the result */
 } ph_exec_stats;
 
 /* ph_exec_stats.scan_kernel */
@@ -231,6 +233,15 @@ enum {
 
 /* ------------------------------------------------------------------ context */
 int ph_ctx_create(int32_t device_ordinal, ph_ctx** out);
+/* One context over a set of GPUs of one node -- a Pinot server's JVM combines every segment of a query in-process
+ * (GroupByCombineOperator.java:125-197).  ph_segment_pin places each segment on the device with the fewest pinned
+ * docs; ph_query_execute scans every device's segments there (one host thread each) into dense partial tables over
+ * one set of table-level dictionaries and merges them in the library: RCCL reduce-scatter over xGMI when the devices
+ * are distinct (each device then finalises its key shard), a device copy + reduce kernel when `device_ordinals`
+ * repeat a device (logical shards); shapes the dense tables do not serve merge per-device results by group value.
+ * The result equals ph_query_execute's over one device (DOUBLE SUM within 1e-9 relative: summation order). */
+int ph_ctx_create_multi(const int32_t* device_ordinals, int32_t num_devices, ph_ctx** out);
+int32_t ph_ctx_num_devices(const ph_ctx* ctx);
 int ph_ctx_destroy(ph_ctx* ctx);
 /* Launch on an external HIP stream (e.g. torch's current stream); NULL restores the context's own. */
 int ph_ctx_set_stream(ph_ctx* ctx, void* hip_stream);
@@ -258,6 +269,7 @@ int ph_segment_unpin(ph_segment* seg);
  * (re-encoded value streams, HLL hash tables, dictId remaps to table-level dictionaries). */
 int64_t ph_segment_device_bytes(const ph_segment* seg);
 int32_t ph_segment_num_docs(const ph_segment* seg);
+int32_t ph_segment_device(const ph_segment* seg);  /* index into the context's device set */
 
 /* Table-level sorted value union for a column (group keys share ids across segments and GPUs).
  * Optional: without it the union of the queried segments' dictionaries is used. */

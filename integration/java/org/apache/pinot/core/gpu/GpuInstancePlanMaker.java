@@ -22,17 +22,45 @@ import org.apache.pinot.spi.env.PinotConfiguration;
  * else, and any PH_ERR_UNSUPPORTED at execution, takes the stock plan of InstancePlanMakerImplV2.
  */
 public class GpuInstancePlanMaker extends InstancePlanMakerImplV2 {
+  // next to the executor's own keys (CommonConstants.Server, pinot.server.query.executor.*)
+  public static final String GPU_ENABLE_KEY = "pinot.server.query.executor.gpu.enable";
+  /** Comma-separated HIP device ordinals the server's context spans (one ph_ctx over all of them). */
+  public static final String GPU_DEVICES_KEY = "pinot.server.query.executor.gpu.devices";
+  /** Single-device form (kept for compatibility): used when gpu.devices is absent. */
   public static final String GPU_DEVICE_KEY = "pinot.server.query.executor.gpu.device";
+  /** HBM the pinned segments may hold per device, in bytes (default: 240 GB of a 288 GB MI355X). */
+  public static final String GPU_HBM_BUDGET_KEY = "pinot.server.query.executor.gpu.hbm.budget";
+  public static final long DEFAULT_HBM_BUDGET = 240L << 30;
   private long _ctx;
   private GpuSegmentRegistry _segments;
+  private boolean _enabled;
 
   @Override
   public void init(PinotConfiguration queryExecutorConfig) {
     super.init(queryExecutorConfig);
-    _ctx = PinotHipJni.ctxCreate(queryExecutorConfig.getProperty(GPU_DEVICE_KEY, 0));
-    _segments = new GpuSegmentRegistry(_ctx);
+    _enabled = queryExecutorConfig.getProperty(GPU_ENABLE_KEY, true);
+    if (!_enabled) {
+      return;  // the stock plan maker, unchanged
+    }
+    String devices = queryExecutorConfig.getProperty(GPU_DEVICES_KEY, "");
+    int[] ords;
+    if (devices.isEmpty()) {
+      ords = new int[]{queryExecutorConfig.getProperty(GPU_DEVICE_KEY, 0)};
+    } else {
+      String[] parts = devices.split(",");
+      ords = new int[parts.length];
+      for (int i = 0; i < parts.length; i++) {
+        ords[i] = Integer.parseInt(parts[i].trim());
+      }
+    }
+    // one context over the device set: segments are placed by pinned rows and a query's per-device partials merge
+    // inside the library (RCCL reduce-scatter over xGMI), as GroupByCombineOperator merges them in this JVM
+    _ctx = ords.length == 1 ? PinotHipJni.ctxCreate(ords[0]) : PinotHipJni.ctxCreateMulti(ords);
+    long budget = queryExecutorConfig.getProperty(GPU_HBM_BUDGET_KEY, DEFAULT_HBM_BUDGET);
+    _segments = new GpuSegmentRegistry(_ctx, budget * ords.length);
   }
 
+  /** null when gpu.enable is false (the server's segment hooks then do nothing). */
   public GpuSegmentRegistry segments() {
     return _segments;
   }
@@ -47,7 +75,7 @@ public class GpuInstancePlanMaker extends InstancePlanMakerImplV2 {
     for (IndexSegment segment : indexSegments) {
       segmentPlans.add(makeSegmentPlanNode(segment, queryContext));
     }
-    GpuQuery q = GpuQuery.compile(queryContext);
+    GpuQuery q = _enabled ? GpuQuery.compile(queryContext) : null;
     long[] handles = q == null ? null : _segments.handles(indexSegments);
     if (handles == null) {
       return super.makeInstancePlan(indexSegments, queryContext, executorService, serverMetrics);

@@ -14,10 +14,14 @@ import org.apache.pinot.segment.spi.IndexSegment;
  */
 public final class GpuSegmentRegistry {
   private final long _ctx;
+  private final long _hbmBudget;  // bytes the pinned segments may hold over the context's devices
   private final ConcurrentHashMap<String, Long> _pinned = new ConcurrentHashMap<>();
+  private final ConcurrentHashMap<String, Long> _bytes = new ConcurrentHashMap<>();
+  private final java.util.concurrent.atomic.AtomicLong _held = new java.util.concurrent.atomic.AtomicLong();
 
-  public GpuSegmentRegistry(long ctx) {
+  public GpuSegmentRegistry(long ctx, long hbmBudget) {
     _ctx = ctx;
+    _hbmBudget = hbmBudget;
   }
 
   /** Hook for ImmutableSegmentLoader.load (after the CPU load succeeded). */
@@ -28,12 +32,25 @@ public final class GpuSegmentRegistry {
     }
     try {
       long handle = PinotHipJni.segmentLoadDir(_ctx, dir.getAbsolutePath(), null);
+      // admission: the segment stays pinned only while every pinned segment fits the HBM budget (its measured
+      // footprint, ph_segment_device_bytes: columns plus the streams derived at pin); past it, the CPU path
+      long bytes = PinotHipJni.segmentDeviceBytes(handle);
+      if (_held.addAndGet(bytes) > _hbmBudget) {
+        _held.addAndGet(-bytes);
+        PinotHipJni.segmentUnpin(handle);
+        return;
+      }
+      Long oldBytes = _bytes.put(segment.getSegmentName(), bytes);
       Long old = _pinned.put(segment.getSegmentName(), handle);
       if (old != null) {
+        if (oldBytes != null) {
+          _held.addAndGet(-oldBytes);
+        }
         PinotHipJni.segmentUnpin(old);  // segment refresh: the new copy replaces the old one
       }
     } catch (RuntimeException e) {
-      // unsupported layout (raw / multi-value columns only, legacy padding, out of HBM): CPU path for this segment
+      // unsupported layout (raw / multi-value columns only, legacy padding, a packed stream past 2 GiB, out of
+      // HBM): CPU path for this segment
     }
   }
 
@@ -41,6 +58,10 @@ public final class GpuSegmentRegistry {
   public void onSegmentDestroyed(String segmentName) {
     Long handle = _pinned.remove(segmentName);
     if (handle != null) {
+      Long bytes = _bytes.remove(segmentName);
+      if (bytes != null) {
+        _held.addAndGet(-bytes);
+      }
       PinotHipJni.segmentUnpin(handle);
     }
   }

@@ -23,6 +23,7 @@ public final class PinotHipJni {
   public static final int EXPR_NONE = 0, EXPR_MULT = 1, EXPR_SUB = 2, EXPR_ADD = 3;
 
   static native long ctxCreate(int device);                                              // ph_ctx_create
+  static native long ctxCreateMulti(int[] devices);                                      // ph_ctx_create_multi
   static native void ctxDestroy(long ctx);                                               // ph_ctx_destroy
 
   static native long segmentLoadDir(long ctx, String segmentDir, String[] columns);      // ph_segment_load_dir

@@ -36,6 +36,18 @@ JNIEXPORT jlong JNICALL FN(ctxCreate)(JNIEnv* env, jclass c, jint device) {
   return (jlong)(intptr_t)ctx;
 }
 
+JNIEXPORT jlong JNICALL FN(ctxCreateMulti)(JNIEnv* env, jclass c, jintArray devices) {
+  ph_ctx* ctx = NULL;
+  const jsize n = devices ? (*env)->GetArrayLength(env, devices) : 0;
+  jint* d = n ? (*env)->GetIntArrayElements(env, devices, NULL) : NULL;
+  if (n && !d) return 0; /* OutOfMemoryError pending */
+  int32_t ords[64];
+  for (jsize i = 0; i < n && i < 64; ++i) ords[i] = (int32_t)d[i];
+  if (d) (*env)->ReleaseIntArrayElements(env, devices, d, JNI_ABORT);
+  throw_ph(env, ph_ctx_create_multi(ords, (int32_t)(n < 64 ? n : 64), &ctx));
+  return (jlong)(intptr_t)ctx;
+}
+
 JNIEXPORT void JNICALL FN(ctxDestroy)(JNIEnv* env, jclass c, jlong ctx) { throw_ph(env, ph_ctx_destroy(PTR(ctx))); }
 
 /* Strings of a Java String[] as UTF-8 for the duration of one call.  The element references are local refs held in

@@ -843,9 +843,10 @@ def _hash_arrays(col: OracleColumn):
     raise NotImplementedError("DISTINCTCOUNTHLL on FLOAT is not pinned")
 
 
-def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> OracleResult:
+def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1, filter_stats: bool = True) -> OracleResult:
     """Run a QueryContext over oracle segments; returns groups (value tuples) and intermediate
-    aggregation results, plus execution statistics."""
+    aggregation results, plus execution statistics.  filter_stats=False skips the numEntriesScannedInFilter
+    iterator simulation (a Python pass: the timed CPU baseline measures the C loop nest only)."""
     keep = []  # keep numpy buffers alive
     used = _used_columns(q)
     col_index = {c: i for i, c in enumerate(used)}
@@ -901,7 +902,8 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1) -> Oracl
             root = _filter_plan(q.filter, s, col_index, used)
             _emit(root, prog, keep)
             # the statistic from the iterator simulation (the C program's own count is not used)
-            extra = filter_entries(_merge_same_column(_plan_filter(q.filter, s, col_index)), s, used)
+            if filter_stats:
+                extra = filter_entries(_merge_same_column(_plan_filter(q.filter, s, col_index)), s, used)
         filter_programs.append(prog)
         extra_entries.append(extra)
 

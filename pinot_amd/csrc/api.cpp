@@ -14,13 +14,14 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc);
 ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const* segs, int32_t nseg,
                               const DenseArgs* dense);
 ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* const* segs, int32_t nseg);  // trim.cpp
+// multi.cpp
+void context_init(Context& c, int ordinal);
+void multi_init(ph_ctx* x, const int32_t* ordinals, int32_t n);
+Context* place_segment(ph_ctx* x, int64_t rows);
+ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, int32_t nseg);
 }  // namespace ph
 
 using namespace ph;
-
-struct ph_ctx {
-  Context c;
-};
 
 template <class F>
 static int guarded(F&& f) {
@@ -43,27 +44,36 @@ static int guarded(F&& f) {
   }
 }
 
+// a multi-device context pins on the device with the fewest docs (its rows reserved during the pin, which then
+// counts them itself)
+template <class F>
+static ph_segment* pin_placed(ph_ctx* ctx, int64_t rows, F&& pin) {
+  Context* c = place_segment(ctx, rows);
+  const int64_t reserved = ctx->devs.size() > 1 ? rows : 0;
+  ph_segment* s = nullptr;
+  try {
+    s = pin(c);
+  } catch (...) {
+    c->pinned_rows -= reserved;
+    throw;
+  }
+  c->pinned_rows -= reserved;
+  return s;
+}
+
 extern "C" {
 
 const char* ph_last_error(void) { return g_last_error.c_str(); }
 const char* ph_version(void) { return "pinot_hip 0.1.0 (gfx950)"; }
 
-int ph_ctx_create(int32_t device_ordinal, ph_ctx** out) {
+int ph_ctx_create(int32_t device_ordinal, ph_ctx** out) { return ph_ctx_create_multi(&device_ordinal, 1, out); }
+
+int ph_ctx_create_multi(const int32_t* device_ordinals, int32_t num_devices, ph_ctx** out) {
   return guarded([&] {
     if (!out) fail(PH_ERR_INVALID_ARGUMENT, "out is null");
-    int n = 0;
-    PH_HIP_CHECK(hipGetDeviceCount(&n));
-    if (device_ordinal < 0 || device_ordinal >= n)
-      fail(PH_ERR_INVALID_ARGUMENT, "device ordinal " + std::to_string(device_ordinal) + " out of range");
     auto* ctx = new ph_ctx();
     try {
-      Context& c = ctx->c;
-      c.device = device_ordinal;
-      PH_HIP_CHECK(hipSetDevice(device_ordinal));
-      c.lane_release(c.lane_acquire());  // one execution lane up front (fails here, not in a query, on a bad device)
-      hipDeviceProp_t prop;
-      PH_HIP_CHECK(hipGetDeviceProperties(&prop, device_ordinal));
-      c.num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+      multi_init(ctx, device_ordinals, num_devices);
     } catch (...) {
       delete ctx;
       throw;
@@ -71,6 +81,8 @@ int ph_ctx_create(int32_t device_ordinal, ph_ctx** out) {
     *out = ctx;
   });
 }
+
+int32_t ph_ctx_num_devices(const ph_ctx* ctx) { return ctx ? (int32_t)ctx->devs.size() : 0; }
 
 int ph_ctx_destroy(ph_ctx* ctx) {
   return guarded([&] {
@@ -83,6 +95,7 @@ int ph_ctx_destroy(ph_ctx* ctx) {
 int ph_ctx_set_stream(ph_ctx* ctx, void* hip_stream) {
   return guarded([&] {
     if (!ctx) fail(PH_ERR_INVALID_ARGUMENT, "ctx is null");
+    if (ctx->devs.size() > 1) fail(PH_ERR_INVALID_ARGUMENT, "a multi-device context runs on its own streams");
     ctx->c.ext_stream.store(static_cast<hipStream_t>(hip_stream));
   });
 }
@@ -90,16 +103,19 @@ int ph_ctx_set_stream(ph_ctx* ctx, void* hip_stream) {
 int ph_segment_pin(ph_ctx* ctx, const ph_segment_desc* desc, ph_segment** out) {
   return guarded([&] {
     if (!ctx || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
-    *out = segment_pin_impl(&ctx->c, desc);
+    *out = nullptr;
+    *out = pin_placed(ctx, desc ? desc->num_docs : 0, [&](Context* c) { return segment_pin_impl(c, desc); });
   });
 }
+
+int32_t ph_segment_device(const ph_segment* seg) { return seg && seg->ctx ? seg->ctx->device_index : -1; }
 
 int ph_segment_load_dir(ph_ctx* ctx, const char* segment_dir, const char* const* columns, int32_t num_columns,
                         ph_segment** out) {
   return guarded([&] {
     if (!ctx || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
     *out = nullptr;
-    *out = segment_load_dir_impl(&ctx->c, segment_dir, columns, num_columns);
+    *out = pin_placed(ctx, 0, [&](Context* c) { return segment_load_dir_impl(c, segment_dir, columns, num_columns); });
   });
 }
 
@@ -201,9 +217,13 @@ int ph_table_set_dictionary(ph_ctx* ctx, const char* column, int32_t data_type, 
     }
     for (int64_t i = 1; i < count; ++i)
       if (d.compare(i - 1, d, i) >= 0) fail(PH_ERR_INVALID_ARGUMENT, "table dictionary must be sorted and unique");
-    g->id = next_object_id();
-    std::lock_guard<std::mutex> lk(ctx->c.mu);
-    ctx->c.table_dicts[column] = g;
+    for (Context* c : ctx->devs) {  // one copy per device: its device-side caches (values, remaps) live there
+      auto gc = std::make_shared<GlobalDict>();
+      gc->dict = g->dict;
+      gc->id = next_object_id();
+      std::lock_guard<std::mutex> lk(c->mu);
+      c->table_dicts[column] = gc;
+    }
   });
 }
 
@@ -211,8 +231,10 @@ int ph_table_set_column_type(ph_ctx* ctx, const char* column, int32_t data_type)
   return guarded([&] {
     if (!ctx || !column) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
     if (data_type < PH_INT || data_type > PH_STRING) fail(PH_ERR_INVALID_ARGUMENT, "data type");
-    std::lock_guard<std::mutex> lk(ctx->c.mu);
-    ctx->c.column_types[column] = data_type;
+    for (Context* c : ctx->devs) {
+      std::lock_guard<std::mutex> lk(c->mu);
+      c->column_types[column] = data_type;
+    }
   });
 }
 
@@ -221,7 +243,9 @@ int ph_query_execute(ph_ctx* ctx, const ph_query* query, ph_segment* const* segm
   return guarded([&] {
     if (!ctx || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
     *out = nullptr;
-    if (query && query->min_segment_group_trim_size > 0 && query->num_group_by > 0 && query->num_order_by > 0)
+    if (ctx->devs.size() > 1)
+      *out = multi_execute(ctx, query, segments, num_segments);  // per device, merged in the library
+    else if (query && query->min_segment_group_trim_size > 0 && query->num_group_by > 0 && query->num_order_by > 0)
       *out = segment_trim_execute(&ctx->c, query, segments, num_segments);  // GroupByOperator segment trim
     else
       *out = query_execute_impl(&ctx->c, query, segments, num_segments, nullptr);
@@ -231,6 +255,14 @@ int ph_query_execute(ph_ctx* ctx, const ph_query* query, ph_segment* const* segm
 // Dense partials merge whole per-device tables, so GroupByOperator's per-segment trim (ORDER BY +
 // minSegmentGroupTrimSize > 0, GroupByOperator.java:114-130) cannot apply: such queries are not served here (the caller
 // takes ph_query_execute, which trims, or the CPU plan).
+// the device context a dense call runs on: the one every segment is pinned on
+static Context* dense_device(ph_ctx* ctx, ph_segment* const* segs, int32_t n) {
+  Context* c = n > 0 && segs && segs[0] ? segs[0]->ctx : &ctx->c;
+  for (int32_t i = 0; i < n; ++i)
+    if (!segs[i] || segs[i]->ctx != c) fail(PH_ERR_INVALID_ARGUMENT, "dense partials take the segments of one device");
+  return c;
+}
+
 static void reject_segment_trim(const ph_query* q) {
   if (q && q->min_segment_group_trim_size > 0 && q->num_group_by > 0 && q->num_order_by > 0)
     fail(PH_ERR_UNSUPPORTED, "segment group trim (minSegmentGroupTrimSize) on dense partials");
@@ -242,7 +274,7 @@ int ph_query_dense_layout(ph_ctx* ctx, const ph_query* query, ph_segment* const*
     if (!ctx || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
     reject_segment_trim(query);
     DenseArgs d{DENSE_LAYOUT, nullptr, 0, 0, out};
-    query_execute_impl(&ctx->c, query, segments, num_segments, &d);
+    query_execute_impl(dense_device(ctx, segments, num_segments), query, segments, num_segments, &d);
   });
 }
 
@@ -252,7 +284,8 @@ int ph_query_execute_dense(ph_ctx* ctx, const ph_query* query, ph_segment* const
     if (!ctx || !device_tables) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
     reject_segment_trim(query);
     DenseArgs d{DENSE_EXECUTE, device_tables, 0, 0, nullptr};
-    std::unique_ptr<ph_result> r(query_execute_impl(&ctx->c, query, segments, num_segments, &d));
+    std::unique_ptr<ph_result> r(query_execute_impl(dense_device(ctx, segments, num_segments), query, segments,
+                                                    num_segments, &d));
     if (stats && r) *stats = r->stats;
   });
 }
@@ -264,7 +297,7 @@ int ph_dense_finalize(ph_ctx* ctx, const ph_query* query, ph_segment* const* seg
     *out = nullptr;
     reject_segment_trim(query);
     DenseArgs d{DENSE_FINALIZE, const_cast<void* const*>(device_tables), group_begin, group_end, nullptr};
-    *out = query_execute_impl(&ctx->c, query, segments, num_segments, &d);
+    *out = query_execute_impl(dense_device(ctx, segments, num_segments), query, segments, num_segments, &d);
   });
 }
 

@@ -505,6 +505,54 @@ void launch_scan_and_entries(const ScanAndJob* jobs, int32_t njobs, int64_t max_
   PH_HIP_CHECK(hipGetLastError());
 }
 
+// The multi-device combine's local transport (logical shards sharing one device, multi.cpp): dst = dst (op) src over n
+// elements of one dense partial table (ph_reduce_op; identities never change a live value)
+__global__ void k_reduce_table(void* dst, const void* src, int64_t n, int32_t op) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    switch (op) {
+      case PH_REDUCE_SUM_I64: static_cast<int64_t*>(dst)[i] += static_cast<const int64_t*>(src)[i]; break;
+      case PH_REDUCE_SUM_F64: static_cast<double*>(dst)[i] += static_cast<const double*>(src)[i]; break;
+      case PH_REDUCE_MIN_I64: {
+        int64_t* d = static_cast<int64_t*>(dst) + i;
+        *d = min(*d, static_cast<const int64_t*>(src)[i]);
+        break;
+      }
+      case PH_REDUCE_MAX_I64: {
+        int64_t* d = static_cast<int64_t*>(dst) + i;
+        *d = max(*d, static_cast<const int64_t*>(src)[i]);
+        break;
+      }
+      default: {
+        uint32_t* d = static_cast<uint32_t*>(dst) + i;
+        *d = max(*d, static_cast<const uint32_t*>(src)[i]);
+      }
+    }
+  }
+}
+
+void launch_reduce_table(void* dst, const void* src, int64_t n, int32_t op, hipStream_t s) {
+  if (n <= 0) return;
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_reduce_table, dim3(grid), dim3(256), 0, s, dst, src, n, op);
+  PH_HIP_CHECK(hipGetLastError());
+}
+
+// identity of a reduce op over [0, n) elements (padding rows, and the tables of a device without segments)
+__global__ void k_fill_identity(void* dst, int64_t n, int32_t op) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (op == PH_REDUCE_MAX_U32) static_cast<uint32_t*>(dst)[i] = 0u;
+    else if (op == PH_REDUCE_SUM_F64) static_cast<double*>(dst)[i] = 0.0;
+    else static_cast<int64_t*>(dst)[i] = op == PH_REDUCE_MIN_I64 ? INT64_MAX : (op == PH_REDUCE_MAX_I64 ? INT64_MIN : 0);
+  }
+}
+
+void launch_fill_identity(void* dst, int64_t n, int32_t op, hipStream_t s) {
+  if (n <= 0) return;
+  const int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_fill_identity, dim3(grid), dim3(256), 0, s, dst, n, op);
+  PH_HIP_CHECK(hipGetLastError());
+}
+
 __global__ void k_fill_i64(int64_t* __restrict__ p, int64_t v, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     p[i] = v;

@@ -1,0 +1,417 @@
+// multi.cpp -- one ph_ctx over several GPUs of a node (ph_ctx_create_multi): segment placement and the combine of the
+// devices' partial results inside the library.
+//
+// A Pinot server runs every segment of a query in one JVM and merges their results in GroupByCombineOperator
+// (GroupByCombineOperator.java:125-197: the per-segment tasks, then IndexedTable upserts keyed by group values).  Here
+// the server's context owns one Context per GPU:
+//  * ph_segment_pin places a segment on the device with the fewest pinned docs (greedy row balance);
+//  * ph_query_execute splits the query's segments by device, scans each device's share into DENSE partial tables
+//    over one set of table-level dictionaries (ph_query_execute_dense's tables: a group is the same dense id on
+//    every device), one host thread per device, and merges the tables:
+//      - distinct devices: RCCL reduce-scatter over xGMI (ncclCommInitAll, in-process; librccl is dlopen'ed), so
+//        device k owns the fully merged key shard k and finalises it (ph_dense_finalize's compaction) in parallel
+//        with the others; the shards concatenate into one ph_result;
+//      - logical shards sharing a device (e.g. a test of two shards on one GPU): a device copy + reduce kernel into
+//        the first shard's tables, finalised whole;
+//  * a query the dense tables do not serve (a key space beyond the dense budget, group trim) runs per device and
+//    the per-device results merge on the host by group value (merge_results_by_value).
+#include <dlfcn.h>
+
+#include <chrono>
+#include <cstring>
+#include <thread>
+
+#include <rccl/rccl.h>
+
+#include "ph_internal.h"
+
+namespace ph {
+
+ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const* segs, int32_t nseg,
+                              const DenseArgs* dense);
+ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* const* segs, int32_t nseg);
+
+namespace {
+
+// librccl.so.1 entry points, loaded on first use (RTLD_LOCAL: no link-time dependency, and no clash with another RCCL
+// already in the process, such as torch's)
+struct Rccl {
+  void* h = nullptr;
+  decltype(&ncclCommInitAll) init_all = nullptr;
+  decltype(&ncclReduceScatter) reduce_scatter = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+const Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    x.h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!x.h) x.h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!x.h) return x;
+    x.init_all = reinterpret_cast<decltype(x.init_all)>(dlsym(x.h, "ncclCommInitAll"));
+    x.reduce_scatter = reinterpret_cast<decltype(x.reduce_scatter)>(dlsym(x.h, "ncclReduceScatter"));
+    x.group_start = reinterpret_cast<decltype(x.group_start)>(dlsym(x.h, "ncclGroupStart"));
+    x.group_end = reinterpret_cast<decltype(x.group_end)>(dlsym(x.h, "ncclGroupEnd"));
+    x.destroy = reinterpret_cast<decltype(x.destroy)>(dlsym(x.h, "ncclCommDestroy"));
+    x.error_string = reinterpret_cast<decltype(x.error_string)>(dlsym(x.h, "ncclGetErrorString"));
+    if (!x.init_all || !x.reduce_scatter || !x.group_start || !x.group_end || !x.destroy || !x.error_string) x.h = nullptr;
+    return x;
+  }();
+  if (!r.h) fail(PH_ERR_UNSUPPORTED, "librccl.so.1 is not loadable: the multi-GPU combine needs RCCL");
+  return r;
+}
+
+void nccl_check(ncclResult_t e, const char* what) {
+  if (e != ncclSuccess) fail(PH_ERR_DEVICE, std::string(what) + ": " + rccl().error_string(e));
+}
+
+ncclDataType_t nccl_type(int op) {
+  return op == PH_REDUCE_SUM_F64 ? ncclFloat64 : (op == PH_REDUCE_MAX_U32 ? ncclUint32 : ncclInt64);
+}
+ncclRedOp_t nccl_op(int op) {
+  return op == PH_REDUCE_MIN_I64 ? ncclMin : ((op == PH_REDUCE_MAX_I64 || op == PH_REDUCE_MAX_U32) ? ncclMax : ncclSum);
+}
+
+double ms_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
+// run f(k) for every k in ks on its own host thread (one per device); the first exception is rethrown after the join
+template <class F>
+void per_device(const std::vector<int>& ks, F&& f) {
+  std::vector<std::exception_ptr> err(ks.size());
+  std::vector<std::thread> th;
+  for (size_t i = 0; i < ks.size(); ++i)
+    th.emplace_back([&, i] {
+      try {
+        f(ks[i]);
+      } catch (...) {
+        err[i] = std::current_exception();
+      }
+    });
+  for (auto& t : th) t.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+}
+
+}  // namespace
+
+struct MultiState {
+  std::mutex place_mu;          // segment placement
+  std::mutex comm_mu;           // communicator creation / use (one collective sequence at a time)
+  std::vector<ncclComm_t> comms;  // one per device (distinct ordinals only), created on first use
+  ~MultiState() {
+    if (!comms.empty())
+      for (auto c : comms) rccl().destroy(c);
+  }
+};
+
+void context_init(Context& c, int ordinal) {
+  int n = 0;
+  PH_HIP_CHECK(hipGetDeviceCount(&n));
+  if (ordinal < 0 || ordinal >= n) fail(PH_ERR_INVALID_ARGUMENT, "device ordinal " + std::to_string(ordinal) + " out of range");
+  c.device = ordinal;
+  PH_HIP_CHECK(hipSetDevice(ordinal));
+  c.lane_release(c.lane_acquire());  // one execution lane up front (fails here, not in a query, on a bad device)
+  hipDeviceProp_t prop;
+  PH_HIP_CHECK(hipGetDeviceProperties(&prop, ordinal));
+  c.num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+}
+
+void multi_init(ph_ctx* x, const int32_t* ordinals, int32_t n) {
+  if (!ordinals || n < 1 || n > 64) fail(PH_ERR_INVALID_ARGUMENT, "device set");
+  context_init(x->c, ordinals[0]);
+  x->devs = {&x->c};
+  x->ordinals = {ordinals[0]};
+  for (int32_t i = 1; i < n; ++i) {
+    x->more.push_back(std::make_unique<Context>());
+    context_init(*x->more.back(), ordinals[i]);
+    x->more.back()->device_index = i;
+    x->devs.push_back(x->more.back().get());
+    x->ordinals.push_back(ordinals[i]);
+  }
+  x->multi = std::make_shared<MultiState>();
+}
+
+// the device a new segment of `rows` docs goes to: the fewest docs pinned so far (its rows are reserved at once, so
+// concurrent pins spread too); the caller unreserves them if the pin fails
+Context* place_segment(ph_ctx* x, int64_t rows) {
+  if (x->devs.size() <= 1) return &x->c;
+  std::lock_guard<std::mutex> lk(x->multi->place_mu);
+  Context* best = x->devs[0];
+  for (Context* c : x->devs)
+    if (c->pinned_rows < best->pinned_rows) best = c;
+  best->pinned_rows += rows;
+  return best;
+}
+
+ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, int32_t nseg) {
+  using clock = std::chrono::steady_clock;
+  const auto t0 = clock::now();
+  if (!q) fail(PH_ERR_INVALID_ARGUMENT, "null query");
+  const int D = (int)x->devs.size();
+  std::vector<std::vector<ph_segment*>> by(D);
+  std::vector<ph_segment*> all;
+  for (int32_t i = 0; i < nseg; ++i) {
+    ph_segment* s = segs[i];
+    if (!s) fail(PH_ERR_INVALID_ARGUMENT, "null segment");
+    const int k = s->ctx->device_index;
+    if (k < 0 || k >= D || x->devs[k] != s->ctx) fail(PH_ERR_INVALID_ARGUMENT, "segment not pinned through this context");
+    by[k].push_back(s);
+    all.push_back(s);
+  }
+  if (q->min_segment_group_trim_size > 0 && q->num_group_by > 0 && q->num_order_by > 0)
+    return segment_trim_execute(&x->c, q, segs, nseg);  // per segment, each on its own device
+  std::vector<int> active;
+  for (int k = 0; k < D; ++k)
+    if (!by[k].empty()) active.push_back(k);
+  if (active.size() <= 1) {
+    const int k = active.empty() ? 0 : active[0];
+    return query_execute_impl(x->devs[k], q, by[k].data(), (int32_t)by[k].size(), nullptr);
+  }
+  // group-by dictionaries: the table-level ones where every device has them, else one union over every device's
+  // segments -- a separate copy per device (their device-side caches live on that device)
+  bool have_tables = true;
+  for (int g = 0; g < q->num_group_by; ++g)
+    for (Context* c : x->devs) {
+      std::lock_guard<std::mutex> lk(c->mu);
+      have_tables &= c->table_dicts.count(q->group_by[g]) > 0;
+    }
+  std::vector<std::vector<std::shared_ptr<GlobalDict>>> dicts(D);
+  if (!have_tables)
+    for (int g = 0; g < q->num_group_by; ++g) {
+      auto u = union_dictionary(q->group_by[g], all);
+      for (int k = 0; k < D; ++k) {
+        auto c = std::make_shared<GlobalDict>();
+        c->dict = u->dict;
+        c->id = next_object_id();
+        dicts[k].push_back(std::move(c));
+      }
+    }
+  auto dense = [&](int k, int op) {
+    DenseArgs a{op, nullptr, 0, 0, nullptr};
+    if (!have_tables) a.dicts = &dicts[k];
+    return a;
+  };
+  // a shape the dense tables do not serve: every device runs the query on its segments, the results merge on the
+  // host by group value
+  auto host_merge = [&]() {
+    std::vector<std::unique_ptr<ph_result>> parts(D);
+    per_device(active, [&](int k) {
+      PH_HIP_CHECK(hipSetDevice(x->ordinals[k]));
+      parts[k].reset(query_execute_impl(x->devs[k], q, by[k].data(), (int32_t)by[k].size(), nullptr));
+    });
+    std::vector<std::unique_ptr<ph_result>> live;
+    for (auto& p : parts)
+      if (p) live.push_back(std::move(p));
+    ph_result* r = merge_results_by_value(q, live);
+    r->stats.num_devices = (int32_t)active.size();
+    r->stats.host_ms = ms_since(t0);
+    return r;
+  };
+  ph_dense_layout L{};
+  try {
+    DenseArgs la = dense(active[0], DENSE_LAYOUT);
+    la.layout = &L;
+    query_execute_impl(x->devs[active[0]], q, by[active[0]].data(), (int32_t)by[active[0]].size(), &la);
+  } catch (const Error& e) {
+    if (e.code != PH_ERR_UNSUPPORTED) throw;
+    return host_merge();
+  }
+  if (getenv("PH_MULTI_HOST_MERGE")) return host_merge();  // the value-keyed merge, forced (tests)
+  const int64_t G = L.num_groups;
+  if (G <= 0) return host_merge();
+  // shard S of every device: a multiple of 64 groups, D shards covering the padded tables
+  int64_t S = (G + D - 1) / D;
+  S = (S + 63) / 64 * 64;
+  const int64_t padded = S * D;
+  // ---- scan: every device fills its tables (identities where it has no segment, and in the padding rows)
+  std::vector<std::vector<std::unique_ptr<DeviceBuffer>>> T(D);
+  std::vector<ph_exec_stats> st(D);
+  std::vector<int> every(D);
+  for (int k = 0; k < D; ++k) every[k] = k;
+  per_device(every, [&](int k) {
+    Context& c = *x->devs[k];
+    PH_HIP_CHECK(hipSetDevice(c.device));
+    std::vector<void*> ptrs;
+    for (int t = 0; t < L.num_tables; ++t) {
+      T[k].push_back(std::make_unique<DeviceBuffer>());
+      T[k].back()->alloc((size_t)padded * L.elems_per_group[t] * L.elem_bytes[t], c.device);
+      ptrs.push_back(T[k].back()->ptr);
+    }
+    LaneGuard lg(&c);
+    const hipStream_t sk = lg.lane->stream;
+    const int64_t live = by[k].empty() ? 0 : G;
+    for (int t = 0; t < L.num_tables; ++t) {
+      const int64_t per = L.elems_per_group[t];
+      launch_fill_identity(static_cast<uint8_t*>(ptrs[t]) + (size_t)live * per * L.elem_bytes[t], (padded - live) * per,
+                           L.reduce_op[t], sk);
+    }
+    PH_HIP_CHECK(hipStreamSynchronize(sk));
+    if (!by[k].empty()) {
+      DenseArgs ea = dense(k, DENSE_EXECUTE);
+      ea.tables = ptrs.data();
+      std::unique_ptr<ph_result> r(query_execute_impl(&c, q, by[k].data(), (int32_t)by[k].size(), &ea));
+      st[k] = r->stats;
+    }
+  });
+  const auto t_scan = clock::now();
+  // ---- merge
+  bool distinct = true;
+  for (int a = 0; a < D; ++a)
+    for (int b = a + 1; b < D; ++b) distinct &= x->ordinals[a] != x->ordinals[b];
+  if (const char* e = getenv("PH_MULTI_TRANSPORT")) distinct = distinct && std::string(e) != "local";
+  std::vector<std::pair<int, std::pair<int64_t, int64_t>>> shards;  // (device, [g0, g1)) to finalise
+  std::vector<std::vector<std::unique_ptr<DeviceBuffer>>> R(D);       // reduce-scatter outputs
+  if (distinct) {
+    const Rccl& api = rccl();
+    std::lock_guard<std::mutex> lk(x->multi->comm_mu);
+    if (x->multi->comms.empty()) {
+      std::vector<ncclComm_t> comms(D);
+      nccl_check(api.init_all(comms.data(), D, x->ordinals.data()), "ncclCommInitAll");
+      x->multi->comms = comms;
+    }
+    std::vector<std::unique_ptr<LaneGuard>> lanes;
+    for (int k = 0; k < D; ++k) {
+      PH_HIP_CHECK(hipSetDevice(x->ordinals[k]));
+      lanes.push_back(std::make_unique<LaneGuard>(x->devs[k]));
+      for (int t = 0; t < L.num_tables; ++t) {
+        R[k].push_back(std::make_unique<DeviceBuffer>());
+        R[k].back()->alloc((size_t)S * L.elems_per_group[t] * L.elem_bytes[t], x->ordinals[k]);
+      }
+    }
+    // one reduce-scatter per table: device k receives the merged key shard [k S, (k + 1) S)
+    nccl_check(api.group_start(), "ncclGroupStart");
+    for (int t = 0; t < L.num_tables; ++t)
+      for (int k = 0; k < D; ++k)
+        nccl_check(api.reduce_scatter(T[k][t]->ptr, R[k][t]->ptr, (size_t)S * L.elems_per_group[t],
+                                      nccl_type(L.reduce_op[t]), nccl_op(L.reduce_op[t]), x->multi->comms[k],
+                                      lanes[k]->lane->stream),
+                   "ncclReduceScatter");
+    nccl_check(api.group_end(), "ncclGroupEnd");
+    for (int k = 0; k < D; ++k) {
+      PH_HIP_CHECK(hipSetDevice(x->ordinals[k]));
+      PH_HIP_CHECK(hipStreamSynchronize(lanes[k]->lane->stream));
+    }
+    for (int k = 0; k < D; ++k) {
+      const int64_t g0 = std::min<int64_t>(G, k * S), g1 = std::min<int64_t>(G, g0 + S);
+      if (g1 > g0) shards.push_back({k, {g0, g1}});
+    }
+  } else {
+    // local transport: every other device's tables copied to the owner's device and reduced into its tables
+    const int owner = active[0];
+    Context& c = *x->devs[owner];
+    PH_HIP_CHECK(hipSetDevice(c.device));
+    LaneGuard lg(&c);
+    const hipStream_t so = lg.lane->stream;
+    for (int k = 0; k < D; ++k) {
+      if (k == owner || by[k].empty()) continue;  // a device without segments holds identities only
+      for (int t = 0; t < L.num_tables; ++t) {
+        const size_t bytes = (size_t)padded * L.elems_per_group[t] * L.elem_bytes[t];
+        const void* src = T[k][t]->ptr;
+        std::unique_ptr<DeviceBuffer> tmp;
+        if (x->ordinals[k] != c.device) {
+          tmp = std::make_unique<DeviceBuffer>();
+          tmp->alloc(bytes, c.device);
+          PH_HIP_CHECK(hipMemcpyPeerAsync(tmp->ptr, c.device, src, x->ordinals[k], bytes, so));
+          src = tmp->ptr;
+        }
+        launch_reduce_table(T[owner][t]->ptr, src, (int64_t)padded * L.elems_per_group[t], L.reduce_op[t], so);
+        PH_HIP_CHECK(hipStreamSynchronize(so));
+      }
+    }
+    shards.push_back({owner, {0, G}});
+  }
+  const auto t_merge = clock::now();
+  // ---- finalise the shards in parallel (a shard on a device without segments moves to the first active device)
+  std::vector<std::unique_ptr<ph_result>> parts(shards.size());
+  std::vector<int> idx(shards.size());
+  for (size_t i = 0; i < shards.size(); ++i) idx[i] = (int)i;
+  per_device(idx, [&](int i) {
+    int k = shards[i].first;
+    const int64_t g0 = shards[i].second.first, g1 = shards[i].second.second;
+    std::vector<void*> ptrs;
+    std::vector<std::unique_ptr<DeviceBuffer>> moved;
+    for (int t = 0; t < L.num_tables; ++t) {
+      uint8_t* p = static_cast<uint8_t*>(distinct ? R[k][t]->ptr : T[k][t]->ptr);
+      ptrs.push_back(distinct ? p : p + (size_t)g0 * L.elems_per_group[t] * L.elem_bytes[t]);
+    }
+    if (by[k].empty()) {
+      const int to = active[0];
+      PH_HIP_CHECK(hipSetDevice(x->ordinals[to]));
+      for (int t = 0; t < L.num_tables; ++t) {
+        const size_t bytes = (size_t)(g1 - g0) * L.elems_per_group[t] * L.elem_bytes[t];
+        moved.push_back(std::make_unique<DeviceBuffer>());
+        moved.back()->alloc(bytes, x->ordinals[to]);
+        PH_HIP_CHECK(hipMemcpyPeer(moved.back()->ptr, x->ordinals[to], ptrs[t], x->ordinals[k], bytes));
+        ptrs[t] = moved.back()->ptr;
+      }
+      k = to;
+    }
+    PH_HIP_CHECK(hipSetDevice(x->ordinals[k]));
+    DenseArgs fa = dense(k, DENSE_FINALIZE);
+    fa.tables = ptrs.data();
+    fa.g0 = g0;
+    fa.g1 = g1;
+    parts[i].reset(query_execute_impl(x->devs[k], q, by[k].data(), (int32_t)by[k].size(), &fa));
+  });
+  const auto t_fin = clock::now();
+  // ---- one result: the shards' groups back to back (ascending key ranges), the devices' scan statistics
+  auto out = std::make_unique<ph_result>();
+  ph_result& f = *parts[0];
+  out->key_types = f.key_types;
+  out->key_entry_size = f.key_entry_size;
+  out->agg_types = f.agg_types;
+  out->agg_log2m = f.agg_log2m;
+  out->mode = f.mode;
+  int64_t total = 0;
+  for (auto& p : parts) total += p->num_groups;
+  out->num_groups = total;
+  out->keys.resize(f.keys.size());
+  out->aggs.resize(f.aggs.size());
+  auto concat = [&](std::vector<ResultBuf> ph_result::*field, size_t i) {
+    size_t bytes = 0;
+    for (auto& p : parts) bytes += ((*p).*field)[i].size();
+    ResultBuf& dst = (out.get()->*field)[i];
+    dst.assign(bytes, 0);
+    size_t o = 0;
+    for (auto& p : parts) {
+      const ResultBuf& src = ((*p).*field)[i];
+      if (src.size()) std::memcpy(dst.data() + o, src.data(), src.size());
+      o += src.size();
+    }
+  };
+  for (size_t i = 0; i < f.keys.size(); ++i) concat(&ph_result::keys, i);
+  for (size_t i = 0; i < f.aggs.size(); ++i) concat(&ph_result::aggs, i);
+  ph_exec_stats& s = out->stats;
+  for (auto& p : parts) {  // matched docs from the merged COUNT table, shard by shard (as ph_dense_finalize)
+    s.num_docs_scanned += p->stats.num_docs_scanned;
+    s.num_entries_scanned_post_filter += p->stats.num_entries_scanned_post_filter;
+  }
+  for (int k : active) {
+    const ph_exec_stats& a = st[k];
+    s.num_entries_scanned_in_filter += a.num_entries_scanned_in_filter;
+    s.num_total_docs += a.num_total_docs;
+    s.num_segments_processed += a.num_segments_processed;
+    s.num_segments_matched += a.num_segments_matched;
+    s.num_groups_limit_reached |= a.num_groups_limit_reached;
+    s.sum_precision_flag |= a.sum_precision_flag;
+    s.device_ms = std::max(s.device_ms, a.device_ms);  // the devices scan concurrently
+    s.plan_mode = a.plan_mode;
+    s.scan_kernel = a.scan_kernel;
+    s.limit_pass = std::max(s.limit_pass, a.limit_pass);
+  }
+  for (auto& p : parts) s.sum_precision_flag |= p->stats.sum_precision_flag;
+  s.num_devices = (int32_t)active.size();
+  s.merge_ms = std::chrono::duration<double, std::milli>(t_merge - t_scan).count();
+  s.finalize_ms = std::chrono::duration<double, std::milli>(t_fin - t_merge).count();
+  s.host_ms = ms_since(t0);
+  return out.release();
+}
+
+}  // namespace ph
+
+ph_ctx::~ph_ctx() { multi.reset(); }

@@ -357,11 +357,15 @@ struct DeviceBuffer {
 
 // ------------------------------------------------------------------ dense partial tables (multi-GPU combine)
 enum : int32_t { DENSE_LAYOUT = 1, DENSE_EXECUTE = 2, DENSE_FINALIZE = 3 };
+struct GlobalDict;
 struct DenseArgs {
   int32_t op;
   void* const* tables;     // DENSE_EXECUTE / DENSE_FINALIZE: caller-owned device tables (layout order)
   int64_t g0, g1;          // DENSE_FINALIZE: the key shard [g0, g1) the tables hold
   ph_dense_layout* layout; // DENSE_LAYOUT output
+  // group-by dictionaries in group-by order, in place of the context's table dictionaries (the multi-device combine
+  // builds one union over every device's segments, one copy per device)
+  const std::vector<std::shared_ptr<GlobalDict>>* dicts = nullptr;
 };
 
 // ------------------------------------------------------------------ host-side segment model
@@ -600,6 +604,8 @@ void launch_merge_overflow(const MergeParams& p, hipStream_t s);
 void launch_encode_values(const uint32_t* fwd, int32_t bits, const int64_t* table, int64_t base, int32_t vbits,
                           int64_t n, uint32_t* out, hipStream_t s);
 void launch_fill_i64(int64_t* p, int64_t v, int64_t n, hipStream_t s);
+void launch_reduce_table(void* dst, const void* src, int64_t n, int32_t op, hipStream_t s);  // dst (op)= src
+void launch_fill_identity(void* dst, int64_t n, int32_t op, hipStream_t s);                 // op's identity
 void launch_hll_table(const void* values, int32_t is_int, int64_t n, int log2m, uint32_t* out, hipStream_t s);
 
 void build_bitmap_directory(Column& c);  // at pin, from c.inverted
@@ -692,6 +698,9 @@ int32_t murmur_hash_bytes(const uint8_t* data, int32_t len, int32_t seed);
 uint32_t hll_entry(int32_t hash, int log2m);
 void segment_check_impl(const ph_segment_desc* desc);                    // segment.cpp
 uint64_t next_object_id();                                               // segment.cpp
+// trim.cpp: per-device results of one query merged keyed by group values (the multi-device host combine)
+ph_result* merge_results_by_value(const ph_query* q, const std::vector<std::unique_ptr<ph_result>>& parts);
+std::shared_ptr<GlobalDict> union_dictionary(const std::string& col, const std::vector<ph_segment*>& segs);
 void build_hll_table(Context* ctx, Column& c, int log2m, hipStream_t st);  // into c.hll_tables (async on st)
 void fixed_bit_pack_host(const int32_t* ids, int64_t n, int bits, uint8_t* out);
 // raw (no-dictionary) forward indexes (rawfwd.cpp): decode a chunk forward index to native values, and
@@ -717,6 +726,20 @@ struct ResultBuf {
   uint8_t* data() { return pinned ? static_cast<uint8_t*>(pinned) : host.data(); }
   const uint8_t* data() const { return pinned ? static_cast<const uint8_t*>(pinned) : host.data(); }
   size_t size() const { return n; }
+};
+
+namespace ph {
+struct MultiState;  // multi.cpp: placement lock, RCCL communicators
+}
+
+// One context per ph_ctx_create (one GPU) or ph_ctx_create_multi (a set of GPUs of one node: one Context each)
+struct ph_ctx {
+  ph::Context c;                                   // device 0 of the set (a single-device context: the only one)
+  std::vector<std::unique_ptr<ph::Context>> more;  // devices 1.. of a multi-device context
+  std::vector<ph::Context*> devs;                  // every device's context, devs[0] == &c
+  std::vector<int32_t> ordinals;                   // their HIP device ordinals (may repeat: logical shards)
+  std::shared_ptr<ph::MultiState> multi;
+  ~ph_ctx();
 };
 
 struct ph_result {

@@ -869,6 +869,11 @@ void fill_tile_pieces(DevSegment& d, int nstage, const int32_t* stage_soff, int 
   d.npieces = np;
 }
 
+// the sorted value union of a column over segments (any devices'): a table-level dictionary for one query
+std::shared_ptr<GlobalDict> union_dictionary(const std::string& col, const std::vector<ph_segment*>& segs) {
+  return build_union(nullptr, col, segs);
+}
+
 ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const* segs_in, int32_t nseg,
                               const DenseArgs* dn) {
   const int dop = dn ? dn->op : 0;
@@ -1254,7 +1259,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     std::shared_ptr<GlobalDict> gd;
     std::lock_guard<std::mutex> dlk(ctx->mu);  // table dictionaries / union cache
     auto it = ctx->table_dicts.find(g);
-    if (it != ctx->table_dicts.end()) {
+    if (dn && dn->dicts) {
+      gd = (*dn->dicts).at(gdicts.size());
+    } else if (it != ctx->table_dicts.end()) {
       gd = it->second;
     } else {
       std::string key = g + "#";
@@ -1303,7 +1310,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     // partial tables of different GPUs line up only over table-level dictionaries
     std::lock_guard<std::mutex> dlk(ctx->mu);
     for (auto& g : group_cols)
-      if (!ctx->table_dicts.count(g))
+      if (!ctx->table_dicts.count(g) && !dn->dicts)
         fail(PH_ERR_INVALID_ARGUMENT, "dense partials need ph_table_set_dictionary for group-by column " + g);
     if (fin && (dn->g0 < 0 || dn->g1 < dn->g0 || dn->g1 > G)) fail(PH_ERR_INVALID_ARGUMENT, "bad key shard");
   }
@@ -1324,6 +1331,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       if (val_ops[j] & 4) add(1, PH_REDUCE_MAX_I64, 8);
     }
     if (num_hll) add(num_hll * m, PH_REDUCE_MAX_U32, 4);
+    double bytes = 0;
+    for (int t = 0; t < L.num_tables; ++t) bytes += (double)G * L.elems_per_group[t] * L.elem_bytes[t];
+    if (bytes > kDenseTableBudget) fail(PH_ERR_UNSUPPORTED, "dense partials over a key space beyond the dense budget");
     return nullptr;
   }
 
@@ -2631,6 +2641,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   }
   if (dop == DENSE_EXECUTE) {
     // partial tables stay on the device for the cross-GPU reduction
+    stats.num_entries_scanned_post_filter = stats.num_docs_scanned * (int64_t)projected.size();
     stats.host_ms = std::chrono::duration<double, std::milli>(clock::now() - t0).count() - dev_ms;
     return res.release();
   }

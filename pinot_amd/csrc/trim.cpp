@@ -82,6 +82,163 @@ struct Row {
   uint64_t raw = 0;         // ArrayBasedHolder raw key over the segment's dictIds
 };
 
+// Results of one query merged keyed by group VALUES -- GroupByCombineOperator / IndexedTable upsert with
+// AggregationFunction.merge (GroupByCombineOperator.java:169-181, AggregationResultsBlockMerger.java:33-45): the
+// segment-trim combine below and the multi-device combine's host path (multi.cpp)
+class ValueMerge {
+ public:
+  explicit ValueMerge(const ph_query* q) : q_(q), ng_(q->num_group_by), na_(q->num_aggregations), key_size_(ng_, 0) {}
+
+  // the shape (types, widths) and the statistics of one more result
+  void note(const ph_result& r, bool add_device_ms = true) {
+    ph_exec_stats& st = out_->stats;
+    const ph_exec_stats& rs = r.stats;
+    st.num_docs_scanned += rs.num_docs_scanned;
+    st.num_entries_scanned_in_filter += rs.num_entries_scanned_in_filter;
+    st.num_entries_scanned_post_filter += rs.num_entries_scanned_post_filter;
+    st.num_total_docs += rs.num_total_docs;
+    st.num_segments_processed += rs.num_segments_processed;
+    st.num_segments_matched += rs.num_segments_matched;
+    st.num_groups_limit_reached |= rs.num_groups_limit_reached;
+    st.sum_precision_flag |= rs.sum_precision_flag;
+    st.device_ms = add_device_ms ? st.device_ms + rs.device_ms : std::max(st.device_ms, rs.device_ms);
+    st.host_ms += rs.host_ms;
+    st.plan_mode = rs.plan_mode;
+    st.scan_kernel = rs.scan_kernel;
+    st.limit_pass = std::max(st.limit_pass, rs.limit_pass);
+    if (!typed_) {
+      out_->key_types = r.key_types;
+      out_->agg_types = r.agg_types;
+      out_->agg_log2m = r.agg_log2m;
+      out_->mode = r.mode;
+      typed_ = true;
+    }
+    for (int c = 0; c < ng_ && c < (int)r.key_entry_size.size(); ++c) key_size_[c] = std::max(key_size_[c], r.key_entry_size[c]);
+  }
+
+  // r's groups as rows; with `seg`, each row also gets its ArrayBasedHolder raw key over seg's dictIds
+  std::vector<Row> rows(const ph_result& r, const ph_segment* seg) const {
+    const int64_t n = r.num_groups;
+    std::vector<Row> out((size_t)n);
+    for (int64_t g = 0; g < n; ++g) {
+      Row& row = out[(size_t)g];
+      uint64_t mult = 1;
+      for (int c = 0; c < ng_; ++c) {
+        const int w = r.key_entry_size[c];
+        const uint8_t* kp = r.keys[c].data() + (size_t)g * w;
+        const size_t len = r.key_types[c] == PH_STRING ? strnlen(reinterpret_cast<const char*>(kp), (size_t)w) : (size_t)w;
+        row.kv.emplace_back(reinterpret_cast<const char*>(kp), len);
+        const uint32_t l32 = (uint32_t)len;
+        row.key.append(reinterpret_cast<const char*>(&l32), 4);
+        row.key.append(row.kv.back());
+        if (!seg) continue;
+        // the key's dictId in this segment's dictionary (ArrayBasedHolder raw key)
+        const Dictionary& d = seg->columns.at(q_->group_by[c])->dict;
+        int64_t id = 0;
+        switch (r.key_types[c]) {
+          case PH_INT: { int32_t v; memcpy(&v, kp, 4); id = std::lower_bound(d.ints.begin(), d.ints.end(), (int64_t)v) - d.ints.begin(); break; }
+          case PH_LONG: { int64_t v; memcpy(&v, kp, 8); id = std::lower_bound(d.ints.begin(), d.ints.end(), v) - d.ints.begin(); break; }
+          case PH_FLOAT: {
+            float v; memcpy(&v, kp, 4);
+            id = std::lower_bound(d.reals.begin(), d.reals.end(), (double)v, [](double a, double b) { return java_double_compare(a, b) < 0; }) - d.reals.begin();
+            break;
+          }
+          case PH_DOUBLE: {
+            double v; memcpy(&v, kp, 8);
+            id = std::lower_bound(d.reals.begin(), d.reals.end(), v, [](double a, double b) { return java_double_compare(a, b) < 0; }) - d.reals.begin();
+            break;
+          }
+          default: id = std::lower_bound(d.strings.begin(), d.strings.end(), row.kv.back()) - d.strings.begin();
+        }
+        row.raw += (uint64_t)id * mult;
+        mult *= (uint64_t)std::max<int64_t>(1, d.size);
+      }
+      row.d.assign((size_t)na_, 0.0);
+      row.c.assign((size_t)na_, 0);
+      row.hll.resize((size_t)na_);
+      for (int k = 0; k < na_; ++k) {
+        const int t = r.agg_types[k];
+        const uint8_t* ap = r.aggs[k].data();
+        if (t == PH_AGG_COUNT) {
+          memcpy(&row.c[k], ap + 8 * g, 8);
+        } else if (t == PH_AGG_DISTINCTCOUNTHLL) {
+          const size_t m = (size_t)1 << r.agg_log2m[k];
+          row.hll[k].assign(ap + m * g, ap + m * (g + 1));
+        } else {
+          memcpy(&row.d[k], ap + 8 * g, 8);
+        }
+      }
+    }
+    return out;
+  }
+
+  // GroupByCombineOperator: merge into the server table (AggregationFunction.merge)
+  void add(std::vector<Row>& rows) {
+    for (auto& row : rows) {
+      auto it = index_.find(row.key);
+      if (it == index_.end()) {
+        index_.emplace(row.key, merged_.size());
+        merged_.push_back(std::move(row));
+        continue;
+      }
+      Row& dst = merged_[it->second];
+      for (int k = 0; k < na_; ++k) {
+        const int t = out_->agg_types[k];
+        if (t == PH_AGG_COUNT) dst.c[k] += row.c[k];
+        else if (t == PH_AGG_SUM) dst.d[k] += row.d[k];
+        else if (t == PH_AGG_MIN) dst.d[k] = std::min(dst.d[k], row.d[k]);
+        else if (t == PH_AGG_MAX) dst.d[k] = std::max(dst.d[k], row.d[k]);
+        else
+          for (size_t i = 0; i < dst.hll[k].size(); ++i) dst.hll[k][i] = std::max(dst.hll[k][i], row.hll[k][i]);
+      }
+    }
+  }
+
+  bool typed() const { return typed_; }
+  ph_exec_stats& stats() { return out_->stats; }
+
+  // the combined rows as a result (host vectors)
+  ph_result* finish() {
+    const int64_t R = (int64_t)merged_.size();
+    out_->num_groups = R;
+    out_->keys.resize((size_t)ng_);
+    out_->aggs.resize((size_t)na_);
+    out_->key_entry_size = key_size_;
+    for (int c = 0; c < ng_; ++c) {
+      const size_t w = (size_t)key_size_[c];
+      out_->keys[c].assign(w * R, 0);
+      for (int64_t g = 0; g < R; ++g) {
+        const std::string& v = merged_[(size_t)g].kv[c];
+        memcpy(out_->keys[c].data() + w * g, v.data(), std::min(w, v.size()));
+      }
+    }
+    for (int k = 0; k < na_; ++k) {
+      const int t = out_->agg_types[k];
+      if (t == PH_AGG_DISTINCTCOUNTHLL) {
+        const size_t m = (size_t)1 << out_->agg_log2m[k];
+        out_->aggs[k].assign(m * R, 0);
+        for (int64_t g = 0; g < R; ++g) memcpy(out_->aggs[k].data() + m * g, merged_[(size_t)g].hll[k].data(), m);
+      } else {
+        out_->aggs[k].assign(8 * (size_t)R, 0);
+        for (int64_t g = 0; g < R; ++g) {
+          if (t == PH_AGG_COUNT) memcpy(out_->aggs[k].data() + 8 * g, &merged_[(size_t)g].c[k], 8);
+          else memcpy(out_->aggs[k].data() + 8 * g, &merged_[(size_t)g].d[k], 8);
+        }
+      }
+    }
+    return out_.release();
+  }
+
+ private:
+  const ph_query* q_;
+  int ng_, na_;
+  std::vector<int32_t> key_size_;
+  bool typed_ = false;
+  std::unordered_map<std::string, size_t> index_;
+  std::vector<Row> merged_;
+  std::unique_ptr<ph_result> out_ = std::make_unique<ph_result>();
+};
+
 }  // namespace
 
 ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* const* segs, int32_t nseg) {
@@ -99,93 +256,13 @@ ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* con
   const int64_t trim = std::max<int64_t>((int64_t)q->limit * 5, q->min_segment_group_trim_size);
   ph_query one = *q;
   one.min_segment_group_trim_size = 0;
-  auto out = std::make_unique<ph_result>();
-  out->ctx = ctx;
-  std::unordered_map<std::string, size_t> index;
-  std::vector<Row> merged;
-  std::vector<int32_t> key_size(ng, 0);
-  bool typed = false;
+  ValueMerge vm(q);
   for (int32_t s = 0; s < nseg; ++s) {
-    std::unique_ptr<ph_result> r(query_execute_impl(ctx, &one, segs + s, 1, nullptr));
-    ph_exec_stats& st = out->stats;
-    const ph_exec_stats& rs = r->stats;
-    st.num_docs_scanned += rs.num_docs_scanned;
-    st.num_entries_scanned_in_filter += rs.num_entries_scanned_in_filter;
-    st.num_entries_scanned_post_filter += rs.num_entries_scanned_post_filter;
-    st.num_total_docs += rs.num_total_docs;
-    st.num_segments_processed += rs.num_segments_processed;
-    st.num_segments_matched += rs.num_segments_matched;
-    st.num_groups_limit_reached |= rs.num_groups_limit_reached;
-    st.sum_precision_flag |= rs.sum_precision_flag;
-    st.device_ms += rs.device_ms;
-    st.host_ms += rs.host_ms;
-    st.plan_mode = rs.plan_mode;
-    st.scan_kernel = rs.scan_kernel;
-    st.limit_pass = std::max(st.limit_pass, rs.limit_pass);
-    if (!typed) {
-      out->key_types = r->key_types;
-      out->agg_types = r->agg_types;
-      out->agg_log2m = r->agg_log2m;
-      out->mode = r->mode;
-      typed = true;
-    }
-    for (int c = 0; c < ng && c < (int)r->key_entry_size.size(); ++c) key_size[c] = std::max(key_size[c], r->key_entry_size[c]);
-    const int64_t n = r->num_groups;
-    std::vector<Row> rows((size_t)n);
-    ph_segment* seg = segs[s];
-    for (int64_t g = 0; g < n; ++g) {
-      Row& row = rows[(size_t)g];
-      uint64_t mult = 1;
-      for (int c = 0; c < ng; ++c) {
-        const int w = r->key_entry_size[c];
-        const uint8_t* kp = r->keys[c].data() + (size_t)g * w;
-        const size_t len = r->key_types[c] == PH_STRING ? strnlen(reinterpret_cast<const char*>(kp), (size_t)w) : (size_t)w;
-        row.kv.emplace_back(reinterpret_cast<const char*>(kp), len);
-        const uint32_t l32 = (uint32_t)len;
-        row.key.append(reinterpret_cast<const char*>(&l32), 4);
-        row.key.append(row.kv.back());
-        // the key's dictId in this segment's dictionary (ArrayBasedHolder raw key)
-        const Column& col = *seg->columns.at(q->group_by[c]);
-        const Dictionary& d = col.dict;
-        int64_t id = 0;
-        switch (r->key_types[c]) {
-          case PH_INT: { int32_t v; memcpy(&v, kp, 4); id = std::lower_bound(d.ints.begin(), d.ints.end(), (int64_t)v) - d.ints.begin(); break; }
-          case PH_LONG: { int64_t v; memcpy(&v, kp, 8); id = std::lower_bound(d.ints.begin(), d.ints.end(), v) - d.ints.begin(); break; }
-          case PH_FLOAT: {
-            float v; memcpy(&v, kp, 4);
-            id = std::lower_bound(d.reals.begin(), d.reals.end(), (double)v, [](double a, double b) { return java_double_compare(a, b) < 0; }) - d.reals.begin();
-            break;
-          }
-          case PH_DOUBLE: {
-            double v; memcpy(&v, kp, 8);
-            id = std::lower_bound(d.reals.begin(), d.reals.end(), v, [](double a, double b) { return java_double_compare(a, b) < 0; }) - d.reals.begin();
-            break;
-          }
-          default: {  // STRING: zero-padded bytes
-            std::string v(reinterpret_cast<const char*>(kp), strnlen(reinterpret_cast<const char*>(kp), (size_t)w));
-            id = std::lower_bound(d.strings.begin(), d.strings.end(), v) - d.strings.begin();
-          }
-        }
-        row.raw += (uint64_t)id * mult;
-        mult *= (uint64_t)std::max<int64_t>(1, d.size);
-      }
-      row.d.assign((size_t)na, 0.0);
-      row.c.assign((size_t)na, 0);
-      row.hll.resize((size_t)na);
-      for (int k = 0; k < na; ++k) {
-        const int t = r->agg_types[k];
-        const uint8_t* ap = r->aggs[k].data();
-        if (t == PH_AGG_COUNT) {
-          memcpy(&row.c[k], ap + 8 * g, 8);
-        } else if (t == PH_AGG_DISTINCTCOUNTHLL) {
-          const size_t m = (size_t)1 << r->agg_log2m[k];
-          row.hll[k].assign(ap + m * g, ap + m * (g + 1));
-        } else {
-          memcpy(&row.d[k], ap + 8 * g, 8);
-        }
-      }
-    }
-    if (n > trim) {
+    // each segment on its own device's context (a multi-device ph_ctx pins segments on different GPUs)
+    std::unique_ptr<ph_result> r(query_execute_impl(segs[s]->ctx, &one, segs + s, 1, nullptr));
+    vm.note(*r);
+    std::vector<Row> rows = vm.rows(*r, segs[s]);
+    if ((int64_t)rows.size() > trim) {
       // TableResizer: the intermediate-record comparator over the ORDER BY values, reversed for the heap
       auto cmp_inter = [&](const Row& a, const Row& b) -> int {
         for (int k = 0; k < q->num_order_by; ++k) {
@@ -246,59 +323,25 @@ ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* con
       for (const Row* h : heap) kept.push_back(*h);
       rows.swap(kept);
     }
-    // GroupByCombineOperator: merge into the server table (AggregationFunction.merge)
-    for (auto& row : rows) {
-      auto it = index.find(row.key);
-      if (it == index.end()) {
-        index.emplace(row.key, merged.size());
-        merged.push_back(std::move(row));
-        continue;
-      }
-      Row& dst = merged[it->second];
-      for (int k = 0; k < na; ++k) {
-        const int t = out->agg_types[k];
-        if (t == PH_AGG_COUNT) dst.c[k] += row.c[k];
-        else if (t == PH_AGG_SUM) dst.d[k] += row.d[k];
-        else if (t == PH_AGG_MIN) dst.d[k] = std::min(dst.d[k], row.d[k]);
-        else if (t == PH_AGG_MAX) dst.d[k] = std::max(dst.d[k], row.d[k]);
-        else
-          for (size_t i = 0; i < dst.hll[k].size(); ++i) dst.hll[k][i] = std::max(dst.hll[k][i], row.hll[k][i]);
-      }
-    }
+    vm.add(rows);
   }
-  // the combined rows as a result (host vectors)
-  const int64_t R = (int64_t)merged.size();
-  out->num_groups = R;
-  out->keys.resize((size_t)ng);
-  out->aggs.resize((size_t)na);
-  if (!typed) {  // no segment: an empty result with the query's shape
+  if (!vm.typed()) {  // no segment: an empty result with the query's shape
     std::unique_ptr<ph_result> r(query_execute_impl(ctx, &one, segs, 0, nullptr));
     return r.release();
   }
-  out->key_entry_size = key_size;
-  for (int c = 0; c < ng; ++c) {
-    const size_t w = (size_t)key_size[c];
-    out->keys[c].assign(w * R, 0);
-    for (int64_t g = 0; g < R; ++g) {
-      const std::string& v = merged[(size_t)g].kv[c];
-      memcpy(out->keys[c].data() + w * g, v.data(), std::min(w, v.size()));
-    }
+  return vm.finish();
+}
+
+// the multi-device combine's host path: per-device results of one query merged by group values (device_ms: the
+// slowest device's)
+ph_result* merge_results_by_value(const ph_query* q, const std::vector<std::unique_ptr<ph_result>>& parts) {
+  ValueMerge vm(q);
+  for (auto& r : parts) {
+    vm.note(*r, false);
+    std::vector<Row> rows = vm.rows(*r, nullptr);
+    vm.add(rows);
   }
-  for (int k = 0; k < na; ++k) {
-    const int t = out->agg_types[k];
-    if (t == PH_AGG_DISTINCTCOUNTHLL) {
-      const size_t m = (size_t)1 << out->agg_log2m[k];
-      out->aggs[k].assign(m * R, 0);
-      for (int64_t g = 0; g < R; ++g) memcpy(out->aggs[k].data() + m * g, merged[(size_t)g].hll[k].data(), m);
-    } else {
-      out->aggs[k].assign(8 * (size_t)R, 0);
-      for (int64_t g = 0; g < R; ++g) {
-        if (t == PH_AGG_COUNT) memcpy(out->aggs[k].data() + 8 * g, &merged[(size_t)g].c[k], 8);
-        else memcpy(out->aggs[k].data() + 8 * g, &merged[(size_t)g].d[k], 8);
-      }
-    }
-  }
-  return out.release();
+  return vm.finish();
 }
 
 }  // namespace ph

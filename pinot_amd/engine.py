@@ -43,6 +43,9 @@ class ExecutionStats:
     mode: int = 0
     limit_pass: int = 0  # numGroupsLimit: 0 not needed, 1 optimistic scan sufficed, 2 first-seen pass + rescan
     scan_kernel: int = 0  # PH_KERNEL_*: the scan's kernel form (SCAN_KERNEL_NAMES)
+    num_devices: int = 0  # multi-device context: devices that scanned segments
+    merge_ms: float = 0.0  # multi-device: partial-table combine (RCCL reduce-scatter / local reduce)
+    finalize_ms: float = 0.0  # multi-device: merged key shards -> result
 
 
 SCAN_KERNEL_NAMES = {0: "none", 1: "k_scan", 2: "k_agg_lean", 3: "k_agg_sparse", 4: "k_group_lds_lean",
@@ -197,12 +200,21 @@ class _ResultHandle:
 
 
 class GpuContext:
-    """One context per GPU (ph_ctx)."""
+    """One context per GPU (ph_ctx), or over a set of GPUs of the node (``devices``: ph_ctx_create_multi -- segments
+    placed by pinned rows, the devices' partial results merged inside the library; a repeated ordinal is a logical
+    shard of that GPU)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices=None):
         import weakref
         h = ctypes.c_void_p()
-        N.check(N.lib().ph_ctx_create(device, ctypes.byref(h)))
+        if devices is None:
+            N.check(N.lib().ph_ctx_create(device, ctypes.byref(h)))
+            self.devices = [device]
+        else:
+            ords = (ctypes.c_int32 * len(devices))(*devices)
+            N.check(N.lib().ph_ctx_create_multi(ords, len(devices), ctypes.byref(h)))
+            self.devices = list(devices)
+            device = devices[0]
         self.handle = h
         self.device = device
         # segments and results of this context: released before it (ph_ctx_destroy contract)
@@ -226,6 +238,10 @@ class GpuContext:
 
     def set_stream(self, stream_ptr: int):
         N.check(N.lib().ph_ctx_set_stream(self.handle, ctypes.c_void_p(stream_ptr)))
+
+    def segment_device(self, seg: PinnedSegment) -> int:
+        """Index (into ``devices``) of the device the segment was placed on."""
+        return N.lib().ph_segment_device(seg.handle)
 
     def pin(self, buffers: SegmentBuffers, hll_columns=(), log2m: int = 8) -> PinnedSegment:
         """ph_segment_pin; hll_columns get their DISTINCTCOUNTHLL table (log2m) built at pin."""
@@ -332,7 +348,7 @@ class GpuContext:
                                st.num_entries_scanned_post_filter, st.num_total_docs, st.num_segments_processed,
                                st.num_segments_matched, bool(st.num_groups_limit_reached),
                                bool(st.sum_precision_flag), st.device_ms, st.host_ms, st.plan_mode,
-                               st.limit_pass, st.scan_kernel)
+                               st.limit_pass, st.scan_kernel, st.num_devices, st.merge_ms, st.finalize_ms)
         return IntermediateResult(key_cols, agg_cols, n, [a.function for a in q.aggregations], stats)
 
     # ---------------------------------------------------------------- dense partials (multi-GPU combine)

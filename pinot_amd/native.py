@@ -123,12 +123,14 @@ class ExecStats(ctypes.Structure):
                 ("num_groups_limit_reached", ctypes.c_int32), ("sum_precision_flag", ctypes.c_int32),
                 ("device_ms", ctypes.c_double), ("host_ms", ctypes.c_double), ("plan_mode", ctypes.c_int32),
                 ("limit_pass", ctypes.c_int32),
-                ("scan_kernel", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("scan_kernel", ctypes.c_int32), ("num_devices", ctypes.c_int32),
+                ("merge_ms", ctypes.c_double), ("finalize_ms", ctypes.c_double)]
 
 
 # every symbol declared in include/pinot_hip.h
 EXPORTED_SYMBOLS = (
-    "ph_ctx_create", "ph_ctx_destroy", "ph_ctx_set_stream", "ph_segment_pin", "ph_segment_check", "ph_segment_load_dir",
+    "ph_ctx_create", "ph_ctx_create_multi", "ph_ctx_num_devices", "ph_segment_device", "ph_ctx_destroy",
+    "ph_ctx_set_stream", "ph_segment_pin", "ph_segment_check", "ph_segment_load_dir",
     "ph_segment_unpin",
     "ph_segment_device_bytes", "ph_segment_num_docs", "ph_table_set_dictionary", "ph_table_set_column_type", "ph_query_execute",
     "ph_result_destroy", "ph_result_stats", "ph_result_num_groups", "ph_result_key_entry_size", "ph_result_key_type",
@@ -170,6 +172,9 @@ def lib():
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     sig = {
         "ph_ctx_create": ([i32, ctypes.POINTER(vp)], ctypes.c_int),
+        "ph_ctx_create_multi": ([ctypes.POINTER(i32), i32, ctypes.POINTER(vp)], ctypes.c_int),
+        "ph_ctx_num_devices": ([vp], i32),
+        "ph_segment_device": ([vp], i32),
         "ph_ctx_destroy": ([vp], ctypes.c_int),
         "ph_ctx_set_stream": ([vp, vp], ctypes.c_int),
         "ph_segment_pin": ([vp, ctypes.POINTER(SegmentDesc), ctypes.POINTER(vp)], ctypes.c_int),
