@@ -389,38 +389,40 @@ int64_t simulate_filter_entries(const SimNode& root, const std::vector<SimLeaf>&
 
 // One gap of AndDocIdIterator(scan_1 .. scan_k).next() from _nextDocId = t, over the scans' match bitmaps: the entries
 // its advance() calls examine (the device pass's fallback for gaps longer than its step cap).
-int64_t scan_and_gap_entries(const uint64_t* const* scans, int k, int64_t num_docs, int64_t t) {
-  std::vector<Bits> s((size_t)k);
-  for (int i = 0; i < k; ++i) {
-    s[(size_t)i].w = scans[i];
-    s[(size_t)i].nw = (num_docs + 63) / 64;
-    s[(size_t)i].n = num_docs;
+int64_t and_walk_entries_host(const uint64_t* bits, int k, int64_t num_docs, int shift) {
+  if (num_docs <= 0) return 0;
+  AndWalkJob J{};
+  J.bits = (const unsigned long long*)bits;
+  J.nwords = (num_docs + 63) / 64;
+  J.ndocs = num_docs;
+  J.k = k;
+  J.shift = shift;
+  J.nchunks = ((num_docs - 1) >> shift) + 1;
+  std::vector<int32_t> pos((size_t)J.nchunks * (kWalkHead + kWalkTail));
+  std::vector<unsigned long long> cum(pos.size());
+  std::vector<uint32_t> cnt((size_t)J.nchunks);
+  J.pos = pos.data();
+  J.cum = cum.data();
+  J.cnt = cnt.data();
+  for (int64_t c = 0; c < J.nchunks; ++c) and_walk_chunk(J, c);
+  unsigned long long sum = 0;
+  for (int64_t c = 0; c < J.nchunks; ++c) {
+    unsigned long long part = 0;
+    if (!and_merge_chunk(J, c, part)) return -1;
+    sum += part;
   }
-  int64_t m = t, cost = 0;
-  int mi = -1, i = 0;
-  if (t >= num_docs) return 0;
-  while (i < k) {
-    if (i == mi) {
-      ++i;
-      continue;
-    }
-    const int64_t d = s[(size_t)i].next(m);
-    if (d < 0) return cost + (num_docs - m);
-    cost += d - m + 1;
-    if (d == m) {
-      ++i;
-    } else {
-      m = d;
-      mi = i;
-      i = 0;
-    }
-  }
-  return cost;
+  return num_docs - 1 + (int64_t)sum;
 }
 
 }  // namespace ph
 
-// test hook (not part of the product boundary, include/pinot_hip.h): the simulator over a flat tree -- node i =
+// test hooks (not part of the product boundary, include/pinot_hip.h).  The chunked walks of k_and_walk /
+// k_and_merge on the host over k leaf bitmaps (leaf-major), so the CPU tests check the merge against the simulator
+extern "C" int64_t phx_and_walk_entries(const uint64_t* bits, int32_t k, int64_t num_docs, int32_t shift) {
+  return ph::and_walk_entries_host(bits, k, num_docs, shift);
+}
+
+// test hook: the simulator over a flat tree -- node i =
 // (op, priority, leaf, first child, child count) -- so the CPU tests can check it against the oracle's restatement
 extern "C" int64_t phx_filter_entries_sim(const int32_t* nodes, int32_t num_nodes, const int32_t* leaf_kinds,
                                           const uint64_t* const* leaf_bits, int32_t num_leaves, int64_t num_docs) {

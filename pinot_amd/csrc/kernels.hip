@@ -382,10 +382,9 @@ void launch_selftest_unpack(const uint32_t* fwd, int64_t n, int bits, int32_t* o
 }
 
 // ------------------------------------------------------------------ filter-entry statistic (AndDocIdIterator)
-// Doc bitmaps of up to kMaxFbProgs sub-programs of one segment's filter (the merged index-based children, the
-// AND's scans, the remaining OR and its scan children), one wave per 64-doc word: the host turns them into the
-// reference's advance()-driven numEntriesScannedInFilter (and_or_entries).  A statistics pass, run only for that
-// filter shape.
+// Doc bitmaps of up to kMaxFbProgs leaves of one segment's filter tree (the leaves k_leaf_bitmaps does not take:
+// sorted ranges, inverted-index bitmaps, large dictId sets), one wave per 64-doc word, each leaf into its output row:
+// the filter-statistic pass walks or simulates the reference's iterators over them (query.cpp).
 __global__ void __launch_bounds__(256) k_filter_bitmaps(const FilterInsn* __restrict__ prog, const DevSegment* segs,
                                                         const FbJob job) {
   SegPtr S = (SegPtr)(segs + job.seg);
@@ -398,7 +397,7 @@ __global__ void __launch_bounds__(256) k_filter_bitmaps(const FilterInsn* __rest
       uint32_t fent = 0;
       const bool b = doc < ndocs && eval_filter((const PH_CONST FilterInsn*)prog + job.off[k], job.len[k], S, doc, fent);
       const unsigned long long bal = __ballot(b);
-      if (lane == 0) job.out[(int64_t)k * job.nwords + w] = bal;
+      if (lane == 0) job.out[(int64_t)job.row[k] * job.nwords + w] = bal;
     }
   }
 }
@@ -408,100 +407,6 @@ void launch_filter_bitmaps(const FilterInsn* prog, const DevSegment* segs, const
   if (blocks <= 0) return;
   PH_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_filter_bitmaps, dim3((unsigned)blocks), dim3(256), 0, s, prog, segs, job);
-  PH_HIP_CHECK(hipGetLastError());
-}
-
-// numEntriesScannedInFilter of an AND of SV scans only: AndDocIdSet.iterator returns AndDocIdIterator(scan_1 ..
-// scan_k) (AndDocIdSet.java:180-183) and DocIdSetOperator drains it with next(), each call leap-frogging the scans'
-// advance() from the previous match + 1 (AndDocIdIterator.java:38-75); every advance(t) examines the docs from t to the
-// scan's next match (SVScanDocIdIterator.java:101-112).  The calls of one next() depend only on the scans between two
-// consecutive matches of the AND, so every gap runs on its own thread: thread w takes the gaps that start in 64-doc
-// word w (doc 0, and a + 1 for each match a of the AND), from the scans' match bitmaps.  A gap whose word steps exceed
-// step_cap (a long run without a common match) is left to the host (fallback list).
-__global__ void __launch_bounds__(256) k_scan_and_entries(const ScanAndJob* __restrict__ jobs, unsigned long long* out,
-                                                          unsigned long long* fb, uint32_t* fb_n, uint32_t fb_cap,
-                                                          int32_t step_cap) {
-  const ScanAndJob J = jobs[blockIdx.y];
-  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  unsigned long long cost = 0;
-  if (w < J.nwords) {
-    const int k = J.k;
-    auto word = [&](int i, int64_t x) { return J.bits[(int64_t)i * J.nwords + x]; };
-    uint64_t I = ~0ull;
-    for (int i = 0; i < k; ++i) I &= word(i, w);
-    uint64_t starts = I << 1;
-    if (w == 0) {
-      starts |= 1ull;
-    } else {
-      uint64_t P = ~0ull;
-      for (int i = 0; i < k; ++i) P &= word(i, w - 1);
-      starts |= P >> 63;
-    }
-    const int64_t base = w * 64, lim = J.ndocs - base;  // a gap starting at ndocs costs nothing
-    if (lim < 64) starts &= lim <= 0 ? 0ull : ((1ull << lim) - 1ull);
-    while (starts) {
-      const int64_t t = base + __builtin_ctzll(starts);
-      starts &= starts - 1;
-      int32_t steps = 0;
-      bool capped = false;
-      // first match of scan i at or after x: -1 none, -2 over the step cap
-      auto nxt = [&](int i, int64_t x) -> int64_t {
-        int64_t wi = x >> 6;
-        uint64_t v = word(i, wi) & (~0ull << (x & 63));
-        while (!v) {
-          if (++wi >= J.nwords) return -1;
-          if (++steps > step_cap) return -2;
-          v = word(i, wi);
-        }
-        return wi * 64 + __builtin_ctzll(v);
-      };
-      unsigned long long c = 0;
-      int64_t m = t;
-      int mi = -1, i = 0;
-      while (i < k) {
-        if (i == mi) {
-          ++i;
-          continue;
-        }
-        if (++steps > step_cap) {
-          capped = true;
-          break;
-        }
-        const int64_t d = nxt(i, m);
-        if (d == -2) {
-          capped = true;
-          break;
-        }
-        if (d < 0 || d >= J.ndocs) {  // EOF: the scan examined the rest of the segment
-          c += (unsigned long long)(J.ndocs - m);
-          break;
-        }
-        c += (unsigned long long)(d - m + 1);
-        if (d == m) {
-          ++i;
-        } else {
-          m = d;
-          mi = i;
-          i = 0;
-        }
-      }
-      if (capped) {
-        const uint32_t slot = atomicAdd(fb_n, 1u);
-        if (slot < fb_cap) fb[slot] = ((unsigned long long)blockIdx.y << 40) | (unsigned long long)t;
-      } else {
-        cost += c;
-      }
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) cost += __shfl_xor(cost, o);
-  if ((threadIdx.x & 63) == 0 && cost) atomicAdd(out + J.slot, cost);
-}
-
-void launch_scan_and_entries(const ScanAndJob* jobs, int32_t njobs, int64_t max_words, unsigned long long* out,
-                             unsigned long long* fb, uint32_t* fb_n, uint32_t fb_cap, int32_t step_cap, hipStream_t s) {
-  if (njobs <= 0 || max_words <= 0) return;
-  const dim3 grid((unsigned)((max_words + 255) / 256), (unsigned)njobs);
-  hipLaunchKernelGGL(k_scan_and_entries, grid, dim3(256), 0, s, jobs, out, fb, fb_n, fb_cap, step_cap);
   PH_HIP_CHECK(hipGetLastError());
 }
 

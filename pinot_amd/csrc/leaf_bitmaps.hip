@@ -1,0 +1,57 @@
+// leaf_bitmaps.hip -- k_leaf_bitmaps: the doc bitmap of one dictId scan leaf (a RANGE [lo, lo + len) or a dictId set)
+// per job, in the register-direct form of reg_decode.h: lane l of a wave owns the 32 consecutive docs [32 l, 32 l + 32)
+// of a 2048-doc tile, decodes them with compile-time bit positions and writes their match bits as ONE 32-bit word --
+// two lanes form the 64-doc word of the bitmap (doc d at bit d & 63 of word d >> 6), so the stores are coalesced.
+// What the filter-statistic pass needs of the scan leaves (query.cpp: the leapfrog of ANDs of scans,
+// k_scan_and_entries, and the host iterator simulation); HBM-bound like k_count_reg, against the generic per-doc
+// program evaluation of k_filter_bitmaps.
+#include "reg_decode.h"
+
+namespace ph {
+
+template <int C>
+__global__ void __launch_bounds__(256) k_leaf_bitmaps(const LeafJob* __restrict__ jobs) {
+  __shared__ uint32_t set_lds[kLeafSetWords];
+  const LeafJob J = jobs[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const bool use_set = J.set != nullptr;
+  if (use_set) {  // the dictId set, staged once per workgroup
+    for (int i = threadIdx.x; i < J.set_words; i += 256) set_lds[i] = J.set[i];
+    __syncthreads();
+  }
+  const int64_t ntiles = (J.ndocs + 2047) / 2048;
+  const int64_t bytes = (J.ndocs * J.bits + 7) / 8;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t d0 = tile * 2048;
+    const int32_t ndoc = (int32_t)min<int64_t>(2048, J.ndocs - d0);
+    const int32_t nv = max(0, min(32, ndoc - lane * 32));
+    u32x4 pool[C];
+    reg_load<C>(true, lane * 32 < ndoc, J.fwd, J.bits, bytes, (int32_t)(d0 >> 5), lane, pool);
+    uint32_t v[32];
+    reg_unpack<C>(pool, J.bits, v);
+    uint32_t mask = 0;
+    if (use_set) {
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        mask |= (v[j] < (uint32_t)J.card && ((set_lds[v[j] >> 5] >> (v[j] & 31)) & 1u) ? 1u : 0u) << j;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 32; ++j) mask |= ((v[j] - J.lo) < J.len ? 1u : 0u) << j;
+    }
+    if (nv < 32) mask &= nv > 0 ? (0xffffffffu >> (32 - nv)) : 0u;
+    const int64_t wi = (d0 >> 5) + lane;  // this lane's 32-doc word (lanes past the end write the zero padding)
+    if (wi < J.out_words) J.out[wi] = mask;
+  }
+}
+
+void launch_leaf_bitmaps(const LeafJob* jobs, int32_t njobs, int64_t max_docs, int32_t max_bits, hipStream_t s) {
+  if (njobs <= 0 || max_docs <= 0) return;
+  const int64_t tiles = (max_docs + 2047) / 2048;
+  const dim3 grid((unsigned)std::min<int64_t>((tiles + 3) / 4, 2048), (unsigned)njobs);
+  if (max_bits <= 16) hipLaunchKernelGGL(k_leaf_bitmaps<4>, grid, dim3(256), 0, s, jobs);
+  else hipLaunchKernelGGL(k_leaf_bitmaps<8>, grid, dim3(256), 0, s, jobs);
+  PH_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace ph

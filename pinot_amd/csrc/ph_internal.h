@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "pinot_hip.h"
+#include "and_walk.h"
 
 namespace ph {
 
@@ -632,20 +633,31 @@ struct FbJob {
   int32_t seg;                 // device segment
   int32_t nprog;
   int32_t off[kMaxFbProgs], len[kMaxFbProgs];  // sub-programs inside the query's program array
+  int32_t row[kMaxFbProgs];    // output row of each sub-program
   int64_t nwords;              // 64-doc words of the segment
-  unsigned long long* out;     // [nprog][nwords] doc bitmaps
+  unsigned long long* out;     // [rows][nwords] doc bitmaps
 };
 void launch_filter_bitmaps(const FilterInsn* prog, const DevSegment* segs, const FbJob& job, hipStream_t s);
-// numEntriesScannedInFilter of AndDocIdIterator(scan_1 .. scan_k) drained by next() (every child an SV scan): the
-// scans' match bitmaps ([k][nwords] words at `bits`), per segment job; gaps longer than `step_cap` word steps go to
-// the fallback list (job << 40 | gap start) for the host
-struct ScanAndJob {
-  const unsigned long long* bits;
-  int64_t nwords, ndocs;
-  int32_t k, slot;  // scans; entries accumulate into out[slot]
+// numEntriesScannedInFilter of ANDs of scans: chunked walks of the leap-frog (and_walk.h, scan_and_walk.hip); the
+// device adds each job's sum of (calls - [match]) into out[slot] and flags bad[slot] when its walks did not meet
+void launch_and_walk(const AndWalkJob* jobs, int32_t njobs, int64_t max_chunks, unsigned long long* out, uint32_t* bad,
+                     hipStream_t s);
+// the same walks on the host (CPU tests): the entries, or -1 when the chunks of 1 << shift docs do not meet
+int64_t and_walk_entries_host(const uint64_t* bits, int k, int64_t num_docs, int shift);
+// the doc bitmap of a dictId scan leaf (leaf_bitmaps.hip): RANGE [lo, lo + len) or, with `set`, a dictId bitset over
+// `card` ids (<= kLeafSetWords * 32); `out` holds ceil(ndocs / 64) * 2 uint32 words (= the uint64 doc-bitmap words)
+constexpr int kLeafSetWords = 4096;
+struct LeafJob {
+  const uint32_t* fwd;
+  int64_t ndocs;
+  int32_t bits;
+  uint32_t lo, len;
+  const uint32_t* set;
+  int32_t set_words, card;
+  uint32_t* out;
+  int64_t out_words;
 };
-void launch_scan_and_entries(const ScanAndJob* jobs, int32_t njobs, int64_t max_words, unsigned long long* out,
-                             unsigned long long* fb, uint32_t* fb_n, uint32_t fb_cap, int32_t step_cap, hipStream_t s);
+void launch_leaf_bitmaps(const LeafJob* jobs, int32_t njobs, int64_t max_docs, int32_t max_bits, hipStream_t s);
 // host iterator simulation of the statistic (filter_sim.cpp): the planned filter tree over per-leaf doc bitmaps
 enum SimOp { SIM_LEAF = 0, SIM_AND = 1, SIM_OR = 2, SIM_NOT = 3 };
 enum SimLeafKind { SIM_SCAN = 0, SIM_SORTED = 1, SIM_BITMAP = 2 };
@@ -660,7 +672,6 @@ struct SimNode {
   std::vector<SimNode> kids;
 };
 int64_t simulate_filter_entries(const SimNode& root, const std::vector<SimLeaf>& leaves, int64_t num_docs);
-int64_t scan_and_gap_entries(const uint64_t* const* scans, int k, int64_t num_docs, int64_t t);
 void launch_selftest_staged(const DevSegment* seg, int32_t tile_words, int32_t stage_stride, int64_t n, int32_t* out,
                             hipStream_t s);
 // the 1 KiB wave-loads of a full tile of every staged stream of `d` (stage offsets per stream)

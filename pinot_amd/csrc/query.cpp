@@ -1102,7 +1102,12 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     std::vector<PNode> leaves;
     std::vector<int32_t> leaf_kinds;
     int32_t dseg = -1;
-    std::vector<size_t> jobs;  // its FbJobs (<= kMaxFbProgs leaves each, in leaf order)
+    std::vector<size_t> jobs;  // its FbJobs (<= kMaxFbProgs leaves each) for the leaves k_leaf_bitmaps does not take
+  };
+  // a leaf k_leaf_bitmaps computes from the forward index: a dictId range or a small dictId set of a scan leaf
+  auto fast_leaf = [&](const PNode& n) {
+    return n.kind == L_NODE && n.scan && n.kids.empty() &&
+           (n.op == OP_RANGE || (n.op == OP_SET && n.set.size() <= (size_t)kLeafSetWords));
   };
   std::vector<StatSeg> stat_segs;
   for (int i = 0; i < nseg && dop != DENSE_LAYOUT && !fin; ++i) {
@@ -1689,7 +1694,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       if (ss.qi != i) continue;
       ss.dseg = (int32_t)si;
       for (size_t l = 0; l < ss.leaves.size(); ++l) {
-        if (l % kMaxFbProgs == 0) {
+        if (fast_leaf(ss.leaves[l])) continue;
+        if (ss.jobs.empty() || fb_jobs[ss.jobs.back()].nprog == kMaxFbProgs) {
           FbJob job{};
           job.seg = (int32_t)si;
           job.nwords = ((int64_t)s->num_docs + 63) / 64;
@@ -1702,6 +1708,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         if (sp.max_depth > kMaxStack || (int)sp.insns.size() > kMaxProg) fail(PH_ERR_UNSUPPORTED, "filter too large");
         job.off[job.nprog] = (int32_t)all_insns.size();
         job.len[job.nprog] = (int32_t)sp.insns.size();
+        job.row[job.nprog] = (int32_t)l;
         ++job.nprog;
         for (auto& pp : sp.payloads) payload_fix.push_back({all_insns.size() + pp.first, pp.second});
         for (auto& bb : sp.bitmap_refs) bitmap_fix.push_back({all_insns.size() + bb.first, bb.second});
@@ -2450,27 +2457,41 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       PH_HIP_CHECK(hipEventRecord(L.ev_stop, st));
     }
     // numEntriesScannedInFilter of the ST_SCANAND / ST_SIM segments (a statistics pass after the scan's device-time
-    // window): the leaves' doc bitmaps (k_filter_bitmaps), then the AND-of-scans gap pass on the device or the
-    // iterator simulation on the host, in batches of segments bounded to kStatBatchWords words of bitmaps
+    // window): the leaves' doc bitmaps (k_leaf_bitmaps from the forward indexes, k_filter_bitmaps for the rest), then
+    // the chunked walks of the AND-of-scans leap-frog on the device (k_and_walk) or the iterator simulation on the
+    // host, in batches of segments bounded to kStatBatchWords words of bitmaps
     if (!stat_segs.empty()) {
       constexpr size_t kStatBatchWords = (size_t)32 << 20;  // 256 MiB
+      constexpr int kWalkShift = 12;                        // 4096-doc walks
       auto seg_words = [&](const StatSeg& ss) {
         return ss.leaves.size() * (size_t)((dsegs[ss.dseg].num_docs + 63) / 64);
       };
-      size_t total = 0, biggest = 0, n_scanand = 0;
+      size_t total = 0, biggest = 0, n_scanand = 0, walk_recs = 0;
       for (auto& ss : stat_segs) {
         if (ss.dseg < 0) continue;
         total += seg_words(ss);
         biggest = std::max(biggest, seg_words(ss));
         n_scanand += ss.kind == ST_SCANAND;
+        if (ss.kind == ST_SCANAND) walk_recs += (size_t)(((dsegs[ss.dseg].num_docs - 1) >> kWalkShift) + 1);
       }
       const size_t cap_words = std::max<size_t>(1, std::min(total, std::max(kStatBatchWords, biggest)));
       unsigned long long* dev = scratch.alloc<unsigned long long>(cap_words);
-      constexpr uint32_t kFbCap = 4096;
-      ScanAndJob* d_jobs = n_scanand ? scratch.alloc<ScanAndJob>(n_scanand) : nullptr;
+      // walk logs, sized for the first level of every job (a rerun's chunks are fewer)
+      int32_t* d_wpos = walk_recs ? scratch.alloc<int32_t>(walk_recs * (kWalkHead + kWalkTail)) : nullptr;
+      unsigned long long* d_wcum = walk_recs ? scratch.alloc<unsigned long long>(walk_recs * (kWalkHead + kWalkTail)) : nullptr;
+      uint32_t* d_wcnt = walk_recs ? scratch.alloc<uint32_t>(walk_recs) : nullptr;
+      AndWalkJob* d_wjobs = n_scanand ? scratch.alloc<AndWalkJob>(n_scanand) : nullptr;
       unsigned long long* d_out = n_scanand ? scratch.alloc<unsigned long long>(n_scanand) : nullptr;
-      unsigned long long* d_fb = n_scanand ? scratch.alloc<unsigned long long>(kFbCap) : nullptr;
-      uint32_t* d_fbn = n_scanand ? scratch.alloc<uint32_t>(1) : nullptr;
+      uint32_t* d_bad = n_scanand ? scratch.alloc<uint32_t>(n_scanand) : nullptr;
+      size_t n_fast = 0, set_words = 0;
+      for (auto& ss : stat_segs)
+        for (auto& l : ss.leaves)
+          if (ss.dseg >= 0 && fast_leaf(l)) {
+            ++n_fast;
+            set_words += l.op == OP_SET ? l.set.size() : 0;
+          }
+      LeafJob* d_ljobs = n_fast ? scratch.alloc<LeafJob>(n_fast) : nullptr;
+      uint32_t* d_lsets = set_words ? scratch.alloc<uint32_t>(set_words) : nullptr;
       std::vector<int64_t> ent(stat_segs.size(), 0);
       size_t next = 0;
       while (next < stat_segs.size()) {
@@ -2486,82 +2507,133 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           used += seg_words(ss);
         }
         if (batch.empty()) break;
-        std::vector<ScanAndJob> sj;
-        std::vector<size_t> sj_seg;  // batch position of each scan-AND job
-        int64_t max_words = 0;
+        // leaf bitmaps: one k_leaf_bitmaps launch for the batch's forward-index leaves
+        std::vector<LeafJob> lj;
+        std::vector<uint32_t> lsets;
+        int64_t max_docs = 0;
+        int32_t max_bits = 1;
         for (size_t b = 0; b < batch.size(); ++b) {
           const StatSeg& ss = stat_segs[batch[b]];
-          const int64_t nw = (dsegs[ss.dseg].num_docs + 63) / 64;
+          const int64_t n = dsegs[ss.dseg].num_docs, nw = (n + 63) / 64;
+          ph_segment* sg = segs[ss.qi];
+          for (size_t l = 0; l < ss.leaves.size(); ++l) {
+            const PNode& lf = ss.leaves[l];
+            if (!fast_leaf(lf)) continue;
+            const Column* col = sg->columns.at(slot_names[lf.col]).get();
+            LeafJob J{};
+            J.fwd = (const uint32_t*)col->d_fwd.ptr;
+            J.ndocs = n;
+            J.bits = col->bits;
+            J.lo = lf.op == OP_RANGE ? lf.lo : 0u;  // a set leaf matches through its bitset only (an empty one: none)
+            J.len = lf.op == OP_RANGE ? lf.len : 0u;
+            if (lf.op == OP_SET && !lf.set.empty()) {
+              J.set = d_lsets + lsets.size();
+              J.set_words = (int32_t)lf.set.size();
+              J.card = (int32_t)std::min<int64_t>(col->cardinality, (int64_t)lf.set.size() * 32);
+              lsets.insert(lsets.end(), lf.set.begin(), lf.set.end());
+            }
+            J.out = (uint32_t*)(dev + base[b] + l * (size_t)nw);
+            J.out_words = 2 * nw;
+            if (!J.fwd) fail(PH_ERR_DEVICE, "scan leaf without a forward index");
+            lj.push_back(J);
+            max_docs = std::max(max_docs, n);
+            max_bits = std::max(max_bits, J.bits);
+          }
           for (size_t j = 0; j < ss.jobs.size(); ++j) {
             FbJob job = fb_jobs[ss.jobs[j]];
-            job.out = dev + base[b] + j * kMaxFbProgs * (size_t)nw;
+            job.out = dev + base[b];
             launch_filter_bitmaps(d_prog, d_segs, job, st);
           }
-          if (ss.kind == ST_SCANAND) {
-            ScanAndJob J{};
-            J.bits = dev + base[b];
-            J.nwords = nw;
-            J.ndocs = dsegs[ss.dseg].num_docs;
-            J.k = (int32_t)ss.leaves.size();
-            J.slot = (int32_t)sj.size();
-            sj.push_back(J);
-            sj_seg.push_back(b);
-            max_words = std::max(max_words, nw);
-          }
         }
-        std::vector<unsigned long long> out(sj.size(), 0);
-        uint32_t fbn = 0;
-        if (!sj.empty()) {
-          PH_HIP_CHECK(hipMemcpyAsync(d_jobs, sj.data(), sizeof(ScanAndJob) * sj.size(), hipMemcpyHostToDevice, st));
-          PH_HIP_CHECK(hipMemsetAsync(d_out, 0, 8 * sj.size(), st));
-          PH_HIP_CHECK(hipMemsetAsync(d_fbn, 0, 4, st));
-          launch_scan_and_entries(d_jobs, (int32_t)sj.size(), max_words, d_out, d_fb, d_fbn, kFbCap, 1 << 14, st);
-          PH_HIP_CHECK(hipMemcpyAsync(out.data(), d_out, 8 * sj.size(), hipMemcpyDeviceToHost, st));
-          PH_HIP_CHECK(hipMemcpyAsync(&fbn, d_fbn, 4, hipMemcpyDeviceToHost, st));
+        if (!lj.empty()) {
+          if (!lsets.empty())
+            PH_HIP_CHECK(hipMemcpyAsync(d_lsets, lsets.data(), 4 * lsets.size(), hipMemcpyHostToDevice, st));
+          PH_HIP_CHECK(hipMemcpyAsync(d_ljobs, lj.data(), sizeof(LeafJob) * lj.size(), hipMemcpyHostToDevice, st));
+          launch_leaf_bitmaps(d_ljobs, (int32_t)lj.size(), max_docs, max_bits, st);
         }
-        // the host side needs the simulated segments' bitmaps (and the fallback ones', below)
-        std::vector<uint64_t> h(used);
-        std::vector<char> on_host(batch.size(), 0);
-        auto fetch = [&](size_t b) {
-          const StatSeg& ss = stat_segs[batch[b]];
-          PH_HIP_CHECK(hipMemcpyAsync(h.data() + base[b], dev + base[b], 8 * seg_words(ss), hipMemcpyDeviceToHost, st));
-          on_host[b] = 1;
-        };
+        // the AND-of-scans walks: chunks of 1 << kWalkShift docs; a job whose walks did not meet runs again with
+        // chunks 32x longer (one chunk is the plain walk: always exact)
+        std::vector<size_t> walk_b;  // batch positions of the scan-AND segments
         for (size_t b = 0; b < batch.size(); ++b)
-          if (stat_segs[batch[b]].kind == ST_SIM) fetch(b);
-        PH_HIP_CHECK(hipStreamSynchronize(st));
-        for (size_t j = 0; j < sj.size(); ++j) ent[batch[sj_seg[j]]] = (int64_t)out[j];
-        // gaps the device left (longer than its step cap): exact on the host from their start; a full list means
-        // those segments are simulated whole
-        std::vector<char> redo(batch.size(), 0);
-        std::vector<unsigned long long> fb(std::min(fbn, kFbCap));
-        if (fbn) {
-          PH_HIP_CHECK(hipMemcpy(fb.data(), d_fb, 8 * fb.size(), hipMemcpyDeviceToHost));
-          for (size_t j = 0; j < sj.size(); ++j)
-            if (fbn > kFbCap) redo[sj_seg[j]] = 1;
-          for (unsigned long long e : fb) {
-            const size_t b = sj_seg[(size_t)(e >> 40)];
-            if (!on_host[b]) fetch(b);
+          if (stat_segs[batch[b]].kind == ST_SCANAND) walk_b.push_back(b);
+        std::vector<int> shift(walk_b.size(), kWalkShift);
+        std::vector<size_t> todo(walk_b.size());
+        for (size_t j = 0; j < todo.size(); ++j) todo[j] = j;
+        std::vector<unsigned long long> out(walk_b.size(), 0);
+        std::vector<uint32_t> bad(walk_b.size(), 0);
+        // the simulated segments' bitmaps go to the host (only theirs: the buffer is not touched otherwise)
+        std::vector<size_t> hbase(batch.size(), 0);
+        size_t hwords = 0;
+        for (size_t b = 0; b < batch.size(); ++b)
+          if (stat_segs[batch[b]].kind == ST_SIM) {
+            hbase[b] = hwords;
+            hwords += seg_words(stat_segs[batch[b]]);
           }
-          for (size_t b = 0; b < batch.size(); ++b)
-            if (redo[b] && !on_host[b]) fetch(b);
-          PH_HIP_CHECK(hipStreamSynchronize(st));
-          if (fbn <= kFbCap) {
-            for (unsigned long long e : fb) {
-              const size_t b = sj_seg[(size_t)(e >> 40)];
-              const StatSeg& ss = stat_segs[batch[b]];
-              const int64_t n = dsegs[ss.dseg].num_docs, nw = (n + 63) / 64;
-              std::vector<const uint64_t*> sc;
-              for (size_t l = 0; l < ss.leaves.size(); ++l) sc.push_back(h.data() + base[b] + l * (size_t)nw);
-              ent[batch[b]] += scan_and_gap_entries(sc.data(), (int)sc.size(), n, (int64_t)(e & ((1ull << 40) - 1ull)));
+        std::unique_ptr<uint64_t[]> h(hwords ? new uint64_t[hwords] : nullptr);
+        for (size_t b = 0; b < batch.size(); ++b)
+          if (stat_segs[batch[b]].kind == ST_SIM)
+            PH_HIP_CHECK(hipMemcpyAsync(h.get() + hbase[b], dev + base[b], 8 * seg_words(stat_segs[batch[b]]),
+                                        hipMemcpyDeviceToHost, st));
+        bool first = true;
+        while (!todo.empty() || first) {
+          std::vector<AndWalkJob> wj;
+          size_t rec = 0;
+          int64_t max_chunks = 0;
+          for (size_t t : todo) {
+            const StatSeg& ss = stat_segs[batch[walk_b[t]]];
+            const int64_t n = dsegs[ss.dseg].num_docs;
+            AndWalkJob J{};
+            J.bits = dev + base[walk_b[t]];
+            J.nwords = (n + 63) / 64;
+            J.ndocs = n;
+            J.k = (int32_t)ss.leaves.size();
+            J.slot = (int32_t)wj.size();
+            J.shift = shift[t];
+            J.nchunks = ((n - 1) >> J.shift) + 1;
+            J.pos = d_wpos + rec * (kWalkHead + kWalkTail);
+            J.cum = d_wcum + rec * (kWalkHead + kWalkTail);
+            J.cnt = d_wcnt + rec;
+            rec += (size_t)J.nchunks;
+            max_chunks = std::max(max_chunks, J.nchunks);
+            if (J.k < 2) fail(PH_ERR_DEVICE, "AND of fewer than two scans");
+            wj.push_back(J);
+          }
+          if (!wj.empty()) {
+            PH_HIP_CHECK(hipMemcpyAsync(d_wjobs, wj.data(), sizeof(AndWalkJob) * wj.size(), hipMemcpyHostToDevice, st));
+            PH_HIP_CHECK(hipMemsetAsync(d_out, 0, 8 * wj.size(), st));
+            PH_HIP_CHECK(hipMemsetAsync(d_bad, 0, 4 * wj.size(), st));
+            launch_and_walk(d_wjobs, (int32_t)wj.size(), max_chunks, d_out, d_bad, st);
+            std::vector<unsigned long long> o(wj.size());
+            std::vector<uint32_t> bd(wj.size());
+            PH_HIP_CHECK(hipMemcpyAsync(o.data(), d_out, 8 * wj.size(), hipMemcpyDeviceToHost, st));
+            PH_HIP_CHECK(hipMemcpyAsync(bd.data(), d_bad, 4 * wj.size(), hipMemcpyDeviceToHost, st));
+            PH_HIP_CHECK(hipStreamSynchronize(st));
+            std::vector<size_t> again;
+            for (size_t x = 0; x < todo.size(); ++x) {
+              const size_t t = todo[x];
+              if (bd[x] && wj[x].nchunks > 1) {
+                shift[t] += 5;
+                again.push_back(t);
+              } else if (bd[x]) {
+                fail(PH_ERR_DEVICE, "single-chunk AND walk did not reach the end");
+              } else {
+                out[t] = o[x];
+              }
             }
+            todo.swap(again);
+          } else {
+            PH_HIP_CHECK(hipStreamSynchronize(st));
           }
+          first = false;
         }
-        // host simulations (ST_SIM segments, and scan-AND segments to redo), on a small pool; an exception in a
-        // worker is rethrown here after the join
+        for (size_t t = 0; t < walk_b.size(); ++t) {
+          const StatSeg& ss = stat_segs[batch[walk_b[t]]];
+          ent[batch[walk_b[t]]] = dsegs[ss.dseg].num_docs - 1 + (int64_t)out[t];
+        }
+        // host simulations (ST_SIM segments), on a small pool; an exception in a worker is rethrown after the join
         std::vector<size_t> work_items;
         for (size_t b = 0; b < batch.size(); ++b)
-          if (stat_segs[batch[b]].kind == ST_SIM || redo[b]) work_items.push_back(b);
+          if (stat_segs[batch[b]].kind == ST_SIM) work_items.push_back(b);
         std::atomic<size_t> next_item{0};
         std::vector<std::exception_ptr> errs;
         std::mutex err_mu;
@@ -2572,7 +2644,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
               const StatSeg& ss = stat_segs[batch[b]];
               const int64_t n = dsegs[ss.dseg].num_docs, nw = (n + 63) / 64;
               std::vector<SimLeaf> lv(ss.leaves.size());
-              for (size_t l = 0; l < lv.size(); ++l) lv[l] = {ss.leaf_kinds[l], h.data() + base[b] + l * (size_t)nw};
+              for (size_t l = 0; l < lv.size(); ++l) lv[l] = {ss.leaf_kinds[l], h.get() + hbase[b] + l * (size_t)nw};
               ent[batch[b]] = simulate_filter_entries(ss.root, lv, n);
             }
           } catch (...) {

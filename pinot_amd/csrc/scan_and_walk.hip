@@ -1,0 +1,60 @@
+// scan_and_walk.hip -- numEntriesScannedInFilter of an AND of SV scans only, as chunked walks of the AND's leap-frog.
+//
+// AndDocIdSet.iterator returns AndDocIdIterator(scan_1 .. scan_k) for such an AND (AndDocIdSet.java:180-183), and
+// DocIdSetOperator drains it with next().  AndDocIdIterator.next() (AndDocIdIterator.java:40-67) keeps a candidate M
+// (maxDocId) and calls advance(M) on the scans in order, skipping the one that set M; a scan's advance(t)
+// (SVScanDocIdIterator.java:101-112) examines the docs t .. its next match (or the rest of the segment at EOF).  So one
+// "epoch" at candidate M that the scan j set (j = -1 right after a match, or at the start) costs
+//   calls(M, j) = f + 1 - [0 <= j < f]   advance() calls, f = the first scan without M, and moves M to scan f's next
+//                                        match after M (or ends the segment: that call returns EOF);
+//   calls(M, j) = k - [j >= 0]           when every scan has M (a match): the next epoch is M + 1 with j = -1;
+//   1                                    for M = numDocs (scan 1's advance returns EOF at once),
+// and the docs the calls examine telescope to  entries = numDocs - |matches| + calls - 1  =  numDocs - 1 + sum over the
+// epochs of (calls - [match]).  The candidate sequence M_0 = 0, M_1, ... is a walk whose next step depends on M only
+// (f and the next match do; the setter only changes an epoch's call count), so two walks that meet at one candidate
+// agree from there on.  That makes the sum parallel:
+//   k_and_walk   -- walker c starts a fresh epoch at doc c * L (one thread per chunk of L docs) and logs its first
+//                   kWalkHead candidates and the first kWalkTail candidates at or past the next chunk (each with its running
+//                   sum, the epoch included), stopping there or at the end (candidate numDocs);
+//   k_and_merge  -- the true walk (walker 0's) meets walker c at q_c = the first candidate of walker c-1's tail log
+//                   that walker c's head log holds; walker c owns the true epochs after q_c up to q_{c+1}:
+//                   sum = cum_0(q_1) + sum_c (cum_c(q_{c+1}) - cum_c(q_c)).  A chunk whose walks do not meet inside the
+//                   logs (or meet out of order) marks the job: the host reruns it with L x 32 (L >= numDocs is one
+//                   walker: always exact).
+// Algorithmic bytes: the k leaf bitmaps (k * numDocs / 8), read once per walk plus the logs; the host checks these
+// sums against the iterator simulation in the parity tests (filter_sim.cpp, oracle.filter_entries).
+#include "ph_internal.h"
+
+namespace ph {
+
+__global__ void __launch_bounds__(256) k_and_walk(const AndWalkJob* __restrict__ jobs) {
+  const AndWalkJob J = jobs[blockIdx.y];
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c < J.nchunks) and_walk_chunk(J, c);
+}
+
+__global__ void __launch_bounds__(256) k_and_merge(const AndWalkJob* __restrict__ jobs, unsigned long long* out,
+                                                   uint32_t* bad) {
+  const AndWalkJob J = jobs[blockIdx.y];
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  unsigned long long part = 0;
+  const bool fail = c < J.nchunks && !and_merge_chunk(J, c, part);
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+  const unsigned long long anyfail = __ballot(fail);
+  if ((threadIdx.x & 63) == 0) {
+    if (part) atomicAdd(out + J.slot, part);
+    if (anyfail) atomicOr(bad + J.slot, 1u);
+  }
+}
+
+void launch_and_walk(const AndWalkJob* jobs, int32_t njobs, int64_t max_chunks, unsigned long long* out, uint32_t* bad,
+                     hipStream_t s) {
+  if (njobs <= 0 || max_chunks <= 0) return;
+  const dim3 grid((unsigned)((max_chunks + 255) / 256), (unsigned)njobs);
+  hipLaunchKernelGGL(k_and_walk, grid, dim3(256), 0, s, jobs);
+  PH_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_and_merge, grid, dim3(256), 0, s, jobs, out, bad);
+  PH_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace ph

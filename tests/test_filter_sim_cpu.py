@@ -2,7 +2,10 @@
 through the test hook phx_filter_entries_sim; the product calls it for filter shapes without a device pass) is checked
 against the oracle's restatement of the reference iterators (oracle.filter_entries_of) on random filter trees and doc
 sets, and the oracle's restatement against a fully literal variant (every next() batch by batch, no drain shortcut).
-The device-side pass for ANDs of scans (k_scan_and_entries) is checked on the GPU (test_gpu_parity.py)."""
+ANDs of scans only are summed by chunked walks of the leap-frog (and_walk.h: k_and_walk / k_and_merge on the device);
+the same walks run on the host through phx_and_walk_entries and are checked against the simulation here, at chunk
+sizes down to 64 docs (where the walks often fail to meet and the pass must say so: -1), and on the GPU in
+test_gpu_parity.py."""
 import ctypes
 
 import numpy as np
@@ -62,6 +65,21 @@ def _flatten(root):
     return np.array(out, dtype=np.int32).ravel()
 
 
+def _bitmap(d, n):
+    nw = (n + 63) // 64
+    padded = np.zeros(nw * 64, bool)
+    padded[:n] = d
+    return np.packbits(padded.reshape(-1, 8)[:, ::-1], axis=1).ravel().view(np.uint64).copy()
+
+
+def _walk(docs, n, shift):
+    f = N.lib().phx_and_walk_entries
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32]
+    bits = np.concatenate([_bitmap(d, n) for d in docs])
+    return f(bits.ctypes.data, len(docs), n, shift)
+
+
 def _native_sim(root, leaves, docs, n):
     L = N.lib()
     f = L.phx_filter_entries_sim
@@ -69,12 +87,7 @@ def _native_sim(root, leaves, docs, n):
     f.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64]
     flat = _flatten(root)
     kinds = np.array([KINDS[l.ikind] for l in leaves], dtype=np.int32)
-    nw = (n + 63) // 64
-    bits = []
-    for d in docs:
-        padded = np.zeros(nw * 64, bool)
-        padded[:n] = d
-        bits.append(np.packbits(padded.reshape(-1, 8)[:, ::-1], axis=1).ravel().view(np.uint64).copy())
+    bits = [_bitmap(d, n) for d in docs]
     ptrs = (ctypes.c_void_p * len(bits))(*[b.ctypes.data for b in bits])
     return f(flat.ctypes.data, len(flat) // 5, kinds.ctypes.data, ptrs, len(bits), n)
 
@@ -144,3 +157,44 @@ def test_scan_and_closed_cases():
     # next() #3 from 8: a.adv(8) -> EOF [2 docs: 8, 9]
     assert O.filter_entries_of(root, n, lambda x: [a, b][x.col_index]) == 3 + 4 + 1 + 2 + 1 + 2
     assert _native_sim(root, [la, lb], [a, b], n) == 13
+    assert _walk([a, b], n, 30) == 13
+    assert _walk([a, b], n, 2) in (13, -1)
+
+
+def _scan_and(k):
+    root = O._Leaf("and")
+    leaves = []
+    for i in range(k):
+        leaf = O._Leaf("leaf", i, None, True)
+        leaf.ikind = "scan"
+        leaves.append(leaf)
+    root.children = leaves
+    return root, leaves
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_and_walk_matches_simulation(seed):
+    rng = np.random.default_rng(3000 + seed)
+    n = int(rng.choice([1, 2, 64, 65, 4095, 4097, 20_000, 70_001]))
+    k = int(rng.integers(2, 6))
+    dens = rng.choice([0.003, 0.02, 0.15, 0.5, 0.9, 1.0], size=k)
+    docs = [rng.random(n) < d for d in dens]
+    root, leaves = _scan_and(k)
+    exp = _native_sim(root, leaves, docs, n)
+    assert exp == O.filter_entries_of(root, n, lambda x: docs[x.col_index])
+    assert _walk(docs, n, 31) == exp  # one chunk: the plain walk
+    for shift in (6, 8, 10, 12):
+        got = _walk(docs, n, shift)
+        assert got in (exp, -1), (seed, shift, got, exp)
+
+
+def test_and_walk_meets_at_bench_densities():
+    # SSB-like densities at the product's 4096-doc chunks: the walks meet (no rerun), and the sum is exact
+    rng = np.random.default_rng(7)
+    n = 200_000
+    for dens in ([1 / 7, 3 / 11, 0.48], [1 / 84, 3 / 11, 0.2], [2 / 250, 2 / 250, 6 / 7], [1 / 25, 1 / 5],
+                 [5e-4, 0.5], [1e-5, 0.5, 0.5], [0.5, 1e-5]):
+        docs = [rng.random(n) < d for d in dens]
+        root, leaves = _scan_and(len(dens))
+        exp = _native_sim(root, leaves, docs, n)
+        assert _walk(docs, n, 12) == exp, dens
