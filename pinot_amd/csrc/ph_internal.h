@@ -86,6 +86,7 @@ enum : int32_t { FK_ALL = 0, FK_RANGE = 1, FK_SET = 2, FK_BITMAP = 3, FK_DOCRANG
 // from the staged tile like a single leaf instead of gathered per doc by the generic program
 constexpr int kMaxConj = 4;
 constexpr int kSparseBitmaps = 6;  // k_group_sparse: inverted-index doc bitmaps per segment filter
+constexpr int kConjSetWords = 256;  // conj_reg.h: a set leaf of <= 8192 dictIds is staged in LDS per chunk
 
 // How an aggregated numeric column is read:
 //   VK_PACKED   frame-of-reference stream (value - base) in `bits`, built once per column in HBM from the
@@ -172,7 +173,8 @@ struct DevSegment {
   // scan leaves (dictId range [sp_lo, sp_lo + sp_len) or bitset sp_set) on column slot sp_slot, evaluated per
   // matched doc by gathers; sp_stats: the AND is an applyAnd one (numEntriesScannedInFilter).  The segment keeps
   // its generic program (fkind) for the numGroupsLimit passes.
-  int32_t sp_nbm, sp_nscan, sp_stats, sp_pad;
+  int32_t sp_nbm, sp_nscan, sp_stats;
+  int32_t sp_reg;  // no bitmaps: the sp scan leaves are evaluated register-direct per wave step (conj_reg.h)
   const uint32_t* sp_bm[kSparseBitmaps];
   int32_t sp_or[kSparseBitmaps];     // bitmap k ORs into bitmap k - 1's group (an OR of inverted leaves)
   int32_t sp_slot[kMaxConj];
@@ -273,6 +275,7 @@ struct KParams {
   int32_t part_dbg;               // lean kernel A timing experiments (PH_PART_DBG; results invalid when set)
   int32_t agg_fast;               // MODE_AGG: run k_agg_lean
   int32_t agg_sparse;             // MODE_AGG over selective bitmap leaves: run k_agg_sparse
+  int32_t sparse_c;               // sparse kernels over sp_reg segments: 16-byte loads per lane of a leaf (4 or 8)
   int32_t lds_fast;               // MODE_GROUP_LDS: run k_group_lds_lean
   int32_t lds_pack;               //   COUNT << 40 | SUM in one 64-bit LDS word
   int32_t lds_copies;             //   table copies (one per wave when they fit)
@@ -499,6 +502,7 @@ struct Lane {
   hipStream_t stream_b = nullptr;
   hipEvent_t ev_start = nullptr, ev_stop = nullptr;
   hipEvent_t ev_bm0 = nullptr, ev_bm1 = nullptr;  // around the inverted-leaf bitmap build (part of device_ms)
+  hipEvent_t ev_uploaded = nullptr;  // the call's segment descriptors and programs are in HBM (statistics pass)
   std::vector<hipEvent_t> ev_pool;
   void* staging[2] = {nullptr, nullptr};  // slot 0: launch parameters; slot 1: the bitmap build's work items
   size_t staging_bytes[2] = {0, 0};
@@ -640,8 +644,8 @@ struct FbJob {
 void launch_filter_bitmaps(const FilterInsn* prog, const DevSegment* segs, const FbJob& job, hipStream_t s);
 // numEntriesScannedInFilter of ANDs of scans: chunked walks of the leap-frog (and_walk.h, scan_and_walk.hip); the
 // device adds each job's sum of (calls - [match]) into out[slot] and flags bad[slot] when its walks did not meet
-void launch_and_walk(const AndWalkJob* jobs, int32_t njobs, int64_t max_chunks, unsigned long long* out, uint32_t* bad,
-                     hipStream_t s);
+void launch_and_walk(const AndWalkJob* jobs, int32_t njobs, int64_t max_chunks, int32_t max_k, unsigned long long* out,
+                     uint32_t* bad, hipStream_t s);
 // the same walks on the host (CPU tests): the entries, or -1 when the chunks of 1 << shift docs do not meet
 int64_t and_walk_entries_host(const uint64_t* bits, int k, int64_t num_docs, int shift);
 // the doc bitmap of a dictId scan leaf (leaf_bitmaps.hip): RANGE [lo, lo + len) or, with `set`, a dictId bitset over

@@ -628,7 +628,9 @@ SparseShape sparse_shape(const PNode& r) {
   }
   size_t nbm = 0;
   for (auto& g : sh.groups) nbm += g.size();
-  sh.ok = !sh.groups.empty() && nbm <= (size_t)kSparseBitmaps && (int)sh.scans.size() <= kMaxConj;
+  // no bitmaps: an AND of >= 2 scan leaves, evaluated register-direct by the sparse kernels (conj_reg.h)
+  sh.ok = nbm <= (size_t)kSparseBitmaps && (int)sh.scans.size() <= kMaxConj &&
+          (!sh.groups.empty() || sh.scans.size() >= 2);
   return sh;
 }
 
@@ -1627,6 +1629,30 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     sparse_plan = ok && docs > 0 && hits * 8 < docs;
     if (const char* e = getenv("PH_GROUP_SPARSE")) sparse_plan = ok && docs > 0 && atoi(e) != 0;  // tuning knob
   }
+  // k_agg_sparse over ANDs of scan leaves only (register-direct leaves, then gathers of the matched docs' values):
+  // aggregation-only queries whose every segment's AND keeps < 1/8 of the docs (same estimate as above)
+  bool agg_conj = false;
+  if (mode == MODE_AGG && nvals >= 1 && (nvals == 1 || std::none_of(val_exprs.begin(), val_exprs.end(), [](int x) { return x != 0; }))) {
+    bool ok = true;
+    double docs = 0, hits = 0;
+    for (int i = 0; i < nseg && ok; ++i) {
+      if (!seg_live[i]) continue;
+      const SparseShape sh = sparse_shape(roots[i]);
+      ok = sh.ok && sh.groups.empty();
+      double est = (double)std::max<int64_t>(1, segs[i]->num_docs);
+      for (const PNode* k : sh.scans) {
+        const double card = (double)std::max<int64_t>(1, segs[i]->columns.at(slot_names[k->col])->cardinality);
+        double ids = k->op == OP_RANGE ? (double)k->len : 0.0;
+        if (k->op == OP_SET)
+          for (uint32_t w : k->set) ids += (double)__builtin_popcount(w);
+        est *= std::min(1.0, ids / card);
+      }
+      hits += ok ? est : 0;
+      docs += (double)segs[i]->num_docs;
+    }
+    agg_conj = ok && docs > 0 && hits * 8 < docs;
+    if (const char* e = getenv("PH_AGG_SPARSE")) agg_conj = ok && docs > 0 && atoi(e) != 0;  // tuning knob
+  }
   std::vector<std::pair<int32_t, int32_t>> dseg_chunks;                // device segment -> its chunk range
   std::vector<int> dseg_src;                                           // device segment -> query segment index
   std::vector<std::pair<int32_t, int32_t>> seg_words;                  // device segment -> [first, end) words to scan
@@ -1715,8 +1741,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         all_insns.insert(all_insns.end(), sp.insns.begin(), sp.insns.end());
       }
     }
-    if (sparse_plan) {
+    if (sparse_plan || agg_conj) {
       const SparseShape sh = sparse_shape(root);
+      d.sp_reg = sh.groups.empty() ? 1 : 0;
       d.sp_nbm = 0;
       for (auto& g : sh.groups)
         for (size_t j = 0; j < g.size(); ++j) {
@@ -1937,10 +1964,16 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       for (auto& d : dsegs) docs += d.num_docs;
       for (auto& fb : fbitmap_fix) hits += bitmap_docs(*pl.bitmaps[fb.second].col, pl.bitmaps[fb.second].dict_ids);
     }
-    kp.agg_sparse = all_bitmap && hits * 8 < docs;
-    if (const char* e = getenv("PH_AGG_SPARSE")) kp.agg_sparse = all_bitmap && atoi(e) != 0;  // tuning knob
+    kp.agg_sparse = (all_bitmap && hits * 8 < docs) || agg_conj;
+    if (const char* e = getenv("PH_AGG_SPARSE")) kp.agg_sparse = (all_bitmap || agg_conj) && atoi(e) != 0;  // tuning knob
     if (kp.agg_sparse) kp.agg_fast = 0;
   }
+  // the register-direct leaves' loads per lane (conj_reg.h): by the widest scan column of an sp_reg segment
+  // (0: none has them)
+  kp.sparse_c = 0;
+  for (auto& d : dsegs)
+    for (int k = 0; d.sp_reg && k < d.sp_nscan; ++k)
+      kp.sparse_c = std::max(kp.sparse_c, d.cols[d.sp_slot[k]].bits > 16 ? 8 : 4);
   // the register-direct COUNT (k_count_reg): every segment a dictId RANGE scan leaf, everything, or a sorted range
   if (mode == MODE_COUNT && !kp.late_prefetch && getenv("PH_COUNT_GENERIC") == nullptr) {
     int fb = 1;
@@ -2039,7 +2072,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     if (sparse_plan) {  // the generic tables (LDS table or group cache) + one matched-doc list per wave
       kp.pl_misc_off = (int32_t)((stage_bytes + lds_tables + 15) / 16 * 16);  // after the generic layout
-      const size_t l2 = (size_t)kp.pl_misc_off + (size_t)kWaves * kSparseStepWords * 64 * sizeof(uint16_t);
+      // + the staged scan-leaf sets when a segment has register-direct leaves (4 KiB: it can cost a bitmap-only
+      // plan its LDS fit)
+      const size_t l2 = (size_t)kp.pl_misc_off + (size_t)kWaves * kSparseStepWords * 64 * sizeof(uint16_t) +
+                        (kp.sparse_c ? (size_t)kMaxConj * kConjSetWords * sizeof(uint32_t) : 0);
       if (l2 <= 160 * 1024) {
         kp.group_sparse = 1;
         kp.group_reg = 0;
@@ -2049,36 +2085,40 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if (kp.agg_sparse) {  // no staging: the HLL registers and one matched-doc list (uint16 offsets) per wave
       kp.lds_hll_off = 0;
       kp.pl_misc_off = (int32_t)(((size_t)num_hll * (m ? m : 1) * 4 + 16 + 15) / 16 * 16);
-      lds = (size_t)kp.pl_misc_off + (size_t)kWaves * kSparseStepWords * 64 * sizeof(uint16_t);
+      lds = (size_t)kp.pl_misc_off + (size_t)kWaves * kSparseStepWords * 64 * sizeof(uint16_t) +
+            (kp.sparse_c ? (size_t)kMaxConj * kConjSetWords * sizeof(uint32_t) : 0);
     }
     // 160 KiB of LDS per CU (gfx950); HLL registers of a large log2m do not fit beside the staging areas
     if (lds > 160 * 1024) fail(PH_ERR_UNSUPPORTED, "aggregation state exceeds the LDS of one CU (HLL log2m too large)");
   }
-  for (auto& pf : payload_fix) {
-    uint32_t* dp = scratch.alloc<uint32_t>(pf.second.size() + 1);
-    PH_HIP_CHECK(hipMemcpyAsync(dp, pf.second.data(), 4 * pf.second.size(), hipMemcpyHostToDevice, st));
-    all_insns[pf.first].ptr = dp;
+  // every predicate payload (program sets / ranges, FK_SET / FK_CONJ / sparse-leaf bitsets) in ONE upload: r4 issued
+  // one small copy per payload (SSB Q3.3 on 60 segments: 120 copies, ~1 ms of setup)
+  {
+    std::vector<uint32_t> blob;
+    std::vector<size_t> at;
+    auto put = [&](const std::vector<uint32_t>& w) {
+      at.push_back(blob.size());
+      blob.insert(blob.end(), w.begin(), w.end());
+      blob.resize((blob.size() + 4) & ~(size_t)3, 0u);  // >= 1 word of pad, 16-byte aligned starts
+    };
+    for (auto& pf : payload_fix) put(pf.second);
+    for (auto& ff : fset_fix) put(ff.second);
+    for (auto& sf : sset_fix) put(sf.second);
+    for (auto& cf : conj_set_fix) put(cf.second);
+    if (!blob.empty()) {
+      uint32_t* dblob = scratch.alloc<uint32_t>(blob.size());
+      PH_HIP_CHECK(hipMemcpyAsync(dblob, blob.data(), 4 * blob.size(), hipMemcpyHostToDevice, st));
+      size_t i = 0;
+      for (auto& pf : payload_fix) all_insns[pf.first].ptr = dblob + at[i++];
+      for (auto& ff : fset_fix) dsegs[ff.first].fptr = dblob + at[i++];
+      for (auto& sf : sset_fix) dsegs[sf.first / kMaxConj].sp_set[sf.first % kMaxConj] = dblob + at[i++];
+      for (auto& cf : conj_set_fix) dsegs[cf.first / kMaxConj].cset[cf.first % kMaxConj] = dblob + at[i++];
+      PH_HIP_CHECK(hipStreamSynchronize(st));  // the pageable copy
+    }
   }
   for (auto& bf : bitmap_fix) all_insns[bf.first].ptr = bitmap_dev[bf.second];
-  for (auto& ff : fset_fix) {
-    uint32_t* dp = scratch.alloc<uint32_t>(ff.second.size() + 1);
-    PH_HIP_CHECK(hipMemcpyAsync(dp, ff.second.data(), 4 * ff.second.size(), hipMemcpyHostToDevice, st));
-    dsegs[ff.first].fptr = dp;
-  }
   for (auto& fb : fbitmap_fix) dsegs[fb.first].fptr = bitmap_dev[fb.second];
   for (auto& sb : sbm_fix) dsegs[sb.first / kSparseBitmaps].sp_bm[sb.first % kSparseBitmaps] = bitmap_dev[sb.second];
-  for (auto& sf : sset_fix) {
-    uint32_t* dp = scratch.alloc<uint32_t>(sf.second.size() + 1);
-    PH_HIP_CHECK(hipMemcpyAsync(dp, sf.second.data(), 4 * sf.second.size(), hipMemcpyHostToDevice, st));
-    dsegs[sf.first / kMaxConj].sp_set[sf.first % kMaxConj] = dp;
-  }
-  for (auto& cf : conj_set_fix) {
-    uint32_t* dp = scratch.alloc<uint32_t>(cf.second.size() + 1);
-    PH_HIP_CHECK(hipMemcpyAsync(dp, cf.second.data(), 4 * cf.second.size(), hipMemcpyHostToDevice, st));
-    dsegs[cf.first / kMaxConj].cset[cf.first % kMaxConj] = dp;
-  }
-  if (!payload_fix.empty() || !fset_fix.empty() || !conj_set_fix.empty() || !sset_fix.empty())
-    PH_HIP_CHECK(hipStreamSynchronize(st));  // pageable copies above
   // the optimistic numGroupsLimit scan's segment table: no keep bitsets, no first-doc tables (copied after every
   // device pointer above is fixed up: r3 copied it before, so FK_CONJ set leaves scanned with null bitsets)
   std::vector<DevSegment> dsegs_opt;
@@ -2109,6 +2149,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if (b2) PH_HIP_CHECK(hipMemcpyAsync(d_prog, stage + b1, b2, hipMemcpyHostToDevice, st));
     PH_HIP_CHECK(hipMemcpyAsync(d_chunks, stage + b1 + b2, b3, hipMemcpyHostToDevice, st));
     if (b4) PH_HIP_CHECK(hipMemcpyAsync(d_segs_opt, stage + b1 + b2 + b3, b4, hipMemcpyHostToDevice, st));
+    PH_HIP_CHECK(hipEventRecord(lane.lane->ev_uploaded, st));  // the statistics pass (stream b) starts here
     kp.segs = d_segs;
     kp.prog = d_prog;
     kp.chunks = d_chunks;
@@ -2456,13 +2497,16 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       PH_HIP_CHECK(hipStreamWaitEvent(st, L.event(2 * batches.size() + 1), 0));
       PH_HIP_CHECK(hipEventRecord(L.ev_stop, st));
     }
-    // numEntriesScannedInFilter of the ST_SCANAND / ST_SIM segments (a statistics pass after the scan's device-time
-    // window): the leaves' doc bitmaps (k_leaf_bitmaps from the forward indexes, k_filter_bitmaps for the rest), then
+    // numEntriesScannedInFilter of the ST_SCANAND / ST_SIM segments (a statistics pass on the second stream, after
+    // the scan's device-time window and overlapping its kernels: it reads only the forward indexes): the leaves' doc
+    // bitmaps (k_leaf_bitmaps from the forward indexes, k_filter_bitmaps for the rest), then
     // the chunked walks of the AND-of-scans leap-frog on the device (k_and_walk) or the iterator simulation on the
     // host, in batches of segments bounded to kStatBatchWords words of bitmaps
     if (!stat_segs.empty()) {
+      hipStream_t sb = lane.lane->stream_b;
+      PH_HIP_CHECK(hipStreamWaitEvent(sb, lane.lane->ev_uploaded, 0));
       constexpr size_t kStatBatchWords = (size_t)32 << 20;  // 256 MiB
-      constexpr int kWalkShift = 12;                        // 4096-doc walks
+      constexpr int kWalkShift = 10;                        // 1024-doc walks (tests/test_filter_sim_cpu.py: they meet)
       auto seg_words = [&](const StatSeg& ss) {
         return ss.leaves.size() * (size_t)((dsegs[ss.dseg].num_docs + 63) / 64);
       };
@@ -2542,14 +2586,14 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           for (size_t j = 0; j < ss.jobs.size(); ++j) {
             FbJob job = fb_jobs[ss.jobs[j]];
             job.out = dev + base[b];
-            launch_filter_bitmaps(d_prog, d_segs, job, st);
+            launch_filter_bitmaps(d_prog, d_segs, job, sb);
           }
         }
         if (!lj.empty()) {
           if (!lsets.empty())
-            PH_HIP_CHECK(hipMemcpyAsync(d_lsets, lsets.data(), 4 * lsets.size(), hipMemcpyHostToDevice, st));
-          PH_HIP_CHECK(hipMemcpyAsync(d_ljobs, lj.data(), sizeof(LeafJob) * lj.size(), hipMemcpyHostToDevice, st));
-          launch_leaf_bitmaps(d_ljobs, (int32_t)lj.size(), max_docs, max_bits, st);
+            PH_HIP_CHECK(hipMemcpyAsync(d_lsets, lsets.data(), 4 * lsets.size(), hipMemcpyHostToDevice, sb));
+          PH_HIP_CHECK(hipMemcpyAsync(d_ljobs, lj.data(), sizeof(LeafJob) * lj.size(), hipMemcpyHostToDevice, sb));
+          launch_leaf_bitmaps(d_ljobs, (int32_t)lj.size(), max_docs, max_bits, sb);
         }
         // the AND-of-scans walks: chunks of 1 << kWalkShift docs; a job whose walks did not meet runs again with
         // chunks 32x longer (one chunk is the plain walk: always exact)
@@ -2573,12 +2617,13 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         for (size_t b = 0; b < batch.size(); ++b)
           if (stat_segs[batch[b]].kind == ST_SIM)
             PH_HIP_CHECK(hipMemcpyAsync(h.get() + hbase[b], dev + base[b], 8 * seg_words(stat_segs[batch[b]]),
-                                        hipMemcpyDeviceToHost, st));
+                                        hipMemcpyDeviceToHost, sb));
         bool first = true;
         while (!todo.empty() || first) {
           std::vector<AndWalkJob> wj;
           size_t rec = 0;
           int64_t max_chunks = 0;
+          int32_t max_k = 0;
           for (size_t t : todo) {
             const StatSeg& ss = stat_segs[batch[walk_b[t]]];
             const int64_t n = dsegs[ss.dseg].num_docs;
@@ -2595,20 +2640,28 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
             J.cnt = d_wcnt + rec;
             rec += (size_t)J.nchunks;
             max_chunks = std::max(max_chunks, J.nchunks);
+            max_k = std::max(max_k, J.k);
             if (J.k < 2) fail(PH_ERR_DEVICE, "AND of fewer than two scans");
             wj.push_back(J);
           }
           if (!wj.empty()) {
-            PH_HIP_CHECK(hipMemcpyAsync(d_wjobs, wj.data(), sizeof(AndWalkJob) * wj.size(), hipMemcpyHostToDevice, st));
-            PH_HIP_CHECK(hipMemsetAsync(d_out, 0, 8 * wj.size(), st));
-            PH_HIP_CHECK(hipMemsetAsync(d_bad, 0, 4 * wj.size(), st));
-            launch_and_walk(d_wjobs, (int32_t)wj.size(), max_chunks, d_out, d_bad, st);
+            PH_HIP_CHECK(hipMemcpyAsync(d_wjobs, wj.data(), sizeof(AndWalkJob) * wj.size(), hipMemcpyHostToDevice, sb));
+            PH_HIP_CHECK(hipMemsetAsync(d_out, 0, 8 * wj.size(), sb));
+            PH_HIP_CHECK(hipMemsetAsync(d_bad, 0, 4 * wj.size(), sb));
+            launch_and_walk(d_wjobs, (int32_t)wj.size(), max_chunks, max_k, d_out, d_bad, sb);
             std::vector<unsigned long long> o(wj.size());
             std::vector<uint32_t> bd(wj.size());
-            PH_HIP_CHECK(hipMemcpyAsync(o.data(), d_out, 8 * wj.size(), hipMemcpyDeviceToHost, st));
-            PH_HIP_CHECK(hipMemcpyAsync(bd.data(), d_bad, 4 * wj.size(), hipMemcpyDeviceToHost, st));
-            PH_HIP_CHECK(hipStreamSynchronize(st));
+            PH_HIP_CHECK(hipMemcpyAsync(o.data(), d_out, 8 * wj.size(), hipMemcpyDeviceToHost, sb));
+            PH_HIP_CHECK(hipMemcpyAsync(bd.data(), d_bad, 4 * wj.size(), hipMemcpyDeviceToHost, sb));
+            PH_HIP_CHECK(hipStreamSynchronize(sb));
             std::vector<size_t> again;
+            if (host_times) {
+              size_t nb = 0;
+              for (uint32_t v : bd) nb += v != 0;
+              fprintf(stderr, "[ph host] stat walk: %zu jobs at shift %d (first), %zu did not meet\n", wj.size(),
+                      wj.empty() ? 0 : wj[0].shift, nb);
+            }
+            stamp("stat walk");
             for (size_t x = 0; x < todo.size(); ++x) {
               const size_t t = todo[x];
               if (bd[x] && wj[x].nchunks > 1) {
@@ -2622,7 +2675,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
             }
             todo.swap(again);
           } else {
-            PH_HIP_CHECK(hipStreamSynchronize(st));
+            PH_HIP_CHECK(hipStreamSynchronize(sb));
           }
           first = false;
         }
@@ -2630,6 +2683,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           const StatSeg& ss = stat_segs[batch[walk_b[t]]];
           ent[batch[walk_b[t]]] = dsegs[ss.dseg].num_docs - 1 + (int64_t)out[t];
         }
+        stamp("stat walks");
         // host simulations (ST_SIM segments), on a small pool; an exception in a worker is rethrown after the join
         std::vector<size_t> work_items;
         for (size_t b = 0; b < batch.size(); ++b)
@@ -2660,6 +2714,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         if (!errs.empty()) std::rethrow_exception(errs.front());
       }
       for (int64_t e : ent) stats.num_entries_scanned_in_filter += e;
+      stamp("stat pass");
     }
     stamp("launched");
     timed = true;

@@ -27,10 +27,84 @@
 
 namespace ph {
 
+// and_walk_chunk with the k leaves' words of the walk's current 64-doc word held in registers: a step inside the word
+// is register work (the first scan without M, the next match of scan f), and the k words are loaded again only when
+// the candidate leaves the word.  Up to K leaves (the padding leaves read as all-ones, so they never fail); the logs
+// are the same as and_walk_chunk's (the host version the CPU tests run).
+template <int K>
 __global__ void __launch_bounds__(256) k_and_walk(const AndWalkJob* __restrict__ jobs) {
   const AndWalkJob J = jobs[blockIdx.y];
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (c < J.nchunks) and_walk_chunk(J, c);
+  if (c >= J.nchunks) return;
+  const int64_t N = J.ndocs, nwords = J.nwords;
+  const int k = J.k;
+  const int64_t rec = kWalkHead + kWalkTail;
+  int32_t* hpos = J.pos + c * rec;
+  int32_t* tpos = hpos + kWalkHead;
+  unsigned long long* hcum = J.cum + c * rec;
+  unsigned long long* tcum = hcum + kWalkHead;
+  const int64_t end = (c + 1) << J.shift;
+  const int64_t thr = end < N ? end : N;
+  int64_t M = c << J.shift;
+  int j = -1, hn = 0, tn = 0;
+  unsigned long long cum = 0;
+  unsigned long long W[K];
+  int64_t cw = M >> 6;
+  auto load = [&](int64_t w) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) W[i] = i < k ? J.bits[(int64_t)i * nwords + w] : ~0ull;
+  };
+  if (M < N) load(cw);
+  for (;;) {
+    bool term = false;
+    int64_t nxt = 0;
+    int jn = -1;
+    if (M >= N) {
+      cum += 1;
+      term = true;
+    } else {
+      const int b = (int)(M & 63);
+      int f = K;
+#pragma unroll
+      for (int i = K - 1; i >= 0; --i)
+        if (!((W[i] >> b) & 1ull)) f = i;
+      if (f == K) {
+        cum += (unsigned long long)(k - 1 - (j >= 0 ? 1 : 0));
+        nxt = M + 1;
+      } else {
+        cum += (unsigned long long)(f + 1 - ((j >= 0 && j < f) ? 1 : 0));
+        unsigned long long v = 0;
+#pragma unroll
+        for (int i = 0; i < K; ++i) v = i == f ? W[i] : v;
+        v &= ~0ull << b;
+        int64_t wi = cw;
+        const unsigned long long* bf = J.bits + (int64_t)f * nwords;
+        while (!v && ++wi < nwords) v = bf[wi];
+        nxt = v ? wi * 64 + __builtin_ctzll(v) : N;
+        term = nxt >= N;
+        jn = f;
+      }
+    }
+    const int32_t P = term ? (int32_t)N : (int32_t)M;
+    if (hn < kWalkHead) {
+      hpos[hn] = P;
+      hcum[hn] = cum;
+      ++hn;
+    }
+    if (P >= thr) {
+      tpos[tn] = P;
+      tcum[tn] = cum;
+      ++tn;
+    }
+    if (term || tn == kWalkTail) break;
+    M = nxt;
+    j = jn;
+    if ((M >> 6) != cw && M < N) {
+      cw = M >> 6;
+      load(cw);
+    }
+  }
+  J.cnt[c] = (uint32_t)hn | ((uint32_t)tn << 16);
 }
 
 __global__ void __launch_bounds__(256) k_and_merge(const AndWalkJob* __restrict__ jobs, unsigned long long* out,
@@ -47,11 +121,15 @@ __global__ void __launch_bounds__(256) k_and_merge(const AndWalkJob* __restrict_
   }
 }
 
-void launch_and_walk(const AndWalkJob* jobs, int32_t njobs, int64_t max_chunks, unsigned long long* out, uint32_t* bad,
-                     hipStream_t s) {
+void launch_and_walk(const AndWalkJob* jobs, int32_t njobs, int64_t max_chunks, int32_t max_k, unsigned long long* out,
+                     uint32_t* bad, hipStream_t s) {
   if (njobs <= 0 || max_chunks <= 0) return;
+  if (max_k > kMaxFbProgs) fail(PH_ERR_DEVICE, "AND walk wider than kMaxFbProgs scans");
   const dim3 grid((unsigned)((max_chunks + 255) / 256), (unsigned)njobs);
-  hipLaunchKernelGGL(k_and_walk, grid, dim3(256), 0, s, jobs);
+  // the widest AND of the launch picks the register set (ST_SCANAND: at most kMaxFbProgs scans)
+  if (max_k <= 4) hipLaunchKernelGGL(k_and_walk<4>, grid, dim3(256), 0, s, jobs);
+  else if (max_k <= 8) hipLaunchKernelGGL(k_and_walk<8>, grid, dim3(256), 0, s, jobs);
+  else hipLaunchKernelGGL(k_and_walk<kMaxFbProgs>, grid, dim3(256), 0, s, jobs);
   PH_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_and_merge, grid, dim3(256), 0, s, jobs, out, bad);
   PH_HIP_CHECK(hipGetLastError());

@@ -1,6 +1,7 @@
 // scan_count.hip -- k_scan instantiations of the aggregation-only plans (MODE_COUNT, MODE_AGG), and the lean
 // aggregation kernel k_agg_lean.
 #include "scan_kernel.h"
+#include "conj_reg.h"
 
 namespace ph {
 
@@ -177,7 +178,11 @@ __global__ void __launch_bounds__(kBlock) k_agg_lean(const KParams p) {
 // one is processed), a wave prefix sum of the lanes' popcounts places every matched doc's offset in a per-wave LDS
 // list, and the list is gathered 64 docs per round with every lane busy -- so a wave pays the dependent gather
 // latency once per ~41 matched docs (1 %), not once per 64-doc word.  Values: read_value on the gathered code
-// (packed offset or dictId); HLL: the segment's per-dictId (register, rank) table, registers in LDS.
+// (packed offset or dictId); HLL: the segment's per-dictId (register, rank) table, registers in LDS.  A segment
+// filtered by an AND of scan leaves only (sp_reg) takes its step words from conj_reg.h (the leaves decoded
+// register-direct) instead of a bitmap; EX: the value term `a <op> b` of one value column (SSB Q1.x's
+// SUM(lo_extendedprice * lo_discount)), exact int64 for integer terms as k_scan's.
+template <int EX, int C>
 __global__ void __launch_bounds__(kBlock) k_agg_sparse(const KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int WAVES = kWaves;
@@ -189,6 +194,7 @@ __global__ void __launch_bounds__(kBlock) k_agg_sparse(const KParams p) {
   const PH_CONST Chunk* chunks = (const PH_CONST Chunk*)p.chunks;
   uint32_t* lds_hll = reinterpret_cast<uint32_t*>(smem + p.lds_hll_off);
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + p.pl_misc_off) + (size_t)wave * (SW * 64);
+  uint32_t* csets = reinterpret_cast<uint32_t*>(smem + p.pl_misc_off + (size_t)WAVES * SW * 64 * sizeof(uint16_t));
   for (int i = threadIdx.x; i < p.num_hll * m; i += kBlock) lds_hll[i] = 0;
   __syncthreads();
   int64_t isum[kMaxVals], vmin[kMaxVals], vmax[kMaxVals];
@@ -209,12 +215,24 @@ __global__ void __launch_bounds__(kBlock) k_agg_sparse(const KParams p) {
     const uint32_t ndocs = (uint32_t)S->num_docs;
     const unsigned long long* bm = reinterpret_cast<const unsigned long long*>(S->fptr);  // 64 docs per word
     const int32_t wb = chunks[c].word_begin, we = chunks[c].word_end;
+    const bool reg = S->sp_reg != 0;  // chunk-uniform: every wave of the workgroup walks the same chunks
+    if (C > 0 && reg) {
+      __syncthreads();
+      conj_stage_sets(S, csets, threadIdx.x, kBlock);
+      __syncthreads();
+    }
     int32_t w = wb + wave * SW;
-    unsigned long long nxt = (w + lane < we) ? bm[w + lane] : 0ull;
+    unsigned long long nxt = (!reg && w + lane < we) ? bm[w + lane] : 0ull;
     for (; w < we; w += WAVES * SW) {
-      unsigned long long bits = nxt;
-      const int32_t wn = w + WAVES * SW;
-      nxt = (wn + lane < we) ? bm[wn + lane] : 0ull;  // the next step's bitmap words are in flight meanwhile
+      unsigned long long bits;
+      if (reg) {
+        if constexpr (C > 0) bits = conj_step_word<C>(S, w, we, lane, csets);
+        else bits = 0ull;  // not reached: the host picks C > 0 when a segment has register-direct leaves
+      } else {
+        bits = nxt;
+        const int32_t wn = w + WAVES * SW;
+        nxt = (wn + lane < we) ? bm[wn + lane] : 0ull;  // the next step's bitmap words are in flight meanwhile
+      }
       const uint32_t d0 = (uint32_t)(w + lane) * 64u;
       if (d0 + 64u > ndocs) bits &= d0 >= ndocs ? 0ull : ((1ull << (ndocs - d0)) - 1ull);
       const uint32_t cnt = (uint32_t)__popcll(bits);
@@ -243,6 +261,20 @@ __global__ void __launch_bounds__(kBlock) k_agg_sparse(const KParams p) {
           int64_t iv;
           double dv;
           read_value(vc.kind, vc.base, vc.table, unpack_bits(vc.fwd, vc.bits, doc), iv, dv);
+          if constexpr (EX != 0) {  // one value column with a 2-operand term (the host picks EX only then)
+            const PH_CONST DevValCol& v2 = S->vals2[0];
+            int64_t ib;
+            double db;
+            read_value(v2.kind, v2.base, v2.table, unpack_bits(v2.fwd, v2.bits, doc), ib, db);
+            if (p.val_is_int[0]) {
+              iv = EX == PH_EXPR_MULT ? iv * ib : (EX == PH_EXPR_SUB ? iv - ib : iv + ib);
+            } else {
+              const double x = vc.kind == VK_DICT_F64 ? dv : (double)iv;
+              const double y = v2.kind == VK_DICT_F64 ? db : (double)ib;
+              dv = EX == PH_EXPR_MULT ? (1.0 * x) * y : (EX == PH_EXPR_SUB ? x - y : x + y);
+              iv = double_order_key(dv);
+            }
+          }
           const int ops = p.val_ops[j];
           if (ops & OPS_SUM) {
             if (p.val_is_int[j]) isum[j] += iv; else dsum[j] += dv;
@@ -286,8 +318,25 @@ __global__ void __launch_bounds__(kBlock) k_agg_sparse(const KParams p) {
 
 void launch_scan_agg(const KParams& p, int mode, int grid, size_t lds, hipStream_t s) {
   if (mode == MODE_AGG && p.agg_sparse) {
-    allow_lds(k_agg_sparse, lds);
-    hipLaunchKernelGGL(k_agg_sparse, dim3(grid), dim3(kBlock), lds, s, p);
+    auto go = [&](auto ex) {
+      constexpr int EX = decltype(ex)::value;
+      if (p.sparse_c > 4) {
+        allow_lds(k_agg_sparse<EX, 8>, lds);
+        hipLaunchKernelGGL((k_agg_sparse<EX, 8>), dim3(grid), dim3(kBlock), lds, s, p);
+      } else if (p.sparse_c > 0) {
+        allow_lds(k_agg_sparse<EX, 4>, lds);
+        hipLaunchKernelGGL((k_agg_sparse<EX, 4>), dim3(grid), dim3(kBlock), lds, s, p);
+      } else {  // bitmap leaves only
+        allow_lds(k_agg_sparse<EX, 0>, lds);
+        hipLaunchKernelGGL((k_agg_sparse<EX, 0>), dim3(grid), dim3(kBlock), lds, s, p);
+      }
+    };
+    switch (p.num_vals == 1 ? p.val_op[0] : 0) {
+      case PH_EXPR_MULT: go(std::integral_constant<int, PH_EXPR_MULT>{}); break;
+      case PH_EXPR_SUB: go(std::integral_constant<int, PH_EXPR_SUB>{}); break;
+      case PH_EXPR_ADD: go(std::integral_constant<int, PH_EXPR_ADD>{}); break;
+      default: go(std::integral_constant<int, 0>{}); break;
+    }
     return;
   }
   if (mode == MODE_COUNT) {

@@ -10,12 +10,14 @@
 // passed scans 1..i, AndDocIdSet.java:168-170, counted into numEntriesScannedInFilter), then the group key (remapped
 // dictIds, mixed radix) and the value are gathered straight from the packed streams.  Aggregation is the generic
 // plan's: MODE_GROUP_LDS into the workgroup's LDS table, MODE_GROUP_GLOBAL through the LDS group cache in front of
-// the HBM table.
+// the HBM table.  A segment filtered by scan leaves only (sp_reg) gets its step words from conj_reg.h instead of
+// bitmaps: the leaves are decoded register-direct and only the matched docs' keys and values are gathered.
 #include "scan_kernel.h"
+#include "conj_reg.h"
 
 namespace ph {
 
-template <int MODE, int EX>
+template <int MODE, int EX, int C>
 __global__ void __launch_bounds__(kBlock) k_group_sparse(const KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int WAVES = kWaves;
@@ -27,6 +29,7 @@ __global__ void __launch_bounds__(kBlock) k_group_sparse(const KParams p) {
   uint32_t* lds_cnt = reinterpret_cast<uint32_t*>(smem + p.lds_cnt_off);
   uint32_t* gkeys = reinterpret_cast<uint32_t*>(smem + p.gc_key_off);
   uint16_t* list = reinterpret_cast<uint16_t*>(smem + p.pl_misc_off) + (size_t)wave * (SW * 64);
+  uint32_t* csets = reinterpret_cast<uint32_t*>(smem + p.pl_misc_off + (size_t)WAVES * SW * 64 * sizeof(uint16_t));
   const bool cached = MODE == MODE_GROUP_GLOBAL && p.gc_slots > 0;
   const int nslots = MODE == MODE_GROUP_LDS ? (int)p.num_groups : (cached ? p.gc_slots : 0);
   const int ops = p.num_vals ? p.val_ops[0] : 0;
@@ -50,8 +53,14 @@ __global__ void __launch_bounds__(kBlock) k_group_sparse(const KParams p) {
   for (int32_t c = c0; c < c1; ++c) {
     SegPtr S = segs + chunks[c].seg;
     const uint32_t ndocs = (uint32_t)S->num_docs;
-    const int nbm = S->sp_nbm, nscan = S->sp_nscan;
+    const bool reg = S->sp_reg != 0;  // chunk-uniform: every wave of the workgroup walks the same chunks
+    const int nbm = S->sp_nbm, nscan = reg ? 0 : S->sp_nscan;
     const int32_t wb = chunks[c].word_begin, we = chunks[c].word_end;
+    if (C > 0 && reg) {
+      __syncthreads();
+      conj_stage_sets(S, csets, threadIdx.x, kBlock);
+      __syncthreads();
+    }
     auto bm_word = [&](int32_t w) -> unsigned long long {  // the AND (of ORs) of the segment's doc bitmaps, 64 docs
       if (w >= we) return 0ull;
       unsigned long long x = ~0ull, grp = 0ull;
@@ -69,10 +78,16 @@ __global__ void __launch_bounds__(kBlock) k_group_sparse(const KParams p) {
       return x & grp;
     };
     int32_t w = wb + wave * SW;
-    unsigned long long nxt = bm_word(w + lane);
+    unsigned long long nxt = reg ? 0ull : bm_word(w + lane);
     for (; w < we; w += WAVES * SW) {
-      unsigned long long bits = nxt;
-      nxt = bm_word(w + WAVES * SW + lane);  // the next step's bitmap words are in flight meanwhile
+      unsigned long long bits;
+      if (reg) {
+        if constexpr (C > 0) bits = conj_step_word<C>(S, w, we, lane, csets);
+        else bits = 0ull;  // not reached: the host picks C > 0 when a segment has register-direct leaves
+      } else {
+        bits = nxt;
+        nxt = bm_word(w + WAVES * SW + lane);  // the next step's bitmap words are in flight meanwhile
+      }
       const uint32_t d0 = (uint32_t)(w + lane) * 64u;
       if (d0 + 64u > ndocs) bits &= d0 >= ndocs ? 0ull : ((1ull << (ndocs - d0)) - 1ull);
       const uint32_t cnt = (uint32_t)__popcll(bits);
@@ -204,13 +219,13 @@ __global__ void __launch_bounds__(kBlock) k_group_sparse(const KParams p) {
   }
 }
 
-template <int MODE>
+template <int MODE, int C>
 static void launch_sparse_mode(const KParams& p, int grid, size_t lds, hipStream_t s) {
   switch (p.num_vals ? p.val_op[0] : 0) {
-#define PH_SPARSE_CASE(e)                                                           \
-  case e:                                                                           \
-    allow_lds(k_group_sparse<MODE, e>, lds);                                        \
-    hipLaunchKernelGGL((k_group_sparse<MODE, e>), dim3(grid), dim3(kBlock), lds, s, p); \
+#define PH_SPARSE_CASE(e)                                                              \
+  case e:                                                                              \
+    allow_lds(k_group_sparse<MODE, e, C>, lds);                                        \
+    hipLaunchKernelGGL((k_group_sparse<MODE, e, C>), dim3(grid), dim3(kBlock), lds, s, p); \
     break;
     PH_SPARSE_CASE(PH_EXPR_MULT) PH_SPARSE_CASE(PH_EXPR_SUB) PH_SPARSE_CASE(PH_EXPR_ADD)
     default: PH_SPARSE_CASE(0)
@@ -219,8 +234,17 @@ static void launch_sparse_mode(const KParams& p, int grid, size_t lds, hipStream
 }
 
 void launch_group_sparse(const KParams& p, int mode, int grid, size_t lds, hipStream_t s) {
-  if (mode == MODE_GROUP_LDS) launch_sparse_mode<MODE_GROUP_LDS>(p, grid, lds, s);
-  else launch_sparse_mode<MODE_GROUP_GLOBAL>(p, grid, lds, s);
+  // register-direct scan leaves (conj_reg.h): 16-byte loads per lane and leaf, by the widest leaf column
+  // (0: no segment has them -- the bitmap-only form)
+  if (mode == MODE_GROUP_LDS) {
+    if (p.sparse_c > 4) launch_sparse_mode<MODE_GROUP_LDS, 8>(p, grid, lds, s);
+    else if (p.sparse_c > 0) launch_sparse_mode<MODE_GROUP_LDS, 4>(p, grid, lds, s);
+    else launch_sparse_mode<MODE_GROUP_LDS, 0>(p, grid, lds, s);
+  } else {
+    if (p.sparse_c > 4) launch_sparse_mode<MODE_GROUP_GLOBAL, 8>(p, grid, lds, s);
+    else if (p.sparse_c > 0) launch_sparse_mode<MODE_GROUP_GLOBAL, 4>(p, grid, lds, s);
+    else launch_sparse_mode<MODE_GROUP_GLOBAL, 0>(p, grid, lds, s);
+  }
   PH_HIP_CHECK(hipGetLastError());
 }
 

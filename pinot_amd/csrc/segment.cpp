@@ -87,6 +87,7 @@ Lane::Lane(int dev) : device(dev) {
   PH_HIP_CHECK(hipEventCreate(&ev_stop));
   PH_HIP_CHECK(hipEventCreate(&ev_bm0));
   PH_HIP_CHECK(hipEventCreate(&ev_bm1));
+  PH_HIP_CHECK(hipEventCreateWithFlags(&ev_uploaded, hipEventDisableTiming));
 }
 
 Lane::~Lane() {
@@ -97,6 +98,7 @@ Lane::~Lane() {
   if (ev_stop) (void)hipEventDestroy(ev_stop);
   if (ev_bm0) (void)hipEventDestroy(ev_bm0);
   if (ev_bm1) (void)hipEventDestroy(ev_bm1);
+  if (ev_uploaded) (void)hipEventDestroy(ev_uploaded);
   for (auto e : ev_pool) (void)hipEventDestroy(e);
   if (stream) (void)hipStreamDestroy(stream);
   if (stream_b) (void)hipStreamDestroy(stream_b);

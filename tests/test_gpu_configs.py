@@ -147,8 +147,32 @@ def test_config4_ssb(ctx, ssb, qid):
     # Q3.2-Q3.4 / Q4.3 have cardinality products of 0.4-1.75M keys (>= the default numGroupsLimit) over a few hundred
     # real groups: the optimistic scan answers them, no first-seen pass (k_limit_*) runs
     assert r.stats.limit_pass != 2 and not r.stats.num_groups_limit_reached
-    if qid.startswith("Q1."):  # AND of range leaves + SUM(a * b): the lean aggregation kernel's FK_CONJ / term form
-        assert r.stats.scan_kernel == 2, r.stats.scan_kernel
+    if qid.startswith("Q1."):  # a selective AND of range leaves + SUM(a * b): k_agg_sparse's register-direct leaves
+        assert r.stats.scan_kernel == 3, r.stats.scan_kernel
+
+
+@pytest.fixture(scope="module")
+def ssb_scan(ctx):
+    # config 4 on the survey's workload: every dimension dictionary-encoded, no inverted index (ANDs of scans only)
+    tables = [W.ssb_columns(n, seed=0xC104 + i) for i, n in enumerate((300_000, 123_457))]
+    gpu = [ctx.pin(create_segment(f"los_{i}", t)) for i, t in enumerate(tables)]
+    ora = [O.build_segment(f"los_{i}", t) for i, t in enumerate(tables)]
+    return gpu, ora
+
+
+@pytest.mark.parametrize("qid", sorted(W.SSB_QUERIES))
+def test_config4_ssb_scan_dims(ctx, ssb_scan, qid, monkeypatch):
+    # the scan-dimension flight: register-direct leaves + matched-doc gathers (k_agg_sparse for Q1.x, k_group_sparse
+    # for the rest), against the oracle and against the streaming kernels with the sparse plans off
+    gpu, ora = ssb_scan
+    r, got = _check(ctx, gpu, ora, W.SSB_QUERIES[qid])
+    assert r.stats.scan_kernel == (3 if qid.startswith("Q1.") else 12), r.stats.scan_kernel
+    monkeypatch.setenv("PH_GROUP_SPARSE", "0")
+    monkeypatch.setenv("PH_AGG_SPARSE", "0")
+    r2, got2 = _check(ctx, gpu, ora, W.SSB_QUERIES[qid])
+    assert r2.stats.scan_kernel not in (3, 12)
+    assert got.rows == got2.rows
+    assert r.stats.num_entries_scanned_in_filter == r2.stats.num_entries_scanned_in_filter
 
 
 SPARSE_SSB = ("Q2.1", "Q2.2", "Q2.3", "Q3.1", "Q3.2", "Q3.3", "Q3.4", "Q4.1", "Q4.2", "Q4.3")
@@ -190,9 +214,10 @@ def test_group_sparse_shapes(ctx, ssb, monkeypatch):
         assert r.stats.num_groups_limit_reached == e.stats.num_groups_limit_reached, sql
 
 
-def test_lean_agg_conj_terms(ctx, ssb):
+def test_lean_agg_conj_terms(ctx, ssb, monkeypatch):
     # k_agg_lean's FK_CONJ + integer-term path against the oracle: MIN / MAX / SUM of a - b and a + b, COUNT, over
-    # 1..4 range leaves (exact int64)
+    # 1..4 range leaves (exact int64); the selective ones would take k_agg_sparse, held off here
+    monkeypatch.setenv("PH_AGG_SPARSE", "0")
     gpu, ora = ssb
     for sql in ("SELECT SUM(lo_revenue - lo_supplycost), MIN(lo_revenue - lo_supplycost), "
                 "MAX(lo_revenue - lo_supplycost), COUNT(*) FROM lineorder WHERE lo_discount BETWEEN 2 AND 8 "
