@@ -48,8 +48,8 @@ __global__ void __launch_bounds__(256) k_leaf_bitmaps(const LeafJob* __restrict_
 void launch_leaf_bitmaps(const LeafJob* jobs, int32_t njobs, int64_t max_docs, int32_t max_bits, hipStream_t s) {
   if (njobs <= 0 || max_docs <= 0) return;
   const int64_t tiles = (max_docs + 2047) / 2048;
-  // each wave takes ~16 tiles: long-lived workgroups, the set staged once per workgroup
-  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>((tiles + 63) / 64, 2048)), (unsigned)njobs);
+  // one tile per wave (r4: ~16 tiles per wave measured 0.51 vs 0.39 ms on the SSB flight: fewer loads in flight)
+  const dim3 grid((unsigned)std::min<int64_t>((tiles + 3) / 4, 2048), (unsigned)njobs);
   if (max_bits <= 16) hipLaunchKernelGGL(k_leaf_bitmaps<4>, grid, dim3(256), 0, s, jobs);
   else hipLaunchKernelGGL(k_leaf_bitmaps<8>, grid, dim3(256), 0, s, jobs);
   PH_HIP_CHECK(hipGetLastError());

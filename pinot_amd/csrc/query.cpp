@@ -2506,7 +2506,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       hipStream_t sb = lane.lane->stream_b;
       PH_HIP_CHECK(hipStreamWaitEvent(sb, lane.lane->ev_uploaded, 0));
       constexpr size_t kStatBatchWords = (size_t)32 << 20;  // 256 MiB
-      constexpr int kWalkShift = 10;                        // 1024-doc walks (tests/test_filter_sim_cpu.py: they meet)
+      constexpr int kWalkShift = 11;                        // 2048-doc walks (tests/test_filter_sim_cpu.py: they meet)
       auto seg_words = [&](const StatSeg& ss) {
         return ss.leaves.size() * (size_t)((dsegs[ss.dseg].num_docs + 63) / 64);
       };
