@@ -6,8 +6,8 @@
 
 namespace ph {
 
-constexpr int kWalkHead = 8;   // candidates a walker logs from its start
-constexpr int kWalkTail = 8;   // candidates it logs at or past the next chunk
+constexpr int kWalkHead = 16;  // candidates a walker logs from its start
+constexpr int kWalkTail = 16;  // candidates it logs at or past the next chunk
 struct AndWalkJob {
   const unsigned long long* bits;  // k leaf doc bitmaps, leaf-major, nwords words each (bits past ndocs zero)
   int64_t nwords, ndocs;

@@ -69,9 +69,17 @@ __device__ __forceinline__ unsigned long long conj_step_word(SegPtr S, int32_t w
 #pragma unroll 1
     for (int k = 0; k < n; ++k) {
       ColRef col = S->cols[S->sp_slot[k]];
-      u32x4 pool[C];
-      reg_load<C>(true, live, col.fwd, col.bits, (ndocs * col.bits + 7) / 8, run0, lane, pool);
-      m &= conj_leaf_mask<C>(S, k, pool, sets);
+      // as many 16-byte loads as the leaf's width needs (a 3-bit column's 12 bytes per lane: one), not the widest's
+      auto leaf = [&](auto cc) {
+        constexpr int CC = decltype(cc)::value;
+        u32x4 pool[CC];
+        reg_load<CC>(true, live, col.fwd, col.bits, (ndocs * col.bits + 7) / 8, run0, lane, pool);
+        m &= conj_leaf_mask<CC>(S, k, pool, sets);
+      };
+      if (col.bits <= 4) leaf(std::integral_constant<int, 1>{});
+      else if (col.bits <= 8) leaf(std::integral_constant<int, 2>{});
+      else if (C <= 4 || col.bits <= 16) leaf(std::integral_constant<int, (C < 4 ? C : 4)>{});
+      else leaf(std::integral_constant<int, C>{});
     }
     half[h] = m;
   }

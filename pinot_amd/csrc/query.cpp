@@ -1536,7 +1536,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       } else {
         // key space beyond the dense budget: open-addressing table over the keys that can occur -- at most one
         // per scanned doc -- with >= 2x slots (DictionaryBasedGroupKeyGenerator's map-based holders, :598/:778)
-        if (num_hll) fail(PH_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL group-by over a key space beyond the dense budget");
+        // (DISTINCTCOUNTHLL: 2^log2m registers per slot, the ObjectGroupByResultHolder of HyperLogLogs)
         if (dop) fail(PH_ERR_UNSUPPORTED, "dense partials over a key space beyond the dense budget");
         // numGroupsLimit here runs optimistically only: the scan goes ahead without truncation and the call fails
         // UNSUPPORTED afterwards if the table ends up with `limit` keys or more (see the launch below)
@@ -1545,7 +1545,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           if (seg_live[i]) live_docs += segs[i]->num_docs;
         int64_t H = 1024;
         while (H < 2 * std::min<int64_t>(G, live_docs)) H <<= 1;
-        if ((double)H * (8.0 * nout + 8.0) > kDenseTableBudget)
+        if ((double)H * (8.0 * nout + 8.0 + 4.0 * num_hll * (m ? m : 1)) > kDenseTableBudget)
           fail(PH_ERR_UNSUPPORTED, "group-by hash table too large for HBM budget");
         mode = MODE_GROUP_HASH;
         TR = H;
@@ -2592,11 +2592,27 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         if (!lj.empty()) {
           if (!lsets.empty())
             PH_HIP_CHECK(hipMemcpyAsync(d_lsets, lsets.data(), 4 * lsets.size(), hipMemcpyHostToDevice, sb));
+          // one launch per load-width class (1, 2, 4 or 8 16-byte loads per lane), jobs grouped by class
+          auto cls = [](int32_t b) { return b <= 4 ? 0 : b <= 8 ? 1 : b <= 16 ? 2 : 3; };
+          std::stable_sort(lj.begin(), lj.end(), [&](const LeafJob& a, const LeafJob& b) { return cls(a.bits) < cls(b.bits); });
           PH_HIP_CHECK(hipMemcpyAsync(d_ljobs, lj.data(), sizeof(LeafJob) * lj.size(), hipMemcpyHostToDevice, sb));
-          launch_leaf_bitmaps(d_ljobs, (int32_t)lj.size(), max_docs, max_bits, sb);
+          for (size_t i = 0; i < lj.size();) {
+            size_t e = i;
+            int64_t nd = 0;
+            int32_t mb = 1;
+            while (e < lj.size() && cls(lj[e].bits) == cls(lj[i].bits)) {
+              nd = std::max(nd, lj[e].ndocs);
+              mb = std::max(mb, lj[e].bits);
+              ++e;
+            }
+            launch_leaf_bitmaps(d_ljobs + i, (int32_t)(e - i), nd, mb, sb);
+            i = e;
+          }
+          (void)max_docs;
+          (void)max_bits;
         }
         // the AND-of-scans walks: chunks of 1 << kWalkShift docs; a job whose walks did not meet runs again with
-        // chunks 32x longer (one chunk is the plain walk: always exact)
+        // chunks 4x longer (one chunk is the plain walk: always exact)
         std::vector<size_t> walk_b;  // batch positions of the scan-AND segments
         for (size_t b = 0; b < batch.size(); ++b)
           if (stat_segs[batch[b]].kind == ST_SCANAND) walk_b.push_back(b);
@@ -2665,7 +2681,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
             for (size_t x = 0; x < todo.size(); ++x) {
               const size_t t = todo[x];
               if (bd[x] && wj[x].nchunks > 1) {
-                shift[t] += 5;
+                shift[t] += 2;  // 4x longer chunks (r4: +5 at once left SSB Q4.3 to a few 64K-doc walks, 110 ms)
                 again.push_back(t);
               } else if (bd[x]) {
                 fail(PH_ERR_DEVICE, "single-chunk AND walk did not reach the end");
@@ -2968,9 +2984,15 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       string_ids[g].pinned = nullptr;
     }
   } else {
-    // group-by with DISTINCTCOUNTHLL registers: host-side materialisation
+    // group-by with DISTINCTCOUNTHLL registers: host-side materialisation (MODE_GROUP_HASH: rows are the occupied
+    // slots, ordered by their raw key like the dense tables' rows)
     std::vector<unsigned long long> cnt(RG);
     PH_HIP_CHECK(hipMemcpy(cnt.data(), kp.out_count, 8 * RG, hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> slot_key;
+    if (mode == MODE_GROUP_HASH) {
+      slot_key.resize(RG);
+      PH_HIP_CHECK(hipMemcpy(slot_key.data(), hkeys, 8 * RG, hipMemcpyDeviceToHost));
+    }
     std::vector<int64_t> live;
     int64_t docs = 0;
     for (int64_t g = 0; g < RG; ++g)
@@ -2978,6 +3000,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         live.push_back(g);
         docs += (int64_t)cnt[g];
       }
+    if (!slot_key.empty())
+      std::sort(live.begin(), live.end(), [&](int64_t a, int64_t b) { return slot_key[a] < slot_key[b]; });
+    auto key_of = [&](int64_t row) -> int64_t { return slot_key.empty() ? RB + live[row] : (int64_t)slot_key[live[row]]; };
     if (fin) stats.num_docs_scanned = docs;
     const int64_t R = (int64_t)live.size();
     res->num_groups = R;
@@ -3023,7 +3048,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       res->key_entry_size[g] = es;
       res->keys[g].assign((size_t)es * R, 0);
       for (int64_t r = 0; r < R; ++r) {
-        const int64_t id = ((RB + live[r]) / kp.group_stride[g]) % std::max<int64_t>(1, d.size);
+        const int64_t id = (key_of(r) / kp.group_stride[g]) % std::max<int64_t>(1, d.size);
         put_key_value(d, id, res->keys[g].data() + (size_t)es * r, es);
       }
     }

@@ -19,7 +19,7 @@
 //   k_and_merge  -- the true walk (walker 0's) meets walker c at q_c = the first candidate of walker c-1's tail log
 //                   that walker c's head log holds; walker c owns the true epochs after q_c up to q_{c+1}:
 //                   sum = cum_0(q_1) + sum_c (cum_c(q_{c+1}) - cum_c(q_c)).  A chunk whose walks do not meet inside the
-//                   logs (or meet out of order) marks the job: the host reruns it with L x 32 (L >= numDocs is one
+//                   logs (or meet out of order) marks the job: the host reruns it with L x 4 (L >= numDocs is one
 //                   walker: always exact).
 // Algorithmic bytes: the k leaf bitmaps (k * numDocs / 8), read once per walk plus the logs; the host checks these
 // sums against the iterator simulation in the parity tests (filter_sim.cpp, oracle.filter_entries).

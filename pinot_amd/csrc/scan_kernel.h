@@ -721,7 +721,7 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
         ColRef col = S->cols[p.hll_slot[h]];
         const uint32_t e = gld(col.hll + unpack_col(col, doc));
         const int64_t ri = (g * p.num_hll + h) * m + (e >> 8);
-        if (MODE == MODE_GROUP_GLOBAL) atomicMax(&p.out_hll[ri], e & 0xffu);
+        if (MODE == MODE_GROUP_GLOBAL || MODE == MODE_GROUP_HASH) atomicMax(&p.out_hll[ri], e & 0xffu);  // g: slot
         else atomicMax(&lds_hll[ri], e & 0xffu);
       }
     }

@@ -346,6 +346,27 @@ def test_hash_group_by_beyond_dense_budget(ctx, where):
     assert len(got.rows) > (300_000 if not where else 100_000)
 
 
+@pytest.mark.parametrize("where", ["", " WHERE f < 300"])
+def test_hash_group_by_hll(ctx, where):
+    # DISTINCTCOUNTHLL per group over a key space beyond the dense budget: MODE_GROUP_HASH with 2^log2m registers
+    # per slot (DistinctCountHLLAggregationFunction over the map-based group key holders); registers compared raw
+    rng = np.random.default_rng(37)
+    tables = []
+    for n in (200_000, 77_777):
+        t = {c: (rng.integers(0, 12_000, n).astype(np.int32) * 3 + k, "INT") for k, c in enumerate(("g1", "g2", "g3"))}
+        t["g1"][0][: n // 4] = 5  # hot keys with many distinct u per group
+        t["g2"][0][: n // 4] = 7
+        t["g3"][0][: n // 4] = 11
+        t["u"] = (rng.integers(0, 1 << 24, n).astype(np.int32), "INT")
+        t["f"] = (rng.integers(0, 1000, n).astype(np.int32), "INT")
+        tables.append(t)
+    sql = (f"SET numGroupsLimit=10000000; SELECT g1, g2, g3, DISTINCTCOUNTHLL(u), COUNT(*) FROM t{where} "
+           f"GROUP BY g1, g2, g3 ORDER BY g1, g2, g3 LIMIT 10000000")
+    r, got = _both(ctx, tables, sql)
+    assert r.stats.mode == 5  # MODE_GROUP_HASH
+    assert len(got.rows) > 50_000
+
+
 @pytest.mark.parametrize("where", ["", " WHERE f < 300", " WHERE f IN (1, 5, 9, 300, 301, 777) OR g1 < 9000"])
 def test_hash_group_by_num_groups_limit(ctx, where):
     # numGroupsLimit over a key space beyond the dense budget (LongMapBasedHolder.getGroupId,
