@@ -22,14 +22,23 @@ __global__ void __launch_bounds__(256) k_leaf_bitmaps(const LeafJob* __restrict_
   }
   const int64_t ntiles = (J.ndocs + 2047) / 2048;
   const int64_t bytes = (J.ndocs * J.bits + 7) / 8;
-  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  // a wave walks its tiles with the next tile's loads in flight while this one is tested
+  int64_t tile = (int64_t)blockIdx.x * 4 + wave;
+  auto load = [&](int64_t t, u32x4 (&pool)[C]) {
+    const int32_t ndoc = t < ntiles ? (int32_t)min<int64_t>(2048, J.ndocs - t * 2048) : 0;
+    reg_load<C>(t < ntiles, lane * 32 < ndoc, J.fwd, J.bits, bytes, (int32_t)((t * 2048) >> 5), lane, pool);
+  };
+  u32x4 cur[C];
+  load(tile, cur);
+  for (; tile < ntiles; tile += stride) {
+    u32x4 nxt[C];
+    load(tile + stride, nxt);
     const int64_t d0 = tile * 2048;
     const int32_t ndoc = (int32_t)min<int64_t>(2048, J.ndocs - d0);
     const int32_t nv = max(0, min(32, ndoc - lane * 32));
-    u32x4 pool[C];
-    reg_load<C>(true, lane * 32 < ndoc, J.fwd, J.bits, bytes, (int32_t)(d0 >> 5), lane, pool);
     uint32_t v[32];
-    reg_unpack<C>(pool, J.bits, v);
+    reg_unpack<C>(cur, J.bits, v);
     uint32_t mask = 0;
     if (use_set) {
 #pragma unroll
@@ -42,14 +51,17 @@ __global__ void __launch_bounds__(256) k_leaf_bitmaps(const LeafJob* __restrict_
     if (nv < 32) mask &= nv > 0 ? (0xffffffffu >> (32 - nv)) : 0u;
     const int64_t wi = (d0 >> 5) + lane;  // this lane's 32-doc word (lanes past the end write the zero padding)
     if (wi < J.out_words) J.out[wi] = mask;
+#pragma unroll
+    for (int i = 0; i < C; ++i) cur[i] = nxt[i];
   }
 }
 
 void launch_leaf_bitmaps(const LeafJob* jobs, int32_t njobs, int64_t max_docs, int32_t max_bits, hipStream_t s) {
   if (njobs <= 0 || max_docs <= 0) return;
   const int64_t tiles = (max_docs + 2047) / 2048;
-  // one tile per wave (r4: ~16 tiles per wave measured 0.51 vs 0.39 ms on the SSB flight: fewer loads in flight)
-  const dim3 grid((unsigned)std::min<int64_t>((tiles + 3) / 4, 2048), (unsigned)njobs);
+  // ~8 tiles per wave, each wave one tile of loads ahead (r4: one tile per wave, a workgroup per 8192 docs, 0.39 ms
+  // on the SSB flight; 16 tiles per wave without the look-ahead 0.51)
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>((tiles + 31) / 32, 2048)), (unsigned)njobs);
   switch (max_bits <= 4 ? 1 : max_bits <= 8 ? 2 : max_bits <= 16 ? 4 : 8) {
     case 1: hipLaunchKernelGGL(k_leaf_bitmaps<1>, grid, dim3(256), 0, s, jobs); break;
     case 2: hipLaunchKernelGGL(k_leaf_bitmaps<2>, grid, dim3(256), 0, s, jobs); break;
