@@ -240,8 +240,9 @@ def flight_main(args, world, rank, dist, device):
                                                                   else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
-                     "kernel": "13 SSB queries (k_agg_lean for Q1.x, k_group_sparse for Q2.x-Q4.x; bytes = the "
-                               "queries' full column bytes, which the sparse gathers touch only in part)",
+                     "kernel": "13 SSB queries (k_agg_sparse for Q1.x, k_group_sparse for Q2.x-Q4.x, leaves from "
+                               "inverted bitmaps or register-direct scans; bytes = the queries' full column bytes, "
+                               "which the sparse gathers touch only in part)",
                      "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": alg},
     }
