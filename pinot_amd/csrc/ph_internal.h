@@ -661,7 +661,8 @@ struct LeafJob {
   uint32_t* out;
   int64_t out_words;
 };
-void launch_leaf_bitmaps(const LeafJob* jobs, int32_t njobs, int64_t max_docs, int32_t max_bits, hipStream_t s);
+void launch_leaf_bitmaps(const LeafJob* jobs, int32_t njobs, int64_t max_docs, int32_t max_bits, int32_t set_words,
+                         hipStream_t s);
 // host iterator simulation of the statistic (filter_sim.cpp): the planned filter tree over per-leaf doc bitmaps
 enum SimOp { SIM_LEAF = 0, SIM_AND = 1, SIM_OR = 2, SIM_NOT = 3 };
 enum SimLeafKind { SIM_SCAN = 0, SIM_SORTED = 1, SIM_BITMAP = 2 };

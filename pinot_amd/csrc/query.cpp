@@ -2506,7 +2506,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       hipStream_t sb = lane.lane->stream_b;
       PH_HIP_CHECK(hipStreamWaitEvent(sb, lane.lane->ev_uploaded, 0));
       constexpr size_t kStatBatchWords = (size_t)32 << 20;  // 256 MiB
-      constexpr int kWalkShift = 11;                        // 2048-doc walks (tests/test_filter_sim_cpu.py: they meet)
+      constexpr int kWalkShift = 13;                        // 8192-doc walks (tests/test_filter_sim_cpu.py: they meet)
       auto seg_words = [&](const StatSeg& ss) {
         return ss.leaves.size() * (size_t)((dsegs[ss.dseg].num_docs + 63) / 64);
       };
@@ -2599,13 +2599,14 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           for (size_t i = 0; i < lj.size();) {
             size_t e = i;
             int64_t nd = 0;
-            int32_t mb = 1;
+            int32_t mb = 1, sw = 0;
             while (e < lj.size() && cls(lj[e].bits) == cls(lj[i].bits)) {
               nd = std::max(nd, lj[e].ndocs);
               mb = std::max(mb, lj[e].bits);
+              if (lj[e].set) sw = std::max(sw, lj[e].set_words);
               ++e;
             }
-            launch_leaf_bitmaps(d_ljobs + i, (int32_t)(e - i), nd, mb, sb);
+            launch_leaf_bitmaps(d_ljobs + i, (int32_t)(e - i), nd, mb, sw, sb);
             i = e;
           }
           (void)max_docs;

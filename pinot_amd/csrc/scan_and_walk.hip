@@ -27,10 +27,12 @@
 
 namespace ph {
 
-// and_walk_chunk with the k leaves' words of the walk's current 64-doc word held in registers: a step inside the word
-// is register work (the first scan without M, the next match of scan f), and the k words are loaded again only when
-// the candidate leaves the word.  Up to K leaves (the padding leaves read as all-ones, so they never fail); the logs
-// are the same as and_walk_chunk's (the host version the CPU tests run).
+// and_walk_chunk with the k leaves' words of the walk's current 64-doc word AND of the next one held in registers: a
+// step inside the word is register work (the first scan without M, the next match of scan f), a candidate that moves
+// on to the next word swaps the next word's set in and issues the loads of the one after (waited on only when that
+// word is reached: r4's one-word form stalled the wave on a reload in most iterations, some lane always crossing a
+// word), and only a jump of two words or more loads on the spot.  Up to K leaves (the padding leaves read as
+// all-ones, so they never fail); the logs are the same as and_walk_chunk's (the host version the CPU tests run).
 template <int K>
 __global__ void __launch_bounds__(256) k_and_walk(const AndWalkJob* __restrict__ jobs) {
   const AndWalkJob J = jobs[blockIdx.y];
@@ -48,13 +50,16 @@ __global__ void __launch_bounds__(256) k_and_walk(const AndWalkJob* __restrict__
   int64_t M = c << J.shift;
   int j = -1, hn = 0, tn = 0;
   unsigned long long cum = 0;
-  unsigned long long W[K];
+  unsigned long long W[K], X[K];  // words cw and cw + 1 of every leaf
   int64_t cw = M >> 6;
-  auto load = [&](int64_t w) {
+  auto load = [&](int64_t w, unsigned long long (&R)[K]) {
 #pragma unroll
-    for (int i = 0; i < K; ++i) W[i] = i < k ? J.bits[(int64_t)i * nwords + w] : ~0ull;
+    for (int i = 0; i < K; ++i) R[i] = i >= k ? ~0ull : (w < nwords ? J.bits[(int64_t)i * nwords + w] : 0ull);
   };
-  if (M < N) load(cw);
+  if (M < N) {
+    load(cw, W);
+    load(cw + 1, X);
+  }
   for (;;) {
     bool term = false;
     int64_t nxt = 0;
@@ -73,14 +78,21 @@ __global__ void __launch_bounds__(256) k_and_walk(const AndWalkJob* __restrict__
         nxt = M + 1;
       } else {
         cum += (unsigned long long)(f + 1 - ((j >= 0 && j < f) ? 1 : 0));
-        unsigned long long v = 0;
+        unsigned long long v = 0, vx = 0;
 #pragma unroll
-        for (int i = 0; i < K; ++i) v = i == f ? W[i] : v;
+        for (int i = 0; i < K; ++i) {
+          v = i == f ? W[i] : v;
+          vx = i == f ? X[i] : vx;
+        }
         v &= ~0ull << b;
         int64_t wi = cw;
-        const unsigned long long* bf = J.bits + (int64_t)f * nwords;
-        while (!v && ++wi < nwords) v = bf[wi];
-        nxt = v ? wi * 64 + __builtin_ctzll(v) : N;
+        if (!v) {  // the next word from registers, then memory
+          v = vx;
+          ++wi;
+          const unsigned long long* bf = J.bits + (int64_t)f * nwords;
+          while (!v && ++wi < nwords) v = bf[wi];
+        }
+        nxt = (v && wi < nwords) ? wi * 64 + __builtin_ctzll(v) : N;
         term = nxt >= N;
         jn = f;
       }
@@ -99,9 +111,16 @@ __global__ void __launch_bounds__(256) k_and_walk(const AndWalkJob* __restrict__
     if (term || tn == kWalkTail) break;
     M = nxt;
     j = jn;
-    if ((M >> 6) != cw && M < N) {
-      cw = M >> 6;
-      load(cw);
+    const int64_t mw = M >> 6;
+    if (mw != cw && M < N) {
+      if (mw == cw + 1) {
+#pragma unroll
+        for (int i = 0; i < K; ++i) W[i] = X[i];
+      } else {
+        load(mw, W);
+      }
+      cw = mw;
+      load(cw + 1, X);
     }
   }
   J.cnt[c] = (uint32_t)hn | ((uint32_t)tn << 16);
