@@ -60,6 +60,32 @@ __device__ __forceinline__ unsigned long long conj_step_word(SegPtr S, int32_t w
   const int n = S->sp_nscan;
   const int64_t ndocs = S->num_docs;
   uint32_t half[2];
+  if constexpr (C <= 2) {
+    // every leaf <= 8 bits (the host picks C = 2 then): all leaves' loads of both passes issued at once (2 x 32 B
+    // per lane and leaf), then tested -- r4's one-leaf-at-a-time form kept one load per wave in flight
+    u32x4 pool[2][kMaxConj][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int32_t run0 = 2 * w + 64 * h;
+      const bool live = (int64_t)(run0 + lane) * 32 < ndocs;
+#pragma unroll
+      for (int k = 0; k < kMaxConj; ++k) {
+        const bool use = k < n;
+        ColRef col = S->cols[use ? S->sp_slot[k] : 0];
+        reg_load<2>(use, live, use ? col.fwd : nullptr, use ? col.bits : 0, use ? (ndocs * col.bits + 7) / 8 : 0,
+                    run0, lane, pool[h][k]);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t d0 = (int64_t)(2 * w + 64 * h + lane) * 32;
+      uint32_t m = d0 >= ndocs ? 0u : (d0 + 32 <= ndocs ? 0xffffffffu : ((1u << (uint32_t)(ndocs - d0)) - 1u));
+#pragma unroll
+      for (int k = 0; k < kMaxConj; ++k)
+        if (k < n) m &= conj_leaf_mask<2>(S, k, pool[h][k], sets);
+      half[h] = m;
+    }
+  } else {
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int32_t run0 = 2 * w + 64 * h;
@@ -82,6 +108,7 @@ __device__ __forceinline__ unsigned long long conj_step_word(SegPtr S, int32_t w
       else leaf(std::integral_constant<int, C>{});
     }
     half[h] = m;
+  }
   }
   const int src = 2 * (lane & 31);
   const uint32_t x0 = __shfl(half[0], src), y0 = __shfl(half[0], src + 1);

@@ -73,10 +73,10 @@ void launch_leaf_bitmaps(const LeafJob* jobs, int32_t njobs, int64_t max_docs, i
   if (njobs <= 0 || max_docs <= 0) return;
   const int64_t tiles = (max_docs + 2047) / 2048;
   const size_t lds = (size_t)std::max(0, set_words) * 4;
-  // ~8 tiles per wave (a batch of G, the next batch's loads in flight); r4: one tile per wave 0.39 ms on the SSB
-  // flight, 8 with one tile of look-ahead 0.33, the leaves' 2-4 bit streams leaving most of HBM idle
+  // ~8 tiles per wave, one tile of look-ahead (r4 on the SSB flight: one tile per wave 0.39 ms, this 0.33, batches of
+  // 4 tiles with the next batch in flight 0.42 -- fewer waves resident)
   auto go = [&](auto c) {
-    constexpr int CC = decltype(c)::value, G = CC >= 8 ? 1 : 8 / CC > 4 ? 4 : 8 / CC;
+    constexpr int CC = decltype(c)::value, G = 1;
     const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>((tiles + 32 - 1) / 32, 2048)), (unsigned)njobs);
     hipLaunchKernelGGL((k_leaf_bitmaps<CC, G>), grid, dim3(256), lds, s, jobs);
   };

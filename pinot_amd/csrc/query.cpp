@@ -1969,11 +1969,11 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if (kp.agg_sparse) kp.agg_fast = 0;
   }
   // the register-direct leaves' loads per lane (conj_reg.h): by the widest scan column of an sp_reg segment
-  // (0: none has them)
+  // (2: every leaf <= 8 bits, all loads hoisted; 0: no segment has register-direct leaves)
   kp.sparse_c = 0;
   for (auto& d : dsegs)
     for (int k = 0; d.sp_reg && k < d.sp_nscan; ++k)
-      kp.sparse_c = std::max(kp.sparse_c, d.cols[d.sp_slot[k]].bits > 16 ? 8 : 4);
+      kp.sparse_c = std::max(kp.sparse_c, d.cols[d.sp_slot[k]].bits > 16 ? 8 : d.cols[d.sp_slot[k]].bits > 8 ? 4 : 2);
   // the register-direct COUNT (k_count_reg): every segment a dictId RANGE scan leaf, everything, or a sorted range
   if (mode == MODE_COUNT && !kp.late_prefetch && getenv("PH_COUNT_GENERIC") == nullptr) {
     int fb = 1;
@@ -2506,7 +2506,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       hipStream_t sb = lane.lane->stream_b;
       PH_HIP_CHECK(hipStreamWaitEvent(sb, lane.lane->ev_uploaded, 0));
       constexpr size_t kStatBatchWords = (size_t)32 << 20;  // 256 MiB
-      constexpr int kWalkShift = 13;                        // 8192-doc walks (tests/test_filter_sim_cpu.py: they meet)
+      constexpr int kWalkShift = 11;                        // 2048-doc walks (r4: 1024 1.17 ms, 2048 0.80, 8192 1.05 per SSB query)
       auto seg_words = [&](const StatSeg& ss) {
         return ss.leaves.size() * (size_t)((dsegs[ss.dseg].num_docs + 63) / 64);
       };

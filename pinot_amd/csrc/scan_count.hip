@@ -323,7 +323,8 @@ void launch_scan_agg(const KParams& p, int mode, int grid, size_t lds, hipStream
       if (p.sparse_c > 4) {
         allow_lds(k_agg_sparse<EX, 8>, lds);
         hipLaunchKernelGGL((k_agg_sparse<EX, 8>), dim3(grid), dim3(kBlock), lds, s, p);
-      } else if (p.sparse_c > 0) {
+      } else if (p.sparse_c > 0) {  // (the hoisted narrow-leaf form, C = 2, measured slower here: 1.01 vs 0.86 ms
+                                    // on SSB Q1.x -- its registers cost the gathers their occupancy)
         allow_lds(k_agg_sparse<EX, 4>, lds);
         hipLaunchKernelGGL((k_agg_sparse<EX, 4>), dim3(grid), dim3(kBlock), lds, s, p);
       } else {  // bitmap leaves only

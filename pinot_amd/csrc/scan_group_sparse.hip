@@ -238,11 +238,13 @@ void launch_group_sparse(const KParams& p, int mode, int grid, size_t lds, hipSt
   // (0: no segment has them -- the bitmap-only form)
   if (mode == MODE_GROUP_LDS) {
     if (p.sparse_c > 4) launch_sparse_mode<MODE_GROUP_LDS, 8>(p, grid, lds, s);
-    else if (p.sparse_c > 0) launch_sparse_mode<MODE_GROUP_LDS, 4>(p, grid, lds, s);
+    else if (p.sparse_c > 2) launch_sparse_mode<MODE_GROUP_LDS, 4>(p, grid, lds, s);
+    else if (p.sparse_c > 0) launch_sparse_mode<MODE_GROUP_LDS, 2>(p, grid, lds, s);
     else launch_sparse_mode<MODE_GROUP_LDS, 0>(p, grid, lds, s);
   } else {
     if (p.sparse_c > 4) launch_sparse_mode<MODE_GROUP_GLOBAL, 8>(p, grid, lds, s);
-    else if (p.sparse_c > 0) launch_sparse_mode<MODE_GROUP_GLOBAL, 4>(p, grid, lds, s);
+    else if (p.sparse_c > 2) launch_sparse_mode<MODE_GROUP_GLOBAL, 4>(p, grid, lds, s);
+    else if (p.sparse_c > 0) launch_sparse_mode<MODE_GROUP_GLOBAL, 2>(p, grid, lds, s);
     else launch_sparse_mode<MODE_GROUP_GLOBAL, 0>(p, grid, lds, s);
   }
   PH_HIP_CHECK(hipGetLastError());

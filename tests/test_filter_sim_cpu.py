@@ -189,7 +189,7 @@ def test_and_walk_matches_simulation(seed):
 
 
 def test_and_walk_meets_at_bench_densities():
-    # SSB-like densities at the product's 8192-doc chunks: the walks meet (no rerun), and the sum is exact
+    # SSB-like densities at the product's 2048-doc chunks: the walks meet (no rerun), and the sum is exact
     rng = np.random.default_rng(7)
     n = 200_000
     for dens in ([1 / 7, 3 / 11, 0.48], [1 / 84, 3 / 11, 0.2], [2 / 250, 2 / 250, 6 / 7], [1 / 25, 1 / 5],
@@ -198,4 +198,4 @@ def test_and_walk_meets_at_bench_densities():
         docs = [rng.random(n) < d for d in dens]
         root, leaves = _scan_and(len(dens))
         exp = _native_sim(root, leaves, docs, n)
-        assert _walk(docs, n, 13) == exp, dens
+        assert _walk(docs, n, 11) == exp, dens
