@@ -86,29 +86,33 @@ __device__ __forceinline__ unsigned long long conj_step_word(SegPtr S, int32_t w
       half[h] = m;
     }
   } else {
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int32_t run0 = 2 * w + 64 * h;
-    const int64_t d0 = (int64_t)(run0 + lane) * 32;
-    const bool live = d0 < ndocs;
-    uint32_t m = !live ? 0u : (d0 + 32 <= ndocs ? 0xffffffffu : ((1u << (uint32_t)(ndocs - d0)) - 1u));
+    // leaf by leaf, both passes' loads of the leaf issued together, as many 16-byte units as its width needs (a
+    // 3-bit column's 12 bytes per lane: one), not the widest leaf's
+    const int32_t ra = 2 * w, rb = 2 * w + 64;
+    const bool la = (int64_t)(ra + lane) * 32 < ndocs, lb = (int64_t)(rb + lane) * 32 < ndocs;
+    auto valid = [&](int32_t run) -> uint32_t {
+      const int64_t d0 = (int64_t)(run + lane) * 32;
+      return d0 >= ndocs ? 0u : (d0 + 32 <= ndocs ? 0xffffffffu : ((1u << (uint32_t)(ndocs - d0)) - 1u));
+    };
+    half[0] = valid(ra);
+    half[1] = valid(rb);
 #pragma unroll 1
     for (int k = 0; k < n; ++k) {
       ColRef col = S->cols[S->sp_slot[k]];
-      // as many 16-byte loads as the leaf's width needs (a 3-bit column's 12 bytes per lane: one), not the widest's
       auto leaf = [&](auto cc) {
         constexpr int CC = decltype(cc)::value;
-        u32x4 pool[CC];
-        reg_load<CC>(true, live, col.fwd, col.bits, (ndocs * col.bits + 7) / 8, run0, lane, pool);
-        m &= conj_leaf_mask<CC>(S, k, pool, sets);
+        u32x4 pa[CC], pb[CC];
+        const int64_t bytes = (ndocs * col.bits + 7) / 8;
+        reg_load<CC>(true, la, col.fwd, col.bits, bytes, ra, lane, pa);
+        reg_load<CC>(true, lb, col.fwd, col.bits, bytes, rb, lane, pb);
+        half[0] &= conj_leaf_mask<CC>(S, k, pa, sets);
+        half[1] &= conj_leaf_mask<CC>(S, k, pb, sets);
       };
       if (col.bits <= 4) leaf(std::integral_constant<int, 1>{});
       else if (col.bits <= 8) leaf(std::integral_constant<int, 2>{});
       else if (C <= 4 || col.bits <= 16) leaf(std::integral_constant<int, (C < 4 ? C : 4)>{});
       else leaf(std::integral_constant<int, C>{});
     }
-    half[h] = m;
-  }
   }
   const int src = 2 * (lane & 31);
   const uint32_t x0 = __shfl(half[0], src), y0 = __shfl(half[0], src + 1);
