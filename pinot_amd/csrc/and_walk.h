@@ -14,10 +14,14 @@ struct AndWalkJob {
   int32_t k, slot;                 // scans; the sum accumulates into out[slot]
   int32_t shift;                   // chunk = 1 << shift docs
   int64_t nchunks;
-  int32_t* pos;                    // [nchunks][kWalkHead + kWalkTail] logged candidates
-  unsigned long long* cum;         // their running sums
+  int32_t* pos;                    // [kWalkHead + kWalkTail][nchunks] logged candidates (entry-major: the walkers
+                                   // of a wave store one entry to consecutive addresses)
+  unsigned long long* cum;         // their running sums, same layout
   uint32_t* cnt;                   // [nchunks] head count | tail count << 16
 };
+
+// index of log entry e (head: 0 .. kWalkHead - 1, tail: kWalkHead + i) of walker c
+__host__ __device__ inline int64_t walk_slot(const AndWalkJob& J, int64_t c, int e) { return (int64_t)e * J.nchunks + c; }
 
 // first set bit of bitmap `w` at or after x (x < nwords * 64), or -1
 __host__ __device__ inline int64_t walk_next_set(const unsigned long long* w, int64_t nwords, int64_t x) {
@@ -34,11 +38,6 @@ __host__ __device__ inline int64_t walk_next_set(const unsigned long long* w, in
 __host__ __device__ inline void and_walk_chunk(const AndWalkJob& J, int64_t c) {
   const int64_t N = J.ndocs;
   const int k = J.k;
-  const int64_t rec = kWalkHead + kWalkTail;
-  int32_t* hpos = J.pos + c * rec;
-  int32_t* tpos = hpos + kWalkHead;
-  unsigned long long* hcum = J.cum + c * rec;
-  unsigned long long* tcum = hcum + kWalkHead;
   const int64_t end = (c + 1) << J.shift;
   const int64_t thr = end < N ? end : N;  // the tail starts at the next chunk (the last walker's: the end)
   int64_t M = c << J.shift;
@@ -68,13 +67,13 @@ __host__ __device__ inline void and_walk_chunk(const AndWalkJob& J, int64_t c) {
     }
     const int32_t P = term ? (int32_t)N : (int32_t)M;  // the end is logged as candidate numDocs
     if (hn < kWalkHead) {
-      hpos[hn] = P;
-      hcum[hn] = cum;
+      J.pos[walk_slot(J, c, hn)] = P;
+      J.cum[walk_slot(J, c, hn)] = cum;
       ++hn;
     }
     if (P >= thr) {
-      tpos[tn] = P;
-      tcum[tn] = cum;
+      J.pos[walk_slot(J, c, kWalkHead + tn)] = P;
+      J.cum[walk_slot(J, c, kWalkHead + tn)] = cum;
       ++tn;
     }
     if (term || tn == kWalkTail) break;
@@ -86,13 +85,10 @@ __host__ __device__ inline void and_walk_chunk(const AndWalkJob& J, int64_t c) {
 
 // where walker b's tail log meets walker b + 1's head log (the first common candidate): the index pair, or false
 __host__ __device__ inline bool and_walk_meet(const AndWalkJob& J, int64_t b, int& ti, int& hi) {
-  const int64_t rec = kWalkHead + kWalkTail;
-  const int32_t* tpos = J.pos + b * rec + kWalkHead;
-  const int32_t* hpos = J.pos + (b + 1) * rec;
   const int tn = (int)(J.cnt[b] >> 16), hn = (int)(J.cnt[b + 1] & 0xffff);
   int x = 0, y = 0;
   while (x < tn && y < hn) {
-    const int32_t a = tpos[x], h = hpos[y];
+    const int32_t a = J.pos[walk_slot(J, b, kWalkHead + x)], h = J.pos[walk_slot(J, b + 1, y)];
     if (a == h) {
       ti = x;
       hi = y;
@@ -106,26 +102,23 @@ __host__ __device__ inline bool and_walk_meet(const AndWalkJob& J, int64_t b, in
 
 // walker c's share of the true walk, cum_c(q_{c+1}) - cum_c(q_c); false when the walks do not meet in order
 __host__ __device__ inline bool and_merge_chunk(const AndWalkJob& J, int64_t c, unsigned long long& part) {
-  const int64_t rec = kWalkHead + kWalkTail;
-  const unsigned long long* hcum = J.cum + c * rec;
-  const unsigned long long* tcum = hcum + kWalkHead;
   int64_t qc = -1, qn = -1;
   unsigned long long lo = 0, hi = 0;
   int ti = 0, h = 0;
   if (c > 0) {  // q_c: the true walk joins walker c
     if (!and_walk_meet(J, c - 1, ti, h)) return false;
-    qc = J.pos[c * rec + h];
-    lo = hcum[h];
+    qc = J.pos[walk_slot(J, c, h)];
+    lo = J.cum[walk_slot(J, c, h)];
   }
   if (c + 1 < J.nchunks) {  // q_{c+1}: walker c + 1 takes over
     if (!and_walk_meet(J, c, ti, h)) return false;
-    qn = J.pos[c * rec + kWalkHead + ti];
-    hi = tcum[ti];
+    qn = J.pos[walk_slot(J, c, kWalkHead + ti)];
+    hi = J.cum[walk_slot(J, c, kWalkHead + ti)];
   } else {  // the last walker runs to the end: its tail holds the end alone
     const int tn = (int)(J.cnt[c] >> 16);
     if (tn < 1) return false;
-    qn = J.pos[c * rec + kWalkHead + tn - 1];
-    hi = tcum[tn - 1];
+    qn = J.pos[walk_slot(J, c, kWalkHead + tn - 1)];
+    hi = J.cum[walk_slot(J, c, kWalkHead + tn - 1)];
   }
   if (qn < qc) return false;
   part = hi - lo;

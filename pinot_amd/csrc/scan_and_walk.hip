@@ -40,11 +40,6 @@ __global__ void __launch_bounds__(256) k_and_walk(const AndWalkJob* __restrict__
   if (c >= J.nchunks) return;
   const int64_t N = J.ndocs, nwords = J.nwords;
   const int k = J.k;
-  const int64_t rec = kWalkHead + kWalkTail;
-  int32_t* hpos = J.pos + c * rec;
-  int32_t* tpos = hpos + kWalkHead;
-  unsigned long long* hcum = J.cum + c * rec;
-  unsigned long long* tcum = hcum + kWalkHead;
   const int64_t end = (c + 1) << J.shift;
   const int64_t thr = end < N ? end : N;
   int64_t M = c << J.shift;
@@ -98,14 +93,14 @@ __global__ void __launch_bounds__(256) k_and_walk(const AndWalkJob* __restrict__
       }
     }
     const int32_t P = term ? (int32_t)N : (int32_t)M;
-    if (hn < kWalkHead) {
-      hpos[hn] = P;
-      hcum[hn] = cum;
+    if (hn < kWalkHead) {  // entry-major logs: the wave's walkers store to consecutive addresses
+      J.pos[walk_slot(J, c, hn)] = P;
+      J.cum[walk_slot(J, c, hn)] = cum;
       ++hn;
     }
     if (P >= thr) {
-      tpos[tn] = P;
-      tcum[tn] = cum;
+      J.pos[walk_slot(J, c, kWalkHead + tn)] = P;
+      J.cum[walk_slot(J, c, kWalkHead + tn)] = cum;
       ++tn;
     }
     if (term || tn == kWalkTail) break;
