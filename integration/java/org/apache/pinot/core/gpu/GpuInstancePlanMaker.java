@@ -57,7 +57,7 @@ public class GpuInstancePlanMaker extends InstancePlanMakerImplV2 {
     // inside the library (RCCL reduce-scatter over xGMI), as GroupByCombineOperator merges them in this JVM
     _ctx = ords.length == 1 ? PinotHipJni.ctxCreate(ords[0]) : PinotHipJni.ctxCreateMulti(ords);
     long budget = queryExecutorConfig.getProperty(GPU_HBM_BUDGET_KEY, DEFAULT_HBM_BUDGET);
-    _segments = new GpuSegmentRegistry(_ctx, budget * ords.length);
+    _segments = new GpuSegmentRegistry(_ctx, budget, ords.length);  // budget per device (ph_segment_device)
   }
 
   /** null when gpu.enable is false (the server's segment hooks then do nothing). */

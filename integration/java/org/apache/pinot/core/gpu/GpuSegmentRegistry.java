@@ -7,21 +7,41 @@ import org.apache.pinot.segment.spi.IndexSegment;
 
 
 /**
- * Device-resident segments of one GPU: pinned from the segment's own directory with ph_segment_load_dir
+ * Device-resident segments of one GPU context: pinned from the segment's own directory with ph_segment_load_dir
  * (SegmentMetadata.getIndexDir(), v3 columns.psf or v1 files) when the server loads it, released when the segment is
  * destroyed (ImmutableSegmentImpl.destroy, ImmutableSegmentImpl.java:249).  A query runs on the GPU only when every
  * segment it touches is pinned (else the CPU plan).
+ *
+ * Entries are keyed by segment NAME (what a query's IndexSegment list resolves through) but carry the IndexSegment
+ * they were pinned for: a refresh loads the new IndexSegment before the old one is destroyed, so the new copy replaces
+ * the old entry (the old copy's bytes are released first when the budget is checked), and the old segment's destroy
+ * hook then finds an entry that is not its own and leaves it alone.  The HBM budget is enforced per device
+ * (ph_segment_device), since the library places each segment on one device of the context.
  */
 public final class GpuSegmentRegistry {
-  private final long _ctx;
-  private final long _hbmBudget;  // bytes the pinned segments may hold over the context's devices
-  private final ConcurrentHashMap<String, Long> _pinned = new ConcurrentHashMap<>();
-  private final ConcurrentHashMap<String, Long> _bytes = new ConcurrentHashMap<>();
-  private final java.util.concurrent.atomic.AtomicLong _held = new java.util.concurrent.atomic.AtomicLong();
+  private static final class Entry {
+    final IndexSegment _segment;
+    final long _handle;
+    final long _bytes;
+    final int _device;
 
-  public GpuSegmentRegistry(long ctx, long hbmBudget) {
+    Entry(IndexSegment segment, long handle, long bytes, int device) {
+      _segment = segment;
+      _handle = handle;
+      _bytes = bytes;
+      _device = device;
+    }
+  }
+
+  private final long _ctx;
+  private final long _hbmBudgetPerDevice;  // bytes the pinned segments may hold on each device of the context
+  private final ConcurrentHashMap<String, Entry> _pinned = new ConcurrentHashMap<>();
+  private final long[] _held;  // pinned bytes per device index, guarded by `this`
+
+  public GpuSegmentRegistry(long ctx, long hbmBudgetPerDevice, int numDevices) {
     _ctx = ctx;
-    _hbmBudget = hbmBudget;
+    _hbmBudgetPerDevice = hbmBudgetPerDevice;
+    _held = new long[Math.max(1, numDevices)];
   }
 
   /** Hook for ImmutableSegmentLoader.load (after the CPU load succeeded). */
@@ -30,51 +50,86 @@ public final class GpuSegmentRegistry {
     if (dir == null) {
       return;  // mutable / consuming segments stay on the CPU path
     }
+    String name = segment.getSegmentName();
+    long handle;
     try {
-      long handle = PinotHipJni.segmentLoadDir(_ctx, dir.getAbsolutePath(), null);
-      // admission: the segment stays pinned only while every pinned segment fits the HBM budget (its measured
-      // footprint, ph_segment_device_bytes: columns plus the streams derived at pin); past it, the CPU path
-      long bytes = PinotHipJni.segmentDeviceBytes(handle);
-      if (_held.addAndGet(bytes) > _hbmBudget) {
-        _held.addAndGet(-bytes);
-        PinotHipJni.segmentUnpin(handle);
+      handle = PinotHipJni.segmentLoadDir(_ctx, dir.getAbsolutePath(), null);
+    } catch (RuntimeException e) {
+      // unsupported layout (raw / multi-value columns only, legacy padding, a packed stream past 2 GiB, out of HBM):
+      // CPU path for this segment -- and never the GPU copy of an older version of it
+      dropStale(name, segment);
+      return;
+    }
+    // admission: the segment stays pinned only while the pinned segments of its device fit that device's budget
+    // (measured footprint, ph_segment_device_bytes: columns plus the streams derived at pin); a refreshed segment's
+    // old copy on the same device does not count against its replacement
+    long bytes = PinotHipJni.segmentDeviceBytes(handle);
+    int device = Math.max(0, Math.min(_held.length - 1, PinotHipJni.segmentDevice(handle)));
+    Entry old;
+    boolean admitted;
+    synchronized (this) {
+      old = _pinned.get(name);
+      long oldOnDevice = old != null && old._device == device ? old._bytes : 0;
+      if (_held[device] - oldOnDevice + bytes > _hbmBudgetPerDevice) {
+        old = _pinned.remove(name);  // the refreshed data is not on the GPU: the old copy must not serve queries
+        if (old != null) {
+          _held[old._device] -= old._bytes;
+        }
+        admitted = false;
+      } else {
+        _pinned.put(name, new Entry(segment, handle, bytes, device));
+        _held[device] += bytes;
+        if (old != null) {
+          _held[old._device] -= old._bytes;
+        }
+        admitted = true;
+      }
+    }
+    if (!admitted) {
+      PinotHipJni.segmentUnpin(handle);  // over the device's budget: CPU path
+    }
+    if (old != null) {
+      PinotHipJni.segmentUnpin(old._handle);  // segment refresh: the new copy (or the CPU path) replaces the old one
+    }
+  }
+
+  /** Hook for ImmutableSegmentImpl.destroy: releases the entry only if it belongs to this IndexSegment. */
+  public void onSegmentDestroyed(IndexSegment segment) {
+    Entry e;
+    synchronized (this) {
+      e = _pinned.get(segment.getSegmentName());
+      if (e == null || e._segment != segment) {
+        return;  // already replaced by a refreshed copy (or never pinned)
+      }
+      _pinned.remove(segment.getSegmentName());
+      _held[e._device] -= e._bytes;
+    }
+    PinotHipJni.segmentUnpin(e._handle);
+  }
+
+  private void dropStale(String name, IndexSegment replacement) {
+    Entry old;
+    synchronized (this) {
+      old = _pinned.get(name);
+      if (old == null || old._segment == replacement) {
         return;
       }
-      Long oldBytes = _bytes.put(segment.getSegmentName(), bytes);
-      Long old = _pinned.put(segment.getSegmentName(), handle);
-      if (old != null) {
-        if (oldBytes != null) {
-          _held.addAndGet(-oldBytes);
-        }
-        PinotHipJni.segmentUnpin(old);  // segment refresh: the new copy replaces the old one
-      }
-    } catch (RuntimeException e) {
-      // unsupported layout (raw / multi-value columns only, legacy padding, a packed stream past 2 GiB, out of
-      // HBM): CPU path for this segment
+      _pinned.remove(name);
+      _held[old._device] -= old._bytes;
     }
+    PinotHipJni.segmentUnpin(old._handle);
   }
 
-  /** Hook for ImmutableSegmentImpl.destroy. */
-  public void onSegmentDestroyed(String segmentName) {
-    Long handle = _pinned.remove(segmentName);
-    if (handle != null) {
-      Long bytes = _bytes.remove(segmentName);
-      if (bytes != null) {
-        _held.addAndGet(-bytes);
-      }
-      PinotHipJni.segmentUnpin(handle);
-    }
-  }
-
-  /** Device handles of the query's segments, or null when one of them is not pinned. */
+  /** Device handles of the query's segments, or null when one of them is not pinned (as this very IndexSegment). */
   public long[] handles(List<IndexSegment> segments) {
     long[] out = new long[segments.size()];
     for (int i = 0; i < out.length; i++) {
-      Long h = _pinned.get(segments.get(i).getSegmentName());
-      if (h == null) {
+      IndexSegment s = segments.get(i);
+      Entry e = _pinned.get(s.getSegmentName());
+      if (e == null || e._segment != s) {
         return null;
       }
-      out[i] = h;
+      out[i] = e._handle;
     }
     return out;
   }

@@ -29,6 +29,7 @@ public final class PinotHipJni {
   static native long segmentLoadDir(long ctx, String segmentDir, String[] columns);      // ph_segment_load_dir
   static native void segmentUnpin(long segment);                                         // ph_segment_unpin
   static native long segmentDeviceBytes(long segment);                                   // ph_segment_device_bytes
+  static native int segmentDevice(long segment);                                         // ph_segment_device
 
   static native void tableSetDictionary(long ctx, String column, int dataType, ByteBuffer sortedValues, long count,
       int entrySize);                                                                    // ph_table_set_dictionary

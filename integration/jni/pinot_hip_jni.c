@@ -27,6 +27,8 @@ static int throw_ph(JNIEnv* env, int rc) {
   return 1;
 }
 
+static void throw_illegal(JNIEnv* env, const char* msg);
+
 #define FN(name) Java_org_apache_pinot_core_gpu_PinotHipJni_##name
 #define PTR(x) ((void*)(intptr_t)(x))
 
@@ -39,12 +41,19 @@ JNIEXPORT jlong JNICALL FN(ctxCreate)(JNIEnv* env, jclass c, jint device) {
 JNIEXPORT jlong JNICALL FN(ctxCreateMulti)(JNIEnv* env, jclass c, jintArray devices) {
   ph_ctx* ctx = NULL;
   const jsize n = devices ? (*env)->GetArrayLength(env, devices) : 0;
+  /* the whole ordinal list goes to the library unchanged (it rejects n > 64 itself); never a truncated set */
   jint* d = n ? (*env)->GetIntArrayElements(env, devices, NULL) : NULL;
   if (n && !d) return 0; /* OutOfMemoryError pending */
-  int32_t ords[64];
-  for (jsize i = 0; i < n && i < 64; ++i) ords[i] = (int32_t)d[i];
+  int32_t* ords = (int32_t*)calloc((size_t)(n ? n : 1), sizeof(int32_t));
+  if (!ords) {
+    if (d) (*env)->ReleaseIntArrayElements(env, devices, d, JNI_ABORT);
+    throw_illegal(env, "out of memory");
+    return 0;
+  }
+  for (jsize i = 0; i < n; ++i) ords[i] = (int32_t)d[i];
   if (d) (*env)->ReleaseIntArrayElements(env, devices, d, JNI_ABORT);
-  throw_ph(env, ph_ctx_create_multi(ords, (int32_t)(n < 64 ? n : 64), &ctx));
+  throw_ph(env, ph_ctx_create_multi(ords, (int32_t)n, &ctx));
+  free(ords);
   return (jlong)(intptr_t)ctx;
 }
 
@@ -107,6 +116,8 @@ JNIEXPORT void JNICALL FN(segmentUnpin)(JNIEnv* env, jclass c, jlong seg) { thro
 JNIEXPORT jlong JNICALL FN(segmentDeviceBytes)(JNIEnv* env, jclass c, jlong seg) {
   return ph_segment_device_bytes(PTR(seg));
 }
+
+JNIEXPORT jint JNICALL FN(segmentDevice)(JNIEnv* env, jclass c, jlong seg) { return ph_segment_device(PTR(seg)); }
 
 /* table-level dictionary of a group-by column (sorted values, fixed width, direct buffer) */
 JNIEXPORT void JNICALL FN(tableSetDictionary)(JNIEnv* env, jclass c, jlong ctx, jstring column, jint dataType,
