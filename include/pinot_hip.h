@@ -242,6 +242,14 @@ int ph_ctx_create(int32_t device_ordinal, ph_ctx** out);
  * The result equals ph_query_execute's over one device (DOUBLE SUM within 1e-9 relative: summation order). */
 int ph_ctx_create_multi(const int32_t* device_ordinals, int32_t num_devices, ph_ctx** out);
 int32_t ph_ctx_num_devices(const ph_ctx* ctx);
+/* How a multi-device context merges its devices' dense partial tables (a reduce-scatter by key shard, either way):
+ * PH_TRANSPORT_PEER (default) -- each device gathers its key shard of the others' tables by peer copy over xGMI and
+ * reduces it with a kernel; PH_TRANSPORT_RCCL -- ncclReduceScatter over xGMI, its communicators created here (not in
+ * the first query).  RCCL needs distinct device ordinals; logical shards sharing a device always take PEER.
+ * Replaces the cross-server half of GroupByCombineOperator's merge (GroupByCombineOperator.java:125-197). */
+#define PH_TRANSPORT_PEER 0
+#define PH_TRANSPORT_RCCL 1
+int ph_ctx_set_multi_transport(ph_ctx* ctx, int32_t transport);
 int ph_ctx_destroy(ph_ctx* ctx);
 /* Launch on an external HIP stream (e.g. torch's current stream); NULL restores the context's own. */
 int ph_ctx_set_stream(ph_ctx* ctx, void* hip_stream);

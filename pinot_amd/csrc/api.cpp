@@ -18,6 +18,7 @@ ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* con
 void context_init(Context& c, int ordinal);
 void multi_init(ph_ctx* x, const int32_t* ordinals, int32_t n);
 Context* place_segment(ph_ctx* x, int64_t rows);
+void multi_set_transport(ph_ctx* x, int32_t transport);
 ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, int32_t nseg);
 }  // namespace ph
 
@@ -84,6 +85,13 @@ int ph_ctx_create_multi(const int32_t* device_ordinals, int32_t num_devices, ph_
 
 int32_t ph_ctx_num_devices(const ph_ctx* ctx) { return ctx ? (int32_t)ctx->devs.size() : 0; }
 
+int ph_ctx_set_multi_transport(ph_ctx* ctx, int32_t transport) {
+  return guarded([&] {
+    if (!ctx) fail(PH_ERR_INVALID_ARGUMENT, "ctx is null");
+    multi_set_transport(ctx, transport);
+  });
+}
+
 int ph_ctx_destroy(ph_ctx* ctx) {
   return guarded([&] {
     if (!ctx) return;
@@ -115,7 +123,9 @@ int ph_segment_load_dir(ph_ctx* ctx, const char* segment_dir, const char* const*
   return guarded([&] {
     if (!ctx || !out) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
     *out = nullptr;
-    *out = pin_placed(ctx, 0, [&](Context* c) { return segment_load_dir_impl(c, segment_dir, columns, num_columns); });
+    // rows reserved from the metadata at placement, so concurrent loads (server start) spread over the devices
+    *out = pin_placed(ctx, segment_dir_num_docs(segment_dir),
+                      [&](Context* c) { return segment_load_dir_impl(c, segment_dir, columns, num_columns); });
   });
 }
 

@@ -177,6 +177,21 @@ int32_t data_type_of(const std::string& t, const std::string& col) {
 
 }  // namespace
 
+// the segment's doc count from its metadata.properties (0 if unreadable: the load itself reports the error), so a
+// multi-device context places concurrent directory loads by their rows before any of them has pinned
+int64_t segment_dir_num_docs(const char* dir_c) {
+  if (!dir_c) return 0;
+  try {
+    std::string dir = dir_c;
+    if (file_exists(dir + "/v3/metadata.properties")) dir += "/v3";
+    auto meta = read_properties(dir + "/metadata.properties");
+    auto it = meta.find("segment.total.docs");
+    return it == meta.end() ? 0 : to_i64(it->second, "segment.total.docs", 0, INT32_MAX);
+  } catch (const Error&) {
+    return 0;
+  }
+}
+
 ph_segment* segment_load_dir_impl(Context* ctx, const char* dir_c, const char* const* want, int32_t nwant) {
   if (!dir_c) fail(PH_ERR_INVALID_ARGUMENT, "null segment directory");
   std::string dir = dir_c;

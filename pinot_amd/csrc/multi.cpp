@@ -136,6 +136,22 @@ void multi_init(ph_ctx* x, const int32_t* ordinals, int32_t n) {
   x->multi = std::make_shared<MultiState>();
 }
 
+// PH_TRANSPORT_RCCL: one communicator per device, created once here (ncclCommInitAll), not inside a query
+void multi_set_transport(ph_ctx* x, int32_t transport) {
+  if (transport != PH_TRANSPORT_PEER && transport != PH_TRANSPORT_RCCL) fail(PH_ERR_INVALID_ARGUMENT, "transport");
+  std::lock_guard<std::mutex> lk(x->multi->comm_mu);
+  bool distinct = true;
+  for (size_t a = 0; a < x->ordinals.size(); ++a)
+    for (size_t b = a + 1; b < x->ordinals.size(); ++b) distinct &= x->ordinals[a] != x->ordinals[b];
+  if (transport == PH_TRANSPORT_RCCL && distinct && x->devs.size() > 1 && x->multi->comms.empty()) {
+    const Rccl& api = rccl();
+    std::vector<ncclComm_t> comms(x->devs.size());
+    nccl_check(api.init_all(comms.data(), (int)comms.size(), x->ordinals.data()), "ncclCommInitAll");
+    x->multi->comms = comms;
+  }
+  x->transport = transport;
+}
+
 // the device a new segment of `rows` docs goes to: the fewest docs pinned so far (its rows are reserved at once, so
 // concurrent pins spread too); the caller unreserves them if the pin fails
 Context* place_segment(ph_ctx* x, int64_t rows) {
@@ -259,29 +275,32 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
     }
   });
   const auto t_scan = clock::now();
-  // ---- merge
+  // ---- merge: a reduce-scatter of every table by key shard, so device k owns the fully merged shard [k S, (k + 1) S)
+  //   RCCL: ncclReduceScatter over xGMI (distinct ordinals, transport PH_TRANSPORT_RCCL);
+  //   PEER (default, and the only form for logical shards sharing a device): device k gathers shard k of every other
+  //   device's tables by peer copy (a device-local copy when the ordinals coincide) and folds each into its own
+  //   shard with k_reduce_table -- the same result as the collective, built from copies the driver always supports
   bool distinct = true;
   for (int a = 0; a < D; ++a)
     for (int b = a + 1; b < D; ++b) distinct &= x->ordinals[a] != x->ordinals[b];
-  if (const char* e = getenv("PH_MULTI_TRANSPORT")) distinct = distinct && std::string(e) != "local";
+  const bool use_rccl = distinct && x->transport == PH_TRANSPORT_RCCL;
   std::vector<std::pair<int, std::pair<int64_t, int64_t>>> shards;  // (device, [g0, g1)) to finalise
   std::vector<std::vector<std::unique_ptr<DeviceBuffer>>> R(D);       // reduce-scatter outputs
-  if (distinct) {
+  for (int k = 0; k < D; ++k) {
+    PH_HIP_CHECK(hipSetDevice(x->ordinals[k]));
+    for (int t = 0; t < L.num_tables; ++t) {
+      R[k].push_back(std::make_unique<DeviceBuffer>());
+      R[k].back()->alloc((size_t)S * L.elems_per_group[t] * L.elem_bytes[t], x->ordinals[k]);
+    }
+  }
+  if (use_rccl) {
     const Rccl& api = rccl();
     std::lock_guard<std::mutex> lk(x->multi->comm_mu);
-    if (x->multi->comms.empty()) {
-      std::vector<ncclComm_t> comms(D);
-      nccl_check(api.init_all(comms.data(), D, x->ordinals.data()), "ncclCommInitAll");
-      x->multi->comms = comms;
-    }
+    if (x->multi->comms.empty()) fail(PH_ERR_DEVICE, "RCCL transport without communicators");
     std::vector<std::unique_ptr<LaneGuard>> lanes;
     for (int k = 0; k < D; ++k) {
       PH_HIP_CHECK(hipSetDevice(x->ordinals[k]));
       lanes.push_back(std::make_unique<LaneGuard>(x->devs[k]));
-      for (int t = 0; t < L.num_tables; ++t) {
-        R[k].push_back(std::make_unique<DeviceBuffer>());
-        R[k].back()->alloc((size_t)S * L.elems_per_group[t] * L.elem_bytes[t], x->ordinals[k]);
-      }
     }
     // one reduce-scatter per table: device k receives the merged key shard [k S, (k + 1) S)
     nccl_check(api.group_start(), "ncclGroupStart");
@@ -296,34 +315,39 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
       PH_HIP_CHECK(hipSetDevice(x->ordinals[k]));
       PH_HIP_CHECK(hipStreamSynchronize(lanes[k]->lane->stream));
     }
-    for (int k = 0; k < D; ++k) {
-      const int64_t g0 = std::min<int64_t>(G, k * S), g1 = std::min<int64_t>(G, g0 + S);
-      if (g1 > g0) shards.push_back({k, {g0, g1}});
-    }
   } else {
-    // local transport: every other device's tables copied to the owner's device and reduced into its tables
-    const int owner = active[0];
-    Context& c = *x->devs[owner];
-    PH_HIP_CHECK(hipSetDevice(c.device));
-    LaneGuard lg(&c);
-    const hipStream_t so = lg.lane->stream;
-    for (int k = 0; k < D; ++k) {
-      if (k == owner || by[k].empty()) continue;  // a device without segments holds identities only
+    per_device(every, [&](int k) {
+      Context& c = *x->devs[k];
+      PH_HIP_CHECK(hipSetDevice(c.device));
+      LaneGuard lg(&c);
+      const hipStream_t sk = lg.lane->stream;
       for (int t = 0; t < L.num_tables; ++t) {
-        const size_t bytes = (size_t)padded * L.elems_per_group[t] * L.elem_bytes[t];
-        const void* src = T[k][t]->ptr;
+        const size_t eb = (size_t)L.elems_per_group[t] * L.elem_bytes[t];
+        const size_t bytes = (size_t)S * eb;
         std::unique_ptr<DeviceBuffer> tmp;
-        if (x->ordinals[k] != c.device) {
-          tmp = std::make_unique<DeviceBuffer>();
-          tmp->alloc(bytes, c.device);
-          PH_HIP_CHECK(hipMemcpyPeerAsync(tmp->ptr, c.device, src, x->ordinals[k], bytes, so));
-          src = tmp->ptr;
+        bool first = true;
+        for (int j = 0; j < D; ++j) {
+          const uint8_t* src = static_cast<const uint8_t*>(T[j][t]->ptr) + (size_t)k * S * eb;
+          if (first) {  // device j's shard k seeds the output (identities where j has no segments)
+            PH_HIP_CHECK(hipMemcpyPeerAsync(R[k][t]->ptr, c.device, src, x->ordinals[j], bytes, sk));
+            first = false;
+            continue;
+          }
+          if (by[j].empty()) continue;  // identities only
+          if (!tmp) {
+            tmp = std::make_unique<DeviceBuffer>();
+            tmp->alloc(bytes, c.device);
+          }
+          PH_HIP_CHECK(hipMemcpyPeerAsync(tmp->ptr, c.device, src, x->ordinals[j], bytes, sk));
+          launch_reduce_table(R[k][t]->ptr, tmp->ptr, (int64_t)S * L.elems_per_group[t], L.reduce_op[t], sk);
         }
-        launch_reduce_table(T[owner][t]->ptr, src, (int64_t)padded * L.elems_per_group[t], L.reduce_op[t], so);
-        PH_HIP_CHECK(hipStreamSynchronize(so));
+        PH_HIP_CHECK(hipStreamSynchronize(sk));  // tmp is reused / freed: the stream drains per table
       }
-    }
-    shards.push_back({owner, {0, G}});
+    });
+  }
+  for (int k = 0; k < D; ++k) {
+    const int64_t g0 = std::min<int64_t>(G, k * S), g1 = std::min<int64_t>(G, g0 + S);
+    if (g1 > g0) shards.push_back({k, {g0, g1}});
   }
   const auto t_merge = clock::now();
   // ---- finalise the shards in parallel (a shard on a device without segments moves to the first active device)
@@ -335,10 +359,7 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
     const int64_t g0 = shards[i].second.first, g1 = shards[i].second.second;
     std::vector<void*> ptrs;
     std::vector<std::unique_ptr<DeviceBuffer>> moved;
-    for (int t = 0; t < L.num_tables; ++t) {
-      uint8_t* p = static_cast<uint8_t*>(distinct ? R[k][t]->ptr : T[k][t]->ptr);
-      ptrs.push_back(distinct ? p : p + (size_t)g0 * L.elems_per_group[t] * L.elem_bytes[t]);
-    }
+    for (int t = 0; t < L.num_tables; ++t) ptrs.push_back(R[k][t]->ptr);
     if (by[k].empty()) {
       const int to = active[0];
       PH_HIP_CHECK(hipSetDevice(x->ordinals[to]));

@@ -619,6 +619,7 @@ typedef std::map<std::pair<std::string, std::string>, std::pair<int64_t, int64_t
 IndexMap read_index_map(const std::string& path);
 ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc);
 ph_segment* segment_load_dir_impl(Context* ctx, const char* dir, const char* const* columns, int32_t num_columns);
+int64_t segment_dir_num_docs(const char* dir);  // metadata.properties segment.total.docs, 0 if unreadable
 // every container of every (leaf, dictId) work item of a query in one launch (one wave per container)
 void launch_roaring_or(const RoaringWork* w, int n, const RoaringTarget* targets, hipStream_t s);
 void launch_roaring_chunk(const RoaringLeaf* leaves, int nleaves, int max_chunks, const RoaringRange* ranges,
@@ -755,6 +756,7 @@ struct ph_ctx {
   std::vector<ph::Context*> devs;                  // every device's context, devs[0] == &c
   std::vector<int32_t> ordinals;                   // their HIP device ordinals (may repeat: logical shards)
   std::shared_ptr<ph::MultiState> multi;
+  int32_t transport = PH_TRANSPORT_PEER;           // merge of the devices' dense partials (ph_ctx_set_multi_transport)
   ~ph_ctx();
 };
 

@@ -204,7 +204,9 @@ class GpuContext:
     placed by pinned rows, the devices' partial results merged inside the library; a repeated ordinal is a logical
     shard of that GPU)."""
 
-    def __init__(self, device: int = 0, devices=None):
+    TRANSPORTS = {"peer": 0, "rccl": 1}  # PH_TRANSPORT_PEER / PH_TRANSPORT_RCCL
+
+    def __init__(self, device: int = 0, devices=None, transport: str = "peer"):
         import weakref
         h = ctypes.c_void_p()
         if devices is None:
@@ -215,6 +217,11 @@ class GpuContext:
             N.check(N.lib().ph_ctx_create_multi(ords, len(devices), ctypes.byref(h)))
             self.devices = list(devices)
             device = devices[0]
+            if transport != "peer":  # RCCL communicators are created here, not in the first query
+                rc = N.lib().ph_ctx_set_multi_transport(h, self.TRANSPORTS[transport])
+                if rc != 0:
+                    N.lib().ph_ctx_destroy(h)
+                    N.check(rc)
         self.handle = h
         self.device = device
         # segments and results of this context: released before it (ph_ctx_destroy contract)

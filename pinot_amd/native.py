@@ -129,7 +129,7 @@ class ExecStats(ctypes.Structure):
 
 # every symbol declared in include/pinot_hip.h
 EXPORTED_SYMBOLS = (
-    "ph_ctx_create", "ph_ctx_create_multi", "ph_ctx_num_devices", "ph_segment_device", "ph_ctx_destroy",
+    "ph_ctx_create", "ph_ctx_create_multi", "ph_ctx_num_devices", "ph_ctx_set_multi_transport", "ph_segment_device", "ph_ctx_destroy",
     "ph_ctx_set_stream", "ph_segment_pin", "ph_segment_check", "ph_segment_load_dir",
     "ph_segment_unpin",
     "ph_segment_device_bytes", "ph_segment_num_docs", "ph_table_set_dictionary", "ph_table_set_column_type", "ph_query_execute",
@@ -173,6 +173,7 @@ def lib():
     sig = {
         "ph_ctx_create": ([i32, ctypes.POINTER(vp)], ctypes.c_int),
         "ph_ctx_create_multi": ([ctypes.POINTER(i32), i32, ctypes.POINTER(vp)], ctypes.c_int),
+        "ph_ctx_set_multi_transport": ([vp, i32], ctypes.c_int),
         "ph_ctx_num_devices": ([vp], i32),
         "ph_segment_device": ([vp], i32),
         "ph_ctx_destroy": ([vp], ctypes.c_int),

@@ -1,10 +1,13 @@
 """GPU: the in-library multi-GPU combine (ph_ctx_create_multi) -- a Pinot server combines all of a query's segments in
 one JVM (GroupByCombineOperator.java:125-197), so one context spans the node's GPUs: segments are placed by pinned
-rows and the devices' dense partial tables merge inside libpinot_hip.  The GPU box has one MI355X, so the context is
-two LOGICAL shards of cuda:0 (devices [0, 0]): each shard scans its own segments into its own tables and the local
-transport (device copy + reduce kernel) merges them; the RCCL reduce-scatter transport needs distinct devices and is
-exercised only on a multi-GPU node.  Every result must equal the oracle's and the one-device context's: bit-exact
-COUNT / integer SUM / MIN / MAX / HLL registers, DOUBLE SUM within 1e-9 relative."""
+rows and the devices' dense partial tables merge inside libpinot_hip by a reduce-scatter over key shards, each device
+finalising its own shard.  The GPU box has one MI355X, so the contexts are LOGICAL shards of cuda:0 (devices [0, 0]
+and [0, 0, 0]): each shard scans its own segments into its own tables, the peer transport (peer copies of the other
+shards' key shards + the reduce kernel, PH_TRANSPORT_PEER) builds every merged shard, and every shard finalises --
+including a shard whose device holds none of the query's segments (moved to an active device) and shards past the
+key space (G < 64 D).  The RCCL transport needs distinct devices: its test runs only where hipGetDeviceCount() >= 2.
+Every result must equal the oracle's and the one-device context's: bit-exact COUNT / integer SUM / MIN / MAX / HLL
+registers, DOUBLE SUM within 1e-9 relative."""
 import numpy as np
 import pytest
 
@@ -118,6 +121,72 @@ def test_forced_host_merge_matches(setup, monkeypatch):
         r = multi.execute(q, segs_m)
         s = single.execute(q, segs_s)
         _rows_equal(reduce_groups(q, r.keys, r.aggs).rows, reduce_groups(q, s.keys, s.aggs).rows)
+
+
+@pytest.fixture(scope="module")
+def setup3():
+    """three logical shards; the queries below touch only the segments placed on shards 0 and 1"""
+    from pinot_amd.engine import GpuContext
+    tables = _tables()
+    multi = GpuContext(devices=[0, 0, 0])
+    single = GpuContext(0)
+    segs_m = [multi.pin(create_segment(f"m3g{i}", t, inverted=("c",)), hll_columns=("u",)) for i, t in enumerate(tables)]
+    segs_s = [single.pin(create_segment(f"s3g{i}", t, inverted=("c",))) for i, t in enumerate(tables)]
+    ora = [O.build_segment(f"o3g{i}", t, inverted=("c",)) for i, t in enumerate(tables)]
+    yield multi, single, segs_m, segs_s, ora
+    multi.close()
+    single.close()
+
+
+@pytest.mark.parametrize("sql", QUERIES[:6])
+def test_sharded_finalize_with_idle_shard(setup3, sql):
+    multi, single, segs_m, segs_s, ora = setup3
+    dev = [multi.segment_device(s) for s in segs_m]
+    # greedy by pinned rows over three shards: 400k -> 0, 250k -> 1, 300k -> 2, 120k -> 1
+    assert dev == [0, 1, 2, 1]
+    pick = [i for i, d in enumerate(dev) if d != 2]  # shard 2 holds none of the query's segments
+    q = parse_sql(sql)
+    r = multi.execute(q, [segs_m[i] for i in pick])
+    e = O.execute(q, [ora[i] for i in pick])
+    _rows_equal(reduce_groups(q, r.keys, r.aggs).rows, reduce_groups(q, e.keys, e.aggs).rows)
+    s = single.execute(q, [segs_s[i] for i in pick])
+    _rows_equal(reduce_groups(q, r.keys, r.aggs).rows, reduce_groups(q, s.keys, s.aggs).rows)
+    assert r.num_groups == s.num_groups
+    assert r.stats.num_devices == 2
+    # and over all three shards
+    r = multi.execute(q, segs_m)
+    e = O.execute(q, ora)
+    _rows_equal(reduce_groups(q, r.keys, r.aggs).rows, reduce_groups(q, e.keys, e.aggs).rows)
+    assert r.stats.num_devices == 3
+
+
+def _device_count():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif("_device_count() < 2")
+@pytest.mark.parametrize("transport", ["peer", "rccl"])
+def test_distinct_devices(transport):
+    """two real GPUs: both transports against the oracle (only on a multi-GPU node)"""
+    from pinot_amd.engine import GpuContext
+    tables = _tables()
+    multi = GpuContext(devices=[0, 1], transport=transport)
+    try:
+        segs = [multi.pin(create_segment(f"dd{i}", t, inverted=("c",)), hll_columns=("u",)) for i, t in enumerate(tables)]
+        ora = [O.build_segment(f"odd{i}", t, inverted=("c",)) for i, t in enumerate(tables)]
+        for sql in QUERIES[:6]:
+            q = parse_sql(sql)
+            r = multi.execute(q, segs)
+            e = O.execute(q, ora)
+            _rows_equal(reduce_groups(q, r.keys, r.aggs).rows, reduce_groups(q, e.keys, e.aggs).rows)
+            # one device idle: shard 1's keys finalise on device 0
+            on0 = [i for i, s in enumerate(segs) if multi.segment_device(s) == 0]
+            r = multi.execute(q, [segs[i] for i in on0])
+            e = O.execute(q, [ora[i] for i in on0])
+            _rows_equal(reduce_groups(q, r.keys, r.aggs).rows, reduce_groups(q, e.keys, e.aggs).rows)
+    finally:
+        multi.close()
 
 
 def test_phases_reported(setup):
