@@ -1,12 +1,12 @@
-// part_tiles.h -- the register-direct tile reader shared by the partitioned group-by's kernel A forms k_part_reg
-// (scan_partition_reg.hip) and k_part_wave (scan_partition_wave.hip).
+// part_tiles.h -- the register-direct tile reader of the partitioned group-by's kernel A (k_part_reg,
+// scan_partition_reg.hip).
 //
 // A workgroup walks its share of the launch's chunks in rounds; in a round each of its waves takes one tile of
 // kRegTileWords 64-doc words (2048 docs) and lane l owns the 32 CONSECUTIVE docs [32 l, 32 l + 32) of it, so its b-bit
 // values of any stream are exactly b whole dwords: ceil(b / 4) 16-byte buffer loads per stream straight into registers
 // (reg_load), decoded with compile-time bit positions (reg_decode).  decode() turns the tile into one 32-bit record
-// per doc -- ((key & kmask) << vbits) | value offset -- and the doc's partition index (key >> klo), 0xffff for a
-// missed or out-of-range doc, packed two per register.
+// per doc -- (key << (32 - klo)) + value offset -- and the doc's ring-word index (key >> klo, or the lane's scratch
+// word P + lane for a missed or out-of-range doc), packed two per register.
 #pragma once
 #include "reg_decode.h"
 
@@ -84,13 +84,15 @@ struct PartTiles {
     }
   }
 
-  // decode the loaded tile: keys into X (mixed radix), the filter reads the partition indices off them into PB, then
-  // the value phase turns each key into its record in place (peak: 48 registers + the loads)
+  // decode the loaded tile: keys into X (mixed radix), the filter turns each into its 16-bit ring-word index in PB
+  // (the partition key >> klo, or the lane's scratch word P + lane for a missed doc), then the value phase turns each
+  // key into its record in place, (key << (32 - klo)) + value offset: the shift drops the partition bits, and kernel B
+  // reads the key as record >> (32 - klo) (peak: 48 registers + the loads)
   __device__ void decode(const Tile& t, int lane, uint32_t (&X)[32], uint32_t (&PB)[16]) const {
-    const uint32_t klo = (uint32_t)p.part_klo, kmask = (1u << klo) - 1u, vbits = (uint32_t)p.part_vbits;
-    const int32_t nv = t.ndoc > 0 ? max(0, min(32, t.ndoc - lane * 32)) : 0;  // this lane's valid docs
+    const uint32_t klo = (uint32_t)p.part_klo, rsh = 32u - klo;
+    const uint32_t dummy = (uint32_t)p.num_parts + (uint32_t)lane;
     if (t.ndoc <= 0) {
-      static_for<0, 16>([&](auto j) { PB[j] = 0xffffffffu; });
+      static_for<0, 16>([&](auto j) { PB[j] = dummy | (dummy << 16); });
       return;
     }
     SegPtr S = t.S;
@@ -100,10 +102,9 @@ struct PartTiles {
       if (g == 0) reg_decode<CK>(pk[g], S->streams[p.g_stream[g]].bits, [&](auto j, uint32_t v) { X[j] = __umul24(v, st); });
       else reg_decode<CK>(pk[g], S->streams[p.g_stream[g]].bits, [&](auto j, uint32_t v) { X[j] += __umul24(v, st); });
     }
-    // filter + doc validity -> the partition index (0xffff: no record)
     auto put = [&](auto j, bool pass) {
       constexpr int J = decltype(j)::value;
-      const uint32_t b = pass && J < nv ? (X[J] >> klo) : 0xffffu;
+      const uint32_t b = pass ? (X[J] >> klo) : dummy;
       if constexpr ((J & 1) == 0) PB[J >> 1] = b;
       else PB[J >> 1] |= b << 16;
     };
@@ -117,12 +118,18 @@ struct PartTiles {
     } else {
       static_for<0, 32>([&](auto j) { put(j, true); });
     }
+    if (t.ndoc < 64 * kRegTileWords) {  // a segment's last tile (wave-uniform): docs past its end append nothing
+      const int32_t nv = t.ndoc - lane * 32;
+      static_for<0, 32>([&](auto j) {
+        constexpr int J = decltype(j)::value;
+        if (J >= nv) PB[J >> 1] = (J & 1) ? ((PB[J >> 1] & 0xffffu) | (dummy << 16)) : ((PB[J >> 1] & 0xffff0000u) | dummy);
+      });
+    }
     if constexpr (HASV != 0) {
       const uint32_t vadd = (uint32_t)(S->vals[0].base - p.part_vbase);
-      reg_decode<CV>(pv, S->streams[p.v_stream[0]].bits,
-                     [&](auto j, uint32_t v) { X[j] = ((X[j] & kmask) << vbits) | (v + vadd); });
+      reg_decode<CV>(pv, S->streams[p.v_stream[0]].bits, [&](auto j, uint32_t v) { X[j] = (X[j] << rsh) + (v + vadd); });
     } else {
-      static_for<0, 32>([&](auto j) { X[j] &= kmask; });
+      static_for<0, 32>([&](auto j) { X[j] <<= rsh; });
     }
   }
 };

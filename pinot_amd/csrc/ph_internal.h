@@ -230,9 +230,6 @@ struct KParams {
   int32_t stage_stride;           // bytes of one wave's staging area
   int32_t tile_words;             // 64-doc words per wave tile
   int32_t late_prefetch;          // decode gathers from HBM: issue the next tile's loads after it
-  int32_t dbg_flags;              // PH_DEBUG_FLAGS (timing experiments only; results are wrong when set):
-                                  // 1 no record stores, 2 no flush, 4 no record append
-  unsigned long long* dbg;        // PH_DEBUG_STAMPS: per-workgroup cycle totals [grid][4] (wave 0)
   int32_t stage_soff[kMaxStage];  // byte offset of staged stream s inside a wave's area
   int32_t lds_cnt_off;            // MODE_GROUP_LDS: byte offset of the count table (MODE_GROUP_GLOBAL: cache counts)
   int32_t gc_slots;               // MODE_GROUP_GLOBAL: LDS group cache slots (power of 2; 0 = off)
@@ -272,7 +269,6 @@ struct KParams {
   int32_t part_vbits;             // value-offset bits in a record (0: COUNT only)
   int32_t num_parts;
   int32_t part_load_first;        // lean kernel A: issue the next tile's loads before the flush (tuning)
-  int32_t part_dbg;               // lean kernel A timing experiments (PH_PART_DBG; results invalid when set)
   int32_t agg_fast;               // MODE_AGG: run k_agg_lean
   int32_t agg_sparse;             // MODE_AGG over selective bitmap leaves: run k_agg_sparse
   int32_t sparse_c;               // sparse kernels over sp_reg segments: 16-byte loads per lane of a leaf (4 or 8)
@@ -289,9 +285,7 @@ struct KParams {
   int32_t part_fast;              // kernel A may run the lean k_part_scan (no gathers; ALL / RANGE / DOCRANGE leaves)
   int32_t part_depth;             // lean kernel A: tiles of loads in flight per wave (1: k_part_scan, 2: k_part_scan2)
   int32_t part_reg;               // kernel A = k_part_reg (register-direct decode; 0: the LDS-staged forms)
-  int32_t part_wave;              // with part_reg: k_part_wave (wave-private rings, no workgroup barriers)
   int32_t part_ck, part_cv;       // k_part_reg: 16-byte loads per lane of a filter / key stream, of the value stream
-  int32_t part_rounds;            // k_part_reg: append rounds (flush + barrier) per tile (1 or 2)
   int32_t count_reg;              // MODE_COUNT: k_count_reg with this many 16-byte loads per lane (ceil(b / 4)); 0 off
   int32_t agg_reg;                // MODE_AGG: k_agg_reg (register-direct k_agg_lean)
   int32_t agg_reg_cf, agg_reg_cv; //   16-byte loads per lane of the filter / value stream
@@ -299,8 +293,6 @@ struct KParams {
   int32_t group_sparse;           // MODE_GROUP_LDS / GLOBAL: k_group_sparse (selective bitmap ANDs, DevSegment sp_*)
   int32_t group_reg_lanes_log2;   //   log2 of the slots per key (lane l updates slot key * L + (l & (L - 1)))
   int32_t group_reg_cf, group_reg_cg, group_reg_cv;  // 16-byte loads per lane: filter / each group / value stream
-  int32_t part_variant;           // k_part_reg append form: bit 0 ring quarters XOR-swizzled by partition, bit 1
-                                  // record-less lanes exec-masked (else they add to a per-lane scratch word / slot)
   unsigned long long* ovf_count;  // overflow table (same layout as out_*), merged at the end
   int64_t* ovf_sum;
   int64_t* ovf_min;
@@ -321,7 +313,7 @@ struct PartAggParams {
   int32_t has_sum, has_min, has_max;
   int32_t pack_cs;        // count and value-offset sum share one 64-bit LDS word (count << 40 | sum)
   int32_t slices;         // workgroups per partition (each aggregates a contiguous range of the regions)
-  int32_t dbg;            // timing experiments (PH_PART_DBG bits 4: loads only, 8: no MIN/MAX); results invalid
+  int32_t dbg_unused;     // (layout pad)
   int32_t mm_blind;       // MIN / MAX as one atomic per record each (else read first, atomic only on improvement)
   int32_t pad;
   int64_t part_vbase;
@@ -587,9 +579,6 @@ size_t part_agg_lds_bytes(const PartAggParams& p);
 size_t partition_lds_bytes(KParams& p);  // fills the pl_* offsets, returns the dynamic LDS size
 int part_reg_blocks_per_cu(const KParams& p, int ng, size_t lds);  // k_part_reg occupancy
 void launch_part_reg(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);  // scan_partition_reg.hip
-size_t part_wave_lds_bytes(int32_t num_parts);                                        // scan_partition_wave.hip
-int part_wave_blocks_per_cu(const KParams& p, int ng, size_t lds);
-void launch_part_wave(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);
 void launch_count_reg(const KParams& p, int grid, hipStream_t s);                      // scan_count_reg.hip
 void launch_agg_reg(const KParams& p, int grid, hipStream_t s);                        // scan_count_reg.hip
 void launch_group_reg(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);   // scan_group_reg.hip

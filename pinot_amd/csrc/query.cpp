@@ -2000,12 +2000,6 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       kp.agg_reg_cv = (vb + 3) / 4;
     }
   }
-  if (const char* e = getenv("PH_DEBUG_FLAGS")) kp.dbg_flags = atoi(e);
-  if (kp.dbg_flags) kp.part_fast = kp.agg_fast = kp.lds_fast = kp.agg_sparse = kp.count_reg = kp.agg_reg = 0;
-  if (getenv("PH_DEBUG_STAMPS")) {
-    kp.dbg = scratch.alloc<unsigned long long>(4 * (size_t)ctx->num_cus * 8);
-    PH_HIP_CHECK(hipMemsetAsync(kp.dbg, 0, 32 * (size_t)ctx->num_cus * 8, st));
-  }
   const size_t stage_bytes = (size_t)(mode == MODE_PARTITION ? kPartWaves : kWaves) * kp.stage_stride;
   size_t lds = 0;
   if (mode == MODE_PARTITION) {
@@ -2065,7 +2059,6 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           kp.group_reg_cf = cf;
           kp.group_reg_cg = cg;
           kp.group_reg_cv = cv;
-          kp.part_dbg = getenv("PH_GROUP_REG_DBG") ? atoi(getenv("PH_GROUP_REG_DBG")) : 0;  // timing experiments
           lds = (size_t)(G + 1) * 16 << lg;
         }
       }
@@ -2348,7 +2341,6 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       // the next tile's loads go out before the flush (r2: 3.78 vs 4.39 ms on one box); PH_PART_FLUSH_FIRST
       // restores the r1 order
       kp.part_load_first = getenv("PH_PART_FLUSH_FIRST") == nullptr;
-      kp.part_dbg = getenv("PH_PART_DBG") ? atoi(getenv("PH_PART_DBG")) : 0;  // timing experiments only
       kp.part_depth = 1;
       if (const char* e = getenv("PH_PART_DEPTH")) kp.part_depth = atoi(e) == 2 ? 2 : 1;  // tuning knob
       // register-direct kernel A (k_part_reg): 32-bit records, <= 3 key columns, filter / key streams <= 16 bits
@@ -2365,28 +2357,19 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           kp.part_reg = 1;
           kp.part_ck = (kb <= 12 && vb <= 20) ? 3 : 4;
           kp.part_cv = kp.part_ck == 3 ? 5 : 8;
-          kp.part_rounds = 2;  // two append rounds per 2048-doc tile: ~8 records per partition per round
-          if (const char* e = getenv("PH_PART_ROUNDS")) kp.part_rounds = atoi(e) == 1 ? 1 : 2;  // tuning knob
-          kp.part_variant = 0;
-          if (const char* e = getenv("PH_PART_VARIANT")) kp.part_variant = atoi(e) & 3;  // tuning knob
           kp.stage_stride = 0;  // no staging
         }
       }
       stats.scan_kernel = !kp.part_fast ? PH_KERNEL_PART_SCAN
                           : kp.part_reg ? PH_KERNEL_PART_REG
                           : kp.part_depth == 2 ? PH_KERNEL_PART_LEAN2 : PH_KERNEL_PART_LEAN;
-      kp.part_vbits = vbits;
+      // record = (key << vbits) | value offset, with vbits = 32 - klo in k_part_reg's form ((key << (32 - klo)) + value
+      // offset: the shift itself drops the partition bits); the LDS-staged forms keep the key's low klo bits masked
+      kp.part_vbits = kp.part_reg ? 32 - klo : vbits;
       kp.num_parts = (int32_t)P;
-      // k_part_wave: the register-direct kernel A with wave-private rings (no workgroup barriers); opt-in
-      // (PH_PART_WAVE=1): measured on config 3 it runs 4.6 ms against k_part_reg's 3.6 (8 waves per CU, LDS-bound)
-      kp.part_wave = 0;
-      if (const char* e = getenv("PH_PART_WAVE")) kp.part_wave = kp.part_reg && atoi(e) != 0 &&
-                                                                 part_wave_lds_bytes((int32_t)P) <= 160 * 1024;
-      if (kp.part_wave) stats.scan_kernel = PH_KERNEL_PART_WAVE;
-      const size_t lds_a = kp.part_wave ? part_wave_lds_bytes((int32_t)P) : partition_lds_bytes(kp);
+      const size_t lds_a = partition_lds_bytes(kp);
       int a_cap = 4;  // 8-wave workgroups: <= 4 per CU (32 waves)
-      if (kp.part_wave) a_cap = part_wave_blocks_per_cu(kp, q->num_group_by, lds_a);
-      else if (kp.part_reg) a_cap = part_reg_blocks_per_cu(kp, q->num_group_by, lds_a);  // 4-wave groups, VGPR-bound
+      if (kp.part_reg) a_cap = part_reg_blocks_per_cu(kp, q->num_group_by, lds_a);  // 4-wave groups, VGPR-bound
       if (const char* e = getenv("PH_PART_WG_PER_CU")) a_cap = std::max(1, std::min(8, atoi(e)));  // tuning knob
       const int a_per_cu = (int)std::max<size_t>(1, std::min<size_t>(a_cap, (160 * 1024) / lds_a));
       const int grid_a = ctx->num_cus * a_per_cu;
@@ -2440,7 +2423,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       bp.num_parts = (int32_t)P;
       bp.part_cap = (int32_t)cap;
       bp.part_klo = klo;
-      bp.part_vbits = vbits;
+      bp.part_vbits = kp.part_vbits;
       bp.rec64 = rec64;
       bp.has_sum = has_sum;
       bp.has_min = has_min;
@@ -2457,7 +2440,6 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       int slices = (int)std::max<int64_t>(1, std::min<int64_t>(8, (int64_t)ctx->num_cus / P));
       if (const char* e = getenv("PH_PART_SLICES")) slices = std::max(1, std::min(16, atoi(e)));  // tuning knob
       bp.slices = slices;
-      bp.dbg = kp.part_dbg;
       bp.mm_blind = getenv("PH_PART_MM_BLIND") ? atoi(getenv("PH_PART_MM_BLIND")) : 0;  // tuning knob
       bp.regions = grid_a;
       const size_t lds_b = part_agg_lds_bytes(bp);
@@ -2735,19 +2717,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     stamp("launched");
     timed = true;
-    if (!defer_sync || kp.dbg) {
+    if (!defer_sync) {
       PH_HIP_CHECK(hipStreamSynchronize(st));  // staging buffer reuse + results
       stamp("kernels done");
       dev_ms = device_elapsed();
-    }
-    if (kp.dbg) {  // PH_DEBUG_STAMPS: where wave 0 of each workgroup spent its cycles (last launch)
-      std::vector<unsigned long long> h(4 * (size_t)ctx->num_cus * 8);
-      PH_HIP_CHECK(hipMemcpy(h.data(), kp.dbg, 8 * h.size(), hipMemcpyDeviceToHost));
-      double a = 0, b = 0, c = 0, n = 0;
-      for (size_t i = 0; i < h.size(); i += 4)
-        if (h[i + 3]) { a += h[i]; b += h[i + 1]; c += h[i + 2]; n += 1; }
-      if (n) fprintf(stderr, "[ph stamps] mode %d workgroups %.0f: stage %.0f  decode %.0f  sync/flush %.0f cycles avg\n",
-                     mode, n, a / n, b / n, c / n);
     }
   } else {
     PH_HIP_CHECK(hipStreamSynchronize(st));
@@ -2821,7 +2794,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   };
   // after the first sync of the result path: the deferred scan timing and group-by statistics
   auto resolve_deferred = [&]() {
-    if (defer_sync && !kp.dbg && timed) {
+    if (defer_sync && timed) {
       stamp("kernels done");
       dev_ms = device_elapsed();
       stats.device_ms = dev_ms;

@@ -92,7 +92,6 @@ __global__ void __launch_bounds__(kBlock) k_group_reg(const KParams p) {
     }
   };
   unsigned long long matched = 0;  // per lane
-  uint32_t sink = 0;
   // one register set of loads: a tile's streams are unpacked into the match mask, the 32 slot indices and the 32
   // value offsets, then the next tile's loads are issued and run under this tile's LDS atomics
   Pool pl;
@@ -144,10 +143,7 @@ __global__ void __launch_bounds__(kBlock) k_group_reg(const KParams p) {
     load(t, pl);
     // branch-free atomics: a missed doc updates the dummy row (key G), whose L slots are as conflict-free as any
     // key's, so no exec-mask juggling per doc; the atomics return nothing and never stall the wave
-    if (p.part_dbg & 1) {  // PH_GROUP_REG_DBG=1 timing experiment: no atomics (results invalid)
-#pragma unroll
-      for (int j = 0; j < 32; ++j) sink ^= key[j] + tmp[j];
-    } else if (any) {
+    if (any) {
       auto run = [&](auto mmode) {
         constexpr int MM = decltype(mmode)::value;
 #pragma unroll
@@ -170,7 +166,6 @@ __global__ void __launch_bounds__(kBlock) k_group_reg(const KParams p) {
       else run(std::integral_constant<int, 3>{});
     }
   }
-  if (sink == 0x5bd1e995u) p.out_count[0] += 1;  // keeps PH_GROUP_REG_DBG's decode alive
   const int64_t mt = wave_sum_i64((int64_t)matched);
   if (lane == 0 && mt && p.matched_total) atomicAdd(p.matched_total, (unsigned long long)mt);
   __syncthreads();

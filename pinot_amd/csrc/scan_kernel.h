@@ -748,7 +748,7 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
 #pragma unroll
       for (int q = 0; q < UB; ++q) tot += (uint32_t)__popcll(__ballot(hit[q]));
       acc.matched += tot;
-      if (tot == 0 || (p.dbg_flags & 4)) continue;
+      if (tot == 0) continue;
       uint32_t bk[UB], rk[UB], rf[UB];
       Rec rec[UB];
 #pragma unroll
@@ -764,9 +764,8 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
           if (LATE && gremap[g]) id = (uint32_t)gld(gremap[g] + id);
           key += id * (uint32_t)p.group_stride[g];
         }
-        if (p.dbg_flags & 16) key = ((uint32_t)lane * 16411u + (uint32_t)(u + q) * 977u) % (uint32_t)p.num_groups;  // timing only: no key decode
         uint32_t vo = 0;
-        if (p.num_vals && !(p.dbg_flags & 16)) {
+        if (p.num_vals) {
           int64_t iv;
           double dv;
           if (LATE) read_value(vkind[0], vbase[0], vtab[0], cursor_value(vcur[0], u + q), iv, dv);
@@ -776,8 +775,7 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
         bk[q] = key >> p.part_klo;
         rec[q] = REC64 ? (Rec)(((unsigned long long)(key & kmask) << 32) | vo) : (Rec)(((key & kmask) << p.part_vbits) | vo);
         if (hit[q]) {
-          // flag 8 (timing only): no rank atomic
-          const uint32_t w = (p.dbg_flags & 8) ? 0u : atomicAdd(&words[bk[q]], 1u);
+          const uint32_t w = atomicAdd(&words[bk[q]], 1u);
           rf[q] = (w >> 16) * CH;  // flushed ranks
           rk[q] = w & 0xffffu;     // pending before this record
         }
@@ -919,16 +917,13 @@ __global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : kBlock) 
   locate();
   if (c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
 
-  unsigned long long t_stage = 0, t_proc = 0, t_sync = 0, t0 = 0, t1 = 0;
-  const bool stamps = p.dbg != nullptr;
   while (c < c_end) {
-    if (stamps) t0 = __builtin_readcyclecounter();
     // stage the prefetched tile, then prefetch the next one of this wave
     tile_store<NL>(S, nvalid, wst, lane, pf);
     if (MODE == MODE_PARTITION) {
       // flush the chunks completed in the previous round here, before this round's prefetch: the stores
       // then complete under the decode instead of stalling the next tile_store (stores count in vmcnt too)
-      if (!(p.dbg_flags & 2)) part_flush<REC64, BLOCK>(p, smem, false);
+      part_flush<REC64, BLOCK>(p, smem, false);
       lds_barrier();  // ring words are final before anyone appends again
     }
     SegPtr cs = S;
@@ -940,11 +935,6 @@ __global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : kBlock) 
     if (!LATE && c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (stamps) {
-      t1 = __builtin_readcyclecounter();
-      t_stage += t1 - t0;
-      t0 = t1;
-    }
 
     if (cnvalid > 0) {
       switch (cs->fkind) {
@@ -960,21 +950,7 @@ __global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : kBlock) 
       }
     }
     if (LATE && c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
-    if (stamps) {
-      t1 = __builtin_readcyclecounter();
-      t_proc += t1 - t0;
-      t0 = t1;
-    }
-    if (MODE == MODE_PARTITION) {
-      lds_barrier();  // this round's appends are complete before the next round's flush check
-      if (stamps) t_sync += __builtin_readcyclecounter() - t0;
-    }
-  }
-  if (stamps && threadIdx.x == 0) {
-    p.dbg[4 * blockIdx.x + 0] = t_stage;
-    p.dbg[4 * blockIdx.x + 1] = t_proc;
-    p.dbg[4 * blockIdx.x + 2] = t_sync;
-    p.dbg[4 * blockIdx.x + 3] = 1;
+    if (MODE == MODE_PARTITION) lds_barrier();  // this round's appends are complete before the next round's flush check
   }
 
   // ---- workgroup epilogue

@@ -12,11 +12,9 @@ namespace ph {
 // position with 16-byte stores, and the < 16 leftovers move to the front of the ring.  Every lane reads before
 // any lane of its wave writes (LDS ops of a wave execute in order), so a leftover never overwrites a record still
 // to be stored.  `matched` gains the appends that went to the overflow table (a full ring).
-// SWZ (k_part_reg): a ring's 16-byte quarters are XOR-swizzled by the partition (ring_swizzle), so the appends of
-// lanes at the same pending count in different partitions hit different LDS banks.
-__device__ __forceinline__ uint32_t ring_swizzle(uint32_t b, uint32_t C) { return (b & ((C >> 2) - 1u)) << 2; }
-
-template <int REC64, int BLOCK, int SWZ = 0>
+// SWEEP (k_part_reg): no list -- every partition's word is read (flist unused, nlisted = P) and a partition with
+// fewer than 16 pending records is skipped.
+template <int REC64, int BLOCK, int SWEEP = 0>
 __device__ __forceinline__ void part_flush_listed(const KParams& p, uint8_t* smem, const uint32_t* flist, uint32_t nlisted,
                                   unsigned long long& matched) {
   using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
@@ -30,21 +28,21 @@ __device__ __forceinline__ void part_flush_listed(const KParams& p, uint8_t* sme
   const uint32_t cap = (uint32_t)p.part_cap;
   const uint32_t total = nlisted * 8u;
   for (uint32_t t = threadIdx.x; t < total; t += BLOCK) {
-    const uint32_t b = flist[t >> 3], i = t & 7u;
+    const uint32_t b = SWEEP ? (t >> 3) : flist[t >> 3], i = t & 7u;
     const uint32_t raw = pend[b];
+    if (SWEEP && raw < CH) continue;  // no whole chunk pending (uniform over the partition's 8 lanes)
     const uint32_t n = min(raw, C);  // records beyond C went to the overflow table
     const uint32_t out = n & ~(CH - 1u), left = n - out;
     const uint32_t g = gpos[b];
     Rec* ring = slots + ((size_t)b << cl);
-    const uint32_t sw = (SWZ && (p.part_variant & 1)) ? ring_swizzle(b, C) : 0u;  // physical = logical ^ sw
     // reads: quarters i and i + 8 of the outgoing records (C / PQ <= 16), leftovers i and i + 8 (< CH <= 16)
     u32x4 q0 = {0u, 0u, 0u, 0u}, q1 = {0u, 0u, 0u, 0u};
     const uint32_t r0 = i * PQ, r1 = (i + 8u) * PQ;
-    if (r0 < out) q0 = *reinterpret_cast<const u32x4*>(ring + (r0 ^ sw));
-    if (r1 < out) q1 = *reinterpret_cast<const u32x4*>(ring + (r1 ^ sw));
+    if (r0 < out) q0 = *reinterpret_cast<const u32x4*>(ring + r0);
+    if (r1 < out) q1 = *reinterpret_cast<const u32x4*>(ring + r1);
     Rec l0 = 0, l1 = 0;
-    if (i < left) l0 = ring[(out + i) ^ sw];
-    if (i + 8u < left) l1 = ring[(out + i + 8u) ^ sw];
+    if (i < left) l0 = ring[out + i];
+    if (i + 8u < left) l1 = ring[out + i + 8u];
     // writes
     Rec* region = reinterpret_cast<Rec*>(p.part_buf) + part_region(p, b, blockIdx.x) * (size_t)cap;
     if (r0 < out) {
@@ -63,8 +61,8 @@ __device__ __forceinline__ void part_flush_listed(const KParams& p, uint8_t* sme
         for (uint32_t k = 0; k < PQ; ++k) part_store<REC64>(p, b, g + r1 + k, e[k]);
       }
     }
-    if (i < left) ring[i ^ sw] = l0;
-    if (i + 8u < left) ring[(i + 8u) ^ sw] = l1;
+    if (i < left) ring[i] = l0;
+    if (i + 8u < left) ring[i + 8u] = l1;
     if (i == 0) {
       pend[b] = left;
       gpos[b] = g + out;
@@ -75,7 +73,7 @@ __device__ __forceinline__ void part_flush_listed(const KParams& p, uint8_t* sme
 
 // Final flush of the lean kernel (after the last listed flush): every partition's < 16 pending records, the
 // region record counts, and the matched docs = the regions' records (overflow appends counted already).
-template <int REC64, int BLOCK, int SWZ = 0>
+template <int REC64, int BLOCK>
 __device__ __forceinline__ void part_flush_final(const KParams& p, uint8_t* smem, unsigned long long& matched) {
   using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
   const Rec* slots = reinterpret_cast<const Rec*>(smem + p.pl_slot_off);
@@ -86,13 +84,18 @@ __device__ __forceinline__ void part_flush_final(const KParams& p, uint8_t* smem
   for (uint32_t t = threadIdx.x; t < total; t += BLOCK) {
     const uint32_t b = t >> 4, i = t & 15u;
     const uint32_t n = pend[b], g = gpos[b];  // n < 16 after the listed flushes
-    const uint32_t sw = (SWZ && (p.part_variant & 1)) ? ring_swizzle(b, 1u << cl) : 0u;
-    if (i < n) part_store<REC64>(p, b, g + i, slots[((size_t)b << cl) + (i ^ sw)]);
+    if (i < n) part_store<REC64>(p, b, g + i, slots[((size_t)b << cl) + i]);
     if (i == 0) {
       p.part_count[(size_t)b * gridDim.x + blockIdx.x] = g + n;  // records of region (b, blockIdx)
       matched += g + n;
     }
   }
+}
+
+// the register-direct kernel A's flush: every partition with a whole pending chunk
+template <int BLOCK>
+__device__ __forceinline__ void part_flush_sweep(const KParams& p, uint8_t* smem, unsigned long long& matched) {
+  part_flush_listed<0, BLOCK, 1>(p, smem, nullptr, (uint32_t)p.num_parts, matched);
 }
 
 }  // namespace ph

@@ -73,7 +73,6 @@ __device__ __forceinline__ void part_tile(const KParams& p, SegPtr S, uint8_t* s
   const uint32_t dummy_word = (uint32_t)p.num_parts + (uint32_t)lane;
   const uint32_t dummy_slot = ((uint32_t)p.num_parts << cl) + (uint32_t)lane;
   uint32_t doc = (uint32_t)w0 * 64u + (uint32_t)lane;
-  const int dbg = p.part_dbg;  // timing experiments: 1 = no key/value decode, 2 = no appends
   for (int u = 0; u < nvalid; u += 4) {
     bool h[4];
     uint32_t widx[4], bk[4];
@@ -83,16 +82,10 @@ __device__ __forceinline__ void part_tile(const KParams& p, SegPtr S, uint8_t* s
       bool hh = (u + q < nvalid) & (doc < ndocs);
       if constexpr (FK == FK_RANGE) hh &= (lds_value(fs.off, fs.rsh, fs.mask) - flo) < flen;
       if constexpr (FK == FK_DOCRANGE) hh &= (doc - flo) < flen;
-      if (dbg & 2) hh = false;
       uint32_t key = 0;
-      uint32_t vo = 0;
-      if (!(dbg & 1)) {
 #pragma unroll
-        for (int g = 0; g < NG; ++g) key += __umul24(lds_value(gs[g].off, gs[g].rsh, gs[g].mask), gstr[g]);  // keys < 2^22
-        vo = HASV ? lds_value(vs.off, vs.rsh, vs.mask) + vadd : 0u;
-      } else {
-        key = ((doc * 2654435761u) >> 8) % ((uint32_t)p.num_parts << klo);  // in range, spread like real keys
-      }
+      for (int g = 0; g < NG; ++g) key += __umul24(lds_value(gs[g].off, gs[g].rsh, gs[g].mask), gstr[g]);  // keys < 2^22
+      const uint32_t vo = HASV ? lds_value(vs.off, vs.rsh, vs.mask) + vadd : 0u;
 #pragma unroll
       for (int g = 0; g < NG; ++g) gs[g].off += gs[g].step;
       if (HASV) vs.off += vs.step;
@@ -177,10 +170,7 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
   Prefetch<NL> pf;
   locate();
   if (c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
-  unsigned long long t_stage = 0, t_proc = 0, t_sync = 0, t0 = 0, t1 = 0;
-  const bool stamps = p.dbg != nullptr;
   while (c < c_end) {
-    if (stamps) t0 = __builtin_readcyclecounter();
     tile_store<NL>(S, nvalid, wst, lane, pf);
     SegPtr cs = S;
     const int32_t cw0 = w0, cnvalid = nvalid;
@@ -200,11 +190,6 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
     if (!load_first && c < c_end) tile_load<NL>(S, w0, nvalid, lane, pf);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (stamps) {
-      t1 = __builtin_readcyclecounter();
-      t_stage += t1 - t0;
-      t0 = t1;
-    }
     if (cnvalid > 0) {
       const int fk = cs->fkind;
       uint32_t* fl = lists + par * p.num_parts;
@@ -213,20 +198,8 @@ __global__ void __launch_bounds__(kPartBlock) k_part_scan(const KParams p) {
       else if (fk == FK_DOCRANGE) part_tile<NG, REC64, HASV, FK_DOCRANGE>(p, cs, smem, wst_off, lane, cw0, cnvalid, fl, fc);
       else part_tile<NG, REC64, HASV, FK_ALL>(p, cs, smem, wst_off, lane, cw0, cnvalid, fl, fc);
     }
-    if (stamps) {
-      t1 = __builtin_readcyclecounter();
-      t_proc += t1 - t0;
-      t0 = t1;
-    }
     lds_barrier();  // this round's appends are complete before the next round's flush
     par ^= 1u;
-    if (stamps) t_sync += __builtin_readcyclecounter() - t0;
-  }
-  if (stamps && threadIdx.x == 0) {
-    p.dbg[4 * blockIdx.x + 0] = t_stage;
-    p.dbg[4 * blockIdx.x + 1] = t_proc;
-    p.dbg[4 * blockIdx.x + 2] = t_sync;
-    p.dbg[4 * blockIdx.x + 3] = 1;
   }
   part_flush_listed<REC64, kPartBlock>(p, smem, lists + (par ^ 1u) * p.num_parts, lcnt[par ^ 1u], matched);
   lds_barrier();
@@ -363,8 +336,7 @@ static void launch_part_fast_ng(const KParams& p, int rec64, int grid, size_t ld
 
 void launch_scan_partition(const KParams& p, int ng, int rec64, int grid, size_t lds, hipStream_t s) {
   if (p.part_reg) {
-    if (p.part_wave) launch_part_wave(p, ng, grid, lds, s);
-    else launch_part_reg(p, ng, grid, lds, s);
+    launch_part_reg(p, ng, grid, lds, s);
     return;
   }
   if (!p.part_fast) {
@@ -434,7 +406,6 @@ __global__ void __launch_bounds__(1024) k_part_agg(const PartAggParams p) {
   constexpr uint32_t SPAN = 64 * PER;             // records per wave-load
   using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
   const Rec* buf = reinterpret_cast<const Rec*>(p.part_buf);
-  unsigned long long sink = 0;  // PH_PART_DBG & 4 (loads only)
   for (int b0 = wave * RPW; b0 < NR; b0 += nwaves * RPW) {
     uint32_t nn[RPW];
     uint32_t maxn = 0;
@@ -471,12 +442,10 @@ __global__ void __launch_bounds__(1024) k_part_agg(const PartAggParams p) {
             k = (uint32_t)r >> p.part_vbits;
             x = (uint32_t)r & vmask;
           }
-          if (p.dbg & 4) sink ^= r;
           rk[q * PER + e] = (i0 + e < nn[q]) ? k : KP + (uint32_t)lane;
           rv[q * PER + e] = x;
         }
       }
-      if (p.dbg & 4) continue;
       constexpr int NREC = RPW * PER;
 #pragma unroll
       for (int i = 0; i < NREC; ++i) {
@@ -487,7 +456,7 @@ __global__ void __launch_bounds__(1024) k_part_agg(const PartAggParams p) {
           if (p.has_sum) atomicAdd(&sum[rk[i]], (unsigned long long)rv[i]);
         }
       }
-      if ((p.has_min | p.has_max) && !(p.dbg & 8)) {
+      if (p.has_min | p.has_max) {
         if (p.mm_blind) {  // every record issues its MIN / MAX atomics (no return: nothing waits)
 #pragma unroll
           for (int i = 0; i < NREC; ++i) {
@@ -507,7 +476,6 @@ __global__ void __launch_bounds__(1024) k_part_agg(const PartAggParams p) {
       }
     }
   }
-  if (sink == 0x5bd1e9955bd1e995ull) p.out_count[0] += 1;  // keeps the loads of PH_PART_DBG & 4 alive
   __syncthreads();
   const bool shared_range = p.slices > 1;
   for (uint32_t k = threadIdx.x; k < KP; k += blockDim.x) {

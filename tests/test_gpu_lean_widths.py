@@ -27,7 +27,7 @@ from tests.seeds import seed_of
 pytestmark = pytest.mark.gpu
 
 PH_KERNEL_AGG_LEAN, PH_KERNEL_GROUP_LDS_LEAN, PH_KERNEL_PART_LEAN, PH_KERNEL_PART_LEAN2, PH_KERNEL_PART_REG = 2, 4, 5, 6, 8
-PH_KERNEL_COUNT_REG, PH_KERNEL_AGG_REG, PH_KERNEL_GROUP_REG, PH_KERNEL_PART_WAVE = 9, 10, 11, 13
+PH_KERNEL_COUNT_REG, PH_KERNEL_AGG_REG, PH_KERNEL_GROUP_REG = 9, 10, 11
 
 
 @pytest.fixture(scope="module")
@@ -109,15 +109,10 @@ def test_lean_kernels_every_width(ctx, w, monkeypatch):
     monkeypatch.delenv("PH_LDS_LEAN")
     part = (f"SET numGroupsLimit=2000000; SELECT g1, g2, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where} "
             f"GROUP BY g1, g2 ORDER BY g1, g2 LIMIT 200000")
-    # k_part_reg / k_part_wave decode from registers (their own per-width switch): filter / key streams <= 16 bits
+    # k_part_reg decodes from registers (its own per-width switch): filter / key streams <= 16 bits
     _check(ctx, gpu, ora, part, PH_KERNEL_PART_REG if min(w, 24) <= 16 else PH_KERNEL_PART_LEAN)
-    monkeypatch.setenv("PH_PART_WAVE", "1")  # wave-private rings (opt-in)
-    _check(ctx, gpu, ora, part, PH_KERNEL_PART_WAVE if min(w, 24) <= 16 else PH_KERNEL_PART_LEAN)
-    monkeypatch.delenv("PH_PART_WAVE")
-    monkeypatch.setenv("PH_PART_ROUNDS", "1")  # one append round per tile (64-slot rings)
-    monkeypatch.setenv("PH_PART_RING_LOG2", "6")
+    monkeypatch.setenv("PH_PART_RING_LOG2", "4")  # 16-slot rings: skewed rounds take the overflow path
     _check(ctx, gpu, ora, part, PH_KERNEL_PART_REG if min(w, 24) <= 16 else PH_KERNEL_PART_LEAN)
-    monkeypatch.delenv("PH_PART_ROUNDS")
     monkeypatch.delenv("PH_PART_RING_LOG2")
     monkeypatch.setenv("PH_PART_LDS", "1")  # the LDS-staged forms
     _check(ctx, gpu, ora, part, PH_KERNEL_PART_LEAN)

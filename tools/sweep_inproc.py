@@ -34,10 +34,11 @@ def main():
         for kv in (s.split(",") if s != "-" else []):
             k, v = kv.split("=", 1)
             os.environ[k] = v
-        for _ in range(2):
+        iters = int(os.environ.get("SWEEP_ITERS", "8"))
+        for _ in range(2 if iters > 1 else 0):
             r = ctx.execute(q, pinned, copy=False)
         ms = []
-        for _ in range(8):
+        for _ in range(iters):
             r = ctx.execute(q, pinned, copy=False)
             ms.append(r.stats.device_ms)
         sig = (r.num_groups, float(np.sum(r.agg_columns[0])) if r.agg_columns else 0.0)
