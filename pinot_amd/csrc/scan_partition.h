@@ -12,9 +12,7 @@ namespace ph {
 // position with 16-byte stores, and the < 16 leftovers move to the front of the ring.  Every lane reads before
 // any lane of its wave writes (LDS ops of a wave execute in order), so a leftover never overwrites a record still
 // to be stored.  `matched` gains the appends that went to the overflow table (a full ring).
-// SWEEP (k_part_reg): no list -- every partition's word is read (flist unused, nlisted = P) and a partition with
-// fewer than 16 pending records is skipped.
-template <int REC64, int BLOCK, int SWEEP = 0>
+template <int REC64, int BLOCK>
 __device__ __forceinline__ void part_flush_listed(const KParams& p, uint8_t* smem, const uint32_t* flist, uint32_t nlisted,
                                   unsigned long long& matched) {
   using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
@@ -28,9 +26,8 @@ __device__ __forceinline__ void part_flush_listed(const KParams& p, uint8_t* sme
   const uint32_t cap = (uint32_t)p.part_cap;
   const uint32_t total = nlisted * 8u;
   for (uint32_t t = threadIdx.x; t < total; t += BLOCK) {
-    const uint32_t b = SWEEP ? (t >> 3) : flist[t >> 3], i = t & 7u;
+    const uint32_t b = flist[t >> 3], i = t & 7u;
     const uint32_t raw = pend[b];
-    if (SWEEP && raw < CH) continue;  // no whole chunk pending (uniform over the partition's 8 lanes)
     const uint32_t n = min(raw, C);  // records beyond C went to the overflow table
     const uint32_t out = n & ~(CH - 1u), left = n - out;
     const uint32_t g = gpos[b];
@@ -92,10 +89,57 @@ __device__ __forceinline__ void part_flush_final(const KParams& p, uint8_t* smem
   }
 }
 
-// the register-direct kernel A's flush: every partition with a whole pending chunk
+// The register-direct kernel A's flush (k_part_reg), one thread per partition: a partition with a whole pending 64-byte
+// chunk writes its whole chunks to its region with 16-byte stores (each thread a whole chunk: the 4 stores of a chunk
+// merge in L2 into one 64-byte write) and copies the partial chunk to the front of its ring.  One LDS word read per
+// partition and round decides; r5 SQ counters: the 8-lanes-per-partition sweep over all partitions issued ~20 VALU per
+// doc, this form ~2.  `final`: every pending record goes out (< 16 after the last round's flush), the region counts
+// are written.
 template <int BLOCK>
-__device__ __forceinline__ void part_flush_sweep(const KParams& p, uint8_t* smem, unsigned long long& matched) {
-  part_flush_listed<0, BLOCK, 1>(p, smem, nullptr, (uint32_t)p.num_parts, matched);
+__device__ __forceinline__ void part_flush_owner(const KParams& p, uint8_t* smem, unsigned long long& matched,
+                                                 bool final) {
+  uint32_t* slots = reinterpret_cast<uint32_t*>(smem + p.pl_slot_off);
+  uint32_t* pend = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
+  uint32_t* gpos = reinterpret_cast<uint32_t*>(smem + p.pl_bcnt_off);
+  const int cl = p.part_slot_log2;
+  const uint32_t C = 1u << cl;
+  const uint32_t cap = (uint32_t)p.part_cap;
+  const uint32_t P = (uint32_t)p.num_parts;
+  for (uint32_t b = threadIdx.x; b < P; b += BLOCK) {
+    const uint32_t raw = pend[b];
+    if (!final && raw < 16u) continue;
+    const uint32_t n = min(raw, C);  // records beyond C went to the overflow table
+    const uint32_t out = final ? n : (n & ~15u), left = n - out;
+    const uint32_t g = gpos[b];
+    uint32_t* ring = slots + ((size_t)b << cl);
+    uint32_t* region = reinterpret_cast<uint32_t*>(p.part_buf) + part_region(p, b, blockIdx.x) * (size_t)cap;
+    for (uint32_t k = 0; k < out; k += 16u) {
+      u32x4 q[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) q[e] = *reinterpret_cast<const u32x4*>(ring + k + 4 * e);
+      if (g + k + 16u <= cap) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) *reinterpret_cast<u32x4*>(region + g + k + 4 * e) = q[e];  // (final: past n unread)
+      } else {
+        const uint32_t m = min(16u, out - k);
+        for (uint32_t e = 0; e < m; ++e) part_store<0>(p, b, g + k + e, ring[k + e]);  // region full (skew)
+      }
+    }
+    if (left) {  // the partial chunk to the front of the ring (whole 16-byte quarters; past `left` is garbage)
+      u32x4 q[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) q[e] = *reinterpret_cast<const u32x4*>(ring + out + 4 * e);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) *reinterpret_cast<u32x4*>(ring + 4 * e) = q[e];
+    }
+    pend[b] = left;
+    gpos[b] = g + out;
+    matched += raw - n;
+    if (final) {
+      p.part_count[(size_t)b * gridDim.x + blockIdx.x] = g + out;  // records of region (b, blockIdx)
+      matched += g + out;
+    }
+  }
 }
 
 }  // namespace ph

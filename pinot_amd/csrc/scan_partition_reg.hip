@@ -19,8 +19,8 @@ namespace ph {
 // count, or the lane's scratch word for a missed doc -- PartTiles::decode already chose it), one compare, one store
 // (a missed doc's or a full ring's record to the lane's scratch slot).  r4 SQ counters on the previous form (runtime
 // append variants, listed flush with per-record "chunk completed" checks): 64.5 VALU + 33 SALU per doc and the VALU
-// busy 62 % of the kernel; this form issues ~20 VALU per doc.  The flush sweeps every partition's word once per round
-// (pending >= 16: its whole 64-byte chunks go out), so no append keeps a list.
+// busy 62 % of the kernel.  The flush is one thread per partition (part_flush_owner: pending >= 16 sends its whole
+// 64-byte chunks out), so no append keeps a list.
 template <int NG, int HASV, int CK, int CV>
 __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -52,7 +52,7 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
     tiles.load(t0, lane);
     // ---- two append rounds: flush the chunks the previous round completed, then append 16 records per lane
     auto append_round = [&](auto jb) {
-      part_flush_sweep<kRegBlock>(p, smem, matched);
+      part_flush_owner<kRegBlock>(p, smem, matched, false);
       lds_barrier();
       // groups of 4: the 4 rank atomics issue back to back, then the 4 stores; a full ring (skewed round) sends its
       // records to the overflow table (rare: one ballot per group)
@@ -80,9 +80,9 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
     append_round(std::integral_constant<int, 0>{});
     append_round(std::integral_constant<int, 16>{});
   }
-  part_flush_sweep<kRegBlock>(p, smem, matched);
+  part_flush_owner<kRegBlock>(p, smem, matched, false);
   lds_barrier();
-  part_flush_final<0, kRegBlock>(p, smem, matched);
+  part_flush_owner<kRegBlock>(p, smem, matched, true);
   if (matched && p.matched_total) atomicAdd(p.matched_total, matched);
 }
 
