@@ -1,128 +1,172 @@
-// and_walk.h -- the chunked walks of an AND of SV scans' leap-frog (scan_and_walk.hip runs them on the device,
-// filter_sim.cpp on the host for the CPU tests); the algorithm and its reference citations are in scan_and_walk.hip.
+// and_walk.h -- numEntriesScannedInFilter of an AND of SV scans only, as a composition of per-chunk transition tables
+// of the AND's leap-frog (scan_and_walk.hip runs it on the device, filter_sim.cpp on the host for the CPU tests).
+//
+// AndDocIdSet.iterator returns AndDocIdIterator(scan_1 .. scan_k) for such an AND (AndDocIdSet.java:180-183), and
+// DocIdSetOperator drains it with next().  AndDocIdIterator.next() (AndDocIdIterator.java:40-67) keeps a candidate M
+// (maxDocId) and calls advance(M) on the scans in order, skipping the one that set M; a scan's advance(t)
+// (SVScanDocIdIterator.java:101-112) examines the docs t .. its next match (or the rest of the segment at EOF).  So one
+// "epoch" at candidate M that scan j set (j = -1 right after a match, or at the start) costs
+//   calls(M, j) = f + 1 - [0 <= j < f]   advance() calls, f = the first scan without M, and moves M to scan f's next
+//                                        match after M (or ends the segment: that call returns EOF);
+//   calls(M, j) = k - [j >= 0]           when every scan has M (a match): the next epoch is M + 1 with j = -1;
+//   1                                    for M = numDocs (scan 1's advance returns EOF at once),
+// and the docs the calls examine telescope to  entries = numDocs - 1 + sum over the epochs of (calls - [match]).
+//
+// The walk as a finite automaton over chunks of L docs.  The true walk enters chunk [c0, c1) in one of k + 1 ways: a
+// fresh epoch at c0 (type -1: the previous chunk ended with a match at c0 - 1, or c0 = 0), or a jump by scan i that
+// found no match of its own in the previous chunk (type i: the epoch at scan i's first match >= c0, set by i --
+// because scan i had no match in [M_prev, c0), its next match after M_prev IS its first match >= c0).  From an entry
+// the walk inside the chunk is fixed, and it leaves the chunk in one of the same k + 1 ways.  So every chunk is a
+// table  type -> (exit type, sum of (calls - [match]) of its epochs),  the tables compose associatively, and the
+// segment's sum is the composition applied to type -1 at doc 0, plus 1 if it ends in type -1 (the epoch at numDocs).
+// No speculation, no logs, no reruns: exact for every input.  A chunk computes its table with one full walk (type -1)
+// whose first kDfaHist candidates it remembers; the other types' walks stop at the first of those they reach (the
+// candidate sequence depends on M only -- the setter changes only an epoch's call count -- so two walks that share a
+// candidate agree from there on) and take the rest from the remembered running sums.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
 namespace ph {
 
-constexpr int kWalkHead = 16;  // candidates a walker logs from its start
-constexpr int kWalkTail = 16;  // candidates it logs at or past the next chunk
+constexpr int kDfaChunkWords = 8;  // a chunk = 8 words of 64 docs = 512 docs
+constexpr int kDfaHist = 8;        // candidates of the type -1 walk a chunk remembers
+
 struct AndWalkJob {
   const unsigned long long* bits;  // k leaf doc bitmaps, leaf-major, nwords words each (bits past ndocs zero)
   int64_t nwords, ndocs;
-  int32_t k, slot;                 // scans; the sum accumulates into out[slot]
-  int32_t shift;                   // chunk = 1 << shift docs
-  int64_t nchunks;
-  int32_t* pos;                    // [kWalkHead + kWalkTail][nchunks] logged candidates (entry-major: the walkers
-                                   // of a wave store one entry to consecutive addresses)
-  unsigned long long* cum;         // their running sums, same layout
-  uint32_t* cnt;                   // [nchunks] head count | tail count << 16
+  int32_t k, slot;                 // scans; the sum goes to out[slot]
+  int64_t nchunks;                 // chunks of kDfaChunkWords words
+  int32_t ngroups;                 // workgroup tables (chunks composed per workgroup on the device)
+  int32_t pad;
+  uint32_t* gdelta;                // [k + 1][ngroups] the workgroups' composed sums (row = entry type + 1)
+  uint8_t* gexit;                  // [k + 1][ngroups] their exit types + 1
 };
 
-// index of log entry e (head: 0 .. kWalkHead - 1, tail: kWalkHead + i) of walker c
-__host__ __device__ inline int64_t walk_slot(const AndWalkJob& J, int64_t c, int e) { return (int64_t)e * J.nchunks + c; }
-
-// first set bit of bitmap `w` at or after x (x < nwords * 64), or -1
-__host__ __device__ inline int64_t walk_next_set(const unsigned long long* w, int64_t nwords, int64_t x) {
-  int64_t wi = x >> 6;
-  unsigned long long v = w[wi] & (~0ull << (x & 63));
-  while (!v) {
-    if (++wi >= nwords) return -1;
-    v = w[wi];
-  }
-  return wi * 64 + __builtin_ctzll(v);
-}
-
-// walker c: a fresh epoch at doc c << shift, logging as described in scan_and_walk.hip
-__host__ __device__ inline void and_walk_chunk(const AndWalkJob& J, int64_t c) {
-  const int64_t N = J.ndocs;
-  const int k = J.k;
-  const int64_t end = (c + 1) << J.shift;
-  const int64_t thr = end < N ? end : N;  // the tail starts at the next chunk (the last walker's: the end)
-  int64_t M = c << J.shift;
-  int j = -1, hn = 0, tn = 0;
-  unsigned long long cum = 0;
-  for (;;) {
-    bool term = false;
-    int64_t nxt = 0;
-    int jn = -1;
-    if (M >= N) {  // scan 1's advance(numDocs) returns EOF at once
-      cum += 1;
-      term = true;
-    } else {
-      const int64_t wi = M >> 6;
-      const unsigned long long bit = 1ull << (M & 63);
-      int f = 0;
-      while (f < k && (J.bits[(int64_t)f * J.nwords + wi] & bit)) ++f;
-      if (f == k) {  // a match: k advance() calls (k - 1 after a move), minus the match
-        cum += (unsigned long long)(k - 1 - (j >= 0 ? 1 : 0));
-        nxt = M + 1;
-      } else {
-        cum += (unsigned long long)(f + 1 - ((j >= 0 && j < f) ? 1 : 0));
-        nxt = walk_next_set(J.bits + (int64_t)f * J.nwords, J.nwords, M);
-        term = nxt < 0 || nxt >= N;
-        jn = f;
+// One chunk's table.  get(i, w): word w (absolute index, inside the chunk) of scan i.  delta[e + 1] / ext[e + 1] for
+// entry type e = -1 .. k - 1 (ext = exit type + 1).
+template <int K, class Get>
+__host__ __device__ inline void dfa_chunk(int k, int64_t c0, int64_t c1, Get&& get, uint32_t (&delta)[K + 1],
+                                          uint8_t (&ext)[K + 1]) {
+  // first scan without doc M (k: every scan has it)
+  auto first_fail = [&](int64_t M) {
+    const int64_t w = M >> 6;
+    const unsigned long long bit = 1ull << (M & 63);
+    int f = 0;
+    while (f < k && (get(f, w) & bit)) ++f;
+    return f;
+  };
+  // scan i's first match in [x, c1), or -1
+  auto next_set = [&](int i, int64_t x) -> int64_t {
+    if (x >= c1) return -1;
+    int64_t w = x >> 6;
+    const int64_t wl = (c1 - 1) >> 6;
+    unsigned long long v = get(i, w) & (~0ull << (x & 63));
+    while (!v) {
+      if (++w > wl) return -1;
+      v = get(i, w);
+    }
+    const int64_t m = w * 64 + __builtin_ctzll(v);
+    return m < c1 ? m : -1;
+  };
+  // one epoch at M set by j: its (calls - [match]); the next candidate (or -1: the walk leaves the chunk) and setter
+  auto epoch = [&](int64_t M, int j, int64_t& nxt, int& jn) -> uint32_t {
+    const int f = first_fail(M);
+    if (f == k) {
+      nxt = M + 1 < c1 ? M + 1 : -1;
+      jn = -1;
+      return (uint32_t)(k - 1 - (j >= 0 ? 1 : 0));
+    }
+    nxt = next_set(f, M + 1);
+    jn = f;
+    return (uint32_t)(f + 1 - ((j >= 0 && j < f) ? 1 : 0));
+  };
+  // type -1: the full walk from c0, remembering its first kDfaHist candidates and the running sums around their
+  // epochs (hcum[q]: before candidate q's epoch, hcum[q + 1]: after it)
+  int64_t hpos[kDfaHist];
+  uint32_t hcum[kDfaHist + 1];
+  int nh = 0;
+  uint32_t sum = 0;
+  {
+    int64_t M = c0;
+    int j = -1;
+    for (;;) {
+      const bool rec = nh < kDfaHist;
+      if (rec) {
+        hpos[nh] = M;
+        hcum[nh] = sum;
       }
+      int64_t nxt;
+      int jn;
+      sum += epoch(M, j, nxt, jn);
+      if (rec) hcum[++nh] = sum;
+      if (nxt < 0) {
+        ext[0] = (uint8_t)(jn + 1);
+        break;
+      }
+      M = nxt;
+      j = jn;
     }
-    const int32_t P = term ? (int32_t)N : (int32_t)M;  // the end is logged as candidate numDocs
-    if (hn < kWalkHead) {
-      J.pos[walk_slot(J, c, hn)] = P;
-      J.cum[walk_slot(J, c, hn)] = cum;
-      ++hn;
-    }
-    if (P >= thr) {
-      J.pos[walk_slot(J, c, kWalkHead + tn)] = P;
-      J.cum[walk_slot(J, c, kWalkHead + tn)] = cum;
-      ++tn;
-    }
-    if (term || tn == kWalkTail) break;
-    M = nxt;
-    j = jn;
+    delta[0] = sum;
   }
-  J.cnt[c] = (uint32_t)hn | ((uint32_t)tn << 16);
+  const uint32_t total = sum;
+  // types 0 .. k - 1: from scan e's first match, until a remembered candidate of the type -1 walk
+  for (int e = 0; e < K; ++e) {
+    if (e >= k) break;
+    int64_t M = next_set(e, c0);
+    if (M < 0) {  // no match of scan e in the chunk: the jump passes through
+      delta[e + 1] = 0;
+      ext[e + 1] = (uint8_t)(e + 1);
+      continue;
+    }
+    int j = e, q = 0;
+    uint32_t own = 0;
+    for (;;) {
+      while (q < nh && hpos[q] < M) ++q;
+      int64_t nxt;
+      int jn;
+      const uint32_t d = epoch(M, j, nxt, jn);
+      if (q < nh && hpos[q] == M) {  // joined the type -1 walk at its candidate q: its epochs after q follow
+        delta[e + 1] = own + d + (total - hcum[q + 1]);
+        ext[e + 1] = ext[0];
+        break;
+      }
+      own += d;
+      if (nxt < 0) {
+        delta[e + 1] = own;
+        ext[e + 1] = (uint8_t)(jn + 1);
+        break;
+      }
+      M = nxt;
+      j = jn;
+    }
+  }
 }
 
-// where walker b's tail log meets walker b + 1's head log (the first common candidate): the index pair, or false
-__host__ __device__ inline bool and_walk_meet(const AndWalkJob& J, int64_t b, int& ti, int& hi) {
-  const int tn = (int)(J.cnt[b] >> 16), hn = (int)(J.cnt[b + 1] & 0xffff);
-  int x = 0, y = 0;
-  while (x < tn && y < hn) {
-    const int32_t a = J.pos[walk_slot(J, b, kWalkHead + x)], h = J.pos[walk_slot(J, b + 1, y)];
-    if (a == h) {
-      ti = x;
-      hi = y;
-      return true;
-    }
-    if (a < h) ++x;
-    else ++y;
+// compose table b after table a (both k + 1 entries): out[e] = b applied to a's exit of e
+template <int K>
+__host__ __device__ inline void dfa_compose(int k, const uint32_t (&ad)[K + 1], const uint8_t (&ax)[K + 1],
+                                            const uint32_t (&bd)[K + 1], const uint8_t (&bx)[K + 1],
+                                            uint32_t (&od)[K + 1], uint8_t (&ox)[K + 1]) {
+  for (int e = 0; e <= K; ++e) {
+    if (e > k) break;
+    const int x = ax[e];
+    uint32_t d = 0;
+    uint8_t t = 0;
+    for (int y = 0; y <= K; ++y)  // register-indexed select (no dynamic register indexing on the device)
+      if (y == x) {
+        d = bd[y];
+        t = bx[y];
+      }
+    od[e] = ad[e] + d;
+    ox[e] = t;
   }
-  return false;
 }
 
-// walker c's share of the true walk, cum_c(q_{c+1}) - cum_c(q_c); false when the walks do not meet in order
-__host__ __device__ inline bool and_merge_chunk(const AndWalkJob& J, int64_t c, unsigned long long& part) {
-  int64_t qc = -1, qn = -1;
-  unsigned long long lo = 0, hi = 0;
-  int ti = 0, h = 0;
-  if (c > 0) {  // q_c: the true walk joins walker c
-    if (!and_walk_meet(J, c - 1, ti, h)) return false;
-    qc = J.pos[walk_slot(J, c, h)];
-    lo = J.cum[walk_slot(J, c, h)];
-  }
-  if (c + 1 < J.nchunks) {  // q_{c+1}: walker c + 1 takes over
-    if (!and_walk_meet(J, c, ti, h)) return false;
-    qn = J.pos[walk_slot(J, c, kWalkHead + ti)];
-    hi = J.cum[walk_slot(J, c, kWalkHead + ti)];
-  } else {  // the last walker runs to the end: its tail holds the end alone
-    const int tn = (int)(J.cnt[c] >> 16);
-    if (tn < 1) return false;
-    qn = J.pos[walk_slot(J, c, kWalkHead + tn - 1)];
-    hi = J.cum[walk_slot(J, c, kWalkHead + tn - 1)];
-  }
-  if (qn < qc) return false;
-  part = hi - lo;
-  return true;
+// the segment's entries from its composed table: entry type -1 at doc 0, + 1 for an end in type -1 (the epoch at
+// numDocs), over numDocs - 1
+inline int64_t dfa_entries(int64_t num_docs, uint32_t delta_m1, uint8_t exit_m1) {
+  return num_docs - 1 + (int64_t)delta_m1 + (exit_m1 == 0 ? 1 : 0);
 }
 
 }  // namespace ph

@@ -387,37 +387,32 @@ int64_t simulate_filter_entries(const SimNode& root, const std::vector<SimLeaf>&
   return b.entries;
 }
 
-// One gap of AndDocIdIterator(scan_1 .. scan_k).next() from _nextDocId = t, over the scans' match bitmaps: the entries
-// its advance() calls examine (the device pass's fallback for gaps longer than its step cap).
+// The AND-of-scans entries by the device's algorithm (and_walk.h) on the host: chunks of 1 << shift docs (any
+// length: dfa_chunk takes arbitrary bounds), their tables composed in order.
 int64_t and_walk_entries_host(const uint64_t* bits, int k, int64_t num_docs, int shift) {
   if (num_docs <= 0) return 0;
-  AndWalkJob J{};
-  J.bits = (const unsigned long long*)bits;
-  J.nwords = (num_docs + 63) / 64;
-  J.ndocs = num_docs;
-  J.k = k;
-  J.shift = shift;
-  J.nchunks = ((num_docs - 1) >> shift) + 1;
-  std::vector<int32_t> pos((size_t)J.nchunks * (kWalkHead + kWalkTail));
-  std::vector<unsigned long long> cum(pos.size());
-  std::vector<uint32_t> cnt((size_t)J.nchunks);
-  J.pos = pos.data();
-  J.cum = cum.data();
-  J.cnt = cnt.data();
-  for (int64_t c = 0; c < J.nchunks; ++c) and_walk_chunk(J, c);
-  unsigned long long sum = 0;
-  for (int64_t c = 0; c < J.nchunks; ++c) {
-    unsigned long long part = 0;
-    if (!and_merge_chunk(J, c, part)) return -1;
-    sum += part;
+  if (k < 1 || k > kMaxFbProgs) return -1;
+  const int64_t nwords = (num_docs + 63) / 64;
+  const int64_t L = shift >= 62 ? num_docs : std::min<int64_t>(num_docs, (int64_t)1 << shift);
+  constexpr int K = kMaxFbProgs;
+  unsigned long long total = 0;  // along entry type -1 only (the composed row a segment needs), in 64 bits
+  int e = 0;
+  for (int64_t c0 = 0; c0 < num_docs; c0 += L) {
+    const int64_t c1 = std::min(num_docs, c0 + L);
+    uint32_t d[K + 1];
+    uint8_t x[K + 1];
+    auto get = [&](int i, int64_t w) -> unsigned long long { return bits[(int64_t)i * nwords + w]; };
+    dfa_chunk<K>(k, c0, c1, get, d, x);
+    total += d[e];
+    e = x[e];
   }
-  return num_docs - 1 + (int64_t)sum;
+  return num_docs - 1 + (int64_t)total + (e == 0 ? 1 : 0);
 }
 
 }  // namespace ph
 
-// test hooks (not part of the product boundary, include/pinot_hip.h).  The chunked walks of k_and_walk /
-// k_and_merge on the host over k leaf bitmaps (leaf-major), so the CPU tests check the merge against the simulator
+// test hooks (not part of the product boundary, include/pinot_hip.h).  k_and_dfa's chunk tables composed on the host
+// over k leaf bitmaps (leaf-major), so the CPU tests check the automaton against the simulator
 extern "C" int64_t phx_and_walk_entries(const uint64_t* bits, int32_t k, int64_t num_docs, int32_t shift) {
   return ph::and_walk_entries_host(bits, k, num_docs, shift);
 }

@@ -62,6 +62,10 @@ struct PartTiles {
 
   // issue the tile's loads (they stay in flight until decode)
   __device__ void load(const Tile& t, int lane) {
+    load_keys(t, lane);
+    load_value(t, lane);
+  }
+  __device__ void load_keys(const Tile& t, int lane) {
     const bool tile = t.ndoc > 0;                        // wave-uniform
     const bool lane_live = tile && lane * 32 < t.ndoc;  // this lane's run holds docs of the tile
     const int32_t run0 = t.w0 * 2;
@@ -77,6 +81,13 @@ struct PartTiles {
       reg_load<CK>(tile, lane_live, tile ? S->streams[gs].fwd : nullptr, tile ? S->streams[gs].bits : 0,
                    tile ? bytes(gs) : 0, run0, lane, pk[g]);
     }
+  }
+  __device__ void load_value(const Tile& t, int lane) {
+    const bool tile = t.ndoc > 0;
+    const bool lane_live = tile && lane * 32 < t.ndoc;
+    const int32_t run0 = t.w0 * 2;
+    SegPtr S = t.S;
+    auto bytes = [&](int st) { return ((int64_t)S->num_docs * S->streams[st].bits + 7) / 8; };
     if constexpr (HASV != 0) {
       const int vs = p.v_stream[0];
       reg_load<CV>(tile, lane_live, tile ? S->streams[vs].fwd : nullptr, tile ? S->streams[vs].bits : 0,

@@ -282,6 +282,8 @@ struct KParams {
   uint32_t* part_count;           // [num_parts][gridDim.x] records written per region (may exceed part_cap)
   int32_t pl_slot_off, pl_lcnt_off, pl_bcnt_off, pl_misc_off;  // LDS layout
   int32_t part_slot_log2;         // C = 1 << part_slot_log2 LDS ring slots per partition
+  int32_t part_ring_stride;       // k_part_reg: words between consecutive partitions' rings (C + 4: the flush's owner
+                                  // threads read their rings at distinct bank offsets)
   int32_t part_fast;              // kernel A may run the lean k_part_scan (no gathers; ALL / RANGE / DOCRANGE leaves)
   int32_t part_depth;             // lean kernel A: tiles of loads in flight per wave (1: k_part_scan, 2: k_part_scan2)
   int32_t part_reg;               // kernel A = k_part_reg (register-direct decode; 0: the LDS-staged forms)
@@ -632,11 +634,13 @@ struct FbJob {
   unsigned long long* out;     // [rows][nwords] doc bitmaps
 };
 void launch_filter_bitmaps(const FilterInsn* prog, const DevSegment* segs, const FbJob& job, hipStream_t s);
-// numEntriesScannedInFilter of ANDs of scans: chunked walks of the leap-frog (and_walk.h, scan_and_walk.hip); the
-// device adds each job's sum of (calls - [match]) into out[slot] and flags bad[slot] when its walks did not meet
-void launch_and_walk(const AndWalkJob* jobs, int32_t njobs, int64_t max_chunks, int32_t max_k, unsigned long long* out,
-                     uint32_t* bad, hipStream_t s);
-// the same walks on the host (CPU tests): the entries, or -1 when the chunks of 1 << shift docs do not meet
+// numEntriesScannedInFilter of ANDs of scans: the leap-frog as composed per-chunk transition tables (and_walk.h,
+// scan_and_walk.hip); out[slot] = the job's sum of (calls - [match]) + [ends after a match]: entries = numDocs - 1 +
+// out.  Each job needs (k + 1) x ngroups table entries, ngroups = ceil(nchunks / and_dfa_block(max_k)).
+int and_dfa_block(int32_t max_k);
+void launch_and_walk(const AndWalkJob* jobs, int32_t njobs, int64_t max_groups, int32_t max_k, unsigned long long* out,
+                     hipStream_t s);
+// the same tables on the host (CPU tests), chunks of 1 << shift docs composed in order: the entries
 int64_t and_walk_entries_host(const uint64_t* bits, int k, int64_t num_docs, int shift);
 // the doc bitmap of a dictId scan leaf (leaf_bitmaps.hip): RANGE [lo, lo + len) or, with `set`, a dictId bitset over
 // `card` ids (<= kLeafSetWords * 32); `out` holds ceil(ndocs / 64) * 2 uint32 words (= the uint64 doc-bitmap words)

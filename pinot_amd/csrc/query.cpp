@@ -2488,27 +2488,33 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       hipStream_t sb = lane.lane->stream_b;
       PH_HIP_CHECK(hipStreamWaitEvent(sb, lane.lane->ev_uploaded, 0));
       constexpr size_t kStatBatchWords = (size_t)32 << 20;  // 256 MiB
-      constexpr int kWalkShift = 11;                        // 2048-doc walks (r4: 1024 1.17 ms, 2048 0.80, 8192 1.05 per SSB query)
       auto seg_words = [&](const StatSeg& ss) {
         return ss.leaves.size() * (size_t)((dsegs[ss.dseg].num_docs + 63) / 64);
       };
-      size_t total = 0, biggest = 0, n_scanand = 0, walk_recs = 0;
+      size_t total = 0, biggest = 0, n_scanand = 0, walk_tab = 0;
+      int32_t walk_k = 2;
+      for (auto& ss : stat_segs)
+        if (ss.dseg >= 0 && ss.kind == ST_SCANAND) walk_k = std::max(walk_k, (int32_t)ss.leaves.size());
+      const int dfa_block = and_dfa_block(walk_k);
+      auto walk_groups = [&](int64_t n) {
+        const int64_t nch = (n + kDfaChunkWords * 64 - 1) / (kDfaChunkWords * 64);
+        return (nch + dfa_block - 1) / dfa_block;
+      };
       for (auto& ss : stat_segs) {
         if (ss.dseg < 0) continue;
         total += seg_words(ss);
         biggest = std::max(biggest, seg_words(ss));
         n_scanand += ss.kind == ST_SCANAND;
-        if (ss.kind == ST_SCANAND) walk_recs += (size_t)(((dsegs[ss.dseg].num_docs - 1) >> kWalkShift) + 1);
+        if (ss.kind == ST_SCANAND)
+          walk_tab += (size_t)(ss.leaves.size() + 1) * (size_t)walk_groups(dsegs[ss.dseg].num_docs);
       }
       const size_t cap_words = std::max<size_t>(1, std::min(total, std::max(kStatBatchWords, biggest)));
       unsigned long long* dev = scratch.alloc<unsigned long long>(cap_words);
-      // walk logs, sized for the first level of every job (a rerun's chunks are fewer)
-      int32_t* d_wpos = walk_recs ? scratch.alloc<int32_t>(walk_recs * (kWalkHead + kWalkTail)) : nullptr;
-      unsigned long long* d_wcum = walk_recs ? scratch.alloc<unsigned long long>(walk_recs * (kWalkHead + kWalkTail)) : nullptr;
-      uint32_t* d_wcnt = walk_recs ? scratch.alloc<uint32_t>(walk_recs) : nullptr;
+      // the walks' workgroup tables ((k + 1) x groups per AND)
+      uint32_t* d_wdelta = walk_tab ? scratch.alloc<uint32_t>(walk_tab) : nullptr;
+      uint8_t* d_wexit = walk_tab ? scratch.alloc<uint8_t>(walk_tab) : nullptr;
       AndWalkJob* d_wjobs = n_scanand ? scratch.alloc<AndWalkJob>(n_scanand) : nullptr;
       unsigned long long* d_out = n_scanand ? scratch.alloc<unsigned long long>(n_scanand) : nullptr;
-      uint32_t* d_bad = n_scanand ? scratch.alloc<uint32_t>(n_scanand) : nullptr;
       size_t n_fast = 0, set_words = 0;
       for (auto& ss : stat_segs)
         for (auto& l : ss.leaves)
@@ -2594,16 +2600,11 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           (void)max_docs;
           (void)max_bits;
         }
-        // the AND-of-scans walks: chunks of 1 << kWalkShift docs; a job whose walks did not meet runs again with
-        // chunks 4x longer (one chunk is the plain walk: always exact)
+        // the AND-of-scans walks: per-chunk transition tables composed per job (exact, one pass)
         std::vector<size_t> walk_b;  // batch positions of the scan-AND segments
         for (size_t b = 0; b < batch.size(); ++b)
           if (stat_segs[batch[b]].kind == ST_SCANAND) walk_b.push_back(b);
-        std::vector<int> shift(walk_b.size(), kWalkShift);
-        std::vector<size_t> todo(walk_b.size());
-        for (size_t j = 0; j < todo.size(); ++j) todo[j] = j;
         std::vector<unsigned long long> out(walk_b.size(), 0);
-        std::vector<uint32_t> bad(walk_b.size(), 0);
         // the simulated segments' bitmaps go to the host (only theirs: the buffer is not touched otherwise)
         std::vector<size_t> hbase(batch.size(), 0);
         size_t hwords = 0;
@@ -2617,13 +2618,12 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           if (stat_segs[batch[b]].kind == ST_SIM)
             PH_HIP_CHECK(hipMemcpyAsync(h.get() + hbase[b], dev + base[b], 8 * seg_words(stat_segs[batch[b]]),
                                         hipMemcpyDeviceToHost, sb));
-        bool first = true;
-        while (!todo.empty() || first) {
+        if (!walk_b.empty()) {
           std::vector<AndWalkJob> wj;
-          size_t rec = 0;
-          int64_t max_chunks = 0;
+          size_t tab = 0;
+          int64_t max_groups = 0;
           int32_t max_k = 0;
-          for (size_t t : todo) {
+          for (size_t t = 0; t < walk_b.size(); ++t) {
             const StatSeg& ss = stat_segs[batch[walk_b[t]]];
             const int64_t n = dsegs[ss.dseg].num_docs;
             AndWalkJob J{};
@@ -2632,52 +2632,22 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
             J.ndocs = n;
             J.k = (int32_t)ss.leaves.size();
             J.slot = (int32_t)wj.size();
-            J.shift = shift[t];
-            J.nchunks = ((n - 1) >> J.shift) + 1;
-            J.pos = d_wpos + rec * (kWalkHead + kWalkTail);
-            J.cum = d_wcum + rec * (kWalkHead + kWalkTail);
-            J.cnt = d_wcnt + rec;
-            rec += (size_t)J.nchunks;
-            max_chunks = std::max(max_chunks, J.nchunks);
+            J.nchunks = (n + kDfaChunkWords * 64 - 1) / (kDfaChunkWords * 64);
+            J.ngroups = (int32_t)walk_groups(n);
+            J.gdelta = d_wdelta + tab;
+            J.gexit = d_wexit + tab;
+            tab += (size_t)(J.k + 1) * (size_t)J.ngroups;
+            max_groups = std::max<int64_t>(max_groups, J.ngroups);
             max_k = std::max(max_k, J.k);
             if (J.k < 2) fail(PH_ERR_DEVICE, "AND of fewer than two scans");
             wj.push_back(J);
           }
-          if (!wj.empty()) {
-            PH_HIP_CHECK(hipMemcpyAsync(d_wjobs, wj.data(), sizeof(AndWalkJob) * wj.size(), hipMemcpyHostToDevice, sb));
-            PH_HIP_CHECK(hipMemsetAsync(d_out, 0, 8 * wj.size(), sb));
-            PH_HIP_CHECK(hipMemsetAsync(d_bad, 0, 4 * wj.size(), sb));
-            launch_and_walk(d_wjobs, (int32_t)wj.size(), max_chunks, max_k, d_out, d_bad, sb);
-            std::vector<unsigned long long> o(wj.size());
-            std::vector<uint32_t> bd(wj.size());
-            PH_HIP_CHECK(hipMemcpyAsync(o.data(), d_out, 8 * wj.size(), hipMemcpyDeviceToHost, sb));
-            PH_HIP_CHECK(hipMemcpyAsync(bd.data(), d_bad, 4 * wj.size(), hipMemcpyDeviceToHost, sb));
-            PH_HIP_CHECK(hipStreamSynchronize(sb));
-            std::vector<size_t> again;
-            if (host_times) {
-              size_t nb = 0;
-              for (uint32_t v : bd) nb += v != 0;
-              fprintf(stderr, "[ph host] stat walk: %zu jobs at shift %d (first), %zu did not meet\n", wj.size(),
-                      wj.empty() ? 0 : wj[0].shift, nb);
-            }
-            stamp("stat walk");
-            for (size_t x = 0; x < todo.size(); ++x) {
-              const size_t t = todo[x];
-              if (bd[x] && wj[x].nchunks > 1) {
-                shift[t] += 2;  // 4x longer chunks (r4: +5 at once left SSB Q4.3 to a few 64K-doc walks, 110 ms)
-                again.push_back(t);
-              } else if (bd[x]) {
-                fail(PH_ERR_DEVICE, "single-chunk AND walk did not reach the end");
-              } else {
-                out[t] = o[x];
-              }
-            }
-            todo.swap(again);
-          } else {
-            PH_HIP_CHECK(hipStreamSynchronize(sb));
-          }
-          first = false;
+          PH_HIP_CHECK(hipMemcpyAsync(d_wjobs, wj.data(), sizeof(AndWalkJob) * wj.size(), hipMemcpyHostToDevice, sb));
+          launch_and_walk(d_wjobs, (int32_t)wj.size(), max_groups, max_k, d_out, sb);
+          PH_HIP_CHECK(hipMemcpyAsync(out.data(), d_out, 8 * wj.size(), hipMemcpyDeviceToHost, sb));
         }
+        PH_HIP_CHECK(hipStreamSynchronize(sb));
+        stamp("stat walk");
         for (size_t t = 0; t < walk_b.size(); ++t) {
           const StatSeg& ss = stat_segs[batch[walk_b[t]]];
           ent[batch[walk_b[t]]] = dsegs[ss.dseg].num_docs - 1 + (int64_t)out[t];

@@ -57,9 +57,15 @@ __device__ __forceinline__ void reg_unpack(const u32x4 (&pool)[C], int bits, uin
 template <int C>
 __device__ __forceinline__ void reg_load(bool use, bool lane_live, const uint32_t* fwd, int32_t bits, int64_t bytes,
                                          int32_t run0, int lane, u32x4 (&pool)[C]) {
+  // the descriptor's base and size are forced into SGPRs: a descriptor the compiler cannot prove wave-uniform (r5: the
+  // size went through a 64-bit min in VGPRs) turns every buffer load into a readfirstlane waterfall loop
+  const uint64_t nb64 = use ? (uint64_t)((bytes + 3) & ~(int64_t)3) + 16u : 0u;
+  const uint32_t nb = __builtin_amdgcn_readfirstlane(nb64 > 0x7fffffffull ? 0x7fffffffu : (uint32_t)nb64);
+  const uint64_t base = use ? (uint64_t)(uintptr_t)fwd : 0u;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint32_t*>(use ? fwd : nullptr), 0, use ? (int)min<int64_t>((bytes + 3) / 4 * 4 + 16, 0x7fffffff) : 0,
-      0x00020000);
+      reinterpret_cast<void*>((uintptr_t)(((uint64_t)hi << 32) | lo)), 0, (int)nb, 0x00020000);
   const uint32_t vo = (use && lane_live) ? (uint32_t)(run0 + lane) * 4u * (uint32_t)bits : 0x80000000u;
 #pragma unroll
   for (int k = 0; k < C; ++k)

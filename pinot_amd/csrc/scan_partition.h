@@ -111,7 +111,7 @@ __device__ __forceinline__ void part_flush_owner(const KParams& p, uint8_t* smem
     const uint32_t n = min(raw, C);  // records beyond C went to the overflow table
     const uint32_t out = final ? n : (n & ~15u), left = n - out;
     const uint32_t g = gpos[b];
-    uint32_t* ring = slots + ((size_t)b << cl);
+    uint32_t* ring = slots + (size_t)b * (uint32_t)p.part_ring_stride;
     uint32_t* region = reinterpret_cast<uint32_t*>(p.part_buf) + part_region(p, b, blockIdx.x) * (size_t)cap;
     for (uint32_t k = 0; k < out; k += 16u) {
       u32x4 q[4];

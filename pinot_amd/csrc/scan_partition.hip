@@ -22,8 +22,12 @@ size_t partition_lds_bytes(KParams& p) {
   // the lean kernel's flush moves a partition's records with 16 lanes, one 16-byte quarter each
   if (p.part_fast) cl = std::min(cl, rec == 4 ? 6 : 5);
   p.part_slot_log2 = cl;
+  // k_part_reg pads each ring by one 16-byte quarter: with 128-byte rings the owner threads of 16 consecutive
+  // partitions would read / write the same 16 bytes of their rings in ONE bank quad (r5: bank conflicts 72 % of the
+  // kernel's LDS cycles); a 144-byte stride puts them on 16 distinct quads
+  p.part_ring_stride = p.part_reg ? (1 << cl) + 4 : (1 << cl);
   // + one scratch slot and one scratch word per lane: k_part_scan appends misses there (branch-free)
-  place(p.pl_slot_off, ((size_t)(p.num_parts << cl) + 64) * rec);
+  place(p.pl_slot_off, ((size_t)p.num_parts * p.part_ring_stride + 64) * rec);
   // generic kernel: (flushed / CH << 16 | pending) per partition; lean kernel: pending per partition
   place(p.pl_lcnt_off, 4 * ((size_t)p.num_parts + 64));
   place(p.pl_bcnt_off, 4 * (size_t)p.num_parts);  // lean kernel: records flushed per partition (region position)

@@ -40,7 +40,8 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
   const uint32_t P = (uint32_t)p.num_parts;
   const int cl = p.part_slot_log2;
   const uint32_t C = 1u << cl;
-  const uint32_t dummy_slot = (P << cl) + (uint32_t)lane;  // scratch slot of a record-less lane
+  const uint32_t RS = (uint32_t)p.part_ring_stride;
+  const uint32_t dummy_slot = P * RS + (uint32_t)lane;  // scratch slot of a record-less lane
   auto t0 = tiles.next();
   tiles.load(t0, lane);
   // per lane and doc j of the tile: X[j] = the 32-bit record; PB packs two 16-bit ring-word indices per register
@@ -67,7 +68,7 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
         static_for<0, 4>([&](auto q) {
           const bool real = b[q] < P;
           ovf |= real & (w[q] >= C);
-          slots[(real & (w[q] < C)) ? (b[q] << cl) + w[q] : dummy_slot] = X[J0 + decltype(q)::value];
+          slots[(real & (w[q] < C)) ? __umul24(b[q], RS) + w[q] : dummy_slot] = X[J0 + decltype(q)::value];
         });
         if (__ballot(ovf)) {
           static_for<0, 4>([&](auto q) {

@@ -2,9 +2,9 @@
 through the test hook phx_filter_entries_sim; the product calls it for filter shapes without a device pass) is checked
 against the oracle's restatement of the reference iterators (oracle.filter_entries_of) on random filter trees and doc
 sets, and the oracle's restatement against a fully literal variant (every next() batch by batch, no drain shortcut).
-ANDs of scans only are summed by chunked walks of the leap-frog (and_walk.h: k_and_walk / k_and_merge on the device);
-the same walks run on the host through phx_and_walk_entries and are checked against the simulation here, at chunk
-sizes down to 64 docs (where the walks often fail to meet and the pass must say so: -1), and on the GPU in
+ANDs of scans only are summed by the leap-frog's per-chunk transition tables (and_walk.h: k_and_dfa / k_and_compose
+on the device); the same tables run on the host through phx_and_walk_entries and are checked against the simulation
+here at chunk sizes from 1 doc to one whole segment (exact at every size: no speculation), and on the GPU in
 test_gpu_parity.py."""
 import ctypes
 
@@ -182,14 +182,13 @@ def test_and_walk_matches_simulation(seed):
     root, leaves = _scan_and(k)
     exp = _native_sim(root, leaves, docs, n)
     assert exp == O.filter_entries_of(root, n, lambda x: docs[x.col_index])
-    assert _walk(docs, n, 31) == exp  # one chunk: the plain walk
-    for shift in (6, 8, 10, 12):
-        got = _walk(docs, n, shift)
-        assert got in (exp, -1), (seed, shift, got, exp)
+    assert _walk(docs, n, 62) == exp  # one chunk: the plain walk
+    for shift in (0, 1, 3, 6, 8, 9, 10, 12):
+        assert _walk(docs, n, shift) == exp, (seed, shift)
 
 
-def test_and_walk_meets_at_bench_densities():
-    # SSB-like densities at the product's 2048-doc chunks: the walks meet (no rerun), and the sum is exact
+def test_and_walk_at_bench_densities():
+    # SSB-like densities at the product's 512-doc chunks (and 64-doc ones): the composed tables are exact
     rng = np.random.default_rng(7)
     n = 200_000
     for dens in ([1 / 7, 3 / 11, 0.48], [1 / 84, 3 / 11, 0.2], [2 / 250, 2 / 250, 6 / 7], [1 / 25, 1 / 5],
@@ -198,4 +197,5 @@ def test_and_walk_meets_at_bench_densities():
         docs = [rng.random(n) < d for d in dens]
         root, leaves = _scan_and(len(dens))
         exp = _native_sim(root, leaves, docs, n)
-        assert _walk(docs, n, 11) == exp, dens
+        assert _walk(docs, n, 9) == exp, dens
+        assert _walk(docs, n, 6) == exp, dens
