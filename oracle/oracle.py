@@ -838,9 +838,13 @@ def _hash_arrays(col: OracleColumn):
         return col.dictionary.astype(np.int64), None
     if col.data_type == "DOUBLE":
         return col.dictionary.astype(np.float64).view(np.int64), None
+    if col.data_type == "FLOAT":
+        # clearspring MurmurHash.hash(Object): Float -> hashLong(Float.floatToRawIntBits(f)), the int widened to long
+        # (parity unpinned: no reference KAT covers a FLOAT column)
+        return col.dictionary.astype(np.float32).view(np.int32).astype(np.int64), None
     if col.data_type == "STRING":
         return None, np.array([murmur_hash_string(s) for s in col.dictionary], dtype=np.int32)
-    raise NotImplementedError("DISTINCTCOUNTHLL on FLOAT is not pinned")
+    raise NotImplementedError(f"DISTINCTCOUNTHLL on {col.data_type}")
 
 
 def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1, filter_stats: bool = True) -> OracleResult:

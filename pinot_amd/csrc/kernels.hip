@@ -496,19 +496,28 @@ __host__ __device__ inline uint32_t hll_entry_of(int32_t hashed, int log2m) {
   return (j << 8) | r;
 }
 
-__global__ void k_hll_table(const void* __restrict__ values, int32_t is_int, int64_t n, int log2m,
+// clearspring MurmurHash.hash(Object) of a dictionary value: Integer / Long -> hashLong(value), Double ->
+// hashLong(doubleToRawLongBits), Float -> hashLong(floatToRawIntBits) (the int bits widened to long); the device table
+// holds every value widened to int64 / float64 (a FLOAT's float64 is exact, so it narrows back to its own bits)
+__global__ void k_hll_table(const void* __restrict__ values, int32_t kind, int64_t n, int log2m,
                             uint32_t* __restrict__ out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    int64_t v = is_int ? reinterpret_cast<const int64_t*>(values)[i]
-                       : __double_as_longlong(reinterpret_cast<const double*>(values)[i]);  // doubleToRawLongBits
+    int64_t v;
+    if (kind == PH_HLL_HASH_INT) {
+      v = reinterpret_cast<const int64_t*>(values)[i];
+    } else if (kind == PH_HLL_HASH_FLOAT) {
+      v = (int64_t)__float_as_int((float)reinterpret_cast<const double*>(values)[i]);  // floatToRawIntBits
+    } else {
+      v = __double_as_longlong(reinterpret_cast<const double*>(values)[i]);  // doubleToRawLongBits
+    }
     out[i] = hll_entry_of(murmur_long(v), log2m);
   }
 }
 
-void launch_hll_table(const void* values, int32_t is_int, int64_t n, int log2m, uint32_t* out, hipStream_t s) {
+void launch_hll_table(const void* values, int32_t kind, int64_t n, int log2m, uint32_t* out, hipStream_t s) {
   if (n <= 0) return;
   int grid = (int)std::min<int64_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(k_hll_table, dim3(grid), dim3(256), 0, s, values, is_int, n, log2m, out);
+  hipLaunchKernelGGL(k_hll_table, dim3(grid), dim3(256), 0, s, values, kind, n, log2m, out);
   PH_HIP_CHECK(hipGetLastError());
 }
 

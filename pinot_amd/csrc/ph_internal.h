@@ -602,7 +602,8 @@ void launch_encode_values(const uint32_t* fwd, int32_t bits, const int64_t* tabl
 void launch_fill_i64(int64_t* p, int64_t v, int64_t n, hipStream_t s);
 void launch_reduce_table(void* dst, const void* src, int64_t n, int32_t op, hipStream_t s);  // dst (op)= src
 void launch_fill_identity(void* dst, int64_t n, int32_t op, hipStream_t s);                 // op's identity
-void launch_hll_table(const void* values, int32_t is_int, int64_t n, int log2m, uint32_t* out, hipStream_t s);
+enum : int32_t { PH_HLL_HASH_INT = 0, PH_HLL_HASH_DOUBLE = 1, PH_HLL_HASH_FLOAT = 2 };
+void launch_hll_table(const void* values, int32_t kind, int64_t n, int log2m, uint32_t* out, hipStream_t s);
 
 void build_bitmap_directory(Column& c);  // at pin, from c.inverted
 // (column, index id) -> (startOffset, size) of a V3 index_map file (loader.cpp)

@@ -455,7 +455,6 @@ static void build_value_stream(Context* ctx, ph_segment* seg, Column& c, hipStre
 // (the caller synchronises)
 void build_hll_table(Context* ctx, Column& c, int log2m, hipStream_t st) {
   if (c.hll_tables.count(log2m)) return;
-  if (c.data_type == PH_FLOAT) fail(PH_ERR_UNSUPPORTED, "DISTINCTCOUNTHLL on FLOAT columns is not on the GPU path");
   HllTable t;
   t.buf = std::make_unique<DeviceBuffer>();
   t.buf->alloc(sizeof(uint32_t) * std::max(1, c.cardinality), ctx->device);
@@ -468,8 +467,11 @@ void build_hll_table(Context* ctx, Column& c, int log2m, hipStream_t st) {
     }
     PH_HIP_CHECK(hipMemcpy(t.buf->ptr, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice));
   } else {
-    // INT / LONG -> hashLong((long) value); DOUBLE -> hashLong(doubleToRawLongBits)
-    launch_hll_table(c.d_values.ptr, c.data_type != PH_DOUBLE, c.cardinality, log2m, t.buf->as<uint32_t>(), st);
+    // INT / LONG -> hashLong((long) value); DOUBLE -> hashLong(doubleToRawLongBits); FLOAT ->
+    // hashLong(floatToRawIntBits) (DistinctCountHLLAggregationFunction.java:127-131 offers the Float itself)
+    const int32_t kind = c.data_type == PH_DOUBLE ? PH_HLL_HASH_DOUBLE
+                         : c.data_type == PH_FLOAT ? PH_HLL_HASH_FLOAT : PH_HLL_HASH_INT;
+    launch_hll_table(c.d_values.ptr, kind, c.cardinality, log2m, t.buf->as<uint32_t>(), st);
   }
   c.hll_tables[log2m] = std::move(t);
 }

@@ -256,6 +256,18 @@ def test_hll_parity(ctx):
     _both(ctx, tables, "SELECT DISTINCTCOUNTHLL(u, 12) FROM t")
 
 
+def test_hll_float_column(ctx):
+    # DISTINCTCOUNTHLL on FLOAT (DistinctCountHLLAggregationFunction.java:127-131 offers the Float: clearspring hashes
+    # hashLong(floatToRawIntBits)); registers compared raw with the oracle's restatement (parity unpinned: no KAT)
+    rng = np.random.default_rng(33)
+    tables = []
+    for n in (40_000, 9_999):
+        tables.append({"fl": (np.round(rng.normal(size=n), 3).astype(np.float32), "FLOAT"),
+                       "c": (rng.integers(0, 100, n).astype(np.int32), "INT")})
+    _both(ctx, tables, "SELECT DISTINCTCOUNTHLL(fl) FROM t WHERE c < 60")
+    _both(ctx, tables, "SELECT c, DISTINCTCOUNTHLL(fl) FROM t WHERE c < 20 GROUP BY c ORDER BY c")
+
+
 def test_inverted_index_containers(ctx):
     # dense values -> bitmap containers; runs -> run containers; sparse -> array containers
     n = 300_000
