@@ -417,6 +417,46 @@ extern "C" int64_t phx_and_walk_entries(const uint64_t* bits, int32_t k, int64_t
   return ph::and_walk_entries_host(bits, k, num_docs, shift);
 }
 
+// test hook: the workgroup tables k_and_dfa writes (chunks of kDfaChunkWords words composed per `block` chunks), on
+// the host: gtab = (k + 1) x groups deltas, then (k + 1) x groups exit types + 1; returns the group count
+extern "C" int64_t phx_and_walk_tables_host(const uint64_t* bits, int32_t k, int64_t num_docs, int32_t block,
+                                            uint32_t* gtab) {
+  using namespace ph;
+  constexpr int K = kMaxFbProgs, CW = kDfaChunkWords;
+  if (num_docs <= 0 || k < 1 || k > K || block < 1) return -1;
+  const int64_t nwords = (num_docs + 63) / 64, nchunks = (num_docs + CW * 64 - 1) / (CW * 64);
+  const int64_t ngroups = (nchunks + block - 1) / block;
+  auto get = [&](int i, int64_t w) -> unsigned long long { return bits[(int64_t)i * nwords + w]; };
+  for (int64_t g = 0; g < ngroups; ++g) {
+    uint32_t d[K + 1];
+    uint8_t x[K + 1];
+    for (int e = 0; e <= K; ++e) {
+      d[e] = 0;
+      x[e] = (uint8_t)e;
+    }
+    for (int64_t c = g * block; c < std::min(nchunks, (g + 1) * block); ++c) {
+      const int64_t c0 = c * CW * 64, c1 = std::min(num_docs, c0 + CW * 64);
+      uint32_t cd[K + 1], od[K + 1];
+      uint8_t cx[K + 1], ox[K + 1];
+      for (int e = 0; e <= K; ++e) {
+        cd[e] = 0;
+        cx[e] = (uint8_t)e;
+      }
+      dfa_chunk<K>(k, c0, c1, get, cd, cx);
+      dfa_compose<K>(k, d, x, cd, cx, od, ox);
+      for (int e = 0; e <= k; ++e) {
+        d[e] = od[e];
+        x[e] = ox[e];
+      }
+    }
+    for (int e = 0; e <= k; ++e) {
+      gtab[(size_t)e * ngroups + g] = d[e];
+      gtab[(size_t)(k + 1) * ngroups + (size_t)e * ngroups + g] = x[e];
+    }
+  }
+  return ngroups;
+}
+
 // test hook: the simulator over a flat tree -- node i =
 // (op, priority, leaf, first child, child count) -- so the CPU tests can check it against the oracle's restatement
 extern "C" int64_t phx_filter_entries_sim(const int32_t* nodes, int32_t num_nodes, const int32_t* leaf_kinds,

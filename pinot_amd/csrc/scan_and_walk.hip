@@ -122,3 +122,48 @@ void launch_and_walk(const AndWalkJob* jobs, int32_t njobs, int64_t max_groups, 
 }
 
 }  // namespace ph
+
+// test hook (not part of the product boundary, include/pinot_hip.h): one AND-of-scans job on the current device over
+// host leaf bitmaps (leaf-major, k x ceil(n / 64) words); the entries, or -1 on a device error.  `gtab` (optional,
+// (k + 1) x 2 x groups words) receives the workgroup tables (delta, exit + 1) for diagnosis.
+extern "C" int64_t phx_and_walk_entries_device(const uint64_t* bits, int32_t k, int64_t num_docs, uint32_t* gtab) {
+  using namespace ph;
+  try {
+    if (num_docs <= 0) return 0;
+    const int64_t nwords = (num_docs + 63) / 64;
+    AndWalkJob J{};
+    J.nwords = nwords;
+    J.ndocs = num_docs;
+    J.k = k;
+    J.slot = 0;
+    J.nchunks = (num_docs + kDfaChunkWords * 64 - 1) / (kDfaChunkWords * 64);
+    const int block = and_dfa_block(k);
+    J.ngroups = (int32_t)((J.nchunks + block - 1) / block);
+    DeviceBuffer b, d, x, jb, o;
+    int dev = 0;
+    PH_HIP_CHECK(hipGetDevice(&dev));
+    b.alloc(8 * (size_t)k * nwords, dev);
+    d.alloc(4 * (size_t)(k + 1) * J.ngroups, dev);
+    x.alloc((size_t)(k + 1) * J.ngroups, dev);
+    jb.alloc(sizeof(AndWalkJob), dev);
+    o.alloc(8, dev);
+    PH_HIP_CHECK(hipMemcpy(b.ptr, bits, 8 * (size_t)k * nwords, hipMemcpyHostToDevice));
+    J.bits = b.as<unsigned long long>();
+    J.gdelta = d.as<uint32_t>();
+    J.gexit = x.as<uint8_t>();
+    PH_HIP_CHECK(hipMemcpy(jb.ptr, &J, sizeof J, hipMemcpyHostToDevice));
+    launch_and_walk(jb.as<AndWalkJob>(), 1, J.ngroups, k, o.as<unsigned long long>(), nullptr);
+    PH_HIP_CHECK(hipDeviceSynchronize());
+    unsigned long long out = 0;
+    PH_HIP_CHECK(hipMemcpy(&out, o.ptr, 8, hipMemcpyDeviceToHost));
+    if (gtab) {
+      std::vector<uint8_t> hx((size_t)(k + 1) * J.ngroups);
+      PH_HIP_CHECK(hipMemcpy(gtab, d.ptr, 4 * (size_t)(k + 1) * J.ngroups, hipMemcpyDeviceToHost));
+      PH_HIP_CHECK(hipMemcpy(hx.data(), x.ptr, hx.size(), hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < hx.size(); ++i) gtab[(size_t)(k + 1) * J.ngroups + i] = hx[i];
+    }
+    return num_docs - 1 + (int64_t)out;
+  } catch (...) {
+    return -1;
+  }
+}
