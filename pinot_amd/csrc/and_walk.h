@@ -43,103 +43,128 @@ struct AndWalkJob {
   uint8_t* gexit;                  // [k + 1][ngroups] their exit types + 1
 };
 
-// One chunk's table.  get(i, w): word w (absolute index, inside the chunk) of scan i.  delta[e + 1] / ext[e + 1] for
-// entry type e = -1 .. k - 1 (ext = exit type + 1).
-template <int K, class Get>
-__host__ __device__ inline void dfa_chunk(int k, int64_t c0, int64_t c1, Get&& get, uint32_t (&delta)[K + 1],
-                                          uint8_t (&ext)[K + 1]) {
+// One chunk's walker: the k scans' words through get(i, w) (absolute word index inside the chunk [c0, c1)).
+template <class Get>
+struct DfaWalker {
+  int k;
+  int64_t c1;
+  Get get;
   // first scan without doc M (k: every scan has it)
-  auto first_fail = [&](int64_t M) {
+  __host__ __device__ int first_fail(int64_t M) const {
     const int64_t w = M >> 6;
     const unsigned long long bit = 1ull << (M & 63);
     int f = 0;
-    while (f < k && (get(f, w) & bit)) ++f;
+    while (f < k && (get(f, w) & bit) != 0ull) ++f;
     return f;
-  };
+  }
   // scan i's first match in [x, c1), or -1
-  auto next_set = [&](int i, int64_t x) -> int64_t {
+  __host__ __device__ int64_t next_set(int i, int64_t x) const {
     if (x >= c1) return -1;
     int64_t w = x >> 6;
     const int64_t wl = (c1 - 1) >> 6;
     unsigned long long v = get(i, w) & (~0ull << (x & 63));
-    while (!v) {
+    while (v == 0ull) {
       if (++w > wl) return -1;
       v = get(i, w);
     }
-    const int64_t m = w * 64 + __builtin_ctzll(v);
+    const int64_t m = w * 64 + (int64_t)__builtin_ctzll(v);
     return m < c1 ? m : -1;
-  };
-  // one epoch at M set by j: its (calls - [match]); the next candidate (or -1: the walk leaves the chunk) and setter
-  auto epoch = [&](int64_t M, int j, int64_t& nxt, int& jn) -> uint32_t {
+  }
+  // one epoch at M set by scan j (-1: none): returns its (calls - [match]) and sets the next candidate (-1: the walk
+  // leaves the chunk) and its setter
+  __host__ __device__ uint32_t epoch(int64_t M, int j, int64_t& nxt, int& jn) const {
     const int f = first_fail(M);
+    const uint32_t skip = (j >= 0) ? 1u : 0u;
     if (f == k) {
       nxt = M + 1 < c1 ? M + 1 : -1;
       jn = -1;
-      return (uint32_t)(k - 1 - (j >= 0 ? 1 : 0));
+      return (uint32_t)k - 1u - skip;
     }
     nxt = next_set(f, M + 1);
     jn = f;
-    return (uint32_t)(f + 1 - ((j >= 0 && j < f) ? 1 : 0));
-  };
+    return (uint32_t)f + 1u - ((skip != 0u && j < f) ? 1u : 0u);
+  }
+};
+
+// One chunk's table: delta[e + 1] / ext[e + 1] for entry type e = -1 .. k - 1 (ext = exit type + 1).
+template <int K, class Get>
+__host__ __device__ inline void dfa_chunk(int k, int64_t c0, int64_t c1, Get&& get, uint32_t (&delta)[K + 1],
+                                          uint8_t (&ext)[K + 1]) {
+  DfaWalker<Get&> W{k, c1, get};
   // type -1: the full walk from c0, remembering its first kDfaHist candidates and the running sums around their
   // epochs (hcum[q]: before candidate q's epoch, hcum[q + 1]: after it)
   int64_t hpos[kDfaHist];
   uint32_t hcum[kDfaHist + 1];
   int nh = 0;
-  uint32_t sum = 0;
+  uint32_t total = 0;
+  uint8_t ext0 = 0;
   {
     int64_t M = c0;
     int j = -1;
+    // (register arrays written and read at compile-time indices only: the device keeps them in VGPRs)
     for (;;) {
-      const bool rec = nh < kDfaHist;
-      if (rec) {
-        hpos[nh] = M;
-        hcum[nh] = sum;
-      }
-      int64_t nxt;
-      int jn;
-      sum += epoch(M, j, nxt, jn);
-      if (rec) hcum[++nh] = sum;
+      const uint32_t before = total;
+      int64_t nxt = -1;
+      int jn = -1;
+      total += W.epoch(M, j, nxt, jn);
+#pragma unroll
+      for (int h = 0; h < kDfaHist; ++h)
+        if (h == nh) {
+          hpos[h] = M;
+          hcum[h] = before;
+          hcum[h + 1] = total;
+        }
+      if (nh < kDfaHist) nh += 1;
       if (nxt < 0) {
-        ext[0] = (uint8_t)(jn + 1);
+        ext0 = (uint8_t)(jn + 1);
         break;
       }
       M = nxt;
       j = jn;
     }
-    delta[0] = sum;
   }
-  const uint32_t total = sum;
+  delta[0] = total;
+  ext[0] = ext0;
   // types 0 .. k - 1: from scan e's first match, until a remembered candidate of the type -1 walk
   for (int e = 0; e < K; ++e) {
     if (e >= k) break;
-    int64_t M = next_set(e, c0);
-    if (M < 0) {  // no match of scan e in the chunk: the jump passes through
-      delta[e + 1] = 0;
-      ext[e + 1] = (uint8_t)(e + 1);
-      continue;
-    }
-    int j = e, q = 0;
-    uint32_t own = 0;
-    for (;;) {
-      while (q < nh && hpos[q] < M) ++q;
-      int64_t nxt;
-      int jn;
-      const uint32_t d = epoch(M, j, nxt, jn);
-      if (q < nh && hpos[q] == M) {  // joined the type -1 walk at its candidate q: its epochs after q follow
-        delta[e + 1] = own + d + (total - hcum[q + 1]);
-        ext[e + 1] = ext[0];
-        break;
+    uint32_t de = 0;
+    uint8_t xe = (uint8_t)(e + 1);
+    int64_t M = W.next_set(e, c0);
+    if (M >= 0) {  // else: no match of scan e in the chunk, the jump passes through
+      int j = e;
+      for (;;) {
+        int64_t nxt = -1;
+        int jn = -1;
+        const uint32_t d = W.epoch(M, j, nxt, jn);
+        uint32_t after = 0;
+        bool joined = false;
+#pragma unroll
+        for (int h = 0; h < kDfaHist; ++h)
+          if (h < nh && hpos[h] == M) {
+            joined = true;
+            after = total - hcum[h + 1];
+          }
+        if (joined) {  // joined the type -1 walk at one of its remembered candidates: its epochs after it follow
+          de += d + after;
+          xe = ext0;
+          break;
+        }
+        de += d;
+        if (nxt < 0) {
+          xe = (uint8_t)(jn + 1);
+          break;
+        }
+        M = nxt;
+        j = jn;
       }
-      own += d;
-      if (nxt < 0) {
-        delta[e + 1] = own;
-        ext[e + 1] = (uint8_t)(jn + 1);
-        break;
-      }
-      M = nxt;
-      j = jn;
     }
+#pragma unroll
+    for (int y = 1; y <= K; ++y)
+      if (y == e + 1) {
+        delta[y] = de;
+        ext[y] = xe;
+      }
   }
 }
 
