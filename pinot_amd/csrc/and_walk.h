@@ -43,26 +43,36 @@ struct AndWalkJob {
   uint8_t* gexit;                  // [k + 1][ngroups] their exit types + 1
 };
 
-// One chunk's walker: the k scans' words through get(i, w) (absolute word index inside the chunk [c0, c1)).
-template <class Get>
+// One chunk's walker: the k scans' words through get(i, w) (absolute word index inside the chunk [c0, c1)).  The k
+// words of the current candidate's 64-doc word stay in registers (read at compile-time indices only: the device keeps
+// them in VGPRs), so an epoch inside the word is register work; a candidate in another word reloads them.
+template <int K, class Get>
 struct DfaWalker {
   int k;
   int64_t c1;
   Get get;
-  // first scan without doc M (k: every scan has it)
-  __host__ __device__ int first_fail(int64_t M) const {
-    const int64_t w = M >> 6;
-    const unsigned long long bit = 1ull << (M & 63);
-    int f = 0;
-    while (f < k && (get(f, w) & bit) != 0ull) ++f;
-    return f;
+  int64_t cw = -1;          // word held in Wc
+  unsigned long long Wc[K];
+  __host__ __device__ void hold(int64_t w) {
+    if (w == cw) return;
+    cw = w;
+#pragma unroll
+    for (int i = 0; i < K; ++i) Wc[i] = i < k ? get(i, w) : ~0ull;
   }
   // scan i's first match in [x, c1), or -1
-  __host__ __device__ int64_t next_set(int i, int64_t x) const {
+  __host__ __device__ int64_t next_set(int i, int64_t x) {
     if (x >= c1) return -1;
     int64_t w = x >> 6;
     const int64_t wl = (c1 - 1) >> 6;
-    unsigned long long v = get(i, w) & (~0ull << (x & 63));
+    unsigned long long v = 0;
+    if (w == cw) {
+#pragma unroll
+      for (int y = 0; y < K; ++y)
+        if (y == i) v = Wc[y];
+    } else {
+      v = get(i, w);
+    }
+    v &= ~0ull << (x & 63);
     while (v == 0ull) {
       if (++w > wl) return -1;
       v = get(i, w);
@@ -72,8 +82,13 @@ struct DfaWalker {
   }
   // one epoch at M set by scan j (-1: none): returns its (calls - [match]) and sets the next candidate (-1: the walk
   // leaves the chunk) and its setter
-  __host__ __device__ uint32_t epoch(int64_t M, int j, int64_t& nxt, int& jn) const {
-    const int f = first_fail(M);
+  __host__ __device__ uint32_t epoch(int64_t M, int j, int64_t& nxt, int& jn) {
+    hold(M >> 6);
+    const int b = (int)(M & 63);
+    int f = k;  // first scan without doc M (k: every scan has it)
+#pragma unroll
+    for (int i = K - 1; i >= 0; --i)
+      if (i < k && ((Wc[i] >> b) & 1ull) == 0ull) f = i;
     const uint32_t skip = (j >= 0) ? 1u : 0u;
     if (f == k) {
       nxt = M + 1 < c1 ? M + 1 : -1;
@@ -90,7 +105,7 @@ struct DfaWalker {
 template <int K, class Get>
 __host__ __device__ inline void dfa_chunk(int k, int64_t c0, int64_t c1, Get&& get, uint32_t (&delta)[K + 1],
                                           uint8_t (&ext)[K + 1]) {
-  DfaWalker<Get&> W{k, c1, get};
+  DfaWalker<K, Get&> W{k, c1, get};
   // type -1: the full walk from c0, remembering its first kDfaHist candidates and the running sums around their
   // epochs (hcum[q]: before candidate q's epoch, hcum[q + 1]: after it)
   int64_t hpos[kDfaHist];

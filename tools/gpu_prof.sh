@@ -12,5 +12,10 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -
 rc=$?
 echo "rocprof $W$TAG rc=$rc"
 python3 -c "import json,sys; d=json.load(open('$OUT/bench.json')); r=d['roofline']; print('ms/step %.3f kernel_ms %.3f frac %.3f GB/s %.0f' % (d['ms_per_step'], r['kernel_ms'], r['frac'], r['achieved']))" || tail -5 $OUT/bench.err
-find $OUT -name "*kernel_stats.csv" | head -1 | while read f; do head -6 "$f" | cut -d, -f1-4 | cut -c1-120; done
+python3 - $OUT <<'PY'
+import csv, glob, sys
+f = sorted(glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True))
+for r in list(csv.DictReader(open(f[-1])))[:14]:
+    print(f"{r['Name'][:60]:60s} calls {r['Calls']:>5s} avg_ms {float(r['AverageNs'])/1e6:8.3f} tot_ms {float(r['TotalDurationNs'])/1e6:9.2f}")
+PY
 exit $rc
