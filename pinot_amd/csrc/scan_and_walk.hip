@@ -105,17 +105,19 @@ static void launch_dfa(const AndWalkJob* jobs, int32_t njobs, int64_t max_groups
   hipLaunchKernelGGL((k_and_dfa<K, BLOCK>), dim3((unsigned)max_groups, (unsigned)njobs), dim3(BLOCK), lds, s, jobs);
 }
 
-// chunks per workgroup of the launch k_and_dfa would use for an AND of k scans (the host sizes the tables with it)
-int and_dfa_block(int32_t max_k) { return max_k <= 8 ? 256 : 128; }
+// chunks per workgroup of the launch k_and_dfa would use for an AND of k scans (the host sizes the tables with it):
+// the LDS staging (K x 72 B per thread) sets the waves per CU -- 128 threads at K <= 4 (37 KiB: 16 waves per CU; r5
+// at 256 threads, 8 waves per CU, 44 % of wave cycles waited on the LDS word reads)
+int and_dfa_block(int32_t max_k) { return max_k <= 4 ? 128 : max_k <= 8 ? 128 : 64; }
 
 void launch_and_walk(const AndWalkJob* jobs, int32_t njobs, int64_t max_groups, int32_t max_k, unsigned long long* out,
                      hipStream_t s) {
   if (njobs <= 0 || max_groups <= 0) return;
   if (max_k > kMaxFbProgs) fail(PH_ERR_DEVICE, "AND walk wider than kMaxFbProgs scans");
   // the widest AND of the launch picks the register set (ST_SCANAND: at most kMaxFbProgs scans); LDS = K x 18 KiB
-  if (max_k <= 4) launch_dfa<4, 256>(jobs, njobs, max_groups, s);
-  else if (max_k <= 8) launch_dfa<8, 256>(jobs, njobs, max_groups, s);
-  else launch_dfa<kMaxFbProgs, 128>(jobs, njobs, max_groups, s);
+  if (max_k <= 4) launch_dfa<4, 128>(jobs, njobs, max_groups, s);
+  else if (max_k <= 8) launch_dfa<8, 128>(jobs, njobs, max_groups, s);
+  else launch_dfa<kMaxFbProgs, 64>(jobs, njobs, max_groups, s);
   PH_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_and_compose, dim3((unsigned)((njobs + 63) / 64)), dim3(64), 0, s, jobs, njobs, out);
   PH_HIP_CHECK(hipGetLastError());

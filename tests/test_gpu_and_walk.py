@@ -42,7 +42,7 @@ def test_device_tables_match_host(seed):
     k = int(rng.integers(2, 13))
     dens = rng.choice([0.003, 0.02, 0.15, 0.5, 0.9, 1.0], size=k)
     docs = [rng.random(n) < d for d in dens]
-    block = 256 if k <= 8 else 128
+    block = 128 if k <= 8 else 64
     exp_t, ng = _host_tables(docs, n, block)
     got_t = np.zeros_like(exp_t)
     got = _device(docs, n, got_t)
