@@ -25,6 +25,13 @@ __device__ __forceinline__ void conj_stage_sets(SegPtr S, uint32_t* sets, int ti
   }
 }
 
+// the leaf's doc bitmap word of run `run` (32 docs), when the filter statistic wants it (conj_reg's leaf masks are
+// the scan's own: the statistic's AND walk then reads no forward index again)
+__device__ __forceinline__ void conj_leaf_out(SegPtr S, int k, int32_t run, uint32_t mask, int64_t ndocs) {
+  uint32_t* out = S->sp_lbits[k];
+  if (out != nullptr && (int64_t)run < (ndocs + 63) / 64 * 2) out[run] = mask;  // the last word's upper half too
+}
+
 // a leaf's test of the 32 values of one lane's run into a 32-bit mask
 template <int C>
 __device__ __forceinline__ uint32_t conj_leaf_mask(SegPtr S, int k, const u32x4 (&pool)[C], const uint32_t* sets) {
@@ -78,11 +85,17 @@ __device__ __forceinline__ unsigned long long conj_step_word(SegPtr S, int32_t w
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int64_t d0 = (int64_t)(2 * w + 64 * h + lane) * 32;
-      uint32_t m = d0 >= ndocs ? 0u : (d0 + 32 <= ndocs ? 0xffffffffu : ((1u << (uint32_t)(ndocs - d0)) - 1u));
+      const int32_t run = 2 * w + 64 * h + lane;
+      const int64_t d0 = (int64_t)run * 32;
+      const uint32_t valid = d0 >= ndocs ? 0u : (d0 + 32 <= ndocs ? 0xffffffffu : ((1u << (uint32_t)(ndocs - d0)) - 1u));
+      uint32_t m = valid;
 #pragma unroll
       for (int k = 0; k < kMaxConj; ++k)
-        if (k < n) m &= conj_leaf_mask<2>(S, k, pool[h][k], sets);
+        if (k < n) {
+          const uint32_t lm = conj_leaf_mask<2>(S, k, pool[h][k], sets) & valid;
+          conj_leaf_out(S, k, run, lm, ndocs);
+          m &= lm;
+        }
       half[h] = m;
     }
   } else {
@@ -105,8 +118,12 @@ __device__ __forceinline__ unsigned long long conj_step_word(SegPtr S, int32_t w
         const int64_t bytes = (ndocs * col.bits + 7) / 8;
         reg_load<CC>(true, la, col.fwd, col.bits, bytes, ra, lane, pa);
         reg_load<CC>(true, lb, col.fwd, col.bits, bytes, rb, lane, pb);
-        half[0] &= conj_leaf_mask<CC>(S, k, pa, sets);
-        half[1] &= conj_leaf_mask<CC>(S, k, pb, sets);
+        const uint32_t ma = conj_leaf_mask<CC>(S, k, pa, sets) & valid(ra);
+        const uint32_t mb = conj_leaf_mask<CC>(S, k, pb, sets) & valid(rb);
+        conj_leaf_out(S, k, ra + lane, ma, ndocs);
+        conj_leaf_out(S, k, rb + lane, mb, ndocs);
+        half[0] &= ma;
+        half[1] &= mb;
       };
       if (col.bits <= 4) leaf(std::integral_constant<int, 1>{});
       else if (col.bits <= 8) leaf(std::integral_constant<int, 2>{});

@@ -180,6 +180,8 @@ struct DevSegment {
   int32_t sp_slot[kMaxConj];
   uint32_t sp_lo[kMaxConj], sp_len[kMaxConj];
   const uint32_t* sp_set[kMaxConj];
+  uint32_t* sp_lbits[kMaxConj];  // sp_reg: each scan leaf's doc bitmap (32-doc words), written by the front end for
+                                 // the filter statistic's AND walk (null: not needed)
   DevColumn cols[kMaxCols];
   DevValCol vals[kMaxVals];
   DevValCol vals2[kMaxVals];       // second operand of a 2-operand expression term (KParams::val_op)

@@ -1105,6 +1105,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     std::vector<int32_t> leaf_kinds;
     int32_t dseg = -1;
     std::vector<size_t> jobs;  // its FbJobs (<= kMaxFbProgs leaves each) for the leaves k_leaf_bitmaps does not take
+    // an AND of scans whose leaves the sparse kernels' register-direct front end evaluates anyway (conj_reg.h): it
+    // writes their doc bitmaps here (leaf-major, ceil(docs / 64) words each), so the walk reads no forward index
+    unsigned long long* fused = nullptr;
   };
   // a leaf k_leaf_bitmaps computes from the forward index: a dictId range or a small dictId set of a scan leaf
   auto fast_leaf = [&](const PNode& n) {
@@ -1588,6 +1591,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
 
   // ---- device segment table, programs, chunks
   std::vector<DevSegment> dsegs;
+  std::vector<std::vector<PNode>> sp_nodes;  // per DevSegment: its sparse scan leaves (SparseShape::scans)
   std::vector<FilterInsn> all_insns;
   std::vector<Chunk> chunks;
   std::vector<std::pair<size_t, std::vector<uint32_t>>> payload_fix;  // global insn index -> payload
@@ -1743,6 +1747,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     if (sparse_plan || agg_conj) {
       const SparseShape sh = sparse_shape(root);
+      if (sp_nodes.size() <= (size_t)si) sp_nodes.resize((size_t)si + 1);
+      for (const PNode* sc : sh.scans) sp_nodes[si].push_back(*sc);
       d.sp_reg = sh.groups.empty() ? 1 : 0;
       d.sp_nbm = 0;
       for (auto& g : sh.groups)
@@ -2112,6 +2118,50 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   for (auto& bf : bitmap_fix) all_insns[bf.first].ptr = bitmap_dev[bf.second];
   for (auto& fb : fbitmap_fix) dsegs[fb.first].fptr = bitmap_dev[fb.second];
   for (auto& sb : sbm_fix) dsegs[sb.first / kSparseBitmaps].sp_bm[sb.first % kSparseBitmaps] = bitmap_dev[sb.second];
+  // ANDs of scans on the register-direct sparse front end: its leaf masks become the statistic's leaf bitmaps
+  // (conj_reg.h conj_leaf_out), one buffer for all of them (their walks run after the scan, on stream b)
+  if ((kp.group_sparse || kp.agg_sparse) && kp.sparse_c > 0 && getenv("PH_STAT_FUSE") == nullptr) {
+    auto same = [](const PNode& a, const PNode& b) {
+      return a.col == b.col && a.op == b.op && a.lo == b.lo && a.len == b.len && a.set == b.set;
+    };
+    size_t words = 0;
+    std::vector<std::pair<size_t, std::vector<int>>> plan;  // (stat seg, sparse leaf of each stat leaf)
+    for (size_t t = 0; t < stat_segs.size(); ++t) {
+      StatSeg& ss = stat_segs[t];
+      if (ss.kind != ST_SCANAND || ss.dseg < 0 || !dsegs[ss.dseg].sp_reg) continue;
+      if ((size_t)ss.dseg >= sp_nodes.size()) continue;
+      const std::vector<PNode>& sp = sp_nodes[ss.dseg];
+      if (sp.size() != ss.leaves.size()) continue;
+      std::vector<int> to(ss.leaves.size(), -1);
+      std::vector<char> used(sp.size(), 0);
+      bool ok = true;
+      for (size_t l = 0; l < ss.leaves.size() && ok; ++l) {
+        for (size_t k = 0; k < sp.size(); ++k)
+          if (!used[k] && same(ss.leaves[l], sp[k])) {
+            to[l] = (int)k;
+            used[k] = 1;
+            break;
+          }
+        ok = to[l] >= 0;
+      }
+      if (!ok) continue;
+      plan.push_back({t, to});
+      words += ss.leaves.size() * (size_t)((dsegs[ss.dseg].num_docs + 63) / 64);
+    }
+    if (!plan.empty()) {
+      unsigned long long* buf = scratch.alloc<unsigned long long>(words);
+      size_t off = 0;
+      for (auto& pl_ : plan) {
+        StatSeg& ss = stat_segs[pl_.first];
+        DevSegment& d = dsegs[ss.dseg];
+        const size_t nw = (size_t)((d.num_docs + 63) / 64);
+        ss.fused = buf + off;
+        for (size_t l = 0; l < ss.leaves.size(); ++l)
+          d.sp_lbits[pl_.second[l]] = reinterpret_cast<uint32_t*>(buf + off + l * nw);
+        off += ss.leaves.size() * nw;
+      }
+    }
+  }
   // the optimistic numGroupsLimit scan's segment table: no keep bitsets, no first-doc tables (copied after every
   // device pointer above is fixed up: r3 copied it before, so FK_CONJ set leaves scanned with null bitsets)
   std::vector<DevSegment> dsegs_opt;
@@ -2502,8 +2552,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       };
       for (auto& ss : stat_segs) {
         if (ss.dseg < 0) continue;
-        total += seg_words(ss);
-        biggest = std::max(biggest, seg_words(ss));
+        if (!ss.fused) {  // a fused AND's bitmaps are the scan's (no batch buffer)
+          total += seg_words(ss);
+          biggest = std::max(biggest, seg_words(ss));
+        }
         n_scanand += ss.kind == ST_SCANAND;
         if (ss.kind == ST_SCANAND)
           walk_tab += (size_t)(ss.leaves.size() + 1) * (size_t)walk_groups(dsegs[ss.dseg].num_docs);
@@ -2525,6 +2577,44 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       LeafJob* d_ljobs = n_fast ? scratch.alloc<LeafJob>(n_fast) : nullptr;
       uint32_t* d_lsets = set_words ? scratch.alloc<uint32_t>(set_words) : nullptr;
       std::vector<int64_t> ent(stat_segs.size(), 0);
+      size_t tab_used = 0;  // walk tables handed out so far (fused ANDs first, then the batches')
+      // the fused ANDs' walks: after the scan that wrote their leaf bitmaps (ev_stop on the scan stream)
+      {
+        std::vector<AndWalkJob> wj;
+        std::vector<size_t> who;
+        int64_t max_groups = 0;
+        int32_t max_k = 0;
+        for (size_t t = 0; t < stat_segs.size(); ++t) {
+          const StatSeg& ss = stat_segs[t];
+          if (!ss.fused || ss.dseg < 0) continue;
+          const int64_t n = dsegs[ss.dseg].num_docs;
+          AndWalkJob J{};
+          J.bits = ss.fused;
+          J.nwords = (n + 63) / 64;
+          J.ndocs = n;
+          J.k = (int32_t)ss.leaves.size();
+          J.slot = (int32_t)wj.size();
+          J.nchunks = (n + kDfaChunkWords * 64 - 1) / (kDfaChunkWords * 64);
+          J.ngroups = (int32_t)walk_groups(n);
+          J.gdelta = d_wdelta + tab_used;
+          J.gexit = d_wexit + tab_used;
+          tab_used += (size_t)(J.k + 1) * (size_t)J.ngroups;
+          max_groups = std::max<int64_t>(max_groups, J.ngroups);
+          max_k = std::max(max_k, J.k);
+          wj.push_back(J);
+          who.push_back(t);
+        }
+        if (!wj.empty()) {
+          PH_HIP_CHECK(hipStreamWaitEvent(sb, lane.lane->ev_stop, 0));
+          PH_HIP_CHECK(hipMemcpyAsync(d_wjobs, wj.data(), sizeof(AndWalkJob) * wj.size(), hipMemcpyHostToDevice, sb));
+          launch_and_walk(d_wjobs, (int32_t)wj.size(), max_groups, max_k, d_out, sb);
+          std::vector<unsigned long long> o(wj.size());
+          PH_HIP_CHECK(hipMemcpyAsync(o.data(), d_out, 8 * wj.size(), hipMemcpyDeviceToHost, sb));
+          PH_HIP_CHECK(hipStreamSynchronize(sb));
+          for (size_t x = 0; x < who.size(); ++x) ent[who[x]] = dsegs[stat_segs[who[x]].dseg].num_docs - 1 + (int64_t)o[x];
+          stamp("stat walk (fused)");
+        }
+      }
       size_t next = 0;
       while (next < stat_segs.size()) {
         // the batch: whole segments up to cap_words words of bitmaps
@@ -2532,7 +2622,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         size_t used = 0;
         for (; next < stat_segs.size(); ++next) {
           const StatSeg& ss = stat_segs[next];
-          if (ss.dseg < 0) continue;
+          if (ss.dseg < 0 || ss.fused) continue;
           if (!batch.empty() && used + seg_words(ss) > cap_words) break;
           batch.push_back(next);
           base.push_back(used);
@@ -2634,8 +2724,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
             J.slot = (int32_t)wj.size();
             J.nchunks = (n + kDfaChunkWords * 64 - 1) / (kDfaChunkWords * 64);
             J.ngroups = (int32_t)walk_groups(n);
-            J.gdelta = d_wdelta + tab;
-            J.gexit = d_wexit + tab;
+            J.gdelta = d_wdelta + tab_used + tab;
+            J.gexit = d_wexit + tab_used + tab;
             tab += (size_t)(J.k + 1) * (size_t)J.ngroups;
             max_groups = std::max<int64_t>(max_groups, J.ngroups);
             max_k = std::max(max_k, J.k);

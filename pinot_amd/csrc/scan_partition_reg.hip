@@ -30,7 +30,9 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
   uint32_t* slots = reinterpret_cast<uint32_t*>(smem + p.pl_slot_off);
   {
     uint32_t* gpos = reinterpret_cast<uint32_t*>(smem + p.pl_bcnt_off);
-    for (int i = threadIdx.x; i < p.num_parts + 64; i += kRegBlock) pend[i] = 0;
+    // the lanes' scratch words start at 2^31 + 64: a scratch rank is then negative as an int, so the overflow test
+    // below (0 <= rank - C as an int) never fires for a missed doc, without a per-record partition compare
+    for (int i = threadIdx.x; i < p.num_parts + 64; i += kRegBlock) pend[i] = i < p.num_parts ? 0u : 0x80000040u;
     for (int i = threadIdx.x; i < p.num_parts; i += kRegBlock) gpos[i] = 0;
   }
   __syncthreads();
@@ -55,8 +57,10 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
     auto append_round = [&](auto jb) {
       part_flush_owner<kRegBlock>(p, smem, matched, false);
       lds_barrier();
-      // groups of 4: the 4 rank atomics issue back to back, then the 4 stores; a full ring (skewed round) sends its
-      // records to the overflow table (rare: one ballot per group)
+      // groups of 4: the 4 rank atomics issue back to back, then the 4 stores.  Branch-free and SGPR-free per record:
+      // slot = min(b * RS + min(rank, C), scratch slot) -- a real partition's ring slot (rank C: the ring's padding
+      // quarter, for a record that overflows), a missed doc's scratch slot; a full ring (skewed round) shows as
+      // 0 <= (int)(rank - C) (scratch ranks are negative), ORed over the group into one sign test
       static_for<0, 4>([&](auto u) {
         constexpr int J0 = decltype(jb)::value + 4 * decltype(u)::value;
         uint32_t b[4], w[4];
@@ -64,15 +68,14 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
           b[q] = part_of<J0 + decltype(q)::value>(PB);
           w[q] = atomicAdd(&pend[b[q]], 1u);
         });
-        bool ovf = false;
+        uint32_t neg = 0xffffffffu;  // bit 31 stays set while no record overflowed
         static_for<0, 4>([&](auto q) {
-          const bool real = b[q] < P;
-          ovf |= real & (w[q] >= C);
-          slots[(real & (w[q] < C)) ? __umul24(b[q], RS) + w[q] : dummy_slot] = X[J0 + decltype(q)::value];
+          neg &= w[q] - C;
+          slots[min(__umul24(b[q], RS) + min(w[q], C), dummy_slot)] = X[J0 + decltype(q)::value];
         });
-        if (__ballot(ovf)) {
+        if (__builtin_expect(__ballot((int32_t)neg >= 0) != 0ull, 0)) {
           static_for<0, 4>([&](auto q) {
-            if (b[q] < P && w[q] >= C) part_overflow<0>(p, b[q], X[J0 + decltype(q)::value]);
+            if ((int32_t)(w[q] - C) >= 0) part_overflow<0>(p, b[q], X[J0 + decltype(q)::value]);
           });
         }
       });
