@@ -345,6 +345,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--workload", default="config3", choices=sorted(list(WORKLOADS) + list(BUILT) + list(FLIGHTS)))
+    ap.add_argument("--devices", default=None,
+                    help="comma-separated HIP ordinals: ONE process drives one multi-device context over them "
+                         "(ph_ctx_create_multi, the Pinot server's drop-in; a repeated ordinal is a logical shard), "
+                         "instead of one process per GPU")
+    ap.add_argument("--transport", default="peer", choices=["peer", "rccl"], help="with --devices")
     args = ap.parse_args()
 
     import torch
@@ -385,7 +390,10 @@ def main():
     seg_rows = rows_total // nseg
     mine = [i for i in range(nseg) if i % world == rank]  # this rank's shard of the table
     t0 = time.time()
-    ctx = GpuContext(device)
+    devices = [int(x) for x in args.devices.split(",")] if args.devices else None
+    if devices and world > 1:
+        raise SystemExit("--devices drives every device from one process: run it without torch.distributed")
+    ctx = GpuContext(device) if not devices else GpuContext(devices=devices, transport=args.transport)
     bufs, pinned, seg_alg, ora_makers = [], [], [], []
     distinct_bufs = {}
     for k, i in enumerate(mine):
@@ -427,16 +435,21 @@ def main():
         r = ctx.execute(q, pinned, copy=False)
         last["res"] = r
         last["kernel"] = r.stats.scan_kernel
+        if devices:
+            phases.append({"scan": r.stats.device_ms, "merge": r.stats.merge_ms, "finalize": r.stats.finalize_ms,
+                           "devices": r.stats.num_devices})
         return r.stats.device_ms, r.stats.mode
 
+    phases = []
     log(f"[rank {rank}] pinned {len(pinned)} segments ({time.time() - t0:.1f}s); warmup")
     for _ in range(args.warmup):
         step()
+    phases.clear()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     log(f"[rank {rank}] timing {args.steps} steps")
-    dev_ms, phases = [], []
+    dev_ms = []
     mode = -1
     ts = time.perf_counter()
     for _ in range(args.steps):
@@ -479,8 +492,11 @@ def main():
                  f"synthetic (tests/workloads.py generators, {min(built[1], nseg)} distinct {seg_rows}-doc segments "
                  f"pinned as {nseg} segments, sharded over {world} GPU(s))"),
         "config": {"workload": wdesc, "table_rows": total_rows, "segments": nseg, "segments_per_gpu": len(mine),
-                   "parallelism": f"segments sharded x{world}" + (", RCCL reduce-scatter by key range" if world > 1
-                                                                  else "")},
+                   "parallelism": (f"one process, multi-device context over ordinals {devices} (segments placed by "
+                                   f"rows, dense partials reduce-scattered by key shard, {args.transport} transport)"
+                                   if devices else
+                                   f"segments sharded x{world}" + (", RCCL reduce-scatter by key range" if world > 1
+                                                                   else ""))},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                      "kernel": kernel_name(mode, last.get("kernel", 1)), "kernel_ms": kernel_ms,
@@ -492,7 +508,10 @@ def main():
         result["phases_ms"] = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}
     if last.get("res") is not None:
         result["groups"] = last["res"].num_groups
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if devices:
+        result["n_gpus"] = len(set(devices))
+        result["devices"] = devices
+    if rank == 0 and world == 1 and not args.no_cpu and not devices:
         threads = host_threads()
         log(f"[rank {rank}] {ms_per_step:.3f} ms/step; CPU baseline on {threads} threads")
         n, dt, dt1, keys, aggs = cpu_baseline(bufs, q, threads, args.cpu_seconds, ora_makers or None)
