@@ -23,6 +23,7 @@
 
 #include <rccl/rccl.h>
 
+#include "host_pool.h"
 #include "ph_internal.h"
 
 namespace ph {
@@ -77,24 +78,6 @@ ncclRedOp_t nccl_op(int op) {
 
 double ms_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
-}
-
-// run f(k) for every k in ks on its own host thread (one per device); the first exception is rethrown after the join
-template <class F>
-void per_device(const std::vector<int>& ks, F&& f) {
-  std::vector<std::exception_ptr> err(ks.size());
-  std::vector<std::thread> th;
-  for (size_t i = 0; i < ks.size(); ++i)
-    th.emplace_back([&, i] {
-      try {
-        f(ks[i]);
-      } catch (...) {
-        err[i] = std::current_exception();
-      }
-    });
-  for (auto& t : th) t.join();
-  for (auto& e : err)
-    if (e) std::rethrow_exception(e);
 }
 
 }  // namespace

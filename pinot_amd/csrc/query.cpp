@@ -31,6 +31,7 @@
 
 #include <functional>
 
+#include "host_pool.h"
 #include "ph_internal.h"
 
 namespace ph {
@@ -2747,30 +2748,14 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         std::vector<size_t> work_items;
         for (size_t b = 0; b < batch.size(); ++b)
           if (stat_segs[batch[b]].kind == ST_SIM) work_items.push_back(b);
-        std::atomic<size_t> next_item{0};
-        std::vector<std::exception_ptr> errs;
-        std::mutex err_mu;
-        auto work = [&]() {
-          try {
-            for (size_t t; (t = next_item.fetch_add(1)) < work_items.size();) {
-              const size_t b = work_items[t];
-              const StatSeg& ss = stat_segs[batch[b]];
-              const int64_t n = dsegs[ss.dseg].num_docs, nw = (n + 63) / 64;
-              std::vector<SimLeaf> lv(ss.leaves.size());
-              for (size_t l = 0; l < lv.size(); ++l) lv[l] = {ss.leaf_kinds[l], h.get() + hbase[b] + l * (size_t)nw};
-              ent[batch[b]] = simulate_filter_entries(ss.root, lv, n);
-            }
-          } catch (...) {
-            std::lock_guard<std::mutex> lk(err_mu);
-            errs.push_back(std::current_exception());
-          }
-        };
-        const size_t nthr = std::min<size_t>(work_items.size(), std::max(1u, std::min(8u, std::thread::hardware_concurrency())));
-        std::vector<std::thread> pool;
-        for (size_t k = 1; k < nthr; ++k) pool.emplace_back(work);
-        if (!work_items.empty()) work();
-        for (auto& th : pool) th.join();
-        if (!errs.empty()) std::rethrow_exception(errs.front());
+        pool_run(work_items.size(), std::min(8u, std::max(1u, std::thread::hardware_concurrency())), [&](size_t t) {
+          const size_t b = work_items[t];
+          const StatSeg& ss = stat_segs[batch[b]];
+          const int64_t n = dsegs[ss.dseg].num_docs, nw = (n + 63) / 64;
+          std::vector<SimLeaf> lv(ss.leaves.size());
+          for (size_t l = 0; l < lv.size(); ++l) lv[l] = {ss.leaf_kinds[l], h.get() + hbase[b] + l * (size_t)nw};
+          ent[batch[b]] = simulate_filter_entries(ss.root, lv, n);
+        });
       }
       for (int64_t e : ent) stats.num_entries_scanned_in_filter += e;
       stamp("stat pass");

@@ -77,3 +77,15 @@ def test_oracle_thread_pool_under_tsan():
                        timeout=600, env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
     assert r.returncode == 0, (r.stdout, r.stderr[-4000:])
     assert "equals the 1-thread run" in r.stdout and "ThreadSanitizer" not in r.stderr
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++ with the sanitizer runtimes")
+def test_library_host_concurrency_under_tsan():
+    # the library's own host threads (host_pool.h) -- the filter statistic's simulation pool over
+    # filter_sim.cpp and multi.cpp's per-device phases with a stub transport -- under ThreadSanitizer
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "sanitize")], check=True, timeout=600)
+    r = subprocess.run([os.path.join(ROOT, "build", "sanitize", "tsan_host")], capture_output=True, text=True,
+                       timeout=600, env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
+    assert r.returncode == 0, (r.stdout, r.stderr[-4000:])
+    assert "equal the 1-thread run" in r.stdout and "exception rethrown" in r.stdout, r.stdout
+    assert "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
