@@ -22,7 +22,11 @@
 // published block formats): LZ4 block format (lz4-java 1.8, LZ4Decompressor.java's safeDecompressor), the
 // LZ4_LENGTH_PREFIXED frame of lz4-java's LZ4CompressorWithLength (4-byte little-endian original length, then
 // one LZ4 block; LZ4WithLengthDecompressor.java), and the Snappy raw format (snappy-java 1.1,
-// SnappyDecompressor.java).  ZSTANDARD is PH_ERR_UNSUPPORTED.
+// SnappyDecompressor.java).  ZSTANDARD chunks are standard zstd frames (ZstandardCompressor.java:
+// Zstd.compress, ZstandardDecompressor.java: Zstd.decompress -- zstd-jni over libzstd): decoded by the system's
+// libzstd.so.1, dlopen'ed on first use (no link-time dependency; without it ZSTANDARD stays PH_ERR_UNSUPPORTED).
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <cstring>
 #include <limits>
@@ -33,6 +37,24 @@
 namespace ph {
 
 namespace {
+
+// libzstd.so.1's one-shot frame decoder (thread-safe: each call owns its context)
+struct Zstd {
+  size_t (*decompress)(void*, size_t, const void*, size_t) = nullptr;
+  unsigned (*is_error)(size_t) = nullptr;
+};
+const Zstd& zstd() {
+  static Zstd z = [] {
+    Zstd x;
+    void* h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return x;
+    x.decompress = reinterpret_cast<size_t (*)(void*, size_t, const void*, size_t)>(dlsym(h, "ZSTD_decompress"));
+    x.is_error = reinterpret_cast<unsigned (*)(size_t)>(dlsym(h, "ZSTD_isError"));
+    if (!x.decompress || !x.is_error) x.decompress = nullptr;
+    return x;
+  }();
+  return z;
+}
 
 inline uint32_t rd_be32(const uint8_t* p) {
   return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
@@ -174,7 +196,7 @@ void raw_forward_index_decode(const uint8_t* buf, uint64_t size, int32_t data_ty
   }
   const int off_size = version <= 2 ? 4 : 8;
   if (data_header + (uint64_t)nchunks * off_size > size) corrupt("chunk offsets beyond the buffer");
-  if (comp == 2) fail(PH_ERR_UNSUPPORTED, "raw forward index: ZSTANDARD chunks are not on the GPU path");
+  if (comp == 2 && !zstd().decompress) fail(PH_ERR_UNSUPPORTED, "raw forward index: ZSTANDARD needs libzstd.so.1");
   if (comp < 0 || comp > 4) corrupt("unknown compression type");
   auto chunk_pos = [&](int64_t c) -> uint64_t {
     const uint8_t* p = buf + data_header + (uint64_t)c * off_size;
@@ -198,6 +220,9 @@ void raw_forward_index_decode(const uint8_t* buf, uint64_t size, int32_t data_ty
         size_t got;
         if (comp == 1) {
           got = snappy_decompress(buf + pos, end - pos, tmp.data(), chunk_bytes);
+        } else if (comp == 2) {
+          got = zstd().decompress(tmp.data(), chunk_bytes, buf + pos, end - pos);
+          if (zstd().is_error(got)) corrupt("bad ZSTANDARD chunk");
         } else if (comp == 3) {
           got = lz4_block_decompress(buf + pos, end - pos, tmp.data(), chunk_bytes);
         } else {  // LZ4_LENGTH_PREFIXED

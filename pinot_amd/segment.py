@@ -237,6 +237,26 @@ def _lz4_block(data: bytes) -> bytes:
     return bytes(out)
 
 
+def _zstd(data: bytes) -> bytes:
+    """ZstandardCompressor (zstd-jni Zstd.compress, level 3): one standard zstd frame, through the system's
+    libzstd.so.1 (test data writer; the library decodes with the same libzstd)."""
+    import ctypes
+    z = ctypes.CDLL("libzstd.so.1")
+    z.ZSTD_compressBound.restype = ctypes.c_size_t
+    z.ZSTD_compressBound.argtypes = [ctypes.c_size_t]
+    z.ZSTD_compress.restype = ctypes.c_size_t
+    z.ZSTD_compress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    z.ZSTD_isError.restype = ctypes.c_uint
+    z.ZSTD_isError.argtypes = [ctypes.c_size_t]
+    cap = z.ZSTD_compressBound(len(data))
+    out = ctypes.create_string_buffer(cap)
+    src = ctypes.create_string_buffer(bytes(data), len(data))
+    n = z.ZSTD_compress(out, cap, src, len(data), 3)
+    if z.ZSTD_isError(n):
+        raise RuntimeError("zstd compression failed")
+    return out.raw[:n]
+
+
 def _snappy(data: bytes) -> bytes:
     """Snappy raw format: varint length, then literals and 2-byte-offset copies (greedy 4-byte hash matches)."""
     n, out = len(data), bytearray()
@@ -299,6 +319,8 @@ def write_raw_forward_index(values, data_type: str, compression: str = "PASS_THR
             body = len(body).to_bytes(4, "little") + _lz4_block(body)
         elif compression == "SNAPPY":
             body = _snappy(body)
+        elif compression == "ZSTANDARD":
+            body = _zstd(body)
         elif compression != "PASS_THROUGH":
             raise ValueError(compression)
         offsets.append(pos)

@@ -78,6 +78,21 @@ def snappy_decompress(src: bytes) -> bytes:
     return bytes(out)
 
 
+def zstd_decompress(src: bytes, cap: int) -> bytes:
+    """zstd frame -> bytes through the system's libzstd.so.1 (ZstandardDecompressor: Zstd.decompress)."""
+    import ctypes
+    z = ctypes.CDLL("libzstd.so.1")
+    z.ZSTD_decompress.restype = ctypes.c_size_t
+    z.ZSTD_decompress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+    z.ZSTD_isError.restype = ctypes.c_uint
+    z.ZSTD_isError.argtypes = [ctypes.c_size_t]
+    out = ctypes.create_string_buffer(max(1, cap))
+    s = ctypes.create_string_buffer(bytes(src), len(src))
+    n = z.ZSTD_decompress(out, cap, s, len(src))
+    assert not z.ZSTD_isError(n)
+    return out.raw[:n]
+
+
 def read_raw(buf: bytes, data_type: str, num_docs: int) -> np.ndarray:
     h = np.frombuffer(buf[:28], ">i4")
     version, nchunks, per, width = (int(x) for x in h[:4])
@@ -91,6 +106,8 @@ def read_raw(buf: bytes, data_type: str, num_docs: int) -> np.ndarray:
             chunk = snappy_decompress(chunk)
         elif comp == 3:
             chunk = lz4_decompress(chunk)
+        elif comp == 2:
+            chunk = zstd_decompress(chunk, per * width)
         elif comp == 4:
             want = int.from_bytes(chunk[:4], "little")
             chunk = lz4_decompress(chunk[4:])

@@ -60,7 +60,7 @@ def _check(ctx, segs, osegs, sql):
 
 
 @pytest.mark.parametrize("comp,version", [("PASS_THROUGH", 2), ("LZ4", 3), ("SNAPPY", 2),
-                                          ("LZ4_LENGTH_PREFIXED", 4)])
+                                          ("LZ4_LENGTH_PREFIXED", 4), ("ZSTANDARD", 3)])
 def test_raw_columns_match_oracle(ctx, comp, version):
     cols = _cols(200_003, 11)
     seg = ctx.pin(create_segment("raw0", cols, raw=("k", "m", "d", "f", "u"), raw_compression=comp,

@@ -1,6 +1,7 @@
 """CPU: raw (no-dictionary) forward indexes -- the library's host reader (ph_raw_forward_index_read, what
 ph_segment_pin runs on a raw column) against an independent Python reader (tests/raw_codecs.py) and the source
-values, for every fixed-width stored type, every supported chunk compression and writer versions 2 / 3 / 4
+values, for every fixed-width stored type, every chunk compression (ZSTANDARD through the system's libzstd.so.1, as
+zstd-jni) and writer versions 2 / 3 / 4
 (BaseChunkForwardIndexWriter.java, FixedByteChunkForwardIndexWriter.java; FixedByteChunkSVForwardIndexReader)."""
 import numpy as np
 import pytest
@@ -25,7 +26,7 @@ def _values(dt, n, seed):
 
 
 @pytest.mark.parametrize("dt", list(TYPES))
-@pytest.mark.parametrize("comp", ["PASS_THROUGH", "LZ4", "LZ4_LENGTH_PREFIXED", "SNAPPY"])
+@pytest.mark.parametrize("comp", ["PASS_THROUGH", "LZ4", "LZ4_LENGTH_PREFIXED", "SNAPPY", "ZSTANDARD"])
 @pytest.mark.parametrize("version", [2, 3, 4])
 def test_raw_reader_round_trip(dt, comp, version):
     v = _values(dt, 4321, seed_of(f"{dt}/{comp}/{version}") & 0xFFFF)
@@ -59,8 +60,12 @@ def test_corrupt_and_unsupported():
     with pytest.raises(N.PinotHipError):
         read_raw_forward_index(bad, "INT", len(v))
     z = write_raw_forward_index(v, "INT", "PASS_THROUGH").copy()
-    z[20:24] = np.frombuffer(np.array([2], ">i4").tobytes(), np.uint8)  # ZSTANDARD
-    with pytest.raises(N.UnsupportedError):
+    z[20:24] = np.frombuffer(np.array([2], ">i4").tobytes(), np.uint8)  # ZSTANDARD over bytes that are no zstd frame
+    with pytest.raises(N.PinotHipError):
+        read_raw_forward_index(z, "INT", len(v))
+    z = write_raw_forward_index(v, "INT", "PASS_THROUGH").copy()
+    z[20:24] = np.frombuffer(np.array([7], ">i4").tobytes(), np.uint8)  # no such ChunkCompressionType
+    with pytest.raises(N.PinotHipError):
         read_raw_forward_index(z, "INT", len(v))
     with pytest.raises(N.PinotHipError):  # lengthOfLongestEntry != the stored type's size
         read_raw_forward_index(write_raw_forward_index(v, "INT"), "LONG", len(v))
