@@ -411,15 +411,17 @@ void segment_check_impl(const ph_segment_desc* desc) {
     const std::string name = d.name;
     if (!d.forward_index) fail(PH_ERR_INVALID_ARGUMENT, "column " + name + ": missing forward index");
     if (d.hll_log2m < 0 || d.hll_log2m > 16) fail(PH_ERR_INVALID_ARGUMENT, "column " + name + ": hll_log2m");
-    // a raw column is dictionary-encoded at pin: at most n distinct values
-    const int64_t card = d.raw_forward_index ? std::max<int64_t>(1, n) : d.cardinality;
-    if (!d.raw_forward_index && d.cardinality <= 0 && n > 0) fail(PH_ERR_INVALID_ARGUMENT, "column " + name + ": cardinality <= 0");
+    // a raw column is dictionary-encoded at pin, where its real cardinality is known: its stream is checked there
+    // (a bound from num_docs distinct values would refuse large raw columns whose encoded stream is small)
+    if (d.raw_forward_index) continue;
+    const int64_t card = d.cardinality;
+    if (d.cardinality <= 0 && n > 0) fail(PH_ERR_INVALID_ARGUMENT, "column " + name + ": cardinality <= 0");
     const int bits = bits_for_card(card);
     const uint64_t packed = ((uint64_t)n * (uint64_t)bits + 7) / 8;
     if (packed > kMaxStreamBytes)
       fail(PH_ERR_UNSUPPORTED, "column " + name + ": packed stream of " + std::to_string(packed) +
                                    " bytes is past the 2 GiB range of the kernels' buffer offsets");
-    if (!d.raw_forward_index && !d.is_sorted && d.forward_index_size < packed)
+    if (!d.is_sorted && d.forward_index_size < packed)
       fail(PH_ERR_INVALID_ARGUMENT, "column " + name + ": forward index too small");
   }
 }
@@ -529,6 +531,9 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
     }
     const int bits = bits_for_card(card);  // PinotDataBitSet.getNumBitsPerValue(cardinality - 1)
     if (col->is_raw) {
+      if (((uint64_t)n * (uint64_t)bits + 7) / 8 > kMaxStreamBytes)
+        fail(PH_ERR_UNSUPPORTED, "column " + col->name + ": dictionary-encoded raw stream past the 2 GiB range of the "
+                                 "kernels' buffer offsets");
       packed.assign((size_t)((n * bits + 7) / 8), 0);
       fixed_bit_pack_host(ids.data(), n, bits, packed.data());
       src = packed.data();
