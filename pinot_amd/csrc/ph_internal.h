@@ -286,6 +286,8 @@ struct KParams {
   int32_t part_slot_log2;         // C = 1 << part_slot_log2 LDS ring slots per partition
   int32_t part_ring_stride;       // k_part_reg: words between consecutive partitions' rings (C + 4: the flush's owner
                                   // threads read their rings at distinct bank offsets)
+  int32_t part_set_words;         // k_part_reg: words between its two ring sets (slots; the pending words follow
+                                  // pl_lcnt_off at a stride of num_parts + 64)
   int32_t part_fast;              // kernel A may run the lean k_part_scan (no gathers; ALL / RANGE / DOCRANGE leaves)
   int32_t part_depth;             // lean kernel A: tiles of loads in flight per wave (1: k_part_scan, 2: k_part_scan2)
   int32_t part_reg;               // kernel A = k_part_reg (register-direct decode; 0: the LDS-staged forms)

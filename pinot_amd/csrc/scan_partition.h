@@ -97,9 +97,9 @@ __device__ __forceinline__ void part_flush_final(const KParams& p, uint8_t* smem
 // are written.
 template <int BLOCK>
 __device__ __forceinline__ void part_flush_owner(const KParams& p, uint8_t* smem, unsigned long long& matched,
-                                                 bool final) {
-  uint32_t* slots = reinterpret_cast<uint32_t*>(smem + p.pl_slot_off);
-  uint32_t* pend = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
+                                                 bool final, int set = 0, bool count = true) {
+  uint32_t* slots = reinterpret_cast<uint32_t*>(smem + p.pl_slot_off) + (size_t)set * p.part_set_words;
+  uint32_t* pend = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off) + (size_t)set * (p.num_parts + 64);
   uint32_t* gpos = reinterpret_cast<uint32_t*>(smem + p.pl_bcnt_off);
   const int cl = p.part_slot_log2;
   const uint32_t C = 1u << cl;
@@ -135,7 +135,7 @@ __device__ __forceinline__ void part_flush_owner(const KParams& p, uint8_t* smem
     pend[b] = left;
     gpos[b] = g + out;
     matched += raw - n;
-    if (final) {
+    if (final && count) {
       p.part_count[(size_t)b * gridDim.x + blockIdx.x] = g + out;  // records of region (b, blockIdx)
       matched += g + out;
     }

@@ -26,10 +26,13 @@ size_t partition_lds_bytes(KParams& p) {
   // partitions would read / write the same 16 bytes of their rings in ONE bank quad (r5: bank conflicts 72 % of the
   // kernel's LDS cycles); a 144-byte stride puts them on 16 distinct quads
   p.part_ring_stride = p.part_reg ? (1 << cl) + 4 : (1 << cl);
-  // + one scratch slot and one scratch word per lane: k_part_scan appends misses there (branch-free)
-  place(p.pl_slot_off, ((size_t)p.num_parts * p.part_ring_stride + 64) * rec);
+  // + one scratch slot and one scratch word per lane: k_part_scan appends misses there (branch-free); k_part_reg has
+  // two ring sets (a round appends to one while the other's completed chunks go out)
+  const int sets = p.part_reg ? 2 : 1;
+  p.part_set_words = (int32_t)((size_t)p.num_parts * p.part_ring_stride + 64);
+  place(p.pl_slot_off, (size_t)sets * p.part_set_words * rec);
   // generic kernel: (flushed / CH << 16 | pending) per partition; lean kernel: pending per partition
-  place(p.pl_lcnt_off, 4 * ((size_t)p.num_parts + 64));
+  place(p.pl_lcnt_off, 4 * ((size_t)p.num_parts + 64) * sets);
   place(p.pl_bcnt_off, 4 * (size_t)p.num_parts);  // lean kernel: records flushed per partition (region position)
   // lean kernel: two lists (round parity) of the partitions whose ring reached a whole chunk, + their counts
   place(p.pl_misc_off, 8 * (size_t)p.num_parts + 16);

@@ -27,12 +27,16 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint32_t* pend = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off);
-  uint32_t* slots = reinterpret_cast<uint32_t*>(smem + p.pl_slot_off);
+  uint32_t* const pend0 = pend;
+  uint32_t* const slots0 = reinterpret_cast<uint32_t*>(smem + p.pl_slot_off);
+  const size_t SW = (size_t)p.part_set_words;
+  uint32_t round = 0;
   {
     uint32_t* gpos = reinterpret_cast<uint32_t*>(smem + p.pl_bcnt_off);
     // the lanes' scratch words start at 2^31 + 64: a scratch rank is then negative as an int, so the overflow test
     // below (0 <= rank - C as an int) never fires for a missed doc, without a per-record partition compare
-    for (int i = threadIdx.x; i < p.num_parts + 64; i += kRegBlock) pend[i] = i < p.num_parts ? 0u : 0x80000040u;
+    for (int i = threadIdx.x; i < 2 * (p.num_parts + 64); i += kRegBlock)
+      pend[i] = (i % (p.num_parts + 64)) < p.num_parts ? 0u : 0x80000040u;
     for (int i = threadIdx.x; i < p.num_parts; i += kRegBlock) gpos[i] = 0;
   }
   __syncthreads();
@@ -53,10 +57,14 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
     // ---- the next tile's loads stay in flight through the append rounds
     t0 = tiles.next();
     tiles.load(t0, lane);
-    // ---- two append rounds: flush the chunks the previous round completed, then append 16 records per lane
+    // ---- two append rounds into alternating ring sets: a round appends 16 records per lane to set `cur` while the
+    // owner threads send out the whole chunks the previous round completed in the other set; one barrier per round
+    // (r4's single set needed two: flush, barrier, append, barrier)
     auto append_round = [&](auto jb) {
-      part_flush_owner<kRegBlock>(p, smem, matched, false);
-      lds_barrier();
+      const int cur = (int)(round & 1);
+      if (round > 0) part_flush_owner<kRegBlock>(p, smem, matched, false, cur ^ 1);
+      uint32_t* pend = pend0 + (size_t)cur * (P + 64);
+      uint32_t* slots = slots0 + (size_t)cur * SW;
       // groups of 4: the 4 rank atomics issue back to back, then the 4 stores.  Branch-free and SGPR-free per record:
       // slot = min(b * RS + min(rank, C), scratch slot) -- a real partition's ring slot (rank C: the ring's padding
       // quarter, for a record that overflows), a missed doc's scratch slot; a full ring (skewed round) shows as
@@ -80,13 +88,17 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
         }
       });
       lds_barrier();
+      ++round;
     };
     append_round(std::integral_constant<int, 0>{});
     append_round(std::integral_constant<int, 16>{});
   }
-  part_flush_owner<kRegBlock>(p, smem, matched, false);
+  // the last round's set still holds its whole chunks; every pending record of both sets then goes out (one owner
+  // thread per partition writes both sets' leftovers, then the region count)
+  if (round > 0) part_flush_owner<kRegBlock>(p, smem, matched, false, (int)((round - 1) & 1));
   lds_barrier();
-  part_flush_owner<kRegBlock>(p, smem, matched, true);
+  part_flush_owner<kRegBlock>(p, smem, matched, true, (int)(round & 1), false);
+  part_flush_owner<kRegBlock>(p, smem, matched, true, (int)((round - 1) & 1), true);
   if (matched && p.matched_total) atomicAdd(p.matched_total, matched);
 }
 
