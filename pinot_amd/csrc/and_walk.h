@@ -29,7 +29,7 @@
 
 namespace ph {
 
-constexpr int kDfaChunkWords = 8;  // a chunk = 8 words of 64 docs = 512 docs
+constexpr int kDfaChunkWords = 4;  // default chunk = 4 words of 64 docs = 256 docs (and_dfa_chunk_words())
 constexpr int kDfaHist = 8;        // candidates of the type -1 walk a chunk remembers
 
 struct AndWalkJob {
@@ -45,25 +45,26 @@ struct AndWalkJob {
 
 // One chunk's walker: the k scans' words through get(i, w) (absolute word index inside the chunk [c0, c1)).  The k
 // words of the current candidate's 64-doc word stay in registers (read at compile-time indices only: the device keeps
-// them in VGPRs), so an epoch inside the word is register work; a candidate in another word reloads them.
+// them in VGPRs), so an epoch inside the word is register work; a candidate in another word reloads them.  Doc
+// positions are 32-bit (a segment's docIds are Java ints), which halves the walk's integer work on the device.
 template <int K, class Get>
 struct DfaWalker {
   int k;
-  int64_t c1;
+  int32_t c1;
   Get get;
-  int64_t cw = -1;          // word held in Wc
+  int32_t cw = -1;          // word held in Wc
   unsigned long long Wc[K];
-  __host__ __device__ void hold(int64_t w) {
+  __host__ __device__ void hold(int32_t w) {
     if (w == cw) return;
     cw = w;
 #pragma unroll
     for (int i = 0; i < K; ++i) Wc[i] = i < k ? get(i, w) : ~0ull;
   }
   // scan i's first match in [x, c1), or -1
-  __host__ __device__ int64_t next_set(int i, int64_t x) {
+  __host__ __device__ int32_t next_set(int i, int32_t x) {
     if (x >= c1) return -1;
-    int64_t w = x >> 6;
-    const int64_t wl = (c1 - 1) >> 6;
+    int32_t w = x >> 6;
+    const int32_t wl = (c1 - 1) >> 6;
     unsigned long long v = 0;
     if (w == cw) {
 #pragma unroll
@@ -77,12 +78,12 @@ struct DfaWalker {
       if (++w > wl) return -1;
       v = get(i, w);
     }
-    const int64_t m = w * 64 + (int64_t)__builtin_ctzll(v);
+    const int32_t m = w * 64 + (int32_t)__builtin_ctzll(v);
     return m < c1 ? m : -1;
   }
   // one epoch at M set by scan j (-1: none): returns its (calls - [match]) and sets the next candidate (-1: the walk
   // leaves the chunk) and its setter
-  __host__ __device__ uint32_t epoch(int64_t M, int j, int64_t& nxt, int& jn) {
+  __host__ __device__ uint32_t epoch(int32_t M, int j, int32_t& nxt, int& jn) {
     hold(M >> 6);
     const int b = (int)(M & 63);
     int f = k;  // first scan without doc M (k: every scan has it)
@@ -105,31 +106,33 @@ struct DfaWalker {
 template <int K, class Get>
 __host__ __device__ inline void dfa_chunk(int k, int64_t c0, int64_t c1, Get&& get, uint32_t (&delta)[K + 1],
                                           uint8_t (&ext)[K + 1]) {
-  DfaWalker<K, Get&> W{k, c1, get};
+  DfaWalker<K, Get&> W{k, (int32_t)c1, get};
   // type -1: the full walk from c0, remembering its first kDfaHist candidates and the running sums around their
   // epochs (hcum[q]: before candidate q's epoch, hcum[q + 1]: after it)
-  int64_t hpos[kDfaHist];
+  int32_t hpos[kDfaHist];
   uint32_t hcum[kDfaHist + 1];
   int nh = 0;
   uint32_t total = 0;
   uint8_t ext0 = 0;
   {
-    int64_t M = c0;
+    int32_t M = (int32_t)c0;
     int j = -1;
     // (register arrays written and read at compile-time indices only: the device keeps them in VGPRs)
     for (;;) {
       const uint32_t before = total;
-      int64_t nxt = -1;
+      int32_t nxt = -1;
       int jn = -1;
       total += W.epoch(M, j, nxt, jn);
+      if (nh < kDfaHist) {  // (a branch: past the first kDfaHist epochs the wave skips the selects)
 #pragma unroll
-      for (int h = 0; h < kDfaHist; ++h)
-        if (h == nh) {
-          hpos[h] = M;
-          hcum[h] = before;
-          hcum[h + 1] = total;
-        }
-      if (nh < kDfaHist) nh += 1;
+        for (int h = 0; h < kDfaHist; ++h)
+          if (h == nh) {
+            hpos[h] = M;
+            hcum[h] = before;
+            hcum[h + 1] = total;
+          }
+        nh += 1;
+      }
       if (nxt < 0) {
         ext0 = (uint8_t)(jn + 1);
         break;
@@ -145,11 +148,11 @@ __host__ __device__ inline void dfa_chunk(int k, int64_t c0, int64_t c1, Get&& g
     if (e >= k) break;
     uint32_t de = 0;
     uint8_t xe = (uint8_t)(e + 1);
-    int64_t M = W.next_set(e, c0);
+    int32_t M = W.next_set(e, (int32_t)c0);
     if (M >= 0) {  // else: no match of scan e in the chunk, the jump passes through
       int j = e;
       for (;;) {
-        int64_t nxt = -1;
+        int32_t nxt = -1;
         int jn = -1;
         const uint32_t d = W.epoch(M, j, nxt, jn);
         uint32_t after = 0;

@@ -417,12 +417,13 @@ extern "C" int64_t phx_and_walk_entries(const uint64_t* bits, int32_t k, int64_t
   return ph::and_walk_entries_host(bits, k, num_docs, shift);
 }
 
-// test hook: the workgroup tables k_and_dfa writes (chunks of kDfaChunkWords words composed per `block` chunks), on
+// test hook: the workgroup tables k_and_dfa writes (chunks of and_dfa_chunk_words() words composed per `block` chunks), on
 // the host: gtab = (k + 1) x groups deltas, then (k + 1) x groups exit types + 1; returns the group count
 extern "C" int64_t phx_and_walk_tables_host(const uint64_t* bits, int32_t k, int64_t num_docs, int32_t block,
                                             uint32_t* gtab) {
   using namespace ph;
-  constexpr int K = kMaxFbProgs, CW = kDfaChunkWords;
+  constexpr int K = kMaxFbProgs;
+  const int CW = and_dfa_chunk_words();
   if (num_docs <= 0 || k < 1 || k > K || block < 1) return -1;
   const int64_t nwords = (num_docs + 63) / 64, nchunks = (num_docs + CW * 64 - 1) / (CW * 64);
   const int64_t ngroups = (nchunks + block - 1) / block;

@@ -643,6 +643,7 @@ void launch_filter_bitmaps(const FilterInsn* prog, const DevSegment* segs, const
 // scan_and_walk.hip); out[slot] = the job's sum of (calls - [match]) + [ends after a match]: entries = numDocs - 1 +
 // out.  Each job needs (k + 1) x ngroups table entries, ngroups = ceil(nchunks / and_dfa_block(max_k)).
 int and_dfa_block(int32_t max_k);
+int and_dfa_chunk_words();  // words of 64 docs per k_and_dfa chunk
 void launch_and_walk(const AndWalkJob* jobs, int32_t njobs, int64_t max_groups, int32_t max_k, unsigned long long* out,
                      hipStream_t s);
 // the same tables on the host (CPU tests), chunks of 1 << shift docs composed in order: the entries

@@ -2548,7 +2548,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         if (ss.dseg >= 0 && ss.kind == ST_SCANAND) walk_k = std::max(walk_k, (int32_t)ss.leaves.size());
       const int dfa_block = and_dfa_block(walk_k);
       auto walk_groups = [&](int64_t n) {
-        const int64_t nch = (n + kDfaChunkWords * 64 - 1) / (kDfaChunkWords * 64);
+        const int64_t nch = (n + and_dfa_chunk_words() * 64 - 1) / (and_dfa_chunk_words() * 64);
         return (nch + dfa_block - 1) / dfa_block;
       };
       for (auto& ss : stat_segs) {
@@ -2595,7 +2595,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           J.ndocs = n;
           J.k = (int32_t)ss.leaves.size();
           J.slot = (int32_t)wj.size();
-          J.nchunks = (n + kDfaChunkWords * 64 - 1) / (kDfaChunkWords * 64);
+          J.nchunks = (n + and_dfa_chunk_words() * 64 - 1) / (and_dfa_chunk_words() * 64);
           J.ngroups = (int32_t)walk_groups(n);
           J.gdelta = d_wdelta + tab_used;
           J.gexit = d_wexit + tab_used;
@@ -2723,7 +2723,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
             J.ndocs = n;
             J.k = (int32_t)ss.leaves.size();
             J.slot = (int32_t)wj.size();
-            J.nchunks = (n + kDfaChunkWords * 64 - 1) / (kDfaChunkWords * 64);
+            J.nchunks = (n + and_dfa_chunk_words() * 64 - 1) / (and_dfa_chunk_words() * 64);
             J.ngroups = (int32_t)walk_groups(n);
             J.gdelta = d_wdelta + tab_used + tab;
             J.gexit = d_wexit + tab_used + tab;

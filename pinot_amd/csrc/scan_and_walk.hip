@@ -5,7 +5,7 @@
 //                     workgroup (coalesced), the thread computes the chunk's table (dfa_chunk: one full walk and the
 //                     other entry types' walks up to where they join it), and the workgroup composes its chunks'
 //                     tables in a tree into one table per workgroup;
-//   k_and_compose  -- one thread per job composes the job's workgroup tables in order, from entry type -1 at doc 0.
+//   k_and_compose  -- one wave per job composes the job's workgroup tables in order, from entry type -1 at doc 0.
 // Exact for every input (no speculative walks, no reruns).  Algorithmic bytes: the k leaf bitmaps (k * numDocs / 8),
 // read once.  The host runs the same dfa_chunk over the same tables (filter_sim.cpp, phx_and_walk_entries) and the
 // parity tests check both against the iterator simulation and the oracle's restatement.
@@ -13,9 +13,9 @@
 
 namespace ph {
 
-template <int K, int BLOCK>
+template <int K, int BLOCK, int CW>
 __global__ void __launch_bounds__(BLOCK) k_and_dfa(const AndWalkJob* __restrict__ jobs) {
-  constexpr int CW = kDfaChunkWords, ST = CW + 1;  // chunk words in LDS with one word of padding (bank spread)
+  constexpr int ST = CW + 1;  // chunk words in LDS with one word of padding (bank spread)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned long long* words = reinterpret_cast<unsigned long long*>(smem);  // [K][BLOCK * ST]
   const AndWalkJob& J = jobs[blockIdx.y];
@@ -38,7 +38,8 @@ __global__ void __launch_bounds__(BLOCK) k_and_dfa(const AndWalkJob* __restrict_
   if (c < J.nchunks) {
     const int64_t c0 = c * CW * 64, c1 = c0 + CW * 64 < N ? c0 + CW * 64 : N;
     const unsigned long long* mine = words + (size_t)threadIdx.x * ST;
-    auto get = [&](int i, int64_t w) { return mine[(size_t)i * BLOCK * ST + (w - c * CW)]; };
+    const int32_t cwb = (int32_t)(c * CW);  // the chunk's first word (32-bit: docIds are Java ints)
+    auto get = [&](int i, int32_t w) { return mine[i * (BLOCK * ST) + (w - cwb)]; };
     dfa_chunk<K>(k, c0, c1, get, d, x);
   } else {  // past the job's last chunk: the identity
 #pragma unroll
@@ -83,31 +84,80 @@ __global__ void __launch_bounds__(BLOCK) k_and_dfa(const AndWalkJob* __restrict_
     }
 }
 
-__global__ void k_and_compose(const AndWalkJob* __restrict__ jobs, int32_t njobs, unsigned long long* out) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= njobs) return;
-  const AndWalkJob& J = jobs[t];
-  int e = 0;  // entry type -1 at doc 0
-  unsigned long long acc = 0;
-  for (int32_t g = 0; g < J.ngroups; ++g) {
-    acc += J.gdelta[(int64_t)e * J.ngroups + g];
-    e = J.gexit[(int64_t)e * J.ngroups + g];
+// one wave per job: lane l composes its slice of the workgroup tables for every entry type (the k + 1 chains' loads
+// interleaved), then lane 0 runs entry type -1 at doc 0 through the 64 slice tables in LDS.  (r5: one thread walking
+// all ~300 tables of a 10M-doc segment serially was 50-70 us per query.)
+__global__ void __launch_bounds__(64) k_and_compose(const AndWalkJob* __restrict__ jobs, unsigned long long* out) {
+  constexpr int K = kMaxFbProgs;
+  __shared__ unsigned long long sd[64][K + 1];
+  __shared__ uint8_t sx[64][K + 1];
+  const AndWalkJob& J = jobs[blockIdx.x];
+  const int lane = threadIdx.x, k = J.k;
+  const int64_t G = J.ngroups;
+  const int64_t g0 = G * lane / 64, g1 = G * (lane + 1) / 64;
+  unsigned long long acc[K + 1];
+  int t[K + 1];
+#pragma unroll
+  for (int e = 0; e <= K; ++e) {
+    acc[e] = 0;
+    t[e] = e;
   }
-  out[J.slot] = acc + (e == 0 ? 1ull : 0ull);  // + the epoch at numDocs when the walk ends after a match
+  for (int64_t g = g0; g < g1; ++g) {
+#pragma unroll
+    for (int e = 0; e <= K; ++e)
+      if (e <= k) {
+        acc[e] += J.gdelta[(int64_t)t[e] * G + g];
+        t[e] = J.gexit[(int64_t)t[e] * G + g];
+      }
+  }
+#pragma unroll
+  for (int e = 0; e <= K; ++e) {
+    sd[lane][e] = acc[e];
+    sx[lane][e] = (uint8_t)t[e];
+  }
+  __syncthreads();
+  if (lane == 0) {
+    int e = 0;  // entry type -1 at doc 0
+    unsigned long long a = 0;
+    for (int l = 0; l < 64; ++l) {
+      a += sd[l][e];
+      e = sx[l][e];
+    }
+    out[J.slot] = a + (e == 0 ? 1ull : 0ull);  // + the epoch at numDocs when the walk ends after a match
+  }
+}
+
+template <int K, int BLOCK, int CW>
+static void launch_dfa_cw(const AndWalkJob* jobs, int32_t njobs, int64_t max_groups, hipStream_t s) {
+  constexpr size_t lds_words = (size_t)K * BLOCK * (CW + 1) * 8;
+  constexpr size_t lds_tabs = (size_t)BLOCK * (K + 1) * 5;
+  constexpr size_t lds = lds_words > lds_tabs ? lds_words : lds_tabs;
+  allow_lds(k_and_dfa<K, BLOCK, CW>, lds);
+  hipLaunchKernelGGL((k_and_dfa<K, BLOCK, CW>), dim3((unsigned)max_groups, (unsigned)njobs), dim3(BLOCK), lds, s, jobs);
 }
 
 template <int K, int BLOCK>
 static void launch_dfa(const AndWalkJob* jobs, int32_t njobs, int64_t max_groups, hipStream_t s) {
-  constexpr size_t lds_words = (size_t)K * BLOCK * (kDfaChunkWords + 1) * 8;
-  constexpr size_t lds_tabs = (size_t)BLOCK * (K + 1) * 5;
-  constexpr size_t lds = lds_words > lds_tabs ? lds_words : lds_tabs;
-  allow_lds(k_and_dfa<K, BLOCK>, lds);
-  hipLaunchKernelGGL((k_and_dfa<K, BLOCK>), dim3((unsigned)max_groups, (unsigned)njobs), dim3(BLOCK), lds, s, jobs);
+  switch (and_dfa_chunk_words()) {
+    case 2: launch_dfa_cw<K, BLOCK, 2>(jobs, njobs, max_groups, s); break;
+    case 8: launch_dfa_cw<K, BLOCK, 8>(jobs, njobs, max_groups, s); break;
+    default: launch_dfa_cw<K, BLOCK, 4>(jobs, njobs, max_groups, s); break;
+  }
+}
+
+// words per chunk (2, 4 or 8; PH_DFA_CW is a tuning knob): the LDS staging of K x (CW + 1) words per thread sets the
+// waves per CU, the per-chunk walks of the other entry types (~4 epochs per chunk) the overhead of small chunks
+int and_dfa_chunk_words() {
+  static const int cw = [] {
+    const char* e = getenv("PH_DFA_CW");
+    const int v = e ? atoi(e) : kDfaChunkWords;
+    return v == 2 || v == 8 ? v : 4;
+  }();
+  return cw;
 }
 
 // chunks per workgroup of the launch k_and_dfa would use for an AND of k scans (the host sizes the tables with it):
-// the LDS staging (K x 72 B per thread) sets the waves per CU -- 128 threads at K <= 4 (37 KiB: 16 waves per CU; r5
-// at 256 threads, 8 waves per CU, 44 % of wave cycles waited on the LDS word reads)
+// 128 threads (r5 at 256 threads and 8-word chunks, 44 % of wave cycles waited on the LDS word reads)
 int and_dfa_block(int32_t max_k) { return max_k <= 4 ? 128 : max_k <= 8 ? 128 : 64; }
 
 void launch_and_walk(const AndWalkJob* jobs, int32_t njobs, int64_t max_groups, int32_t max_k, unsigned long long* out,
@@ -119,11 +169,14 @@ void launch_and_walk(const AndWalkJob* jobs, int32_t njobs, int64_t max_groups, 
   else if (max_k <= 8) launch_dfa<8, 128>(jobs, njobs, max_groups, s);
   else launch_dfa<kMaxFbProgs, 64>(jobs, njobs, max_groups, s);
   PH_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_and_compose, dim3((unsigned)((njobs + 63) / 64)), dim3(64), 0, s, jobs, njobs, out);
+  hipLaunchKernelGGL(k_and_compose, dim3((unsigned)njobs), dim3(64), 0, s, jobs, out);
   PH_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace ph
+
+// test hook: the chunk size (words of 64 docs) k_and_dfa runs with
+extern "C" int32_t phx_and_dfa_chunk_words() { return ph::and_dfa_chunk_words(); }
 
 // test hook (not part of the product boundary, include/pinot_hip.h): one AND-of-scans job on the current device over
 // host leaf bitmaps (leaf-major, k x ceil(n / 64) words); the entries, or -1 on a device error.  `gtab` (optional,
@@ -138,7 +191,7 @@ extern "C" int64_t phx_and_walk_entries_device(const uint64_t* bits, int32_t k, 
     J.ndocs = num_docs;
     J.k = k;
     J.slot = 0;
-    J.nchunks = (num_docs + kDfaChunkWords * 64 - 1) / (kDfaChunkWords * 64);
+    J.nchunks = (num_docs + and_dfa_chunk_words() * 64 - 1) / (and_dfa_chunk_words() * 64);
     const int block = and_dfa_block(k);
     J.ngroups = (int32_t)((J.nchunks + block - 1) / block);
     DeviceBuffer b, d, x, jb, o;

@@ -1,7 +1,7 @@
 """GPU: k_and_dfa / k_and_compose (numEntriesScannedInFilter of an AND of scans, and_walk.h) through the test hooks
 phx_and_walk_entries_device / phx_and_walk_tables_host: the device's workgroup tables and entries against the host's
 composition of the same chunk tables and against the iterator simulation, on random leaves, and the longest walk a chunk can
-take (every doc a match of 12 scans), which must finish within a stated bound (a chunk's walks are bounded by its 512
+take (every doc a match of 12 scans), which must finish within a stated bound (a chunk's walks are bounded by its 128-512
 docs: there is no rerun cliff) (AndDocIdIterator.java:40-72, SVScanDocIdIterator.java:101-112)."""
 import ctypes
 import time
@@ -29,7 +29,8 @@ def _host_tables(docs, n, block):
     f.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]
     bits = np.concatenate([_bitmap(d, n) for d in docs])
     k = len(docs)
-    ng = ((n + 511) // 512 + block - 1) // block
+    cw = N.lib().phx_and_dfa_chunk_words()  # the chunk size the device uses (words of 64 docs)
+    ng = ((n + 64 * cw - 1) // (64 * cw) + block - 1) // block
     t = np.zeros(2 * (k + 1) * ng, np.uint32)
     assert f(bits.ctypes.data, k, n, block, t.ctypes.data) == ng
     return t, ng
@@ -57,7 +58,7 @@ def test_device_tables_match_host(seed):
 
 
 def test_worst_case_is_bounded():
-    # every doc matches all 12 scans: every chunk walks 512 epochs of 12 advance() calls (the longest walk a chunk can
+    # every doc matches all 12 scans: every chunk walks one epoch per doc of 12 advance() calls (the longest walk a chunk can
     # take); the sum has a closed form, numDocs x k (k calls per doc, the last epoch at numDocs included), and 2^24
     # docs must finish within 2 s
     n, k = 1 << 24, 12
