@@ -502,8 +502,9 @@ struct Lane {
   hipEvent_t ev_bm0 = nullptr, ev_bm1 = nullptr;  // around the inverted-leaf bitmap build (part of device_ms)
   hipEvent_t ev_uploaded = nullptr;  // the call's segment descriptors and programs are in HBM (statistics pass)
   std::vector<hipEvent_t> ev_pool;
-  void* staging[2] = {nullptr, nullptr};  // slot 0: launch parameters; slot 1: the bitmap build's work items
-  size_t staging_bytes[2] = {0, 0};
+  // slot 0: launch parameters; slot 1: the bitmap build's work items; slot 2: predicate payloads (sets / ranges)
+  void* staging[3] = {nullptr, nullptr, nullptr};
+  size_t staging_bytes[3] = {0, 0, 0};
   explicit Lane(int dev);
   ~Lane();
   void* host_staging(size_t n, int slot = 0);  // valid until the lane's stream passes this call's uploads

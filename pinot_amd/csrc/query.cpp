@@ -2107,13 +2107,16 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     for (auto& cf : conj_set_fix) put(cf.second);
     if (!blob.empty()) {
       uint32_t* dblob = scratch.alloc<uint32_t>(blob.size());
-      PH_HIP_CHECK(hipMemcpyAsync(dblob, blob.data(), 4 * blob.size(), hipMemcpyHostToDevice, st));
+      // from pinned staging (slot 2): no host wait for the copy (r5: a pageable copy here synchronised the stream,
+      // so the host waited for the bitmap build before it could finish the setup)
+      uint32_t* hblob = static_cast<uint32_t*>(lane.lane->host_staging(4 * blob.size(), 2));
+      memcpy(hblob, blob.data(), 4 * blob.size());
+      PH_HIP_CHECK(hipMemcpyAsync(dblob, hblob, 4 * blob.size(), hipMemcpyHostToDevice, st));
       size_t i = 0;
       for (auto& pf : payload_fix) all_insns[pf.first].ptr = dblob + at[i++];
       for (auto& ff : fset_fix) dsegs[ff.first].fptr = dblob + at[i++];
       for (auto& sf : sset_fix) dsegs[sf.first / kMaxConj].sp_set[sf.first % kMaxConj] = dblob + at[i++];
       for (auto& cf : conj_set_fix) dsegs[cf.first / kMaxConj].cset[cf.first % kMaxConj] = dblob + at[i++];
-      PH_HIP_CHECK(hipStreamSynchronize(st));  // the pageable copy
     }
   }
   for (auto& bf : bitmap_fix) all_insns[bf.first].ptr = bitmap_dev[bf.second];

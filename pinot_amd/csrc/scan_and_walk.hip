@@ -145,16 +145,6 @@ static void launch_dfa(const AndWalkJob* jobs, int32_t njobs, int64_t max_groups
   }
 }
 
-// words per chunk (2, 4 or 8; PH_DFA_CW is a tuning knob): the LDS staging of K x (CW + 1) words per thread sets the
-// waves per CU, the per-chunk walks of the other entry types (~4 epochs per chunk) the overhead of small chunks
-int and_dfa_chunk_words() {
-  static const int cw = [] {
-    const char* e = getenv("PH_DFA_CW");
-    const int v = e ? atoi(e) : kDfaChunkWords;
-    return v == 2 || v == 8 ? v : 4;
-  }();
-  return cw;
-}
 
 // chunks per workgroup of the launch k_and_dfa would use for an AND of k scans (the host sizes the tables with it):
 // 128 threads (r5 at 256 threads and 8-word chunks, 44 % of wave cycles waited on the LDS word reads)
