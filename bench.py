@@ -88,6 +88,8 @@ def kernel_name(mode, scan_kernel):
         name = f"k_scan<{MODE_NAMES.get(mode, mode)}>"
     if scan_kernel == 3:
         name += " (+ k_roaring_chunk bitmap build)"
+    if scan_kernel == 14:
+        name = "k_agg_sparse<containers> (no bitmap build)"
     return name
 
 

@@ -228,7 +228,9 @@ enum {
   PH_KERNEL_AGG_REG = 10,      /* k_agg_reg: k_agg_lean's aggregation in the register-direct form */
   PH_KERNEL_GROUP_REG = 11,    /* k_group_reg: k_group_lds_lean's group-by in the register-direct form */
   PH_KERNEL_GROUP_SPARSE = 12, /* k_group_sparse: group-by over selective inverted-index ANDs, matched-doc gathers */
-  PH_KERNEL_PART_WAVE = 13     /* k_part_wave + k_part_agg: partitioned group-by, wave-private rings, no barriers */
+  /* 13: retired (round 4's wave-private-ring kernel A, removed in round 5) */
+  PH_KERNEL_AGG_CONTAINERS = 14 /* k_agg_sparse straight from one inverted dictId's roaring containers (no doc
+                                   bitmaps; BitmapInvertedIndexReader.java:45-62) */
 };
 
 /* ------------------------------------------------------------------ context */

@@ -150,6 +150,8 @@ struct DevPiece {
 };
 constexpr int kMaxPieces = 12;  // == kPrefetchOther >= kPrefetchCount
 
+struct RoaringContainer;
+
 struct DevSegment {
   int32_t num_docs;
   int32_t npieces;
@@ -182,6 +184,10 @@ struct DevSegment {
   const uint32_t* sp_set[kMaxConj];
   uint32_t* sp_lbits[kMaxConj];  // sp_reg: each scan leaf's doc bitmap (32-doc words), written by the front end for
                                  // the filter statistic's AND walk (null: not needed)
+  // k_agg_sparse container mode (KParams::agg_cont): the FK_BITMAP leaf's dictIds as their roaring containers in
+  // the column's device directory (the chunks name ranges of them) and the inverted buffer they point into
+  const RoaringContainer* cdir;
+  const uint8_t* cbase;
   DevColumn cols[kMaxCols];
   DevValCol vals[kMaxVals];
   DevValCol vals2[kMaxVals];       // second operand of a 2-operand expression term (KParams::val_op)
@@ -273,6 +279,8 @@ struct KParams {
   int32_t part_load_first;        // lean kernel A: issue the next tile's loads before the flush (tuning)
   int32_t agg_fast;               // MODE_AGG: run k_agg_lean
   int32_t agg_sparse;             // MODE_AGG over selective bitmap leaves: run k_agg_sparse
+  int32_t agg_cont;               // k_agg_sparse straight from each segment's roaring containers (no doc bitmaps):
+                                  // chunks are container ranges of DevSegment::cdir
   int32_t sparse_c;               // sparse kernels over sp_reg segments: 16-byte loads per lane of a leaf (4 or 8)
   int32_t lds_fast;               // MODE_GROUP_LDS: run k_group_lds_lean
   int32_t lds_pack;               //   COUNT << 40 | SUM in one 64-bit LDS word

@@ -1253,9 +1253,25 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
   };
   stamp("plan");
+  // Aggregation-only queries whose every segment is filtered by ONE inverted leaf (EQ / IN) may run k_agg_sparse
+  // straight from the leaf's roaring containers (KParams::agg_cont, decided with the sparse plan below): the dictIds
+  // of a single-value column have disjoint doc sets, so the leaf's docs are the disjoint union of its ids'
+  // containers and no doc bitmap is needed.  The bitmaps are built only if that plan is not taken
+  bool cont_defer = q->num_group_by == 0 && !pl.bitmaps.empty() && dop != DENSE_LAYOUT && !fin;
+  if (const char* e = getenv("PH_AGG_CONT")) cont_defer = cont_defer && atoi(e) != 0;  // tuning knob
+  {
+    int live = 0;
+    for (int i = 0; i < nseg && cont_defer; ++i) {
+      if (!seg_live[i]) continue;
+      ++live;
+      const PNode& r = roots[i];
+      cont_defer = r.kind == L_NODE && r.op == OP_BITMAP && !r.exclusive && r.bitmap_leaf >= 0;
+    }
+    cont_defer = cont_defer && live == (int)pl.bitmaps.size();  // no other bitmap leaf anywhere
+  }
   // the bitmap build's device time is part of the query's device_ms (its own event pair: host setup follows it)
   bool bm_timed = false;
-  if (!pl.bitmaps.empty() && dop != DENSE_LAYOUT && !fin) {
+  if (!pl.bitmaps.empty() && dop != DENSE_LAYOUT && !fin && !cont_defer) {
     PH_HIP_CHECK(hipEventRecord(lane.lane->ev_bm0, st));
     build_bitmaps();
     PH_HIP_CHECK(hipEventRecord(lane.lane->ev_bm1, st));
@@ -1974,6 +1990,31 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     kp.agg_sparse = (all_bitmap && hits * 8 < docs) || agg_conj;
     if (const char* e = getenv("PH_AGG_SPARSE")) kp.agg_sparse = (all_bitmap || agg_conj) && atoi(e) != 0;  // tuning knob
     if (kp.agg_sparse) kp.agg_fast = 0;
+    kp.agg_cont = cont_defer && kp.agg_sparse && all_bitmap && !agg_conj;
+    if (cont_defer && !kp.agg_cont) {  // the deferred doc bitmaps after all
+      PH_HIP_CHECK(hipEventRecord(lane.lane->ev_bm0, st));
+      build_bitmaps();
+      PH_HIP_CHECK(hipEventRecord(lane.lane->ev_bm1, st));
+      bm_timed = true;
+    }
+    if (kp.agg_cont) {
+      // chunks = ranges of <= 8 containers of each dictId of each segment's leaf (a wave takes one at a time)
+      chunks.clear();
+      for (auto& fb : fbitmap_fix) {
+        const BitmapLeaf& bl = pl.bitmaps[fb.second];
+        const Column& col = *bl.col;
+        DevSegment& d = dsegs[fb.first];
+        d.cdir = col.d_dir.as<RoaringContainer>();
+        d.cbase = col.d_inverted.as<uint8_t>();
+        dseg_chunks[fb.first].first = (int32_t)chunks.size();
+        for (int32_t id : bl.dict_ids) {
+          const int64_t f = col.dir_begin[id], e = col.dir_begin[id + 1];
+          for (int64_t x = f; x < e; x += 8)
+            chunks.push_back({(int32_t)fb.first, (int32_t)x, (int32_t)std::min<int64_t>(e, x + 8), 0});
+        }
+        dseg_chunks[fb.first].second = (int32_t)chunks.size();
+      }
+    }
   }
   // the register-direct leaves' loads per lane (conj_reg.h): by the widest scan column of an sp_reg segment
   // (2: every leaf <= 8 bits, all loads hoisted; 0: no segment has register-direct leaves)
@@ -2210,6 +2251,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       const int grid = (int)std::min<int64_t>((int64_t)chunks.size(), (int64_t)ctx->num_cus * blocks_per_cu);
       stats.scan_kernel = kp.count_reg  ? PH_KERNEL_COUNT_REG
                           : kp.agg_reg    ? PH_KERNEL_AGG_REG
+                          : kp.agg_cont   ? PH_KERNEL_AGG_CONTAINERS
                           : kp.agg_sparse ? PH_KERNEL_AGG_SPARSE
                           : kp.agg_fast  ? PH_KERNEL_AGG_LEAN
                           : kp.group_sparse ? PH_KERNEL_GROUP_SPARSE

@@ -182,6 +182,9 @@ __global__ void __launch_bounds__(kBlock) k_agg_lean(const KParams p) {
 // filtered by an AND of scan leaves only (sp_reg) takes its step words from conj_reg.h (the leaves decoded
 // register-direct) instead of a bitmap; EX: the value term `a <op> b` of one value column (SSB Q1.x's
 // SUM(lo_extendedprice * lo_discount)), exact int64 for integer terms as k_scan's.
+// a little-endian uint16 of a roaring payload (payloads need not be 2-byte aligned in the inverted buffer)
+__device__ __forceinline__ uint32_t cont_u16(const uint8_t* b) { return (uint32_t)b[0] | ((uint32_t)b[1] << 8); }
+
 template <int EX, int C>
 __global__ void __launch_bounds__(kBlock) k_agg_sparse(const KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -206,13 +209,138 @@ __global__ void __launch_bounds__(kBlock) k_agg_sparse(const KParams p) {
     vmin[j] = INT64_MAX;
     vmax[j] = INT64_MIN;
   }
-  unsigned long long matched = 0;
+  unsigned long long matched = 0;  // wave-uniform
+  // one matched doc: its value terms / HLL entries
+  auto agg_doc = [&](SegPtr S, uint32_t doc) {
+    for (int j = 0; j < p.num_vals && j < kMaxVals; ++j) {
+      const PH_CONST DevValCol& vc = S->vals[j];
+      int64_t iv;
+      double dv;
+      read_value(vc.kind, vc.base, vc.table, unpack_bits(vc.fwd, vc.bits, doc), iv, dv);
+      if constexpr (EX != 0) {  // one value column with a 2-operand term (the host picks EX only then)
+        const PH_CONST DevValCol& v2 = S->vals2[0];
+        int64_t ib;
+        double db;
+        read_value(v2.kind, v2.base, v2.table, unpack_bits(v2.fwd, v2.bits, doc), ib, db);
+        if (p.val_is_int[0]) {
+          iv = EX == PH_EXPR_MULT ? iv * ib : (EX == PH_EXPR_SUB ? iv - ib : iv + ib);
+        } else {
+          const double x = vc.kind == VK_DICT_F64 ? dv : (double)iv;
+          const double y = v2.kind == VK_DICT_F64 ? db : (double)ib;
+          dv = EX == PH_EXPR_MULT ? (1.0 * x) * y : (EX == PH_EXPR_SUB ? x - y : x + y);
+          iv = double_order_key(dv);
+        }
+      }
+      const int ops = p.val_ops[j];
+      if (ops & OPS_SUM) {
+        if (p.val_is_int[j]) isum[j] += iv; else dsum[j] += dv;
+      }
+      if (ops & OPS_MIN) vmin[j] = iv < vmin[j] ? iv : vmin[j];
+      if (ops & OPS_MAX) vmax[j] = iv > vmax[j] ? iv : vmax[j];
+    }
+    for (int h = 0; h < p.num_hll && h < kMaxHll; ++h) {
+      ColRef col = S->cols[p.hll_slot[h]];
+      const uint32_t e = gld(col.hll + unpack_col(col, doc));
+      atomicMax(&lds_hll[h * m + (e >> 8)], e & 0xffu);
+    }
+  };
+  // one wave step: lane l holds the 64-doc word of docs sb + 64 l ..; a wave prefix sum of the popcounts places every
+  // matched doc in the wave's LDS list, gathered 64 docs per round with every lane busy
+  auto step = [&](SegPtr S, uint32_t sb, unsigned long long bits) {
+    const uint32_t cnt = (uint32_t)__popcll(bits);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    if (total == 0) return;
+    uint32_t pos = incl - cnt;
+    while (bits) {
+      list[pos++] = (uint16_t)(lane * 64 + __builtin_ctzll(bits));
+      bits &= bits - 1ull;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    matched += total;
+    for (uint32_t base = 0; base < total; base += 64)
+      if (base + (uint32_t)lane < total) agg_doc(S, sb + list[base + lane]);
+    // every lane has read its list entries before the next step rewrites the list
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
   const int64_t nch = p.chunk_end - p.chunk_begin;
   const int32_t c0 = p.chunk_begin + (int32_t)(nch * blockIdx.x / gridDim.x);
   const int32_t c1 = p.chunk_begin + (int32_t)(nch * (blockIdx.x + 1) / gridDim.x);
   for (int32_t c = c0; c < c1; ++c) {
     SegPtr S = segs + chunks[c].seg;
     const uint32_t ndocs = (uint32_t)S->num_docs;
+    if constexpr (C < 0) {
+      // container mode (InvertedIndexFilterOperator over EQ / IN, BitmapInvertedIndexReader.java:45-62): the chunk
+      // is a range of one dictId's roaring containers (a single-value column's ids have disjoint doc sets, so the
+      // leaf is their disjoint union), a wave takes one at a time -- an array container IS the matched-doc list
+      // (no doc bitmap is built, written or re-read)
+      for (int32_t ci = chunks[c].word_begin + wave; ci < chunks[c].word_end; ci += WAVES) {
+        const RoaringContainer ct = S->cdir[ci];
+        const uint8_t* pay = S->cbase + ct.offset;
+        const uint32_t hi = (uint32_t)ct.key << 16;
+        const bool arr = ct.type == 0;
+        // an array container is one pass over its sorted low halves; bitmap / run containers are 16 wave steps of
+        // 4096 docs whose 64-doc words (read, or OR-ed from the runs) are listed in LDS first
+        for (int st = 0; st < (arr ? 1 : 16); ++st) {
+          uint32_t n = (uint32_t)ct.card, sb = hi;
+          if (!arr) {
+            const uint32_t wd = hi + 4096u * (uint32_t)st + 64u * (uint32_t)lane;  // this lane's 64-doc word
+            unsigned long long bits = 0;
+            if (ct.type == 1) {
+              const uint8_t* q = pay + 8 * (st * 64 + lane);
+#pragma unroll
+              for (int y = 0; y < 8; ++y) bits |= (unsigned long long)q[y] << (8 * y);
+            } else {
+              for (int r = 0; r < ct.card; ++r) {  // (start, length - 1) pairs; runs are rare on this path
+                const uint32_t rs = hi | cont_u16(pay + 2 + 4 * r), re = rs + cont_u16(pay + 4 + 4 * r);
+                if (re < wd || rs >= wd + 64u) continue;
+                const uint32_t lo = rs > wd ? rs - wd : 0u, up = re - wd < 63u ? re - wd : 63u;
+                bits |= (up - lo == 63u ? ~0ull : ((1ull << (up - lo + 1u)) - 1ull)) << lo;
+              }
+            }
+            if (wd + 64u > ndocs) bits &= wd >= ndocs ? 0ull : ((1ull << (ndocs - wd)) - 1ull);
+            const uint32_t cnt = (uint32_t)__popcll(bits);
+            uint32_t incl = cnt;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+              const uint32_t t = __shfl_up(incl, o, 64);
+              if (lane >= o) incl += t;
+            }
+            n = __shfl(incl, 63, 64);
+            if (n == 0) continue;
+            uint32_t pos = incl - cnt;
+            while (bits) {
+              list[pos++] = (uint16_t)(lane * 64 + __builtin_ctzll(bits));
+              bits &= bits - 1ull;
+            }
+            sb = hi + 4096u * (uint32_t)st;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          }
+          for (uint32_t base = 0; base < n; base += 64) {
+            const uint32_t i = base + (uint32_t)lane;
+            const uint32_t doc = i < n ? sb + (arr ? cont_u16(pay + 2 * i) : (uint32_t)list[i]) : 0xffffffffu;
+            const bool ok = doc < ndocs;
+            matched += (unsigned long long)__popcll(__ballot(ok));
+            if (ok) agg_doc(S, doc);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+      }
+      continue;
+    } else {
     const unsigned long long* bm = reinterpret_cast<const unsigned long long*>(S->fptr);  // 64 docs per word
     const int32_t wb = chunks[c].word_begin, we = chunks[c].word_end;
     const bool reg = S->sp_reg != 0;  // chunk-uniform: every wave of the workgroup walks the same chunks
@@ -235,63 +363,8 @@ __global__ void __launch_bounds__(kBlock) k_agg_sparse(const KParams p) {
       }
       const uint32_t d0 = (uint32_t)(w + lane) * 64u;
       if (d0 + 64u > ndocs) bits &= d0 >= ndocs ? 0ull : ((1ull << (ndocs - d0)) - 1ull);
-      const uint32_t cnt = (uint32_t)__popcll(bits);
-      uint32_t incl = cnt;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
-      }
-      const uint32_t total = __shfl(incl, 63, 64);
-      if (total == 0) continue;
-      uint32_t pos = incl - cnt;
-      while (bits) {
-        list[pos++] = (uint16_t)(lane * 64 + __builtin_ctzll(bits));
-        bits &= bits - 1ull;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      matched += total;
-      for (uint32_t base = 0; base < total; base += 64) {
-        if (base + (uint32_t)lane >= total) continue;
-        const uint32_t doc = (uint32_t)w * 64u + list[base + lane];
-        for (int j = 0; j < p.num_vals && j < kMaxVals; ++j) {
-          const PH_CONST DevValCol& vc = S->vals[j];
-          int64_t iv;
-          double dv;
-          read_value(vc.kind, vc.base, vc.table, unpack_bits(vc.fwd, vc.bits, doc), iv, dv);
-          if constexpr (EX != 0) {  // one value column with a 2-operand term (the host picks EX only then)
-            const PH_CONST DevValCol& v2 = S->vals2[0];
-            int64_t ib;
-            double db;
-            read_value(v2.kind, v2.base, v2.table, unpack_bits(v2.fwd, v2.bits, doc), ib, db);
-            if (p.val_is_int[0]) {
-              iv = EX == PH_EXPR_MULT ? iv * ib : (EX == PH_EXPR_SUB ? iv - ib : iv + ib);
-            } else {
-              const double x = vc.kind == VK_DICT_F64 ? dv : (double)iv;
-              const double y = v2.kind == VK_DICT_F64 ? db : (double)ib;
-              dv = EX == PH_EXPR_MULT ? (1.0 * x) * y : (EX == PH_EXPR_SUB ? x - y : x + y);
-              iv = double_order_key(dv);
-            }
-          }
-          const int ops = p.val_ops[j];
-          if (ops & OPS_SUM) {
-            if (p.val_is_int[j]) isum[j] += iv; else dsum[j] += dv;
-          }
-          if (ops & OPS_MIN) vmin[j] = iv < vmin[j] ? iv : vmin[j];
-          if (ops & OPS_MAX) vmax[j] = iv > vmax[j] ? iv : vmax[j];
-        }
-        for (int h = 0; h < p.num_hll && h < kMaxHll; ++h) {
-          ColRef col = S->cols[p.hll_slot[h]];
-          const uint32_t e = gld(col.hll + unpack_col(col, doc));
-          atomicMax(&lds_hll[h * m + (e >> 8)], e & 0xffu);
-        }
-      }
-      // every lane has read its list entries before the next step rewrites the list
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      step(S, (uint32_t)w * 64u, bits);
+    }
     }
   }
   // epilogue: one set of device atomics per wave, registers once per workgroup
@@ -327,6 +400,9 @@ void launch_scan_agg(const KParams& p, int mode, int grid, size_t lds, hipStream
                                     // on SSB Q1.x -- its registers cost the gathers their occupancy)
         allow_lds(k_agg_sparse<EX, 4>, lds);
         hipLaunchKernelGGL((k_agg_sparse<EX, 4>), dim3(grid), dim3(kBlock), lds, s, p);
+      } else if (p.agg_cont) {  // straight from the leaves' roaring containers
+        allow_lds(k_agg_sparse<EX, -1>, lds);
+        hipLaunchKernelGGL((k_agg_sparse<EX, -1>), dim3(grid), dim3(kBlock), lds, s, p);
       } else {  // bitmap leaves only
         allow_lds(k_agg_sparse<EX, 0>, lds);
         hipLaunchKernelGGL((k_agg_sparse<EX, 0>), dim3(grid), dim3(kBlock), lds, s, p);

@@ -5,8 +5,9 @@ segment twice and the broker merges two server copies, so every count/sum is 4x 
 (BaseSingleValueQueriesTest.java:142, BaseQueriesTest.java:220-238).
 
 Each entry: (query, expected rows, expected stats (numDocsScanned, numEntriesScannedPostFilter,
-numTotalDocs), source).  numEntriesScannedInFilter is reported under this build's own definition
-(full-column entries per scan leaf) and is checked separately.
+numTotalDocs), source).  numEntriesScannedInFilter is the reference's own iterator count (the docs its scan
+iterators examine); it is checked separately, against the KAT's 63 064 per segment
+(InnerSegmentAggregationSingleValueQueriesTest.java:56) and against oracle.filter_entries for every filter.
 """
 import os
 

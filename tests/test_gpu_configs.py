@@ -244,7 +244,8 @@ def hll_segs(ctx):
 def test_config5_hll_inverted_in(ctx, hll_segs):
     gpu, ora = hll_segs
     ids = list(range(3, 1000, 100))  # 10 ids, ~1 % selectivity
-    _check(ctx, gpu, ora, W.hll_sql(ids))
+    r, _ = _check(ctx, gpu, ora, W.hll_sql(ids))
+    assert r.stats.scan_kernel == 14, r.stats.scan_kernel  # k_agg_sparse from the containers, no doc bitmaps
     _check(ctx, gpu, ora, W.hll_sql(ids, 12))
 
 

@@ -281,6 +281,33 @@ def test_inverted_index_containers(ctx):
             _both(ctx, [t], f"SELECT COUNT(*), SUM(m) FROM t WHERE {where}", inverted=("a",), run_opt=run_opt)
 
 
+@pytest.mark.parametrize("force", [False, True])
+def test_agg_sparse_from_containers(ctx, monkeypatch, force):
+    # k_agg_sparse straight from the roaring containers of EQ / IN leaves (PH_KERNEL_AGG_CONTAINERS: no doc bitmap):
+    # array, bitmap and run containers, several ids per leaf (disjoint doc sets), segments ending mid-container,
+    # COUNT / SUM / MIN / MAX / DISTINCTCOUNTHLL against the oracle; forced also onto the non-selective leaves
+    if force:
+        monkeypatch.setenv("PH_AGG_SPARSE", "1")
+    rng = np.random.default_rng(77)
+    tables = []
+    for n in (300_000, 65_536, 131_171):
+        a = rng.integers(10, 400, n).astype(np.int32)  # sparse ids -> array containers
+        a[::2] = 1  # dense -> bitmap containers
+        a[n // 3: n // 3 + 70_000] = 2  # a long run -> run containers (run_opt) / bitmap containers
+        a[-5:] = 3
+        tables.append({"a": (a, "INT"), "m": (rng.integers(-5000, 5000, n).astype(np.int32), "INT")})
+    sel = "COUNT(*), SUM(m), MIN(m), MAX(m), DISTINCTCOUNTHLL(m)"
+    for run_opt in (False, True):
+        for where, selective in (("a = 17", True), ("a IN (17, 99, 3, 250)", True), ("a = 1", False),
+                                 ("a IN (2, 3)", False), ("a IN (1, 2, 17)", False), ("a = 12345", True)):
+            r, _ = _both(ctx, tables, f"SELECT {sel} FROM t WHERE {where}", inverted=("a",), run_opt=run_opt)
+            if (force or selective) and "12345" not in where:
+                assert r.stats.scan_kernel == 14, (where, run_opt, r.stats.scan_kernel)
+    monkeypatch.setenv("PH_AGG_CONT", "0")  # the bitmap form of the same plan
+    r, _ = _both(ctx, tables, f"SELECT {sel} FROM t WHERE a IN (17, 99, 3, 250)", inverted=("a",))
+    assert r.stats.scan_kernel == 3
+
+
 @pytest.mark.parametrize("atomic", [False, True])
 @pytest.mark.parametrize("n", [131072, 131172, 65536 * 3 - 1])
 def test_inverted_bitmap_chunk_edges(ctx, monkeypatch, n, atomic):
