@@ -1463,6 +1463,18 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // (one host round trip instead of three)
   const bool defer_sync = q->num_group_by > 0 && num_hll == 0 && dop != DENSE_EXECUTE && !fin;
   std::unique_ptr<PinnedBlock> dsc;  // pinned: matched total, then 3 words per limit segment
+  // the fused AND walks' sums (pinned, stream b): read at the end of the call, so the result compaction and copies
+  // on the main stream overlap the walks instead of waiting behind them
+  std::unique_ptr<PinnedBlock> fused_blk;
+  std::vector<int64_t> fused_docs;  // numDocs of each walk's segment
+  auto finish_fused = [&]() {
+    if (!fused_blk) return;
+    PH_HIP_CHECK(hipStreamSynchronize(lane.lane->stream_b));
+    const unsigned long long* o = fused_blk->as<unsigned long long>();
+    for (size_t x = 0; x < fused_docs.size(); ++x) stats.num_entries_scanned_in_filter += fused_docs[x] - 1 + (int64_t)o[x];
+    fused_blk.reset();
+    stamp("stat walk (fused)");
+  };
   size_t dsc_nlim = 0;
   bool timed = false;  // this call recorded ev_start / ev_stop (some chunk was scanned)
   // device time of the call: the scan launches (ev_start .. ev_stop, including a numGroupsLimit pass) + the
@@ -2654,11 +2666,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           PH_HIP_CHECK(hipStreamWaitEvent(sb, lane.lane->ev_stop, 0));
           PH_HIP_CHECK(hipMemcpyAsync(d_wjobs, wj.data(), sizeof(AndWalkJob) * wj.size(), hipMemcpyHostToDevice, sb));
           launch_and_walk(d_wjobs, (int32_t)wj.size(), max_groups, max_k, d_out, sb);
-          std::vector<unsigned long long> o(wj.size());
-          PH_HIP_CHECK(hipMemcpyAsync(o.data(), d_out, 8 * wj.size(), hipMemcpyDeviceToHost, sb));
-          PH_HIP_CHECK(hipStreamSynchronize(sb));
-          for (size_t x = 0; x < who.size(); ++x) ent[who[x]] = dsegs[stat_segs[who[x]].dseg].num_docs - 1 + (int64_t)o[x];
-          stamp("stat walk (fused)");
+          fused_blk = std::make_unique<PinnedBlock>(ctx, sb, 8 * wj.size());
+          PH_HIP_CHECK(hipMemcpyAsync(fused_blk->p, d_out, 8 * wj.size(), hipMemcpyDeviceToHost, sb));
+          fused_docs.clear();  // summed by finish_fused() at the end of the call
+          for (size_t t : who) fused_docs.push_back(dsegs[stat_segs[t].dseg].num_docs);
         }
       }
       size_t next = 0;
@@ -2847,6 +2858,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     stats.num_entries_scanned_in_filter += (int64_t)fe;
   }
   if (dop == DENSE_EXECUTE) {
+    finish_fused();
     // partial tables stay on the device for the cross-GPU reduction
     stats.num_entries_scanned_post_filter = stats.num_docs_scanned * (int64_t)projected.size();
     stats.host_ms = std::chrono::duration<double, std::milli>(clock::now() - t0).count() - dev_ms;
@@ -3117,6 +3129,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
     }
   }
+  finish_fused();
   stats.num_entries_scanned_post_filter = stats.num_docs_scanned * ncols_proj;
   stamp("done");
   stats.host_ms = std::chrono::duration<double, std::milli>(clock::now() - t0).count() - dev_ms;
