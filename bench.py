@@ -90,6 +90,8 @@ def kernel_name(mode, scan_kernel):
         name += " (+ k_roaring_chunk bitmap build)"
     if scan_kernel == 14:
         name = "k_agg_sparse<containers> (no bitmap build)"
+    if scan_kernel == 15:
+        name = "k_group_sparse<containers> (chunk bitmaps built in LDS)"
     return name
 
 
@@ -229,6 +231,8 @@ def flight_main(args, world, rank, dist, device):
     total_rows = nseg * seg_rows
     kernel_ms = float(np.mean(dev_ms))
     achieved = alg / (kernel_ms / 1000.0) / 1e9 if kernel_ms > 0 else None
+    traffic = load_traffic(args.workload, 1) if world == 1 else None
+    moved_gbs = (traffic / (kernel_ms / 1000.0) / 1e9) if traffic and kernel_ms else None
     result = {
         "metric": "filter+group-by rows/s and achieved HBM GB/s, 1B rows",
         "value": len(queries) * total_rows / (ms_per_step / 1000.0), "unit": "rows/s", "n_gpus": world,
@@ -241,7 +245,12 @@ def flight_main(args, world, rank, dist, device):
                    "parallelism": f"segments sharded x{world}" + (", RCCL reduce-scatter by key range" if world > 1
                                                                   else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                     # the step's PMC FETCH + WRITE bytes (profiles/<round>_pmc_<workload>.json) over the same
+                     # device time: the fraction of peak the sparse kernels actually MOVE (frac divides full-column
+                     # bytes, most of which the gathers never touch)
+                     "achieved_traffic_gbs": moved_gbs,
+                     "frac_moved": (moved_gbs / HBM_PEAK_GBS) if moved_gbs else None,
                      "kernel": "13 SSB queries (k_agg_sparse for Q1.x, k_group_sparse for Q2.x-Q4.x, leaves from "
                                "inverted bitmaps or register-direct scans; bytes = the queries' full column bytes, "
                                "which the sparse gathers touch only in part)",
@@ -504,7 +513,9 @@ def main():
                      "kernel": kernel_name(mode, last.get("kernel", 1)), "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": alg,
                      # bytes the kernels actually moved (PMC FETCH + WRITE, profiles/) over the same device time
-                     "achieved_traffic_gbs": (traffic / (kernel_ms / 1000.0) / 1e9) if traffic and kernel_ms else None},
+                     "achieved_traffic_gbs": (traffic / (kernel_ms / 1000.0) / 1e9) if traffic and kernel_ms else None,
+                     "frac_moved": (traffic / (kernel_ms / 1000.0) / 1e9 / HBM_PEAK_GBS) if traffic and kernel_ms
+                     else None},
     }
     if phases:
         result["phases_ms"] = {k: float(np.mean([p[k] for p in phases])) for k in phases[0]}

@@ -229,8 +229,10 @@ enum {
   PH_KERNEL_GROUP_REG = 11,    /* k_group_reg: k_group_lds_lean's group-by in the register-direct form */
   PH_KERNEL_GROUP_SPARSE = 12, /* k_group_sparse: group-by over selective inverted-index ANDs, matched-doc gathers */
   /* 13: retired (round 4's wave-private-ring kernel A, removed in round 5) */
-  PH_KERNEL_AGG_CONTAINERS = 14 /* k_agg_sparse straight from one inverted dictId's roaring containers (no doc
-                                   bitmaps; BitmapInvertedIndexReader.java:45-62) */
+  PH_KERNEL_AGG_CONTAINERS = 14, /* k_agg_sparse straight from the roaring containers of an EQ / IN inverted leaf
+                                    (no doc bitmaps; BitmapInvertedIndexReader.java:45-62) */
+  PH_KERNEL_GROUP_CONTAINERS = 15 /* k_group_sparse with each chunk's leaf bitmaps built in LDS from the roaring
+                                     containers (no doc bitmaps in HBM) */
 };
 
 /* ------------------------------------------------------------------ context */

@@ -151,6 +151,7 @@ struct DevPiece {
 constexpr int kMaxPieces = 12;  // == kPrefetchOther >= kPrefetchCount
 
 struct RoaringContainer;
+struct RoaringRange;
 
 struct DevSegment {
   int32_t num_docs;
@@ -188,6 +189,12 @@ struct DevSegment {
   // the column's device directory (the chunks name ranges of them) and the inverted buffer they point into
   const RoaringContainer* cdir;
   const uint8_t* cbase;
+  // k_group_sparse container mode (KParams::group_cont): bitmap leaf k as its dictIds' container ranges sp_rng[k]
+  // (sp_nrng[k] of them) in the column directory sp_cdir[k], payloads in the inverted buffer sp_cbase[k]
+  const RoaringRange* sp_rng[kSparseBitmaps];
+  int32_t sp_nrng[kSparseBitmaps];
+  const RoaringContainer* sp_cdir[kSparseBitmaps];
+  const uint8_t* sp_cbase[kSparseBitmaps];
   DevColumn cols[kMaxCols];
   DevValCol vals[kMaxVals];
   DevValCol vals2[kMaxVals];       // second operand of a 2-operand expression term (KParams::val_op)
@@ -281,6 +288,9 @@ struct KParams {
   int32_t agg_sparse;             // MODE_AGG over selective bitmap leaves: run k_agg_sparse
   int32_t agg_cont;               // k_agg_sparse straight from each segment's roaring containers (no doc bitmaps):
                                   // chunks are container ranges of DevSegment::cdir
+  int32_t group_cont;             // k_group_sparse builds each chunk's leaf bitmaps in LDS from the containers
+                                  // (no doc bitmaps in HBM): chunks are kChunkWords-aligned, LDS at cont_bm_off
+  int32_t cont_bm_off;
   int32_t sparse_c;               // sparse kernels over sp_reg segments: 16-byte loads per lane of a leaf (4 or 8)
   int32_t lds_fast;               // MODE_GROUP_LDS: run k_group_lds_lean
   int32_t lds_pack;               //   COUNT << 40 | SUM in one 64-bit LDS word

@@ -1269,9 +1269,24 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     cont_defer = cont_defer && live == (int)pl.bitmaps.size();  // no other bitmap leaf anywhere
   }
+  // Group-bys whose every segment's filter is a sparse_shape AND with bitmap leaves (SSB Q2-Q4 on inverted
+  // dimensions) may run k_group_sparse with each chunk's leaf bitmaps built in LDS from the containers
+  // (KParams::group_cont, decided with the sparse plan below): their doc bitmaps too are built only if not taken
+  bool gs_defer = q->num_group_by > 0 && !pl.bitmaps.empty() && dop != DENSE_LAYOUT && !fin;
+  if (const char* e = getenv("PH_GROUP_CONT")) gs_defer = gs_defer && atoi(e) != 0;  // tuning knob
+  {
+    size_t leaves = 0;
+    for (int i = 0; i < nseg && gs_defer; ++i) {
+      if (!seg_live[i]) continue;
+      const SparseShape sh = sparse_shape(roots[i]);
+      gs_defer = sh.ok && !sh.groups.empty();
+      for (auto& g : sh.groups) leaves += g.size();
+    }
+    gs_defer = gs_defer && leaves == pl.bitmaps.size();  // no bitmap leaf outside the sparse ANDs
+  }
   // the bitmap build's device time is part of the query's device_ms (its own event pair: host setup follows it)
   bool bm_timed = false;
-  if (!pl.bitmaps.empty() && dop != DENSE_LAYOUT && !fin && !cont_defer) {
+  if (!pl.bitmaps.empty() && dop != DENSE_LAYOUT && !fin && !cont_defer && !gs_defer) {
     PH_HIP_CHECK(hipEventRecord(lane.lane->ev_bm0, st));
     build_bitmaps();
     PH_HIP_CHECK(hipEventRecord(lane.lane->ev_bm1, st));
@@ -1630,6 +1645,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<std::pair<size_t, std::vector<uint32_t>>> conj_set_fix; // segment index * kMaxConj + leaf -> bitset
   std::vector<FbJob> fb_jobs;                                          // statistic passes: leaf doc bitmaps
   std::vector<std::pair<size_t, int>> sbm_fix;                         // segment index * kSparseBitmaps + k -> bitmap leaf
+  std::vector<std::pair<size_t, std::vector<uint32_t>>> srng_fix;     // same index -> (first, count) container ranges
   std::vector<std::pair<size_t, std::vector<uint32_t>>> sset_fix;     // segment index * kMaxConj + k -> bitset
   // k_group_sparse: every live segment's filter is a sparse_shape AND whose bitmaps keep < 1/8 of the docs (the
   // leaves' densities multiplied: an independence estimate) -> gather the matched docs instead of streaming every
@@ -2003,12 +2019,6 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if (const char* e = getenv("PH_AGG_SPARSE")) kp.agg_sparse = (all_bitmap || agg_conj) && atoi(e) != 0;  // tuning knob
     if (kp.agg_sparse) kp.agg_fast = 0;
     kp.agg_cont = cont_defer && kp.agg_sparse && all_bitmap && !agg_conj;
-    if (cont_defer && !kp.agg_cont) {  // the deferred doc bitmaps after all
-      PH_HIP_CHECK(hipEventRecord(lane.lane->ev_bm0, st));
-      build_bitmaps();
-      PH_HIP_CHECK(hipEventRecord(lane.lane->ev_bm1, st));
-      bm_timed = true;
-    }
     if (kp.agg_cont) {
       // chunks = ranges of <= 8 containers of each dictId of each segment's leaf (a wave takes one at a time)
       chunks.clear();
@@ -2141,8 +2151,51 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       lds = (size_t)kp.pl_misc_off + (size_t)kWaves * kSparseStepWords * 64 * sizeof(uint16_t) +
             (kp.sparse_c ? (size_t)kMaxConj * kConjSetWords * sizeof(uint32_t) : 0);
     }
+    if (gs_defer) {
+      // k_group_sparse from the containers: no limit pass or filter-statistic pass may need the doc bitmaps
+      const size_t cbm = (size_t)kSparseBitmaps * kChunkWords * 8;
+      const size_t off = (lds + 15) / 16 * 16;
+      kp.group_cont = kp.group_sparse && limit_segs.empty() && stat_segs.empty() && off + cbm <= 160 * 1024;
+      if (kp.group_cont) {
+        kp.cont_bm_off = (int32_t)off;
+        lds = off + cbm;
+        // chunks of exactly kChunkWords words from each segment's first doc (a chunk never spans two containers)
+        chunks.clear();
+        for (size_t si = 0; si < dsegs.size(); ++si) {
+          const int32_t nw = (int32_t)((dsegs[si].num_docs + 63) / 64);
+          dseg_chunks[si].first = (int32_t)chunks.size();
+          for (int32_t w = 0; w < nw; w += kChunkWords) chunks.push_back({(int32_t)si, w, std::min(nw, w + kChunkWords), 0});
+          dseg_chunks[si].second = (int32_t)chunks.size();
+        }
+        // leaf k of a segment: its dictIds' container ranges (uploaded with the predicate payloads)
+        for (auto& sb : sbm_fix) {
+          const BitmapLeaf& bl = pl.bitmaps[sb.second];
+          DevSegment& d = dsegs[sb.first / kSparseBitmaps];
+          const int k = (int)(sb.first % kSparseBitmaps);
+          d.sp_cdir[k] = bl.col->d_dir.as<RoaringContainer>();
+          d.sp_cbase[k] = bl.col->d_inverted.as<uint8_t>();
+          std::vector<uint32_t> rg;
+          for (int32_t id : bl.dict_ids) {
+            const int64_t f = bl.col->dir_begin[id], n = bl.col->dir_begin[id + 1] - f;
+            if (n > 0) {
+              rg.push_back((uint32_t)f);
+              rg.push_back((uint32_t)n);
+            }
+          }
+          d.sp_nrng[k] = (int32_t)(rg.size() / 2);
+          srng_fix.push_back({sb.first, std::move(rg)});
+        }
+      }
+    }
     // 160 KiB of LDS per CU (gfx950); HLL registers of a large log2m do not fit beside the staging areas
     if (lds > 160 * 1024) fail(PH_ERR_UNSUPPORTED, "aggregation state exceeds the LDS of one CU (HLL log2m too large)");
+  }
+  // the deferred doc bitmaps, when neither container plan was taken (any mode: the plans that read them)
+  if ((cont_defer || gs_defer) && !kp.agg_cont && !kp.group_cont) {
+    PH_HIP_CHECK(hipEventRecord(lane.lane->ev_bm0, st));
+    build_bitmaps();
+    PH_HIP_CHECK(hipEventRecord(lane.lane->ev_bm1, st));
+    bm_timed = true;
   }
   // every predicate payload (program sets / ranges, FK_SET / FK_CONJ / sparse-leaf bitsets) in ONE upload: r4 issued
   // one small copy per payload (SSB Q3.3 on 60 segments: 120 copies, ~1 ms of setup)
@@ -2158,6 +2211,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     for (auto& ff : fset_fix) put(ff.second);
     for (auto& sf : sset_fix) put(sf.second);
     for (auto& cf : conj_set_fix) put(cf.second);
+    for (auto& rf : srng_fix) put(rf.second);
     if (!blob.empty()) {
       uint32_t* dblob = scratch.alloc<uint32_t>(blob.size());
       // from pinned staging (slot 2): no host wait for the copy (r5: a pageable copy here synchronised the stream,
@@ -2170,6 +2224,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       for (auto& ff : fset_fix) dsegs[ff.first].fptr = dblob + at[i++];
       for (auto& sf : sset_fix) dsegs[sf.first / kMaxConj].sp_set[sf.first % kMaxConj] = dblob + at[i++];
       for (auto& cf : conj_set_fix) dsegs[cf.first / kMaxConj].cset[cf.first % kMaxConj] = dblob + at[i++];
+      for (auto& rf : srng_fix)
+        dsegs[rf.first / kSparseBitmaps].sp_rng[rf.first % kSparseBitmaps] = reinterpret_cast<const RoaringRange*>(dblob + at[i++]);
     }
   }
   for (auto& bf : bitmap_fix) all_insns[bf.first].ptr = bitmap_dev[bf.second];
@@ -2266,6 +2322,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
                           : kp.agg_cont   ? PH_KERNEL_AGG_CONTAINERS
                           : kp.agg_sparse ? PH_KERNEL_AGG_SPARSE
                           : kp.agg_fast  ? PH_KERNEL_AGG_LEAN
+                          : kp.group_cont ? PH_KERNEL_GROUP_CONTAINERS
                           : kp.group_sparse ? PH_KERNEL_GROUP_SPARSE
                           : kp.group_reg  ? PH_KERNEL_GROUP_REG
                           : kp.lds_fast  ? PH_KERNEL_GROUP_LDS_LEAN

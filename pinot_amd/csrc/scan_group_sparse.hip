@@ -17,6 +17,49 @@
 
 namespace ph {
 
+__device__ __forceinline__ uint32_t gs_u16(const uint8_t* b) { return (uint32_t)b[0] | ((uint32_t)b[1] << 8); }
+
+// Container mode (C < 0): OR the docs [lo, lo + n) of container key `key` of one dictId (its containers dir[rg], keys
+// ascending) into a chunk bitmap of 32-doc words in LDS (bit d - lo), by one wave.  lo is a multiple of 16384 and
+// n <= 16384: a kChunkWords chunk never spans two containers.
+__device__ void gs_or_range(const RoaringContainer* __restrict__ dir, const uint8_t* __restrict__ base,
+                            const RoaringRange rg, uint32_t key, uint32_t lo, uint32_t n, uint32_t* bm, int lane) {
+  int found = -1;
+  for (int b = 0; b < rg.count && found < 0; b += 64) {  // the container whose key is the chunk's
+    const int i = b + lane;
+    const unsigned long long m = __ballot(i < rg.count && (uint32_t)dir[rg.first + i].key == key);
+    if (m) found = b + (int)__ffsll((long long)m) - 1;
+  }
+  if (found < 0) return;
+  const RoaringContainer c = dir[rg.first + found];
+  const uint8_t* pay = base + c.offset;
+  if (c.type == 0) {  // array: sorted low halves
+    for (int i = lane; i < c.card; i += 64) {
+      const uint32_t d = gs_u16(pay + 2 * i) - lo;
+      if (d < n) atomicOr(&bm[d >> 5], 1u << (d & 31u));
+    }
+  } else if (c.type == 1) {  // bitmap: 2048 little-endian 32-bit words, the chunk's n / 32 of them
+    for (uint32_t i = (uint32_t)lane; i < (n + 31u) / 32u; i += 64u) {
+      const uint8_t* q = pay + 4 * (lo / 32u + i);
+      uint32_t v = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+      if (n - 32u * i < 32u) v &= (1u << (n - 32u * i)) - 1u;
+      if (v) atomicOr(&bm[i], v);
+    }
+  } else {  // run: (start, length - 1) pairs
+    for (int r = lane; r < c.card; r += 64) {
+      const uint32_t s0 = gs_u16(pay + 2 + 4 * r), e0 = s0 + gs_u16(pay + 4 + 4 * r);  // inclusive
+      if (e0 < lo || s0 >= lo + n) continue;
+      uint32_t d = s0 > lo ? s0 - lo : 0u;
+      const uint32_t last = min(e0 - lo, n - 1u);
+      while (d <= last) {
+        const uint32_t w = d >> 5, b0 = d & 31u, hi = min(last, (w << 5) + 31u), nb = hi - d + 1u;
+        atomicOr(&bm[w], (nb >= 32u ? 0xffffffffu : ((1u << nb) - 1u)) << b0);
+        d = hi + 1u;
+      }
+    }
+  }
+}
+
 template <int MODE, int EX, int C>
 __global__ void __launch_bounds__(kBlock) k_group_sparse(const KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -61,13 +104,32 @@ __global__ void __launch_bounds__(kBlock) k_group_sparse(const KParams p) {
       conj_stage_sets(S, csets, threadIdx.x, kBlock);
       __syncthreads();
     }
+    uint32_t* cbm = reinterpret_cast<uint32_t*>(smem + p.cont_bm_off);  // C < 0: [nbm][kChunkWords * 2] words
+    if constexpr (C < 0) {
+      // the chunk's leaf bitmaps straight from the roaring containers (no doc bitmap in HBM): the 4 waves take the
+      // leaves' dictIds round-robin (InvertedIndexFilterOperator -> BitmapInvertedIndexReader.java:45-62)
+      __syncthreads();  // every wave is done with the previous chunk's words
+      for (int i = threadIdx.x; i < nbm * kChunkWords * 2; i += kBlock) cbm[i] = 0u;
+      __syncthreads();
+      const uint32_t dlo = (uint32_t)wb * 64u;
+      const uint32_t n = min((uint32_t)(we - wb) * 64u, ndocs - dlo);
+      int t = 0;
+      for (int k = 0; k < nbm; ++k)
+        for (int r = 0; r < S->sp_nrng[k]; ++r, ++t)
+          if ((t & (WAVES - 1)) == wave)
+            gs_or_range(S->sp_cdir[k], S->sp_cbase[k], S->sp_rng[k][r], dlo >> 16, dlo & 0xffffu, n,
+                        cbm + k * kChunkWords * 2, lane);
+      __syncthreads();
+    }
     auto bm_word = [&](int32_t w) -> unsigned long long {  // the AND (of ORs) of the segment's doc bitmaps, 64 docs
       if (w >= we) return 0ull;
       unsigned long long x = ~0ull, grp = 0ull;
 #pragma unroll
       for (int k = 0; k < kSparseBitmaps; ++k) {
         if (k >= nbm) continue;
-        const unsigned long long v = reinterpret_cast<const unsigned long long*>(S->sp_bm[k])[w];
+        const unsigned long long v =
+            C < 0 ? reinterpret_cast<const unsigned long long*>(cbm + k * kChunkWords * 2)[w - wb]
+                  : reinterpret_cast<const unsigned long long*>(S->sp_bm[k])[w];
         if (k > 0 && S->sp_or[k]) {
           grp |= v;
         } else {
@@ -236,7 +298,10 @@ static void launch_sparse_mode(const KParams& p, int grid, size_t lds, hipStream
 void launch_group_sparse(const KParams& p, int mode, int grid, size_t lds, hipStream_t s) {
   // register-direct scan leaves (conj_reg.h): 16-byte loads per lane and leaf, by the widest leaf column
   // (0: no segment has them -- the bitmap-only form)
-  if (mode == MODE_GROUP_LDS) {
+  if (p.group_cont) {  // chunk bitmaps built in LDS from the containers
+    if (mode == MODE_GROUP_LDS) launch_sparse_mode<MODE_GROUP_LDS, -1>(p, grid, lds, s);
+    else launch_sparse_mode<MODE_GROUP_GLOBAL, -1>(p, grid, lds, s);
+  } else if (mode == MODE_GROUP_LDS) {
     if (p.sparse_c > 4) launch_sparse_mode<MODE_GROUP_LDS, 8>(p, grid, lds, s);
     else if (p.sparse_c > 2) launch_sparse_mode<MODE_GROUP_LDS, 4>(p, grid, lds, s);
     else if (p.sparse_c > 0) launch_sparse_mode<MODE_GROUP_LDS, 2>(p, grid, lds, s);

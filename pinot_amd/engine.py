@@ -52,7 +52,8 @@ SCAN_KERNEL_NAMES = {0: "none", 1: "k_scan", 2: "k_agg_lean", 3: "k_agg_sparse",
                      5: "k_part_scan + k_part_agg", 6: "k_part_scan2 + k_part_agg",
                      7: "k_scan<MODE_PARTITION> + k_part_agg", 8: "k_part_reg + k_part_agg",
                      9: "k_count_reg", 10: "k_agg_reg",
-                     11: "k_group_reg", 12: "k_group_sparse", 14: "k_agg_sparse over roaring containers"}
+                     11: "k_group_reg", 12: "k_group_sparse", 14: "k_agg_sparse over roaring containers",
+                     15: "k_group_sparse over roaring containers"}
 
 
 @dataclass
