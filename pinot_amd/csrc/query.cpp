@@ -2152,10 +2152,11 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
             (kp.sparse_c ? (size_t)kMaxConj * kConjSetWords * sizeof(uint32_t) : 0);
     }
     if (gs_defer) {
-      // k_group_sparse from the containers: no limit pass or filter-statistic pass may need the doc bitmaps
+      // k_group_sparse from the containers: no filter-statistic pass may need the doc bitmaps (a numGroupsLimit
+      // first-seen pass, which runs the generic program, builds them when it runs: late_bitmaps)
       const size_t cbm = (size_t)kSparseBitmaps * kChunkWords * 8;
       const size_t off = (lds + 15) / 16 * 16;
-      kp.group_cont = kp.group_sparse && limit_segs.empty() && stat_segs.empty() && off + cbm <= 160 * 1024;
+      kp.group_cont = kp.group_sparse && stat_segs.empty() && off + cbm <= 160 * 1024;
       if (kp.group_cont) {
         kp.cont_bm_off = (int32_t)off;
         lds = off + cbm;
@@ -2306,6 +2307,26 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     PH_HIP_CHECK(hipMemcpyAsync(d_chunks, stage + b1 + b2, b3, hipMemcpyHostToDevice, st));
     if (b4) PH_HIP_CHECK(hipMemcpyAsync(d_segs_opt, stage + b1 + b2 + b3, b4, hipMemcpyHostToDevice, st));
     PH_HIP_CHECK(hipEventRecord(lane.lane->ev_uploaded, st));  // the statistics pass (stream b) starts here
+    // container mode skipped the doc bitmaps; a numGroupsLimit first-seen pass runs the segments' generic programs,
+    // which read them: build them then, patch the programs / segment tables and upload them again
+    bool late_built = false;
+    auto late_bitmaps = [&]() {
+      if (!kp.group_cont || late_built) return;
+      build_bitmaps();
+      for (auto& bf : bitmap_fix) all_insns[bf.first].ptr = bitmap_dev[bf.second];
+      for (auto* v : {&dsegs, &dsegs_opt}) {
+        if (v->empty()) continue;
+        for (auto& fb : fbitmap_fix) (*v)[fb.first].fptr = bitmap_dev[fb.second];
+        for (auto& sb : sbm_fix) (*v)[sb.first / kSparseBitmaps].sp_bm[sb.first % kSparseBitmaps] = bitmap_dev[sb.second];
+      }
+      PH_HIP_CHECK(hipStreamSynchronize(st));  // nothing in flight reads the tables while they are replaced
+      if (!all_insns.empty())
+        PH_HIP_CHECK(hipMemcpy(d_prog, all_insns.data(), sizeof(FilterInsn) * all_insns.size(), hipMemcpyHostToDevice));
+      PH_HIP_CHECK(hipMemcpy(d_segs, dsegs.data(), sizeof(DevSegment) * dsegs.size(), hipMemcpyHostToDevice));
+      if (d_segs_opt)
+        PH_HIP_CHECK(hipMemcpy(d_segs_opt, dsegs_opt.data(), sizeof(DevSegment) * dsegs_opt.size(), hipMemcpyHostToDevice));
+      late_built = true;
+    };
     kp.segs = d_segs;
     kp.prog = d_prog;
     kp.chunks = d_chunks;
@@ -2361,6 +2382,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           scanned = true;  // no segment can hold `limit` keys: the untruncated scan is the reference's result
           stats.limit_pass = 1;
         } else if (mode == MODE_GROUP_HASH) {
+          late_bitmaps();
           // truncation over a key space beyond the dense budget (LongMapBasedHolder / ArrayMapBasedHolder regime,
           // DictionaryBasedGroupKeyGenerator.java:629-637,809-817): the segments that cannot reach the limit are
           // rescanned in one launch; each limit segment then runs, one at a time, (1) a first-seen pass into its
@@ -2443,6 +2465,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         }
       }
       if (!scanned && !limit_segs.empty()) {
+        late_bitmaps();
         stats.limit_pass = 2;
         // first-seen pass over every limit segment in ONE launch (MODE_GROUP_GLOBAL records each key's first
         // matching doc in the segment's own table), then the kept keys of every segment in one select step; the

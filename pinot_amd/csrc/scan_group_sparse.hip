@@ -33,10 +33,19 @@ __device__ void gs_or_range(const RoaringContainer* __restrict__ dir, const uint
   if (found < 0) return;
   const RoaringContainer c = dir[rg.first + found];
   const uint8_t* pay = base + c.offset;
-  if (c.type == 0) {  // array: sorted low halves
-    for (int i = lane; i < c.card; i += 64) {
-      const uint32_t d = gs_u16(pay + 2 * i) - lo;
+  if (c.type == 0) {  // array: sorted low halves; start near the chunk's first entry, stop past its last
+    int i0 = 0;
+    if (c.card > 256) {  // one probe per lane at card / 64 strides: the lanes below lo are a prefix
+      const int idx = (int)((int64_t)lane * c.card / 64);
+      const int nb = __popcll(__ballot(gs_u16(pay + 2 * idx) < lo));
+      i0 = nb > 0 ? (int)((int64_t)(nb - 1) * c.card / 64) : 0;
+    }
+    for (int b0 = i0; b0 < c.card; b0 += 64) {
+      const int i = b0 + lane;
+      const uint32_t v = i < c.card ? gs_u16(pay + 2 * i) : 0xffffffffu;
+      const uint32_t d = v - lo;
       if (d < n) atomicOr(&bm[d >> 5], 1u << (d & 31u));
+      if (__ballot(v < lo + n) == 0ull) break;  // every later entry is past the chunk too
     }
   } else if (c.type == 1) {  // bitmap: 2048 little-endian 32-bit words, the chunk's n / 32 of them
     for (uint32_t i = (uint32_t)lane; i < (n + 31u) / 32u; i += 64u) {
