@@ -184,12 +184,13 @@ def test_group_sparse_matches_streaming(ctx, ssb, qid, monkeypatch):
     # k_scan (PH_GROUP_SPARSE=0) and the oracle agree on rows, numDocsScanned and numEntriesScannedInFilter
     gpu, ora = ssb
     r, got = _check(ctx, gpu, ora, W.SSB_QUERIES[qid])
-    assert r.stats.scan_kernel == 15, r.stats.scan_kernel  # chunk bitmaps built in LDS from the containers
-    monkeypatch.setenv("PH_GROUP_CONT", "0")  # the same plan over k_roaring_chunk's doc bitmaps
+    assert r.stats.scan_kernel == 12, r.stats.scan_kernel
+    monkeypatch.setenv("PH_GROUP_CONT", "1")  # the same plan with the chunk bitmaps built in LDS from the containers
     r1, got1 = _check(ctx, gpu, ora, W.SSB_QUERIES[qid])
-    assert r1.stats.scan_kernel == 12, r1.stats.scan_kernel
+    assert r1.stats.scan_kernel == 15, r1.stats.scan_kernel
     assert got.rows == got1.rows
     assert r.stats.num_entries_scanned_in_filter == r1.stats.num_entries_scanned_in_filter
+    monkeypatch.setenv("PH_GROUP_CONT", "0")
     monkeypatch.setenv("PH_GROUP_SPARSE", "0")
     r2, got2 = _check(ctx, gpu, ora, W.SSB_QUERIES[qid])
     assert r2.stats.scan_kernel not in (12, 15)
@@ -199,11 +200,14 @@ def test_group_sparse_matches_streaming(ctx, ssb, qid, monkeypatch):
     assert r.stats.num_entries_scanned_in_filter == e.stats.num_entries_scanned_in_filter
 
 
-def test_group_sparse_shapes(ctx, ssb, monkeypatch):
+@pytest.mark.parametrize("cont", ["0", "1"])
+def test_group_sparse_shapes(ctx, ssb, monkeypatch, cont):
     # forced onto k_group_sparse: MIN / MAX / COUNT-only, a set scan leaf, a plain-bitmap filter, a numGroupsLimit
-    # that truncates (the keep bitsets of the rescan), DOUBLE-free integer terms
+    # that truncates (the keep bitsets of the rescan; with the container form the first-seen pass builds the doc
+    # bitmaps late), DOUBLE-free integer terms
     gpu, ora = ssb
     monkeypatch.setenv("PH_GROUP_SPARSE", "1")
+    monkeypatch.setenv("PH_GROUP_CONT", cont)
     for sql in ("SELECT d_year, MIN(lo_revenue), MAX(lo_revenue), COUNT(*) FROM lineorder WHERE s_region = 'ASIA' "
                 "AND lo_quantity IN (3, 7, 11, 40) GROUP BY d_year ORDER BY d_year LIMIT 100",
                 "SELECT c_nation, COUNT(*) FROM lineorder WHERE c_region = 'EUROPE' GROUP BY c_nation "
