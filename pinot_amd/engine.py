@@ -339,8 +339,9 @@ class GpuContext:
             raw = view(L.ph_result_key_data(r, g), n * es)
             t = L.ph_result_key_type(r, g)
             if t == N.PH_STRING:
-                m = raw[:n * es].reshape(n, es)
-                key_cols.append([bytes(row).rstrip(b"\x00").decode("utf-8") for row in m])
+                # fixed-width NUL-padded entries: numpy's bytes dtype drops the padding, one vectorised UTF-8 decode
+                m = np.ascontiguousarray(raw[:n * es]).view(f"S{es}") if n else np.zeros(0, "S1")
+                key_cols.append(np.char.decode(m, "utf-8").tolist())
             else:
                 key_cols.append(raw.view(_KEY_DTYPE[t]))
         agg_cols = []
