@@ -195,6 +195,8 @@ struct DevSegment {
   int32_t sp_nrng[kSparseBitmaps];
   const RoaringContainer* sp_cdir[kSparseBitmaps];
   const uint8_t* sp_cbase[kSparseBitmaps];
+  const int32_t* sp_ctab;  // [65536-doc key][sp_ntot]: the directory index of range t's container of that key, or -1
+  int32_t sp_ntot;         // ranges over all leaves (sum of sp_nrng)
   DevColumn cols[kMaxCols];
   DevValCol vals[kMaxVals];
   DevValCol vals2[kMaxVals];       // second operand of a 2-operand expression term (KParams::val_op)

@@ -1649,6 +1649,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<FbJob> fb_jobs;                                          // statistic passes: leaf doc bitmaps
   std::vector<std::pair<size_t, int>> sbm_fix;                         // segment index * kSparseBitmaps + k -> bitmap leaf
   std::vector<std::pair<size_t, std::vector<uint32_t>>> srng_fix;     // same index -> (first, count) container ranges
+  std::vector<std::pair<size_t, std::vector<uint32_t>>> ctab_fix;     // segment index -> container table (group_cont)
   std::vector<std::pair<size_t, std::vector<uint32_t>>> sset_fix;     // segment index * kMaxConj + k -> bitset
   // k_group_sparse: every live segment's filter is a sparse_shape AND whose bitmaps keep < 1/8 of the docs (the
   // leaves' densities multiplied: an independence estimate) -> gather the matched docs instead of streaming every
@@ -2189,6 +2190,29 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           d.sp_nrng[k] = (int32_t)(rg.size() / 2);
           srng_fix.push_back({sb.first, std::move(rg)});
         }
+        // per segment: [65536-doc key][range t over its leaves] -> the range's container of that key (or -1), so
+        // the kernel indexes the directory instead of searching it
+        std::vector<std::vector<std::pair<const Column*, std::pair<int64_t, int64_t>>>> segr(dsegs.size());
+        for (auto& sb : sbm_fix) {
+          const BitmapLeaf& bl = pl.bitmaps[sb.second];
+          for (int32_t id : bl.dict_ids) {
+            const int64_t f = bl.col->dir_begin[id], e = bl.col->dir_begin[id + 1];
+            if (e > f) segr[sb.first / kSparseBitmaps].push_back({bl.col, {f, e}});
+          }
+        }
+        for (size_t si = 0; si < dsegs.size(); ++si) {
+          const size_t ntot = segr[si].size(), nkeys = ((size_t)dsegs[si].num_docs + 65535) / 65536;
+          std::vector<uint32_t> tab(std::max<size_t>(1, nkeys * ntot), 0xffffffffu);
+          for (size_t t = 0; t < ntot; ++t) {
+            const Column* col = segr[si][t].first;
+            for (int64_t x = segr[si][t].second.first; x < segr[si][t].second.second; ++x) {
+              const size_t key = (size_t)col->dir[x].key;
+              if (key < nkeys) tab[key * ntot + t] = (uint32_t)x;
+            }
+          }
+          dsegs[si].sp_ntot = (int32_t)ntot;
+          ctab_fix.push_back({si, std::move(tab)});
+        }
       }
     }
     // 160 KiB of LDS per CU (gfx950); HLL registers of a large log2m do not fit beside the staging areas
@@ -2216,6 +2240,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     for (auto& sf : sset_fix) put(sf.second);
     for (auto& cf : conj_set_fix) put(cf.second);
     for (auto& rf : srng_fix) put(rf.second);
+    for (auto& tf : ctab_fix) put(tf.second);
     if (!blob.empty()) {
       uint32_t* dblob = scratch.alloc<uint32_t>(blob.size());
       // from pinned staging (slot 2): no host wait for the copy (r5: a pageable copy here synchronised the stream,
@@ -2230,6 +2255,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       for (auto& cf : conj_set_fix) dsegs[cf.first / kMaxConj].cset[cf.first % kMaxConj] = dblob + at[i++];
       for (auto& rf : srng_fix)
         dsegs[rf.first / kSparseBitmaps].sp_rng[rf.first % kSparseBitmaps] = reinterpret_cast<const RoaringRange*>(dblob + at[i++]);
+      for (auto& tf : ctab_fix) dsegs[tf.first].sp_ctab = reinterpret_cast<const int32_t*>(dblob + at[i++]);
     }
   }
   for (auto& bf : bitmap_fix) all_insns[bf.first].ptr = bitmap_dev[bf.second];

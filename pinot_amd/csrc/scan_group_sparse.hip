@@ -19,19 +19,12 @@ namespace ph {
 
 __device__ __forceinline__ uint32_t gs_u16(const uint8_t* b) { return (uint32_t)b[0] | ((uint32_t)b[1] << 8); }
 
-// Container mode (C < 0): OR the docs [lo, lo + n) of container key `key` of one dictId (its containers dir[rg], keys
-// ascending) into a chunk bitmap of 32-doc words in LDS (bit d - lo), by one wave.  lo is a multiple of 16384 and
-// n <= 16384: a kChunkWords chunk never spans two containers.
-__device__ void gs_or_range(const RoaringContainer* __restrict__ dir, const uint8_t* __restrict__ base,
-                            const RoaringRange rg, uint32_t key, uint32_t lo, uint32_t n, uint32_t* bm, int lane) {
-  int found = -1;
-  for (int b = 0; b < rg.count && found < 0; b += 64) {  // the container whose key is the chunk's
-    const int i = b + lane;
-    const unsigned long long m = __ballot(i < rg.count && (uint32_t)dir[rg.first + i].key == key);
-    if (m) found = b + (int)__ffsll((long long)m) - 1;
-  }
-  if (found < 0) return;
-  const RoaringContainer c = dir[rg.first + found];
+// Container mode (C < 0): OR the docs [lo, lo + n) of container c into a chunk bitmap of 32-doc words in LDS (bit
+// d - lo).  lo is a multiple of 16384 and n <= 16384: a kChunkWords chunk never spans two containers.  A bitmap
+// container's words are split over the workgroup's waves (part `part` of `parts`); array / run containers take
+// one wave (part 0 of 1).
+__device__ void gs_or_container(const RoaringContainer c, const uint8_t* __restrict__ base, uint32_t lo, uint32_t n,
+                                uint32_t* bm, int lane, int part, int parts) {
   const uint8_t* pay = base + c.offset;
   if (c.type == 0) {  // array: sorted low halves; start near the chunk's first entry, stop past its last
     int i0 = 0;
@@ -48,9 +41,11 @@ __device__ void gs_or_range(const RoaringContainer* __restrict__ dir, const uint
       if (__ballot(v < lo + n) == 0ull) break;  // every later entry is past the chunk too
     }
   } else if (c.type == 1) {  // bitmap: 2048 little-endian 32-bit words, the chunk's n / 32 of them
-    for (uint32_t i = (uint32_t)lane; i < (n + 31u) / 32u; i += 64u) {
+    const bool al = ((uintptr_t)pay & 3u) == 0u;  // 4-byte aligned payload: one dword load per word
+    for (uint32_t i = (uint32_t)(part * 64 + lane); i < (n + 31u) / 32u; i += 64u * (uint32_t)parts) {
       const uint8_t* q = pay + 4 * (lo / 32u + i);
-      uint32_t v = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+      uint32_t v = al ? *reinterpret_cast<const uint32_t*>(q)
+                      : (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
       if (n - 32u * i < 32u) v &= (1u << (n - 32u * i)) - 1u;
       if (v) atomicOr(&bm[i], v);
     }
@@ -122,12 +117,19 @@ __global__ void __launch_bounds__(kBlock) k_group_sparse(const KParams p) {
       __syncthreads();
       const uint32_t dlo = (uint32_t)wb * 64u;
       const uint32_t n = min((uint32_t)(we - wb) * 64u, ndocs - dlo);
+      // the host's table names each range's container of this key (no directory search)
+      const int32_t* ct = S->sp_ctab + (size_t)(dlo >> 16) * (size_t)S->sp_ntot;
       int t = 0;
       for (int k = 0; k < nbm; ++k)
-        for (int r = 0; r < S->sp_nrng[k]; ++r, ++t)
-          if ((t & (WAVES - 1)) == wave)
-            gs_or_range(S->sp_cdir[k], S->sp_cbase[k], S->sp_rng[k][r], dlo >> 16, dlo & 0xffffu, n,
-                        cbm + k * kChunkWords * 2, lane);
+        for (int r = 0; r < S->sp_nrng[k]; ++r, ++t) {
+          const int32_t ci = ct[t];
+          if (ci < 0) continue;
+          const RoaringContainer c = S->sp_cdir[k][ci];
+          if (c.type == 1)  // bitmap: every wave takes a quarter of the chunk's words
+            gs_or_container(c, S->sp_cbase[k], dlo & 0xffffu, n, cbm + k * kChunkWords * 2, lane, wave, WAVES);
+          else if ((t & (WAVES - 1)) == wave)
+            gs_or_container(c, S->sp_cbase[k], dlo & 0xffffu, n, cbm + k * kChunkWords * 2, lane, 0, 1);
+        }
       __syncthreads();
     }
     auto bm_word = [&](int32_t w) -> unsigned long long {  // the AND (of ORs) of the segment's doc bitmaps, 64 docs
