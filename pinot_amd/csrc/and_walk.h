@@ -54,11 +54,17 @@ struct DfaWalker {
   Get get;
   int32_t cw = -1;          // word held in Wc
   unsigned long long Wc[K];
+  unsigned long long Pc[K];  // prefix ANDs Wc[0] & .. & Wc[i]: bit b of Pc[i] = scans 0..i all have doc b
   __host__ __device__ void hold(int32_t w) {
     if (w == cw) return;
     cw = w;
+    unsigned long long a = ~0ull;
 #pragma unroll
-    for (int i = 0; i < K; ++i) Wc[i] = i < k ? get(i, w) : ~0ull;
+    for (int i = 0; i < K; ++i) {
+      Wc[i] = i < k ? get(i, w) : ~0ull;
+      a &= Wc[i];
+      Pc[i] = a;
+    }
   }
   // scan i's first match in [x, c1), or -1
   __host__ __device__ int32_t next_set(int i, int32_t x) {
@@ -86,10 +92,11 @@ struct DfaWalker {
   __host__ __device__ uint32_t epoch(int32_t M, int j, int32_t& nxt, int& jn) {
     hold(M >> 6);
     const int b = (int)(M & 63);
-    int f = k;  // first scan without doc M (k: every scan has it)
+    // first scan without doc M (k: every scan has it) = how many of the nested prefix ANDs still hold doc M
+    int f = 0;
 #pragma unroll
-    for (int i = K - 1; i >= 0; --i)
-      if (i < k && ((Wc[i] >> b) & 1ull) == 0ull) f = i;
+    for (int i = 0; i < K; ++i)
+      if (i < k) f += (int)((Pc[i] >> b) & 1ull);
     const uint32_t skip = (j >= 0) ? 1u : 0u;
     if (f == k) {
       nxt = M + 1 < c1 ? M + 1 : -1;

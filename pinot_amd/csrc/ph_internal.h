@@ -123,6 +123,8 @@ constexpr int kRegBlock = 256;
 constexpr int kRegWaves = kRegBlock / 64;
 constexpr int kRegTileWords = 32;
 constexpr int kSparseStepWords = 64;              // k_agg_sparse: bitmap words (4096 docs) per wave step
+constexpr int kContWords = 1024;                      // k_group_sparse container mode: one 65536-doc container key
+                                                      // per chunk (its leaf bitmaps built in LDS once per chunk)
 constexpr int kChunkWords = 256;                     // 16384 docs per chunk (a multiple of every round)
 constexpr int kInterruptChunks = 8192;               // an interruptible scan checks every 8192 chunks (~134M docs)
 // 16-byte-per-lane loads (1 KiB per wave-instruction) a wave keeps in flight per tile, over all streams

@@ -2158,18 +2158,20 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if (gs_defer) {
       // k_group_sparse from the containers: no filter-statistic pass may need the doc bitmaps (a numGroupsLimit
       // first-seen pass, which runs the generic program, builds them when it runs: late_bitmaps)
-      const size_t cbm = (size_t)kSparseBitmaps * kChunkWords * 8;
+      int max_nbm = 1;
+      for (auto& d : dsegs) max_nbm = std::max(max_nbm, (int)d.sp_nbm);
+      const size_t cbm = (size_t)max_nbm * kContWords * 8;
       const size_t off = (lds + 15) / 16 * 16;
       kp.group_cont = kp.group_sparse && stat_segs.empty() && off + cbm <= 160 * 1024;
       if (kp.group_cont) {
         kp.cont_bm_off = (int32_t)off;
         lds = off + cbm;
-        // chunks of exactly kChunkWords words from each segment's first doc (a chunk never spans two containers)
+        // chunks of whole 65536-doc container keys (kContWords words): one LDS build per key and leaf
         chunks.clear();
         for (size_t si = 0; si < dsegs.size(); ++si) {
           const int32_t nw = (int32_t)((dsegs[si].num_docs + 63) / 64);
           dseg_chunks[si].first = (int32_t)chunks.size();
-          for (int32_t w = 0; w < nw; w += kChunkWords) chunks.push_back({(int32_t)si, w, std::min(nw, w + kChunkWords), 0});
+          for (int32_t w = 0; w < nw; w += kContWords) chunks.push_back({(int32_t)si, w, std::min(nw, w + kContWords), 0});
           dseg_chunks[si].second = (int32_t)chunks.size();
         }
         // leaf k of a segment: its dictIds' container ranges (uploaded with the predicate payloads)

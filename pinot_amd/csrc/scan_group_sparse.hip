@@ -20,7 +20,7 @@ namespace ph {
 __device__ __forceinline__ uint32_t gs_u16(const uint8_t* b) { return (uint32_t)b[0] | ((uint32_t)b[1] << 8); }
 
 // Container mode (C < 0): OR the docs [lo, lo + n) of container c into a chunk bitmap of 32-doc words in LDS (bit
-// d - lo).  lo is a multiple of 16384 and n <= 16384: a kChunkWords chunk never spans two containers.  A bitmap
+// d - lo).  Chunks are whole 65536-doc container keys (kContWords words): lo = 0 today, n <= 65536.  A bitmap
 // container's words are split over the workgroup's waves (part `part` of `parts`); array / run containers take
 // one wave (part 0 of 1).
 __device__ void gs_or_container(const RoaringContainer c, const uint8_t* __restrict__ base, uint32_t lo, uint32_t n,
@@ -108,12 +108,12 @@ __global__ void __launch_bounds__(kBlock) k_group_sparse(const KParams p) {
       conj_stage_sets(S, csets, threadIdx.x, kBlock);
       __syncthreads();
     }
-    uint32_t* cbm = reinterpret_cast<uint32_t*>(smem + p.cont_bm_off);  // C < 0: [nbm][kChunkWords * 2] words
+    uint32_t* cbm = reinterpret_cast<uint32_t*>(smem + p.cont_bm_off);  // C < 0: [nbm][kContWords * 2] words
     if constexpr (C < 0) {
       // the chunk's leaf bitmaps straight from the roaring containers (no doc bitmap in HBM): the 4 waves take the
       // leaves' dictIds round-robin (InvertedIndexFilterOperator -> BitmapInvertedIndexReader.java:45-62)
       __syncthreads();  // every wave is done with the previous chunk's words
-      for (int i = threadIdx.x; i < nbm * kChunkWords * 2; i += kBlock) cbm[i] = 0u;
+      for (int i = threadIdx.x; i < nbm * kContWords * 2; i += kBlock) cbm[i] = 0u;
       __syncthreads();
       const uint32_t dlo = (uint32_t)wb * 64u;
       const uint32_t n = min((uint32_t)(we - wb) * 64u, ndocs - dlo);
@@ -126,9 +126,9 @@ __global__ void __launch_bounds__(kBlock) k_group_sparse(const KParams p) {
           if (ci < 0) continue;
           const RoaringContainer c = S->sp_cdir[k][ci];
           if (c.type == 1)  // bitmap: every wave takes a quarter of the chunk's words
-            gs_or_container(c, S->sp_cbase[k], dlo & 0xffffu, n, cbm + k * kChunkWords * 2, lane, wave, WAVES);
+            gs_or_container(c, S->sp_cbase[k], dlo & 0xffffu, n, cbm + k * kContWords * 2, lane, wave, WAVES);
           else if ((t & (WAVES - 1)) == wave)
-            gs_or_container(c, S->sp_cbase[k], dlo & 0xffffu, n, cbm + k * kChunkWords * 2, lane, 0, 1);
+            gs_or_container(c, S->sp_cbase[k], dlo & 0xffffu, n, cbm + k * kContWords * 2, lane, 0, 1);
         }
       __syncthreads();
     }
@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(kBlock) k_group_sparse(const KParams p) {
       for (int k = 0; k < kSparseBitmaps; ++k) {
         if (k >= nbm) continue;
         const unsigned long long v =
-            C < 0 ? reinterpret_cast<const unsigned long long*>(cbm + k * kChunkWords * 2)[w - wb]
+            C < 0 ? reinterpret_cast<const unsigned long long*>(cbm + k * kContWords * 2)[w - wb]
                   : reinterpret_cast<const unsigned long long*>(S->sp_bm[k])[w];
         if (k > 0 && S->sp_or[k]) {
           grp |= v;
