@@ -163,6 +163,9 @@ class OracleColumn:
     is_sorted: bool
     has_inverted: bool = False
     has_range_index: bool = False  # an exact bit-sliced range index (rangeIndexColumns)
+    # a legacy version-1 range index (RangeIndexReaderImpl, inexact) over dictIds: its range starts + the last
+    # range's end (inclusive), as RangeIndexCreator's header holds them
+    legacy_ranges: Optional[np.ndarray] = None
     fwd: Optional[np.ndarray] = None      # packed big-endian fixed-bit bytes (unsorted)
     sorted_ranges: Optional[np.ndarray] = None  # int32 [card, 2]
 
@@ -203,13 +206,17 @@ def build_column(name: str, values: np.ndarray, data_type: str, inverted: bool =
 
 
 def build_segment(name: str, columns: Dict[str, tuple], inverted: Sequence[str] = (),
-                  range_index: Sequence[str] = ()) -> OracleSegment:
-    """columns: name -> (values, data_type)"""
+                  range_index: Sequence[str] = (), legacy_ranges: Optional[Dict[str, np.ndarray]] = None
+                  ) -> OracleSegment:
+    """columns: name -> (values, data_type); legacy_ranges: name -> a version-1 range index's dictId range starts
+    followed by the last range's end"""
     n = None
     seg = OracleSegment(name, 0)
     for c, (vals, dt) in columns.items():
         col = build_column(c, vals, dt, c in inverted)
         col.has_range_index = c in range_index
+        if legacy_ranges and c in legacy_ranges:
+            col.legacy_ranges = np.asarray(legacy_ranges[c], np.int64)
         seg.columns[c] = col
         n = len(vals) if n is None else n
         assert n == len(vals)
@@ -326,6 +333,10 @@ def _plan_filter(f, seg: OracleSegment, col_index: Dict[str, int]):
             is_scan, ikind = False, "inverted"
         elif col.has_range_index and p.TYPE in ("RANGE", "EQ"):
             is_scan, ikind = False, "range"
+        elif col.legacy_ranges is not None and p.TYPE == "RANGE":
+            # an inexact index evaluates RANGE only (RangeIndexBasedFilterOperator.canEvaluate :56-61): a
+            # BitmapDocIdSet of the exact docs, whose entries are the partial ranges' scan (:82-107)
+            is_scan, ikind = False, "legacy"
         else:
             is_scan, ikind = True, "scan"
         leaf = _Leaf("leaf", col_index[p.column], match, is_scan)
@@ -382,6 +393,15 @@ def _merge_same_column(node: _Leaf) -> _Leaf:
     is_and = node.kind == "and"
     out, first = [], {}
     for k in (_merge_same_column(c) for c in node.children):
+        if is_and and k.kind == "leaf" and getattr(k, "ikind", "") == "legacy":
+            # MergeRangeFilterOptimizer: ranges of one column under an AND become one RANGE, planned once
+            j = first.get(("legacy", k.col_index))
+            if j is not None:
+                a = out[j]
+                out[j] = _Leaf("leaf", a.col_index, (a.match & k.match).astype(a.match.dtype), False)
+                out[j].ikind = "legacy"
+                continue
+            first[("legacy", k.col_index)] = len(out)
         if k.kind == "leaf" and k.is_scan:
             j = first.get(k.col_index)
             if j is not None:
@@ -394,6 +414,10 @@ def _merge_same_column(node: _Leaf) -> _Leaf:
         out.append(k)
     kids = []
     for k in out:
+        if k.kind == "leaf" and getattr(k, "ikind", "") == "legacy" and not k.match.any():
+            k = _Leaf("none")
+        elif k.kind == "leaf" and getattr(k, "ikind", "") == "legacy" and k.match.all():
+            k = _Leaf("all")  # the merged RANGE is always true: no range-index leaf
         if k.kind == "leaf" and k.is_scan and not k.match.any():
             k = _Leaf("none")
         elif k.kind == "leaf" and k.is_scan and k.match.all():
@@ -751,7 +775,7 @@ def _or_set(makers, n):
     return make
 
 
-_PRIORITY = {"sorted": 0, "range": 200, "and": 300, "or": 400, "scan": 500, "inverted": 10000}
+_PRIORITY = {"sorted": 0, "range": 200, "legacy": 200, "and": 300, "or": 400, "scan": 500, "inverted": 10000}
 
 
 def _priority(node: _Leaf) -> int:
@@ -768,6 +792,37 @@ def _priority(node: _Leaf) -> int:
 def filter_entries(root: _Leaf, seg: OracleSegment, used: list) -> int:
     """numEntriesScannedInFilter of one segment (see filter_entries_of)."""
     return filter_entries_of(root, seg.num_docs, lambda node: _eval_docs(node, seg, used))
+
+
+def legacy_partial_entries(root: _Leaf, seg: OracleSegment, used: list) -> int:
+    """The legacy range-index leaves' scans (RangeIndexBasedFilterOperator.evaluateLegacyRangeFilter :82-107): each
+    scans the docs of the ranges holding its bounds -- RangeIndexReaderImpl.findRangeId (:236-243) of the inclusive
+    lower and upper dictIds, getPartialMatchesInRange (:300-308; a bound outside every range contributes none, both
+    bounds in one range scan it once) -- counted by ScanBasedDocIdIterator.applyAnd (SVScanDocIdIterator.java:115-140).
+    Every leaf is evaluated, whatever the tree above it."""
+    if root.kind in ("and", "or", "not"):
+        return sum(legacy_partial_entries(c, seg, used) for c in root.children)
+    if root.kind != "leaf" or getattr(root, "ikind", "") != "legacy":
+        return 0
+    col = seg.columns[used[root.col_index]]
+    ids = np.flatnonzero(root.match)
+    lo, hi = int(ids[0]), int(ids[-1])
+    starts, last_end = col.legacy_ranges[:-1], int(col.legacy_ranges[-1])
+
+    def find(v):
+        for i, st in enumerate(starts):
+            if v < st:
+                return i - 1
+        return len(starts) - 1 if v <= last_end else len(starts)
+
+    a, b = find(lo), find(hi)
+    rids = {r for r in (a, b) if 0 <= r < len(starts)}
+    dict_ids = _doc_ids(col, seg.num_docs)
+    total = 0
+    for r in rids:
+        end = int(starts[r + 1]) if r + 1 < len(starts) else last_end + 1
+        total += int(((dict_ids >= starts[r]) & (dict_ids < end)).sum())
+    return total
 
 
 def filter_entries_of(root: _Leaf, n: int, docs_of) -> int:
@@ -907,7 +962,8 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1, filter_s
             _emit(root, prog, keep)
             # the statistic from the iterator simulation (the C program's own count is not used)
             if filter_stats:
-                extra = filter_entries(_merge_same_column(_plan_filter(q.filter, s, col_index)), s, used)
+                merged = _merge_same_column(_plan_filter(q.filter, s, col_index))
+                extra = filter_entries(merged, s, used) + legacy_partial_entries(merged, s, used)
         filter_programs.append(prog)
         extra_entries.append(extra)
 

@@ -457,6 +457,22 @@ struct RoaringLeaf {
 // the chunked build applies when every dictId has at most this many containers (each wave scans them 256 at a time)
 constexpr int64_t kRoaringChunkMaxContainers = 1024;
 
+// k_range_slices: one exact bit-sliced range-index leaf (BitSlicedRangeIndexReader.getMatchingDocIds) -- docs whose
+// value v has lo <= v <= hi, composed from the RangeBitmap's slices (slice i = the docs whose bit i is 0)
+struct RangeSliceLeaf {
+  const uint8_t* payload;  // the RangeBitmap bytes after its 12-byte header (device)
+  const int32_t* dir;      // [nkeys][nslices]: byte offset in payload of the (key, slice) container, -1 = none
+  uint32_t* bitmap;        // doc bitmap, padded_words words
+  int32_t num_docs;
+  int32_t padded_words;
+  int32_t nkeys;
+  int32_t nslices;
+  uint64_t hi;             // v <= hi (hi < 2^nslices)
+  uint64_t lo_m1;          // and, when use_lo, NOT v <= lo - 1
+  int32_t use_lo;
+  int32_t pad;
+};
+
 struct Column {
   std::string name;
   int32_t data_type = PH_INT;
@@ -466,6 +482,16 @@ struct Column {
   bool is_raw = false;                // pinned from a raw forward index (dictionary-encoded at pin)
   bool has_range_index = false;       // an exact (version 2) bit-sliced range index came with the column
   bool has_inexact_range_index = false;  // a legacy version-1 range index (ranges + a partial scan)
+  // the exact index's RangeBitmap parsed at pin (dictionary columns; segment.cpp parse_range_bitmap): leaves are
+  // evaluated from its slices by k_range_slices
+  bool range_slices = false;
+  int32_t range_nkeys = 0, range_nslices = 0;
+  DeviceBuffer d_range;                // the RangeBitmap bytes (header + masks + containers)
+  DeviceBuffer d_range_dir;            // [nkeys][nslices] container offsets into d_range's container area, -1 none
+  // a legacy version-1 index over dictIds (parse_legacy_range_index): range starts, last end, docs per range
+  bool legacy_range = false;
+  std::vector<int64_t> legacy_starts, legacy_cards;
+  int64_t legacy_last_end = 0;
   Dictionary dict;
   std::vector<int32_t> sorted_ranges;  // [card][2] (sorted columns)
   std::vector<uint8_t> inverted;       // host copy of the inverted index (offsets + roaring blobs)
@@ -525,8 +551,8 @@ struct Lane {
   hipEvent_t ev_uploaded = nullptr;  // the call's segment descriptors and programs are in HBM (statistics pass)
   std::vector<hipEvent_t> ev_pool;
   // slot 0: launch parameters; slot 1: the bitmap build's work items; slot 2: predicate payloads (sets / ranges)
-  void* staging[3] = {nullptr, nullptr, nullptr};
-  size_t staging_bytes[3] = {0, 0, 0};
+  void* staging[4] = {nullptr, nullptr, nullptr, nullptr};
+  size_t staging_bytes[4] = {0, 0, 0, 0};
   explicit Lane(int dev);
   ~Lane();
   void* host_staging(size_t n, int slot = 0);  // valid until the lane's stream passes this call's uploads
@@ -633,6 +659,11 @@ enum : int32_t { PH_HLL_HASH_INT = 0, PH_HLL_HASH_DOUBLE = 1, PH_HLL_HASH_FLOAT 
 void launch_hll_table(const void* values, int32_t kind, int64_t n, int log2m, uint32_t* out, hipStream_t s);
 
 void build_bitmap_directory(Column& c);  // at pin, from c.inverted
+// at pin: the (key, slice) container directory of an exact range index's RangeBitmap (after Pinot's 12-byte header)
+void parse_legacy_range_index(const uint8_t* b, uint64_t size, std::vector<int64_t>* starts, int64_t* last_end,
+                              std::vector<int64_t>* cards);
+std::vector<int32_t> parse_range_bitmap(const uint8_t* b, uint64_t size, int64_t num_docs, int32_t* nkeys,
+                                        int32_t* nslices);
 // (column, index id) -> (startOffset, size) of a V3 index_map file (loader.cpp)
 typedef std::map<std::pair<std::string, std::string>, std::pair<int64_t, int64_t>> IndexMap;
 IndexMap read_index_map(const std::string& path);
@@ -641,6 +672,7 @@ ph_segment* segment_load_dir_impl(Context* ctx, const char* dir, const char* con
 int64_t segment_dir_num_docs(const char* dir);  // metadata.properties segment.total.docs, 0 if unreadable
 // every container of every (leaf, dictId) work item of a query in one launch (one wave per container)
 void launch_roaring_or(const RoaringWork* w, int n, const RoaringTarget* targets, hipStream_t s);
+void launch_range_slices(const RangeSliceLeaf* leaves, int nleaves, int max_chunks, hipStream_t s);
 void launch_roaring_chunk(const RoaringLeaf* leaves, int nleaves, int max_chunks, const RoaringRange* ranges,
                           hipStream_t s);
 void launch_selftest_unpack(const uint32_t* fwd, int64_t n, int bits, int32_t* out, hipStream_t s);

@@ -53,6 +53,7 @@ struct PNode {
   bool exclusive = false;    // OP_NOT over OP_BITMAP built for an exclusive predicate (InvertedIndexFilterOperator's
                              // flipped bitmap: a BitmapDocIdSet, not a user NOT)
   bool range_index = false;  // a scan-evaluated RangeIndexBasedFilterOperator leaf: index-based for the statistics
+  bool legacy_range = false;  // ... over a legacy version-1 index (its boundary ranges scanned: legacy_partial_entries)
   // AND whose children are index-based leaves (sorted, bitmap, range index, ORs / NOTs of them) followed by scan
   // leaves: the reference's AndDocIdSet applies the scans one after another to the index-based result
   // (ScanBasedDocIdIterator.applyAnd), so its filter entries are |D0| + |D0 n S1| + ... (counted on the device)
@@ -63,7 +64,9 @@ struct PNode {
 struct BitmapLeaf {
   ph_segment* seg;
   Column* col;
-  std::vector<int32_t> dict_ids;
+  std::vector<int32_t> dict_ids;  // inverted-index leaf: the OR of these dictIds' bitmaps
+  bool range = false;             // exact range-index leaf: dictIds [lo, hi] from the bit slices (k_range_slices)
+  int64_t lo = 0, hi = -1;
 };
 
 struct DictIdSet {
@@ -296,10 +299,29 @@ struct Planner {
     // exact range index, or EQ on one without an inverted index.  Same doc set as a scan of the dictIds, which is
     // how the kernels evaluate it; it scans no entries (BitmapDocIdSet)
     n.range_index = c.has_range_index && (p.type == PH_PRED_RANGE || (p.type == PH_PRED_EQ && !c.has_inverted()));
-    // a legacy version-1 range index is a RangeIndexBasedFilterOperator too (RangeIndexBasedFilterOperator.java:59-60),
-    // whose partial scan of the boundary ranges the statistics here do not model: such leaves take the CPU plan
-    if (c.has_inexact_range_index && (p.type == PH_PRED_RANGE || (p.type == PH_PRED_EQ && !c.has_inverted())))
-      fail(PH_ERR_UNSUPPORTED, "column " + c.name + ": a version-1 (inexact) range index leaf");
+    if (n.range_index && c.range_slices && !s.exclusive && (s.is_range || s.ids.size() == 1)) {
+      // BitSlicedRangeIndexReader.getMatchingDocIds(min, max) / (value) (:123-171): the dictId interval's doc
+      // bitmap from the index's slices; a bitmap-based leaf like an inverted one (RangeIndexBasedFilterOperator
+      // :78-92), priority 200 in the AND order
+      BitmapLeaf b{seg, &c, {}};
+      b.range = true;
+      b.lo = s.is_range ? s.start : s.ids[0];
+      b.hi = s.is_range ? s.end - 1 : s.ids[0];
+      n.scan = false;
+      n.col = -1;
+      n.op = OP_BITMAP;
+      n.bitmap_leaf = (int)bitmaps.size();
+      bitmaps.push_back(std::move(b));
+      return n;
+    }
+    // a legacy version-1 range index evaluates RANGE only (RangeIndexBasedFilterOperator.canEvaluate :56-61): a
+    // BitmapDocIdSet of the exact docs (scanned from the dictIds here) whose entries are the scan of its boundary
+    // ranges (evaluateLegacyRangeFilter :82-107), added per segment by legacy_partial_entries
+    if (c.has_inexact_range_index && p.type == PH_PRED_RANGE) {
+      if (!c.legacy_range) fail(PH_ERR_UNSUPPORTED, "column " + c.name + ": a version-1 range index over raw values");
+      n.range_index = true;
+      n.legacy_range = true;
+    }
     if (s.is_range) {
       n.op = OP_RANGE;
       n.lo = (uint32_t)s.start;
@@ -446,8 +468,12 @@ void merge_same_column_leaves(PNode& n, const CardOf& card_of) {
   std::map<int, size_t> first_of;  // column slot -> index of its first scan leaf
   std::vector<PNode> kids;
   for (auto& k : n.kids) {
-    if (k.kind == L_NODE && k.scan && (k.op == OP_RANGE || k.op == OP_SET)) {
-      auto it = first_of.find(k.col);
+    // a legacy range-index leaf merges only with another under an AND (MergeRangeFilterOptimizer: one RANGE,
+    // planned once); the other scans merge as before, never with it
+    const bool legacy = k.kind == L_NODE && k.legacy_range;
+    if (k.kind == L_NODE && k.scan && (k.op == OP_RANGE || k.op == OP_SET) && (!legacy || is_and)) {
+      const int key = legacy ? -2 - k.col : k.col;
+      auto it = first_of.find(key);
       if (it != first_of.end()) {
         PNode& a = kids[it->second];
         const int64_t card = card_of(k.col);
@@ -456,7 +482,7 @@ void merge_same_column_leaves(PNode& n, const CardOf& card_of) {
         leaf_from_bits(a, x, card);
         continue;
       }
-      first_of[k.col] = kids.size();
+      first_of[key] = kids.size();
     }
     kids.push_back(std::move(k));
   }
@@ -573,7 +599,7 @@ SimNode to_sim(const PNode& n, std::vector<PNode>& leaves, std::vector<int32_t>&
     // FilterOperatorUtils priorities (:197-241): SortedIndexBasedFilterOperator 0, RangeIndexBasedFilterOperator 200,
     // ScanBasedFilterOperator 500; InvertedIndexFilterOperator is none of the listed classes (10000)
     if (n.op == OP_DOCRANGES) { kinds.push_back(SIM_SORTED); x.priority = 0; }
-    else if (n.scan && n.range_index) { kinds.push_back(SIM_BITMAP); x.priority = 200; }
+    else if (n.range_index) { kinds.push_back(SIM_BITMAP); x.priority = 200; }  // scan- or slice-evaluated
     else if (n.scan) { kinds.push_back(SIM_SCAN); x.priority = 500; }
     else { kinds.push_back(SIM_BITMAP); x.priority = 10000; }
     return x;
@@ -677,10 +703,53 @@ void emit(const PNode& n, SegProgram& p) {
 
 // docs of the dictIds' bitmaps: a single-value column's bitmaps are disjoint, so the OR's cardinality is the sum
 // (InvertedIndexFilterOperator.getNumMatchingDocs :101-127)
+// RangeIndexReaderImpl.findRangeId over dictIds (:236-243)
+int64_t legacy_range_id(const Column& c, int64_t v) {
+  for (size_t i = 0; i < c.legacy_starts.size(); ++i)
+    if (v < c.legacy_starts[i]) return (int64_t)i - 1;
+  return v <= c.legacy_last_end ? (int64_t)c.legacy_starts.size() - 1 : (int64_t)c.legacy_starts.size();
+}
+
+// the legacy range-index leaves' boundary-range scans of one segment's (merged) tree: getPartialMatchesInRange
+// (RangeIndexReaderImpl.java:300-308) of the leaf's inclusive dictId bounds, counted by ScanBasedDocIdIterator.applyAnd
+// (SVScanDocIdIterator.java:115-140); every leaf's getTrues runs, whatever the tree above it
+template <class ColOf>
+int64_t legacy_partial_entries(const PNode& n, const ColOf& col_of) {
+  if (n.kind != L_NODE) return 0;
+  int64_t e = 0;
+  for (auto& k : n.kids) e += legacy_partial_entries(k, col_of);
+  if (!n.legacy_range || !n.kids.empty()) return e;
+  const Column& c = col_of(n.col);
+  int64_t lo = -1, hi = -1;
+  if (n.op == OP_RANGE) {
+    lo = n.lo;
+    hi = (int64_t)n.lo + n.len - 1;
+  } else {
+    for (int64_t i = 0; i < (int64_t)n.set.size() * 32; ++i)
+      if ((n.set[i >> 5] >> (i & 31)) & 1u) {
+        if (lo < 0) lo = i;
+        hi = i;
+      }
+    if (lo < 0) return e;
+  }
+  const int64_t R = (int64_t)c.legacy_starts.size();
+  const int64_t a = legacy_range_id(c, lo), b = legacy_range_id(c, hi);
+  if (a >= 0 && a < R) e += c.legacy_cards[a];
+  if (b >= 0 && b < R && b != a) e += c.legacy_cards[b];
+  return e;
+}
+
 int64_t bitmap_docs(const Column& c, const std::vector<int32_t>& ids) {
   int64_t n = 0;
   for (int32_t id : ids) n += c.id_docs[id];
   return n;
+}
+
+// a bitmap leaf's docs for the plan's cost estimates: exact for an inverted leaf; a range-index leaf's count is not
+// known before its bitmap is built, so uniform dictIds are assumed
+double leaf_docs_estimate(const BitmapLeaf& b) {
+  if (!b.range) return (double)bitmap_docs(*b.col, b.dict_ids);
+  return (double)b.seg->num_docs * (double)(b.hi - b.lo + 1) / (double)std::max<int32_t>(1, b.col->cardinality);
 }
 
 }  // namespace
@@ -1124,6 +1193,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     // (MergeEqInFilterOptimizer: `d_year = 1997 OR d_year = 1998` -> one IN; MergeRangeFilterOptimizer: ranges of
     // one column under an AND), so the statistics below see the reference's operator tree
     merge_same_column_leaves(root, [&](int slot) { return (int64_t)segs[i]->columns.at(slot_names[slot])->cardinality; });
+    if (segs[i]->num_docs > 0)
+      stats.num_entries_scanned_in_filter += legacy_partial_entries(
+          root, [&](int slot) -> const Column& { return *segs[i]->columns.at(slot_names[slot]); });
     const int sk = stat_kind(root);
     if (sk != ST_DEVICE && segs[i]->num_docs > 0) {
       StatSeg ss;
@@ -1155,6 +1227,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
       if (n.op == OP_BITMAP) {
         const BitmapLeaf& b = pl.bitmaps[n.bitmap_leaf];
+        if (b.range) return -1;  // counted from its bitmap
         return bitmap_docs(*b.col, b.dict_ids);
       }
       if (n.op == OP_NOT && n.kids.size() == 1) {
@@ -1199,12 +1272,44 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     uint32_t* block = scratch.alloc<uint32_t>(std::max<size_t>(2, woff.back()));
     for (size_t i = 0; i < nl; ++i) bitmap_dev[i] = block + woff[i];
+    // range-index leaves: k_range_slices writes every word of theirs (after the atomic build's memset, below)
+    auto build_range_leaves = [&]() {
+      std::vector<RangeSliceLeaf> rl;
+      int max_chunks = 0;
+      for (size_t i = 0; i < nl; ++i) {
+        const BitmapLeaf& b = pl.bitmaps[i];
+        if (!b.range) continue;
+        const Column& col = *b.col;
+        const int32_t pw = (int32_t)(woff[i + 1] - woff[i]);
+        RangeSliceLeaf L{};
+        L.payload = col.d_range.as<uint8_t>();
+        L.dir = col.d_range_dir.as<int32_t>();
+        L.bitmap = bitmap_dev[i];
+        L.num_docs = b.seg->num_docs;
+        L.padded_words = pw;
+        L.nkeys = col.range_nkeys;
+        L.nslices = col.range_nslices;
+        L.hi = (uint64_t)b.hi;  // <= cardinality - 1 < 2^nslices (checked at pin)
+        L.use_lo = b.lo > 0;
+        L.lo_m1 = b.lo > 0 ? (uint64_t)(b.lo - 1) : 0;
+        rl.push_back(L);
+        max_chunks = std::max(max_chunks, (pw + 2047) / 2048);
+      }
+      if (rl.empty()) return;
+      const size_t bytes = sizeof(RangeSliceLeaf) * rl.size();
+      uint8_t* dev = scratch.alloc<uint8_t>(bytes);
+      uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(bytes, 3));
+      memcpy(stage, rl.data(), bytes);
+      PH_HIP_CHECK(hipMemcpyAsync(dev, stage, bytes, hipMemcpyHostToDevice, st));
+      launch_range_slices(reinterpret_cast<RangeSliceLeaf*>(dev), (int)rl.size(), max_chunks, st);
+    };
     if (chunked) {
       // k_roaring_chunk: one workgroup per (65536-doc chunk, leaf) builds the chunk in LDS and stores every word
       std::vector<RoaringLeaf> lv(nl);
       std::vector<RoaringRange> rg;
       int max_chunks = 0;
       for (size_t i = 0; i < nl; ++i) {
+        if (pl.bitmaps[i].range) continue;
         const Column& col = *pl.bitmaps[i].col;
         const int32_t first = (int32_t)rg.size();
         for (int32_t id : pl.bitmaps[i].dict_ids) {
@@ -1216,15 +1321,20 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
                             pl.bitmaps[i].seg->num_docs, pw, first, (int32_t)rg.size() - first};
         max_chunks = std::max(max_chunks, (pw + 2047) / 2048);
       }
-      const size_t b1 = sizeof(RoaringLeaf) * nl, b2 = sizeof(RoaringRange) * std::max<size_t>(1, rg.size());
-      uint8_t* dev = scratch.alloc<uint8_t>(b1 + b2);
-      // staging slot 1: nothing else in this call writes it, so the build overlaps the rest of the host setup
-      uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(b1 + b2, 1));
-      memcpy(stage, lv.data(), b1);
-      if (!rg.empty()) memcpy(stage + b1, rg.data(), sizeof(RoaringRange) * rg.size());
-      PH_HIP_CHECK(hipMemcpyAsync(dev, stage, b1 + b2, hipMemcpyHostToDevice, st));
-      launch_roaring_chunk(reinterpret_cast<RoaringLeaf*>(dev), (int)nl, max_chunks,
-                           reinterpret_cast<RoaringRange*>(dev + b1), st);
+      lv.erase(std::remove_if(lv.begin(), lv.end(), [](const RoaringLeaf& l) { return l.bitmap == nullptr; }),
+               lv.end());
+      if (!lv.empty()) {
+        const size_t b1 = sizeof(RoaringLeaf) * lv.size(), b2 = sizeof(RoaringRange) * std::max<size_t>(1, rg.size());
+        uint8_t* dev = scratch.alloc<uint8_t>(b1 + b2);
+        // staging slot 1: nothing else in this call writes it, so the build overlaps the rest of the host setup
+        uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(b1 + b2, 1));
+        memcpy(stage, lv.data(), b1);
+        if (!rg.empty()) memcpy(stage + b1, rg.data(), sizeof(RoaringRange) * rg.size());
+        PH_HIP_CHECK(hipMemcpyAsync(dev, stage, b1 + b2, hipMemcpyHostToDevice, st));
+        launch_roaring_chunk(reinterpret_cast<RoaringLeaf*>(dev), (int)lv.size(), max_chunks,
+                             reinterpret_cast<RoaringRange*>(dev + b1), st);
+      }
+      build_range_leaves();
       return;
     }
     // device-atomic build: a zeroed block, every container of every leaf OR-ed in by ONE launch
@@ -1232,6 +1342,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     std::vector<RoaringTarget> tg(nl);
     for (size_t i = 0; i < nl; ++i) {
       const Column& col = *pl.bitmaps[i].col;
+      if (pl.bitmaps[i].range) continue;  // its target stays unused
       for (int32_t id : pl.bitmaps[i].dict_ids) {
         const int64_t f = col.dir_begin[id], n = col.dir_begin[id + 1] - f;
         for (int64_t k = 0; k < n; k += kRoaringWorkContainers)  // 4 containers per wave keeps the grid wide
@@ -1265,7 +1376,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       if (!seg_live[i]) continue;
       ++live;
       const PNode& r = roots[i];
-      cont_defer = r.kind == L_NODE && r.op == OP_BITMAP && !r.exclusive && r.bitmap_leaf >= 0;
+      cont_defer = r.kind == L_NODE && r.op == OP_BITMAP && !r.exclusive && r.bitmap_leaf >= 0 &&
+                   !pl.bitmaps[r.bitmap_leaf].range;
     }
     cont_defer = cont_defer && live == (int)pl.bitmaps.size();  // no other bitmap leaf anywhere
   }
@@ -1286,6 +1398,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       for (auto& g : sh.groups) leaves += g.size();
     }
     gs_defer = gs_defer && leaves == pl.bitmaps.size();  // no bitmap leaf outside the sparse ANDs
+    for (auto& b : pl.bitmaps) gs_defer = gs_defer && !b.range;
   }
   // the bitmap build's device time is part of the query's device_ms (its own event pair: host setup follows it)
   bool bm_timed = false;
@@ -1666,7 +1779,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       double est = n;
       for (auto& g : sh.groups) {
         double d = 0;
-        for (int b : g) d += (double)bitmap_docs(*pl.bitmaps[b].col, pl.bitmaps[b].dict_ids) / n;
+        for (int b : g) d += leaf_docs_estimate(pl.bitmaps[b]) / n;
         est *= std::min(1.0, d);
       }
       for (const PNode* k : sh.scans) {  // uniform dictIds: matched ids / cardinality
@@ -2017,7 +2130,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     int64_t docs = 0, hits = 0;
     if (all_bitmap) {
       for (auto& d : dsegs) docs += d.num_docs;
-      for (auto& fb : fbitmap_fix) hits += bitmap_docs(*pl.bitmaps[fb.second].col, pl.bitmaps[fb.second].dict_ids);
+      for (auto& fb : fbitmap_fix) hits += (int64_t)leaf_docs_estimate(pl.bitmaps[fb.second]);
     }
     kp.agg_sparse = (all_bitmap && hits * 8 < docs) || agg_conj;
     if (const char* e = getenv("PH_AGG_SPARSE")) kp.agg_sparse = (all_bitmap || agg_conj) && atoi(e) != 0;  // tuning knob

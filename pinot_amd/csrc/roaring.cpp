@@ -115,4 +115,98 @@ void build_bitmap_directory(Column& c) {
 }
 
 
+// A legacy version-1 range index (RangeIndexCreator.seal :300-380; RangeIndexReaderImpl :46-88): int32 BE version 1,
+// int32 BE type-name length + the name ("INT": a dictionary column's index over dictIds), int32 BE range count R,
+// R + 1 values (the ranges' first values, then the last range's end), R + 1 int64 BE absolute offsets of the ranges'
+// portable roaring bitmaps.  Kept: the starts, the end and each range's doc count -- the leaf's doc set is exact
+// from the dictIds; its statistic is the docs of its boundary ranges (getPartialMatchesInRange :300-308)
+void parse_legacy_range_index(const uint8_t* b, uint64_t size, std::vector<int64_t>* starts, int64_t* last_end,
+                              std::vector<int64_t>* cards) {
+  auto need = [&](uint64_t at) {
+    if (at > size) fail(PH_ERR_INVALID_ARGUMENT, "legacy range index: truncated");
+  };
+  need(8);
+  const uint32_t tl = be32u(b + 4);
+  need(8 + (uint64_t)tl + 4);
+  const std::string type(reinterpret_cast<const char*>(b + 8), tl);
+  if (type != "INT") fail(PH_ERR_UNSUPPORTED, "legacy range index over " + type + " values");
+  uint64_t at = 8 + tl;
+  const uint32_t R = be32u(b + at);
+  at += 4;
+  if (R == 0 || R > (1u << 24)) fail(PH_ERR_INVALID_ARGUMENT, "legacy range index: bad range count");
+  need(at + 4ull * (R + 1) + 8ull * (R + 1));
+  starts->assign(R, 0);
+  for (uint32_t r = 0; r < R; ++r) (*starts)[r] = (int32_t)be32u(b + at + 4ull * r);
+  *last_end = (int32_t)be32u(b + at + 4ull * R);
+  at += 4ull * (R + 1);
+  auto off = [&](uint32_t r) {
+    return ((uint64_t)be32u(b + at + 8ull * r) << 32) | be32u(b + at + 8ull * r + 4);
+  };
+  if (off(R) != size) fail(PH_ERR_INVALID_ARGUMENT, "legacy range index: last offset differs from the size");
+  cards->assign(R, 0);
+  std::vector<RoaringContainer> dir;
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint64_t s0 = off(r), s1 = off(r + 1);
+    if (s1 < s0 || s1 > size) fail(PH_ERR_INVALID_ARGUMENT, "legacy range index: bad offsets");
+    dir.clear();
+    parse_roaring(b + s0, s1 - s0, s0, dir);
+    int64_t docs = 0;
+    for (const RoaringContainer& rc : dir) {
+      if (rc.type != 2) {
+        docs += rc.card;
+      } else {
+        const uint8_t* q = b + rc.offset + 2;
+        for (int32_t j = 0; j < rc.card; ++j) docs += (int64_t)le16(q + 4 * j + 2) + 1;
+      }
+    }
+    (*cards)[r] = docs;
+  }
+}
+
+// RoaringBitmap's RangeBitmap as BitSlicedRangeIndexCreator.seal writes it after its header (int32 BE version 2,
+// int64 BE min; BitSlicedRangeIndexCreator.java:123-133) and BitSlicedRangeIndexReader maps it (:240-244).  The format
+// belongs to org.roaringbitmap:RoaringBitmap 0.9.38 (pom.xml), which /root/reference does not vendor; restated from
+// its published RangeBitmap.map / Appender.serialize (little-endian throughout):
+//   u16 cookie 0xF00D, u8 base (2), u8 slice count S, u16 key count K, u32 row count
+//   K masks of ceil(S / 8) bytes: bit i of key k's mask = slice i has a container for key k
+//   the containers, key-major, slices ascending: u8 kind (0 bitmap, 1 run, 2 array), u16 size, then 8192 bytes of
+//   bitmap / size (start, length - 1) u16 pairs / size u16 values; slice i of key k = the key's rows with bit i CLEAR
+// Returns dir[k * S + i] = byte offset (from b) of that container, or -1.  The bytes are pinned by this restatement
+// and the test writer only: the reference holds no range-index file (parity unpinned for the byte format).
+std::vector<int32_t> parse_range_bitmap(const uint8_t* b, uint64_t size, int64_t num_docs, int32_t* nkeys,
+                                        int32_t* nslices) {
+  const uint64_t h = 12;  // Pinot's header
+  if (size < h + 10) fail(PH_ERR_INVALID_ARGUMENT, "range index: truncated RangeBitmap header");
+  if (size > (uint64_t)INT32_MAX) fail(PH_ERR_UNSUPPORTED, "range index past 2 GiB");
+  const uint8_t* r = b + h;
+  if (le16(r) != 0xF00D) fail(PH_ERR_INVALID_ARGUMENT, "range index: bad RangeBitmap cookie");
+  if (r[2] != 2) fail(PH_ERR_INVALID_ARGUMENT, "range index: unsupported RangeBitmap base");
+  const int32_t S = r[3], K = le16(r + 4);
+  const uint64_t rows = (uint64_t)r[6] | (uint64_t)r[7] << 8 | (uint64_t)r[8] << 16 | (uint64_t)r[9] << 24;
+  if (S < 1 || S > 64) fail(PH_ERR_INVALID_ARGUMENT, "range index: bad slice count");
+  if ((int64_t)rows != num_docs || (int64_t)K != (num_docs + 65535) / 65536)
+    fail(PH_ERR_INVALID_ARGUMENT, "range index: row / key count differs from the segment's");
+  const int32_t bpm = (S + 7) / 8;
+  uint64_t at = h + 10 + (uint64_t)K * bpm;
+  if (at > size) fail(PH_ERR_INVALID_ARGUMENT, "range index: truncated slice masks");
+  std::vector<int32_t> dir((size_t)K * S, -1);
+  for (int32_t k = 0; k < K; ++k) {
+    const uint8_t* m = r + 10 + (size_t)k * bpm;
+    for (int32_t i = 0; i < S; ++i) {
+      if (!((m[i >> 3] >> (i & 7)) & 1)) continue;
+      if (at + 3 > size) fail(PH_ERR_INVALID_ARGUMENT, "range index: truncated container");
+      const int kind = b[at];
+      const uint64_t n = le16(b + at + 1);
+      const uint64_t body = kind == 0 ? 8192 : kind == 1 ? 4 * n : kind == 2 ? 2 * n : ~0ull;
+      if (body == ~0ull) fail(PH_ERR_INVALID_ARGUMENT, "range index: bad container kind");
+      if (at + 3 + body > size) fail(PH_ERR_INVALID_ARGUMENT, "range index: truncated container");
+      dir[(size_t)k * S + i] = (int32_t)at;
+      at += 3 + body;
+    }
+  }
+  *nkeys = K;
+  *nslices = S;
+  return dir;
+}
+
 }  // namespace ph

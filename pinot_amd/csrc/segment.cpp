@@ -507,6 +507,10 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
       const uint32_t version = (uint32_t)h[0] << 24 | (uint32_t)h[1] << 16 | (uint32_t)h[2] << 8 | h[3];
       col->has_range_index = version == 2;
       col->has_inexact_range_index = version != 2;
+      if (version == 1 && !col->is_raw) {
+        parse_legacy_range_index(h, d.range_index_size, &col->legacy_starts, &col->legacy_last_end, &col->legacy_cards);
+        col->legacy_range = true;
+      }
     }
     const uint8_t* fwd = static_cast<const uint8_t*>(d.forward_index);
     if (!fwd) fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": missing forward index");
@@ -592,6 +596,26 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
         PH_HIP_CHECK(hipMemcpyAsync(col->d_dir.ptr, col->dir.data(), sizeof(RoaringContainer) * col->dir.size(),
                                     hipMemcpyHostToDevice, st));
       seg->device_bytes += col->d_dir.bytes;
+    }
+    // an exact range index over dictIds: its RangeBitmap pinned with the (key, slice) container directory, so its
+    // leaves are evaluated from the bit slices (k_range_slices).  A raw column's index is over raw values (minus the
+    // header's min), not the dictIds it is pinned as: its leaves scan the dictIds (same doc set)
+    std::vector<int32_t> range_dir;
+    if (col->has_range_index && !col->is_raw && d.range_index_size > 12) {
+      const uint8_t* ri = static_cast<const uint8_t*>(d.range_index);
+      for (int j = 4; j < 12; ++j)
+        if (ri[j]) fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": dictionary range index with min != 0");
+      range_dir = parse_range_bitmap(ri, d.range_index_size, n, &col->range_nkeys, &col->range_nslices);
+      if (card > 0 && (uint64_t)(card - 1) >> (col->range_nslices - 1) >> 1)
+        fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": range index slices narrower than the dictionary");
+      col->d_range.alloc(d.range_index_size, ctx->device);
+      PH_HIP_CHECK(hipMemcpyAsync(col->d_range.ptr, ri, d.range_index_size, hipMemcpyHostToDevice, st));
+      col->d_range_dir.alloc(sizeof(int32_t) * std::max<size_t>(1, range_dir.size()), ctx->device);
+      if (!range_dir.empty())
+        PH_HIP_CHECK(hipMemcpyAsync(col->d_range_dir.ptr, range_dir.data(), sizeof(int32_t) * range_dir.size(),
+                                    hipMemcpyHostToDevice, st));
+      seg->device_bytes += col->d_range.bytes + col->d_range_dir.bytes;
+      col->range_slices = true;
     }
     // derived streams, on the pin stream: no query builds them (nor waits for one another doing so)
     build_value_stream(ctx, seg.get(), *col, st);

@@ -18,6 +18,8 @@ import ctypes
 from dataclasses import dataclass, field
 from typing import Dict, Optional, Sequence
 
+import struct
+
 import numpy as np
 
 from . import native as N
@@ -140,10 +142,56 @@ class ColumnBuffers:
 
 def range_index_header(min_value: int = 0) -> np.ndarray:
     """The BitSlicedRangeIndexCreator header (BitSlicedRangeIndexCreator.java:125-131: int32 BE version 2, int64 BE
-    min -- 0 for a dictionary column, whose index is built over dictIds).  The GPU path reads only this header: it
-    evaluates a range-indexed leaf from the packed dictIds (the same doc set as the exact index), so the serialized
-    RoaringBitmap RangeBitmap that follows in a reference-written file is not built here."""
+    min -- 0 for a dictionary column, whose index is built over dictIds)."""
     return np.frombuffer(np.array([2], ">i4").tobytes() + np.array([min_value], ">i8").tobytes(), np.uint8).copy()
+
+
+RB_COOKIE, RB_BITMAP, RB_RUN, RB_ARRAY = 0xF00D, 0, 1, 2
+
+
+def _rb_container(rows: np.ndarray) -> bytes:
+    """One RangeBitmap container of a key's sorted rows (u16): the smallest of run / array / bitmap."""
+    card = int(rows.size)
+    brk = np.flatnonzero(np.diff(rows.astype(np.int32)) != 1) + 1
+    starts = np.concatenate(([0], brk))
+    ends = np.concatenate((brk, [card]))
+    nruns = int(starts.size)
+    if 4 * nruns < min(2 * card, 8192):
+        pairs = np.empty(2 * nruns, "<u2")
+        pairs[0::2] = rows[starts]
+        pairs[1::2] = ends - starts - 1
+        return struct.pack("<BH", RB_RUN, nruns) + pairs.tobytes()
+    if card <= 4096:
+        return struct.pack("<BH", RB_ARRAY, card) + rows.astype("<u2").tobytes()
+    bits = np.zeros(65536, np.uint8)
+    bits[rows] = 1
+    return struct.pack("<BH", RB_BITMAP, (card - 1) & 0xFFFF) + np.packbits(bits, bitorder="little").tobytes()
+
+
+def range_index_bytes(values: np.ndarray, max_value: int, min_value: int = 0) -> np.ndarray:
+    """An exact range index as BitSlicedRangeIndexCreator writes it (dictionary column: values = dictIds, max =
+    cardinality - 1): the header, then RoaringBitmap 0.9.38's RangeBitmap (Appender.serialize; the dependency is not
+    vendored in the reference, its layout is restated in pinot_amd/csrc/roaring.cpp parse_range_bitmap): LE u16
+    cookie 0xF00D, u8 base 2, u8 slice count S, u16 key count, u32 rows; per 65536-row key a ceil(S/8)-byte mask of
+    the slices present; the containers (key-major, slices ascending), slice i = the key's rows whose value has bit i
+    clear."""
+    v = np.asarray(values).astype(np.uint64) - np.uint64(min_value)
+    n = int(v.size)
+    S = max(1, int(max_value - min_value).bit_length())
+    nkeys = (n + 65535) >> 16
+    bpm = (S + 7) >> 3
+    masks = np.zeros((nkeys, bpm), np.uint8)
+    parts = []
+    for k in range(nkeys):
+        chunk = v[k << 16:(k + 1) << 16]
+        for i in range(S):
+            rows = np.flatnonzero(((chunk >> np.uint64(i)) & np.uint64(1)) == 0).astype(np.uint16)
+            if rows.size == 0:
+                continue
+            masks[k, i >> 3] |= np.uint8(1 << (i & 7))
+            parts.append(_rb_container(rows))
+    body = struct.pack("<HBBHI", RB_COOKIE, 2, S, nkeys, n) + masks.tobytes() + b"".join(parts)
+    return np.concatenate([range_index_header(min_value), np.frombuffer(body, np.uint8)])
 
 
 @dataclass
@@ -363,7 +411,12 @@ def create_segment(name: str, columns: Dict[str, tuple], inverted: Sequence[str]
         else:
             seg.columns[c] = create_column(c, vals, dt, c in inverted, run_optimize)
         if c in range_index:
-            seg.columns[c].range_index = range_index_header()
+            cb = seg.columns[c]
+            if cb.raw:
+                seg.columns[c].range_index = range_index_header()  # raw columns: the leaf scans (header only)
+            else:
+                ids = np.searchsorted(np.asarray(cb.dictionary_values), np.asarray(vals))
+                seg.columns[c].range_index = range_index_bytes(ids, max(len(cb.dictionary_values) - 1, 0))
         n = len(vals) if n is None else n
         if n != len(vals):
             raise ValueError("columns of different lengths")

@@ -1,17 +1,18 @@
 """GPU: range-indexed columns (FilterOperatorUtils.java:97-120, RangeIndexBasedFilterOperator,
 BitSlicedRangeIndexReader).  A column with an exact (version 2) bit-sliced range index turns RANGE -- and EQ when the
 column has no inverted index -- into an index-based leaf: no entries scanned in filter, bitmap-based in the AND
-order; RANGE never uses an inverted index.  The kernels evaluate the leaf from the packed dictIds (the same doc set
-as the exact index).  Checked against the oracle's leaf choice on pinned buffers and on V3 / V1 directories whose
-index_map / <col>.bitmap.range carry the index (the fixture writes the BitSlicedRangeIndexCreator header; the GPU
-path reads no bit slice).  Bar: bit-exact results and identical ExecutionStatistics."""
+order; RANGE never uses an inverted index.  On a dictionary column the leaf's doc bitmap is composed from the index's
+bit slices by k_range_slices (BitSlicedRangeIndexReader.getMatchingDocIds :123-211 over RoaringBitmap's RangeBitmap);
+test_leaf_reads_the_slices proves it by pinning a forward index that disagrees with the index.  Checked against the
+oracle's leaf choice on pinned buffers and on V3 / V1 directories whose index_map / <col>.bitmap.range carry the
+index.  Bar: bit-exact results and identical ExecutionStatistics."""
 import numpy as np
 import pytest
 
 from oracle import oracle as O
 from pinot_amd.query import parse_sql
 from pinot_amd.reduce import reduce_groups
-from pinot_amd.segment import create_segment
+from pinot_amd.segment import create_segment, range_index_bytes
 from tests import segment_dirs as SD
 
 pytestmark = pytest.mark.gpu
@@ -94,3 +95,55 @@ def test_inexact_range_index_takes_the_cpu_plan(ctx):
         ctx.execute(parse_sql("SELECT COUNT(*) FROM t WHERE r BETWEEN 100 AND 700"), [seg])
     r = ctx.execute(parse_sql("SELECT COUNT(*) FROM t WHERE r IN (3, 5, 9)"), [seg])
     assert r.stats.num_entries_scanned_in_filter == 20_000
+
+
+SLICE_SQL = [
+    "SELECT COUNT(*), SUM(m) FROM t WHERE k BETWEEN 0 AND 1022",        # skewed: array containers
+    "SELECT COUNT(*), MIN(m) FROM t WHERE k = 1023",
+    "SELECT COUNT(*), MAX(m) FROM t WHERE k < 7",
+    "SELECT COUNT(*), SUM(m) FROM t WHERE q BETWEEN 1000 AND 30000",   # nearly sorted: run containers
+    "SELECT COUNT(*) FROM t WHERE q >= 49000",
+    "SELECT g, COUNT(*), SUM(m) FROM t WHERE q < 20000 AND k > 100 GROUP BY g ORDER BY g LIMIT 100",
+    "SELECT g, MAX(m) FROM t WHERE r BETWEEN 0 AND 999 GROUP BY g ORDER BY g LIMIT 100",  # the whole dictionary
+    "SELECT COUNT(*) FROM t WHERE r BETWEEN 500 AND 500 OR q < 100",
+]
+
+
+def _slice_cols(n, seed):
+    rng = np.random.default_rng(seed)
+    c = _cols(n, seed)
+    k = np.full(n, 1023, np.int32)
+    k[rng.integers(0, n, n // 200)] = rng.integers(0, 1023, n // 200)
+    q = np.sort(rng.integers(0, 50_000, n)).astype(np.int32)
+    sw = rng.integers(0, n - 1, 50)
+    q[sw], q[sw + 1] = q[sw + 1].copy(), q[sw].copy()  # not sorted: no sorted-index leaf
+    c["k"], c["q"] = (k, "INT"), (q, "INT")
+    return c
+
+
+@pytest.mark.parametrize("n", [131_072, 200_003, 40_000])
+def test_slice_containers_every_kind(ctx, n):
+    t = _slice_cols(n, n)
+    seg = ctx.pin(create_segment("sl", t, range_index=("r", "k", "q")))
+    ora = O.build_segment("sl", t, range_index=("r", "k", "q"))
+    for sql in SLICE_SQL:
+        _check(ctx, [seg], [ora], sql, None)
+
+
+def test_leaf_reads_the_slices(ctx):
+    # the index says A's r, the forward index holds B's r (same dictionary): a range-index leaf must follow the
+    # index (the reference never reads the forward index for it), a scan leaf (IN) the forward index
+    a, b = _cols(100_000, 21), _cols(100_000, 22)
+    assert np.array_equal(np.unique(a["r"][0]), np.unique(b["r"][0]))
+    buf = create_segment("mix", b, range_index=("r",))
+    ids_a = np.searchsorted(buf.columns["r"].dictionary_values, a["r"][0])
+    buf.columns["r"].range_index = range_index_bytes(ids_a, len(buf.columns["r"].dictionary_values) - 1)
+    seg = ctx.pin(buf)
+    for lo, hi in [(100, 700), (0, 17), (950, 999), (17, 17)]:
+        q = parse_sql(f"SELECT COUNT(*) FROM t WHERE r BETWEEN {lo} AND {hi}")
+        r = ctx.execute(q, [seg])
+        got = reduce_groups(q, r.keys, r.aggs).rows[0][0]
+        assert got == int(((a["r"][0] >= lo) & (a["r"][0] <= hi)).sum()), (lo, hi)
+    q = parse_sql("SELECT COUNT(*) FROM t WHERE r IN (3, 5, 9)")
+    r = ctx.execute(q, [seg])
+    assert reduce_groups(q, r.keys, r.aggs).rows[0][0] == int(np.isin(b["r"][0], [3, 5, 9]).sum())
