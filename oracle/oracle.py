@@ -996,7 +996,7 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1, filter_s
             LIB.or_execute(ctypes.byref(qs), one, 1, 1, ctypes.byref(res))
             keep_rows = None
             if trim_size is not None and res.num_groups > trim_size:
-                keep_rows = _segment_trim(res, q, segments[si], unions, nagg, trim_size)
+                keep_rows = _segment_trim(res, q, segments[si], unions, nagg, trim_size, hll_idx, log2m)
             _merge(res, q, merged_keys, merged, key_list, nagg, hll_idx, m, keep_rows)
             stats[0] += res.num_docs_scanned
             stats[1] += extra_entries[si]
@@ -1131,11 +1131,16 @@ def _java_compare(a, b) -> int:
     return (a > b) - (a < b)
 
 
-def _segment_trim(res, q, seg: OracleSegment, unions, nagg, size):
+def _segment_trim(res, q, seg: OracleSegment, unions, nagg, size, hll_idx=(), log2m=8):
     """TableResizer.trimInSegmentResults (TableResizer.java:321-343, makeHeap / downHeap :233-262) over one segment's
     groups fed in ArrayBasedHolder order (ascending raw key over the segment's dictIds, column 0 least significant,
-    DictionaryBasedGroupKeyGenerator.java:254-377).  Returns the indices of the kept rows of `res`."""
+    DictionaryBasedGroupKeyGenerator.java:254-377).  An aggregation's order-by value is its extractFinalResult
+    (TableResizer.AggregationFunctionExtractor :425-447): a DISTINCTCOUNTHLL orders by HyperLogLog.cardinality()
+    (a long).  Returns the indices of the kept rows of `res`."""
     n = res.num_groups
+    m = 1 << log2m
+    hll = (np.ctypeslib.as_array(res.hll, (n * len(hll_idx) * m,)).reshape(n, len(hll_idx), m)
+           if hll_idx and n else None)
     gkeys = np.ctypeslib.as_array(res.keys, (n,))
     aggs = np.ctypeslib.as_array(res.aggs, (n * max(nagg, 1),)).reshape(n, max(nagg, 1))
     recs = []
@@ -1152,7 +1157,11 @@ def _segment_trim(res, q, seg: OracleSegment, unions, nagg, size):
         for o in q.order_by:
             if o.kind == "aggregation":
                 f = q.aggregations[o.ref].function
-                ob.append(int(aggs[g, o.ref]) if f == "COUNT" else float(aggs[g, o.ref]))
+                if f == "DISTINCTCOUNTHLL":
+                    reg = np.ascontiguousarray(hll[g, list(hll_idx).index(o.ref)])
+                    ob.append(int(LIB.or_hll_cardinality(reg.ctypes.data, log2m)))
+                else:
+                    ob.append(int(aggs[g, o.ref]) if f == "COUNT" else float(aggs[g, o.ref]))
             else:
                 ob.append(vals[q.group_by.index(o.ref)])
         recs.append((raw, g, ob))

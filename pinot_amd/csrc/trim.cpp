@@ -30,6 +30,26 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
 
 namespace {
 
+// clearspring HyperLogLog.cardinality() (stream 2.7.0; DistinctCountHLLAggregationFunction.extractFinalResult
+// :362-364) over 1-byte registers: alpha_m m^2 / sum 2^-r, linear counting m ln(m / zeros) at or below 5m/2, Java
+// Math.round (an empty register set's ln(inf) rounds to Long.MAX_VALUE)
+int64_t hll_cardinality(const uint8_t* reg, int log2m) {
+  const int64_t m = (int64_t)1 << log2m;
+  double sum = 0, zeros = 0;
+  for (int64_t j = 0; j < m; ++j) {
+    sum += 1.0 / (double)(1LL << reg[j]);
+    if (reg[j] == 0) zeros += 1;
+  }
+  const double mm = (double)m * (double)m;
+  const double alpha_mm = log2m == 4 ? 0.673 * mm : log2m == 5 ? 0.697 * mm : log2m == 6 ? 0.709 * mm
+                                                                                 : (0.7213 / (1 + 1.079 / m)) * mm;
+  const double est = alpha_mm * (1 / sum);
+  const double x = est <= 2.5 * (double)m ? (double)m * std::log((double)m / zeros) : est;
+  if (std::isnan(x)) return 0;
+  if (x >= 9.2233720368547758e18) return INT64_MAX;
+  return (int64_t)std::floor(x + 0.5);
+}
+
 // Java's Double.compare / Float.compare order (NaN largest, -0.0 < 0.0): the natural order of the boxed values
 int java_double_compare(double a, double b) {
   if (a < b) return -1;
@@ -79,6 +99,7 @@ struct Row {
   std::vector<double> d;    // per aggregation: SUM/MIN/MAX value (COUNT in c)
   std::vector<int64_t> c;   // per aggregation: COUNT
   std::vector<std::vector<uint8_t>> hll;
+  std::vector<int64_t> hc;  // per aggregation: a DISTINCTCOUNTHLL order-by value (its cardinality), set for the trim
   uint64_t raw = 0;         // ArrayBasedHolder raw key over the segment's dictIds
 };
 
@@ -247,8 +268,6 @@ ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* con
     const ph_order_by& o = q->order_by[k];
     if (o.kind == PH_ORDER_AGGREGATION) {
       if (o.index < 0 || o.index >= na) fail(PH_ERR_BAD_QUERY, "ORDER BY aggregation index");
-      if (q->aggregations[o.index].type == PH_AGG_DISTINCTCOUNTHLL)
-        fail(PH_ERR_UNSUPPORTED, "segment group trim ordered by DISTINCTCOUNTHLL");
     } else if (o.index < 0 || o.index >= ng) {
       fail(PH_ERR_BAD_QUERY, "ORDER BY group-by index");
     }
@@ -263,6 +282,17 @@ ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* con
     vm.note(*r);
     std::vector<Row> rows = vm.rows(*r, segs[s]);
     if ((int64_t)rows.size() > trim) {
+      // an aggregation orders by its extractFinalResult (TableResizer.AggregationFunctionExtractor :425-447): a
+      // DISTINCTCOUNTHLL by HyperLogLog.cardinality(), a long -- computed once per row
+      for (int k = 0; k < q->num_order_by; ++k) {
+        const ph_order_by& o = q->order_by[k];
+        if (o.kind != PH_ORDER_AGGREGATION || r->agg_types[o.index] != PH_AGG_DISTINCTCOUNTHLL) continue;
+        const int log2m = q->aggregations[o.index].log2m > 0 ? q->aggregations[o.index].log2m : 8;
+        for (auto& row : rows) {
+          row.hc.resize((size_t)na, 0);
+          row.hc[o.index] = hll_cardinality(row.hll[o.index].data(), log2m);
+        }
+      }
       // TableResizer: the intermediate-record comparator over the ORDER BY values, reversed for the heap
       auto cmp_inter = [&](const Row& a, const Row& b) -> int {
         for (int k = 0; k < q->num_order_by; ++k) {
@@ -271,6 +301,7 @@ ph_result* segment_trim_execute(Context* ctx, const ph_query* q, ph_segment* con
           if (o.kind == PH_ORDER_AGGREGATION) {
             const int j = o.index;
             if (r->agg_types[j] == PH_AGG_COUNT) c = a.c[j] < b.c[j] ? -1 : (a.c[j] > b.c[j] ? 1 : 0);
+            else if (r->agg_types[j] == PH_AGG_DISTINCTCOUNTHLL) c = a.hc[j] < b.hc[j] ? -1 : (a.hc[j] > b.hc[j] ? 1 : 0);
             else c = java_double_compare(a.d[j], b.d[j]);
           } else {
             const uint8_t* pa = reinterpret_cast<const uint8_t*>(a.kv[o.index].data());

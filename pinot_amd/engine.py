@@ -94,15 +94,11 @@ def check_plan_supported(q: QueryContext):
 
     * Segment group trim (GroupByOperator.java:114-130, ORDER BY + ``minSegmentGroupTrimSize`` > 0) runs in the
       library (ph_query.min_segment_group_trim_size): per-segment tables, TableResizer.trimInSegmentResults' heap,
-      then the combine.  An ORDER BY over DISTINCTCOUNTHLL is the one trim shape it leaves to the CPU plan.
+      then the combine (an ORDER BY over DISTINCTCOUNTHLL orders by each group's HyperLogLog.cardinality()).
     * Server trim (IndexedTable.java:63-91, resize when the table exceeds ``groupTrimThreshold``) needs no gate:
       its finish keeps the top records by the same ORDER BY, so the broker's final ORDER BY ... LIMIT over the
       GPU's exact (untrimmed) groups is the same result whenever the reference's own merge is exact."""
-    seg_trim = int(q.options.get("minSegmentGroupTrimSize", -1))
-    if q.group_by and q.order_by and seg_trim > 0:
-        for ob in q.order_by:
-            if ob.kind == "aggregation" and q.aggregations[ob.ref].function == DISTINCTCOUNTHLL:
-                raise N.UnsupportedError(N.PH_ERR_UNSUPPORTED, "segment group trim ordered by DISTINCTCOUNTHLL")
+
 
 
 class _QueryStruct:

@@ -194,6 +194,40 @@ def range_index_bytes(values: np.ndarray, max_value: int, min_value: int = 0) ->
     return np.concatenate([range_index_header(min_value), np.frombuffer(body, np.uint8)])
 
 
+def legacy_range_index_bytes(ids: np.ndarray, num_ranges: int = 20) -> tuple:
+    """A legacy version-1 range index over dictIds as RangeIndexCreator.seal lays it out (RangeIndexCreator.java:
+    283-380): ranges of about ceil(n / num_ranges) sorted values that never split a value, then int32 BE version 1,
+    the type name "INT", the range count, the ranges' first values + the last range's end, (R + 1) int64 BE absolute
+    offsets and each range's doc bitmap (portable roaring).  -> (bytes, starts + [last end]) -- the second for the
+    oracle."""
+    ids = np.asarray(ids, np.int64)
+    n = int(ids.size)
+    order = np.argsort(ids, kind="stable")
+    sv = ids[order]
+    per = (n + num_ranges - 1) // num_ranges
+    change = np.flatnonzero(sv[1:] != sv[:-1]) + 1  # i with sv[i] != sv[i - 1]
+    ranges, start = [], 0
+    while True:
+        j = int(np.searchsorted(change, start + per, side="right"))  # first change i > start + per
+        if j >= change.size:
+            break
+        i = int(change[j])
+        ranges.append((start, i - 1))
+        start = i
+    ranges.append((start, n - 1))
+    bitmaps = [roaring_serialize(np.sort(order[a:b + 1]).astype(np.uint32)) for a, b in ranges]
+    R = len(ranges)
+    head = struct.pack(">ii", 1, 3) + b"INT" + struct.pack(">i", R)
+    head += np.array([sv[a] for a, _ in ranges] + [sv[-1]], ">i4").tobytes()
+    off = len(head) + 8 * (R + 1)
+    offs = [off]
+    for bm in bitmaps:
+        off += len(bm)
+        offs.append(off)
+    blob = head + np.array(offs, ">i8").tobytes() + b"".join(bitmaps)
+    return np.frombuffer(blob, np.uint8).copy(), np.array([sv[a] for a, _ in ranges] + [sv[-1]], np.int64)
+
+
 @dataclass
 class SegmentBuffers:
     name: str

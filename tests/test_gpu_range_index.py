@@ -80,21 +80,38 @@ def test_range_index_from_directories(ctx, tmp_path, layout):
         _check(ctx, [seg], [ora], sql, entries)
 
 
-def test_inexact_range_index_takes_the_cpu_plan(ctx):
-    # a legacy version-1 range index (ranges + a partial scan of the boundary ranges) is still a
-    # RangeIndexBasedFilterOperator leaf in the reference (RangeIndexBasedFilterOperator.java:59-60), whose entries
-    # the GPU statistics do not model: its RANGE / EQ leaves are PH_ERR_UNSUPPORTED (the plan maker's CPU fallback);
-    # other predicates on the column still run on the GPU
-    from pinot_amd import native as N
-    buf = create_segment("riv1", _cols(20_000, 9), range_index=("r",))
-    hdr = buf.columns["r"].range_index.copy()
-    hdr[:4] = np.frombuffer(np.array([1], ">i4").tobytes(), np.uint8)  # version 1
-    buf.columns["r"].range_index = hdr
-    seg = ctx.pin(buf)
-    with pytest.raises(N.UnsupportedError):
-        ctx.execute(parse_sql("SELECT COUNT(*) FROM t WHERE r BETWEEN 100 AND 700"), [seg])
-    r = ctx.execute(parse_sql("SELECT COUNT(*) FROM t WHERE r IN (3, 5, 9)"), [seg])
-    assert r.stats.num_entries_scanned_in_filter == 20_000
+LEGACY_SQL = [
+    ("SELECT COUNT(*), SUM(m) FROM t WHERE r BETWEEN 100 AND 700", None),
+    ("SELECT COUNT(*) FROM t WHERE r > 950", None),                      # upper bound past every range
+    ("SELECT COUNT(*), MAX(m) FROM t WHERE r BETWEEN 3 AND 5", None),     # both bounds in one range
+    ("SELECT COUNT(*), MIN(m) FROM t WHERE r = 17", None),                # EQ: an inexact index cannot (scan)
+    ("SELECT COUNT(*) FROM t WHERE r > 100 AND r < 300", None),          # merged into one RANGE, planned once
+    ("SELECT g, COUNT(*), SUM(m) FROM t WHERE r < 400 AND f < 300 GROUP BY g ORDER BY g LIMIT 100", None),
+    ("SELECT COUNT(*), SUM(m) FROM t WHERE r < 100 OR f BETWEEN 10 AND 20", None),
+    ("SELECT COUNT(*) FROM t WHERE NOT r BETWEEN 200 AND 800", None),
+]
+
+
+@pytest.mark.parametrize("nr", [20, 7])
+def test_legacy_range_index(ctx, nr):
+    # a legacy version-1 range index (RangeIndexReaderImpl, inexact): RANGE leaves are index-based with the exact
+    # doc set, and scan the docs of their boundary ranges (RangeIndexBasedFilterOperator.evaluateLegacyRangeFilter
+    # :82-107) -- numEntriesScannedInFilter checked against the oracle's restatement of the reader
+    from pinot_amd.segment import legacy_range_index_bytes
+    tables = [_cols(60_000, 31), _cols(45_001, 32)]
+    segs, osegs = [], []
+    for i, t in enumerate(tables):
+        buf = create_segment(f"lg{i}", t)
+        ids = np.searchsorted(buf.columns["r"].dictionary_values, t["r"][0])
+        blob, ranges = legacy_range_index_bytes(ids, nr)
+        buf.columns["r"].range_index = blob
+        segs.append(ctx.pin(buf))
+        osegs.append(O.build_segment(f"lg{i}", t, legacy_ranges={"r": ranges}))
+    for sql, entries in LEGACY_SQL:
+        _check(ctx, segs, osegs, sql, entries)
+    q = parse_sql("SELECT COUNT(*) FROM t WHERE r BETWEEN 100 AND 700")
+    r = ctx.execute(q, segs)
+    assert 0 < r.stats.num_entries_scanned_in_filter < sum(len(t["r"][0]) for t in tables)
 
 
 SLICE_SQL = [

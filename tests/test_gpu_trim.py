@@ -43,6 +43,11 @@ SMALL = [  # a x b = 50 x 40 groups: ArrayBasedHolder
     "SET minSegmentGroupTrimSize=25; SELECT a, b, MAX(m), MIN(d) FROM t GROUP BY a, b ORDER BY b DESC, a LIMIT 3",
     "SET minSegmentGroupTrimSize=30; SELECT a, COUNT(*), SUM(d) FROM t GROUP BY a ORDER BY COUNT(*), a DESC LIMIT 6",
     "SET minSegmentGroupTrimSize=100000; SELECT a, b, COUNT(*) FROM t GROUP BY a, b ORDER BY COUNT(*) DESC LIMIT 5",
+    # extractFinalResult order (TableResizer.java:425-447): HyperLogLog.cardinality() of each group's registers
+    "SET minSegmentGroupTrimSize=30; SELECT a, b, DISTINCTCOUNTHLL(m), COUNT(*) FROM t GROUP BY a, b "
+    "ORDER BY DISTINCTCOUNTHLL(m) DESC, a LIMIT 5",
+    "SET minSegmentGroupTrimSize=20; SELECT a, DISTINCTCOUNTHLL(f, 6), SUM(m) FROM t GROUP BY a "
+    "ORDER BY DISTINCTCOUNTHLL(f, 6), a DESC LIMIT 4",
 ]
 
 

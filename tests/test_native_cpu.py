@@ -149,15 +149,13 @@ def test_expression_result_column_names():
 
 def test_segment_group_trim_gate():
     # minSegmentGroupTrimSize > 0 with ORDER BY runs on the GPU path (per-segment tables + the TableResizer heap,
-    # trim.cpp); only an ORDER BY over DISTINCTCOUNTHLL declines (UNSUPPORTED -> CPU plan)
+    # trim.cpp), an ORDER BY over DISTINCTCOUNTHLL included (by each group's HyperLogLog.cardinality())
     from pinot_amd.engine import check_plan_supported
-    from pinot_amd.native import UnsupportedError
     from pinot_amd.query import parse_sql
     base = "SELECT a, SUM(m) FROM t GROUP BY a"
     check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=100; " + base + " ORDER BY SUM(m) DESC LIMIT 5"))
-    with pytest.raises(UnsupportedError):
-        check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=100; SELECT a, DISTINCTCOUNTHLL(m) FROM t "
-                                       "GROUP BY a ORDER BY DISTINCTCOUNTHLL(m) DESC LIMIT 5"))
+    check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=100; SELECT a, DISTINCTCOUNTHLL(m) FROM t "
+                                   "GROUP BY a ORDER BY DISTINCTCOUNTHLL(m) DESC LIMIT 5"))
     check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=-1; " + base + " ORDER BY SUM(m) DESC LIMIT 5"))
     check_plan_supported(parse_sql("SET minSegmentGroupTrimSize=100; " + base + " LIMIT 5"))
     check_plan_supported(parse_sql(base + " ORDER BY a LIMIT 5"))
