@@ -2075,19 +2075,18 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       dsegs[limit_segs[t]].first_doc = limit_first + t * (size_t)G;
     }
     limit_scal = scratch.alloc<unsigned long long>(3 * limit_segs.size());
-    PH_HIP_CHECK(hipMemsetAsync(limit_scal, 0, 24 * limit_segs.size(), st));
+    if (!limit_segs.empty()) PH_HIP_CHECK(hipMemsetAsync(limit_scal, 0, 24 * limit_segs.size(), st));
     if (!limit_segs.empty()) kp.late_prefetch = 1;
   }
-  if (q->num_group_by > 0) {
-    kp.matched_total = scratch.alloc<unsigned long long>(1);
-    PH_HIP_CHECK(hipMemsetAsync(kp.matched_total, 0, 8, st));
-  }
   {
+    // the matched-doc total and the applyAnd entry count: one zeroed 16-byte block (one fill, not two)
     bool apply_and = false;
     for (size_t i = 0; i < progs.size(); ++i) apply_and |= seg_live[i] && progs[i].apply_and;
-    if (apply_and) {
-      kp.filter_entries = scratch.alloc<unsigned long long>(1);
-      PH_HIP_CHECK(hipMemsetAsync(kp.filter_entries, 0, 8, st));
+    if (q->num_group_by > 0 || apply_and) {
+      unsigned long long* sc = scratch.alloc<unsigned long long>(2);
+      PH_HIP_CHECK(hipMemsetAsync(sc, 0, 16, st));
+      if (q->num_group_by > 0) kp.matched_total = sc;
+      if (apply_and) kp.filter_entries = sc + 1;
     }
   }
   // per-segment tile pieces: the 1 KiB wave-loads of a full tile, stream by stream

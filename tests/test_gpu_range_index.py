@@ -164,3 +164,20 @@ def test_leaf_reads_the_slices(ctx):
     q = parse_sql("SELECT COUNT(*) FROM t WHERE r IN (3, 5, 9)")
     r = ctx.execute(q, [seg])
     assert reduce_groups(q, r.keys, r.aggs).rows[0][0] == int(np.isin(b["r"][0], [3, 5, 9]).sum())
+
+
+def test_slices_full_segment(ctx):
+    # one 10M-doc segment, cardinality 2^20 (20 slices, 153 keys, a ragged last key): the leaf's count and SUM equal
+    # the dictId interval's, for bounds on both sides of every power-of-two boundary tried
+    rng = np.random.default_rng(77)
+    n = 10_000_000
+    r = rng.integers(0, 1 << 20, n).astype(np.int32)
+    r[:1 << 20] = np.arange(1 << 20)  # every value present: dictIds == values
+    m = rng.integers(0, 1000, n).astype(np.int32)
+    seg = ctx.pin(create_segment("big", {"r": (r, "INT"), "m": (m, "INT")}, range_index=("r",)))
+    for lo, hi in [(0, (1 << 19) - 1), (1 << 19, (1 << 20) - 2), (12345, 987654), (65535, 65536), (777, 777)]:
+        q = parse_sql(f"SELECT COUNT(*), SUM(m) FROM t WHERE r BETWEEN {lo} AND {hi}")
+        res = ctx.execute(q, [seg])
+        sel = (r >= lo) & (r <= hi)
+        assert reduce_groups(q, res.keys, res.aggs).rows[0] == [int(sel.sum()), float(m[sel].sum())], (lo, hi)
+        assert res.stats.num_entries_scanned_in_filter == 0
