@@ -41,7 +41,7 @@ def main():
         tot[1] += r.stats.device_ms
         tot[2] += r.stats.host_ms
         print(f"{name:6s} wall {wall:7.3f}  device {r.stats.device_ms:7.3f}  host {r.stats.host_ms:7.3f}  "
-              f"mode {r.stats.plan_mode}", flush=True)
+              f"mode {r.stats.mode}", flush=True)
     print(f"flight wall {tot[0]:.3f} device {tot[1]:.3f} host {tot[2]:.3f}", flush=True)
     if os.environ.get("STAMPS"):
         os.environ["PH_HOST_TIMES"] = "1"
