@@ -6,10 +6,13 @@
 //   state = c_i ? (state | Z_i) : (state & Z_i),   state_0 = all docs
 // (O'Neil & Quass's range evaluation over a bit-sliced index).  lo <= v <= hi is lte(hi) AND NOT lte(lo - 1).
 //
-// One workgroup per (key, leaf): thread t owns the key's 32-bit words t + 256 j (j < 8) and keeps both running states
-// in registers; each slice's container is expanded to its eight words -- a bitmap container read straight from HBM,
-// an array / run container scattered into an 8 KB LDS bitmap first.  Bytes: the leaf's containers once, the bitmap
-// written once (HBM-bound; tiny against the queries that read it).
+// One workgroup per (eighth of a key, leaf): thread t owns the part's 32-bit word t and keeps both running states in
+// registers.  The key's (container offset, kind, size) per slice are staged in LDS first (one dependent load chain
+// per workgroup, not one per slice); a bitmap container's word is read with two aligned dword loads and a funnel
+// shift (containers start at any byte), the words of the next kBatch bitmap slices all in flight before the batch
+// composes; an array / run container is scattered into a 1 KB LDS bitmap of the part.  Bytes: the leaf's containers
+// once, the doc bitmap written once -- HBM-bound (r5: 4 parts with one slice of look-ahead 215 us on a 10M-doc,
+// 20-slice segment; one part per key with no look-ahead 530 us).
 #include "ph_internal.h"
 
 namespace ph {
@@ -17,86 +20,105 @@ namespace ph {
 namespace {
 constexpr int kRbBitmap = 0, kRbRun = 1, kRbArray = 2;  // RangeBitmap container kinds
 constexpr int kKeyWords = 2048;                          // 32-bit words of a 65536-doc key
-constexpr int kPerThread = kKeyWords / 256;
+constexpr int kParts = 8;                                // workgroups per key
+constexpr int kPartWords = kKeyWords / kParts;           // 256: one per thread
+constexpr int kBatch = 8;                                // bitmap slices whose words are loaded together
+constexpr int kMaxSlices = 64;
 
 __device__ inline uint32_t ld_u16(const uint8_t* p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8; }
-__device__ inline uint32_t ld_u32(const uint8_t* p) {
-  return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+
+// the 32-bit little-endian word at byte address p (any alignment) from two aligned dword loads; the payload buffer
+// carries 16 bytes of padding, so the second load never leaves the allocation
+__device__ inline uint32_t ld_u32_any(const uint8_t* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3) * 8;
+  const uint32_t lo = w[0], hi = w[1];
+  return sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
 }
 }  // namespace
 
 __global__ void __launch_bounds__(256) k_range_slices(const RangeSliceLeaf* __restrict__ leaves) {
-  __shared__ uint32_t z[kKeyWords];
+  __shared__ uint32_t z[kPartWords];
+  __shared__ int32_t s_off[kMaxSlices];
+  __shared__ int32_t s_kind[kMaxSlices];
+  __shared__ int32_t s_size[kMaxSlices];
   const RangeSliceLeaf L = leaves[blockIdx.y];
-  const int key = blockIdx.x, t = threadIdx.x;
-  const int64_t w0 = (int64_t)key * kKeyWords;
+  const int key = blockIdx.x / kParts, part = blockIdx.x % kParts, t = threadIdx.x;
+  const int64_t w0 = (int64_t)key * kKeyWords + part * kPartWords;  // this workgroup's first bitmap word
   if (w0 >= L.padded_words) return;  // uniform over the workgroup
-  uint32_t le_hi[kPerThread], le_lo[kPerThread];
+  const uint32_t d_lo = (uint32_t)part * kPartWords * 32, d_hi = d_lo + kPartWords * 32;  // docs of the part
+  uint32_t le_hi = ~0u, le_lo = ~0u;
+  const int S = key < L.nkeys ? L.nslices : 0;
+  if (t < S) {
+    const int32_t off = L.dir[(int64_t)key * L.nslices + t];
+    s_off[t] = off;
+    s_kind[t] = off >= 0 ? (int32_t)L.payload[off] : -1;
+    s_size[t] = off >= 0 ? (int32_t)ld_u16(L.payload + off + 1) : 0;
+  }
+  __syncthreads();
+  for (int i0 = 0; i0 < S; i0 += kBatch) {
+    // straight-line loads (no branch per slice): a slice without a bitmap container reads the payload's first
+    // bytes and discards them; kinds and offsets are wave-uniform (readfirstlane: scalar branches below)
+    uint32_t bw[kBatch];
+    bool isbm[kBatch];
 #pragma unroll
-  for (int j = 0; j < kPerThread; ++j) le_hi[j] = le_lo[j] = ~0u;
-  if (key < L.nkeys) {
-    for (int i = 0; i < L.nslices; ++i) {
-      const int32_t off = L.dir[(int64_t)key * L.nslices + i];
-      uint32_t zw[kPerThread];
+    for (int b = 0; b < kBatch; ++b) {
+      const int i = min(i0 + b, S - 1);
+      isbm[b] = i0 + b < S && __builtin_amdgcn_readfirstlane(s_kind[i]) == kRbBitmap;
+      const int32_t off = isbm[b] ? __builtin_amdgcn_readfirstlane(s_off[i]) + 3 + 4 * part * kPartWords : 0;
+      bw[b] = ld_u32_any(L.payload + off + 4 * t);
+    }
 #pragma unroll
-      for (int j = 0; j < kPerThread; ++j) zw[j] = 0;  // no container: no doc of the key has bit i clear
-      if (off >= 0) {
-        const uint8_t* c = L.payload + off;
-        const int type = c[0];
-        const uint32_t size = ld_u16(c + 1);
-        const uint8_t* p = c + 3;
-        if (type == kRbBitmap) {
-#pragma unroll
-          for (int j = 0; j < kPerThread; ++j) zw[j] = ld_u32(p + 4 * (t + 256 * j));
+    for (int b = 0; b < kBatch; ++b) {
+      const int i = i0 + b;
+      if (i >= S) break;
+      if (!isbm[b]) bw[b] = 0;
+      const int kind = __builtin_amdgcn_readfirstlane(s_kind[i]);
+      uint32_t zw = bw[b];  // a bitmap container's word; none: no doc of the key has bit i clear
+      if (kind == kRbArray || kind == kRbRun) {
+        z[t] = 0;
+        __syncthreads();
+        const uint8_t* p = L.payload + s_off[i] + 3;
+        const uint32_t size = (uint32_t)s_size[i];
+        if (kind == kRbArray) {
+          for (uint32_t k = t; k < size; k += 256) {
+            const uint32_t r = ld_u16(p + 2 * k);
+            if (r >= d_lo && r < d_hi) atomicOr(&z[(r - d_lo) >> 5], 1u << (r & 31));
+          }
         } else {
-#pragma unroll
-          for (int j = 0; j < kPerThread; ++j) z[t + 256 * j] = 0;
-          __syncthreads();
-          if (type == kRbArray) {
-            for (uint32_t k = t; k < size; k += 256) {
-              const uint32_t r = ld_u16(p + 2 * k);
-              atomicOr(&z[r >> 5], 1u << (r & 31));
-            }
-          } else if (type == kRbRun) {
-            for (uint32_t k = t; k < size; k += 256) {
-              const uint32_t s = ld_u16(p + 4 * k);
-              const uint32_t e = min(65536u, s + ld_u16(p + 4 * k + 2) + 1);  // [s, e)
-              uint32_t d = s;
-              while (d < e) {
-                const uint32_t w = d >> 5, b = d & 31, n = min(32u - b, e - d);
-                atomicOr(&z[w], (n == 32 ? ~0u : ((1u << n) - 1)) << b);
-                d += n;
-              }
+          for (uint32_t k = t; k < size; k += 256) {
+            const uint32_t r0 = ld_u16(p + 4 * k);
+            const uint32_t rs = max(r0, d_lo), re = min(d_hi, min(65536u, r0 + ld_u16(p + 4 * k + 2) + 1));
+            uint32_t d = rs;  // [rs, re)
+            while (d < re) {
+              const uint32_t w = (d - d_lo) >> 5, bit = d & 31, n = min(32u - bit, re - d);
+              atomicOr(&z[w], (n == 32 ? ~0u : ((1u << n) - 1)) << bit);
+              d += n;
             }
           }
-          __syncthreads();
-#pragma unroll
-          for (int j = 0; j < kPerThread; ++j) zw[j] = z[t + 256 * j];
-          // the next slice's zeroing touches only this thread's own words, read just above; the other threads'
-          // scatters into them wait behind that slice's first barrier
         }
+        __syncthreads();
+        zw = z[t];
+        // the next such slice's zeroing touches only this thread's own word, read just above; the other threads'
+        // scatters into it wait behind that slice's first barrier
       }
-      const bool hb = (L.hi >> i) & 1, lb = (L.lo_m1 >> i) & 1;
-#pragma unroll
-      for (int j = 0; j < kPerThread; ++j) {
-        le_hi[j] = hb ? (le_hi[j] | zw[j]) : (le_hi[j] & zw[j]);
-        le_lo[j] = lb ? (le_lo[j] | zw[j]) : (le_lo[j] & zw[j]);
-      }
+      le_hi = ((L.hi >> i) & 1) ? (le_hi | zw) : (le_hi & zw);
+      le_lo = ((L.lo_m1 >> i) & 1) ? (le_lo | zw) : (le_lo & zw);
     }
   }
-#pragma unroll
-  for (int j = 0; j < kPerThread; ++j) {
-    const int64_t gw = w0 + t + 256 * j;
-    if (gw >= L.padded_words) continue;
+  const int64_t gw = w0 + t;
+  if (gw < L.padded_words) {
     const int64_t rem = (int64_t)L.num_docs - 32 * gw;
     const uint32_t live = rem >= 32 ? ~0u : (rem <= 0 ? 0u : ((1u << rem) - 1));
-    L.bitmap[gw] = le_hi[j] & (L.use_lo ? ~le_lo[j] : ~0u) & live;
+    L.bitmap[gw] = le_hi & (L.use_lo ? ~le_lo : ~0u) & live;
   }
 }
 
 void launch_range_slices(const RangeSliceLeaf* leaves, int nleaves, int max_chunks, hipStream_t s) {
   if (nleaves <= 0 || max_chunks <= 0) return;
-  hipLaunchKernelGGL(k_range_slices, dim3((unsigned)max_chunks, (unsigned)nleaves), dim3(256), 0, s, leaves);
+  hipLaunchKernelGGL(k_range_slices, dim3((unsigned)(max_chunks * kParts), (unsigned)nleaves), dim3(256), 0, s,
+                     leaves);
 }
 
 }  // namespace ph

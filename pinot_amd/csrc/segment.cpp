@@ -608,7 +608,7 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
       range_dir = parse_range_bitmap(ri, d.range_index_size, n, &col->range_nkeys, &col->range_nslices);
       if (card > 0 && (uint64_t)(card - 1) >> (col->range_nslices - 1) >> 1)
         fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": range index slices narrower than the dictionary");
-      col->d_range.alloc(d.range_index_size, ctx->device);
+      col->d_range.alloc(d.range_index_size + 16, ctx->device);  // + the padding k_range_slices' paired loads read
       PH_HIP_CHECK(hipMemcpyAsync(col->d_range.ptr, ri, d.range_index_size, hipMemcpyHostToDevice, st));
       col->d_range_dir.alloc(sizeof(int32_t) * std::max<size_t>(1, range_dir.size()), ctx->device);
       if (!range_dir.empty())
