@@ -10,9 +10,10 @@
 // registers.  The key's (container offset, kind, size) per slice are staged in LDS first (one dependent load chain
 // per workgroup, not one per slice); a bitmap container's word is read with two aligned dword loads and a funnel
 // shift (containers start at any byte), the words of the next kBatch bitmap slices all in flight before the batch
-// composes; an array / run container is scattered into a 1 KB LDS bitmap of the part.  Bytes: the leaf's containers
-// once, the doc bitmap written once -- HBM-bound (r5: 4 parts with one slice of look-ahead 215 us on a 10M-doc,
-// 20-slice segment; one part per key with no look-ahead 530 us).
+// composes; an array / run container's u16 payload is staged in LDS and each thread binary-searches its 32 docs.  Bytes: the leaf's containers
+// once, the doc bitmap written once -- HBM-bound.  r5 on a 10M-doc, 20-slice segment (23.2 MB of containers):
+// one workgroup per key 530 us; 4 parts, one slice of look-ahead 215 us; 8 parts, batched loads 128 us (its runs
+// expanded serially per thread with LDS atomics); this form 24 us (~1.0 TB/s; profiles/r5_range_slices_kernel_stats.csv).
 #include "ph_internal.h"
 
 namespace ph {
@@ -24,6 +25,7 @@ constexpr int kParts = 8;                                // workgroups per key
 constexpr int kPartWords = kKeyWords / kParts;           // 256: one per thread
 constexpr int kBatch = 8;                                // bitmap slices whose words are loaded together
 constexpr int kMaxSlices = 64;
+constexpr int kStageU16 = 4096;                          // an array / run container's u16 payload (checked at pin)
 
 __device__ inline uint32_t ld_u16(const uint8_t* p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8; }
 
@@ -39,7 +41,7 @@ __device__ inline uint32_t ld_u32_any(const uint8_t* p) {
 }  // namespace
 
 __global__ void __launch_bounds__(256) k_range_slices(const RangeSliceLeaf* __restrict__ leaves) {
-  __shared__ uint32_t z[kPartWords];
+  __shared__ uint16_t u16s[kStageU16];
   __shared__ int32_t s_off[kMaxSlices];
   __shared__ int32_t s_kind[kMaxSlices];
   __shared__ int32_t s_size[kMaxSlices];
@@ -47,7 +49,7 @@ __global__ void __launch_bounds__(256) k_range_slices(const RangeSliceLeaf* __re
   const int key = blockIdx.x / kParts, part = blockIdx.x % kParts, t = threadIdx.x;
   const int64_t w0 = (int64_t)key * kKeyWords + part * kPartWords;  // this workgroup's first bitmap word
   if (w0 >= L.padded_words) return;  // uniform over the workgroup
-  const uint32_t d_lo = (uint32_t)part * kPartWords * 32, d_hi = d_lo + kPartWords * 32;  // docs of the part
+  const uint32_t d_lo = (uint32_t)part * kPartWords * 32;  // the part's first doc in the key
   uint32_t le_hi = ~0u, le_lo = ~0u;
   const int S = key < L.nkeys ? L.nslices : 0;
   if (t < S) {
@@ -77,31 +79,37 @@ __global__ void __launch_bounds__(256) k_range_slices(const RangeSliceLeaf* __re
       const int kind = __builtin_amdgcn_readfirstlane(s_kind[i]);
       uint32_t zw = bw[b];  // a bitmap container's word; none: no doc of the key has bit i clear
       if (kind == kRbArray || kind == kRbRun) {
-        z[t] = 0;
+        // the container's u16 payload (<= 4096 values / < 2048 run pairs: <= 8 KB) staged in LDS, then each thread
+        // builds its own word by a binary search -- no serial per-run expansion, no atomics
+        const uint8_t* p = L.payload + __builtin_amdgcn_readfirstlane(s_off[i]) + 3;
+        const uint32_t size = (uint32_t)__builtin_amdgcn_readfirstlane(s_size[i]);
+        const uint32_t nv = min(kind == kRbArray ? size : 2 * size, (uint32_t)kStageU16);
+        __syncthreads();  // the previous such slice's searches are done with the stage
+        for (uint32_t k = t; k < nv; k += 256) u16s[k] = (uint16_t)ld_u16(p + 2 * k);
         __syncthreads();
-        const uint8_t* p = L.payload + s_off[i] + 3;
-        const uint32_t size = (uint32_t)s_size[i];
+        const uint32_t a = d_lo + 32 * t;  // this thread's 32 docs [a, a + 32)
+        uint32_t w = 0;
         if (kind == kRbArray) {
-          for (uint32_t k = t; k < size; k += 256) {
-            const uint32_t r = ld_u16(p + 2 * k);
-            if (r >= d_lo && r < d_hi) atomicOr(&z[(r - d_lo) >> 5], 1u << (r & 31));
+          uint32_t lo = 0, hi = nv;  // first value >= a
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (u16s[mid] < a) lo = mid + 1; else hi = mid;
           }
+          for (uint32_t k = lo; k < nv && u16s[k] < a + 32; ++k) w |= 1u << (u16s[k] - a);
         } else {
-          for (uint32_t k = t; k < size; k += 256) {
-            const uint32_t r0 = ld_u16(p + 4 * k);
-            const uint32_t rs = max(r0, d_lo), re = min(d_hi, min(65536u, r0 + ld_u16(p + 4 * k + 2) + 1));
-            uint32_t d = rs;  // [rs, re)
-            while (d < re) {
-              const uint32_t w = (d - d_lo) >> 5, bit = d & 31, n = min(32u - bit, re - d);
-              atomicOr(&z[w], (n == 32 ? ~0u : ((1u << n) - 1)) << bit);
-              d += n;
-            }
+          const uint32_t nr = nv / 2;
+          uint32_t lo = 0, hi = nr;  // first run whose end (start + length) > a
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((uint32_t)u16s[2 * mid] + u16s[2 * mid + 1] + 1 <= a) lo = mid + 1; else hi = mid;
+          }
+          for (uint32_t k = lo; k < nr && u16s[2 * k] < a + 32; ++k) {
+            const uint32_t rs = max((uint32_t)u16s[2 * k], a);
+            const uint32_t re = min((uint32_t)u16s[2 * k] + u16s[2 * k + 1] + 1, a + 32);
+            if (re > rs) w |= (re - rs == 32 ? ~0u : ((1u << (re - rs)) - 1)) << (rs - a);
           }
         }
-        __syncthreads();
-        zw = z[t];
-        // the next such slice's zeroing touches only this thread's own word, read just above; the other threads'
-        // scatters into it wait behind that slice's first barrier
+        zw = w;
       }
       le_hi = ((L.hi >> i) & 1) ? (le_hi | zw) : (le_hi & zw);
       le_lo = ((L.lo_m1 >> i) & 1) ? (le_lo | zw) : (le_lo & zw);

@@ -199,6 +199,8 @@ std::vector<int32_t> parse_range_bitmap(const uint8_t* b, uint64_t size, int64_t
       const uint64_t n = le16(b + at + 1);
       const uint64_t body = kind == 0 ? 8192 : kind == 1 ? 4 * n : kind == 2 ? 2 * n : ~0ull;
       if (body == ~0ull) fail(PH_ERR_INVALID_ARGUMENT, "range index: bad container kind");
+      if ((kind == 2 && n > 4096) || (kind == 1 && n > 2048))  // k_range_slices stages <= 8 KB of u16 payload
+        fail(PH_ERR_UNSUPPORTED, "range index: array / run container larger than a bitmap");
       if (at + 3 + body > size) fail(PH_ERR_INVALID_ARGUMENT, "range index: truncated container");
       dir[(size_t)k * S + i] = (int32_t)at;
       at += 3 + body;
