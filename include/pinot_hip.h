@@ -95,9 +95,12 @@ typedef struct {
    * RoaringBitmap RangeBitmap; V1 file <column>.bitmap.range, V3 index_map key range_index); NULL when the column has
    * none.  A version-2 (exact) index makes RANGE, and EQ on a column without an inverted index, a
    * RangeIndexBasedFilterOperator leaf (FilterOperatorUtils.java:97-120): index-based for the AND order and the
-   * statistics (no entries scanned in filter).  The kernels evaluate such a leaf from the packed dictIds -- the same
-   * doc set as the exact bit-sliced bitmaps, at b bits per doc, which is what reading every bit slice costs too --
-   * so the slices themselves are not read. */
+   * statistics (no entries scanned in filter).  On a dictionary column the RangeBitmap is parsed at pin and such a
+   * leaf's doc bitmap is composed from its bit slices on the device (BitSlicedRangeIndexReader.getMatchingDocIds
+   * :123-211); on a raw column the leaf scans the dictIds the pin encoded (same doc set).  A version-1 index over
+   * dictIds (RangeIndexCreator, type "INT") makes RANGE an index-based leaf whose statistic is its boundary ranges'
+   * docs (RangeIndexBasedFilterOperator.evaluateLegacyRangeFilter :82-107); over raw values it is UNSUPPORTED at query
+   * time.  An array / run container wider than a bitmap container is UNSUPPORTED at pin. */
   const void* range_index;
   uint64_t range_index_size;
   /* > 0: build the column's DISTINCTCOUNTHLL table for this log2m at pin -- the per-dictId (register, rank) pairs of
