@@ -100,7 +100,8 @@ typedef struct {
    * :123-211); on a raw column the leaf scans the dictIds the pin encoded (same doc set).  A version-1 index over
    * dictIds (RangeIndexCreator, type "INT") makes RANGE an index-based leaf whose statistic is its boundary ranges'
    * docs (RangeIndexBasedFilterOperator.evaluateLegacyRangeFilter :82-107); over raw values it is UNSUPPORTED at query
-   * time.  An array / run container wider than a bitmap container is UNSUPPORTED at pin. */
+   * time.  (An array / run container wider than a bitmap container, which RoaringBitmap never writes, makes the
+   * exact leaf scan the dictIds instead.) */
   const void* range_index;
   uint64_t range_index_size;
   /* > 0: build the column's DISTINCTCOUNTHLL table for this log2m at pin -- the per-dictId (register, rank) pairs of

@@ -663,7 +663,7 @@ void build_bitmap_directory(Column& c);  // at pin, from c.inverted
 void parse_legacy_range_index(const uint8_t* b, uint64_t size, std::vector<int64_t>* starts, int64_t* last_end,
                               std::vector<int64_t>* cards);
 std::vector<int32_t> parse_range_bitmap(const uint8_t* b, uint64_t size, int64_t num_docs, int32_t* nkeys,
-                                        int32_t* nslices);
+                                        int32_t* nslices, bool* stageable);
 // (column, index id) -> (startOffset, size) of a V3 index_map file (loader.cpp)
 typedef std::map<std::pair<std::string, std::string>, std::pair<int64_t, int64_t>> IndexMap;
 IndexMap read_index_map(const std::string& path);

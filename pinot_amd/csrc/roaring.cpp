@@ -174,7 +174,8 @@ void parse_legacy_range_index(const uint8_t* b, uint64_t size, std::vector<int64
 // Returns dir[k * S + i] = byte offset (from b) of that container, or -1.  The bytes are pinned by this restatement
 // and the test writer only: the reference holds no range-index file (parity unpinned for the byte format).
 std::vector<int32_t> parse_range_bitmap(const uint8_t* b, uint64_t size, int64_t num_docs, int32_t* nkeys,
-                                        int32_t* nslices) {
+                                        int32_t* nslices, bool* stageable) {
+  *stageable = true;
   const uint64_t h = 12;  // Pinot's header
   if (size < h + 10) fail(PH_ERR_INVALID_ARGUMENT, "range index: truncated RangeBitmap header");
   if (size > (uint64_t)INT32_MAX) fail(PH_ERR_UNSUPPORTED, "range index past 2 GiB");
@@ -200,7 +201,7 @@ std::vector<int32_t> parse_range_bitmap(const uint8_t* b, uint64_t size, int64_t
       const uint64_t body = kind == 0 ? 8192 : kind == 1 ? 4 * n : kind == 2 ? 2 * n : ~0ull;
       if (body == ~0ull) fail(PH_ERR_INVALID_ARGUMENT, "range index: bad container kind");
       if ((kind == 2 && n > 4096) || (kind == 1 && n > 2048))  // k_range_slices stages <= 8 KB of u16 payload
-        fail(PH_ERR_UNSUPPORTED, "range index: array / run container larger than a bitmap");
+        *stageable = false;
       if (at + 3 + body > size) fail(PH_ERR_INVALID_ARGUMENT, "range index: truncated container");
       dir[(size_t)k * S + i] = (int32_t)at;
       at += 3 + body;

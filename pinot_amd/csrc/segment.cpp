@@ -601,13 +601,20 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
     // leaves are evaluated from the bit slices (k_range_slices).  A raw column's index is over raw values (minus the
     // header's min), not the dictIds it is pinned as: its leaves scan the dictIds (same doc set)
     std::vector<int32_t> range_dir;
+    bool range_stageable = false;
     if (col->has_range_index && !col->is_raw && d.range_index_size > 12) {
       const uint8_t* ri = static_cast<const uint8_t*>(d.range_index);
       for (int j = 4; j < 12; ++j)
         if (ri[j]) fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": dictionary range index with min != 0");
-      range_dir = parse_range_bitmap(ri, d.range_index_size, n, &col->range_nkeys, &col->range_nslices);
+      range_dir = parse_range_bitmap(ri, d.range_index_size, n, &col->range_nkeys, &col->range_nslices,
+                                     &range_stageable);
       if (card > 0 && (uint64_t)(card - 1) >> (col->range_nslices - 1) >> 1)
         fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": range index slices narrower than the dictionary");
+    }
+    // (an array / run container wider than a bitmap one, which RoaringBitmap never writes: the leaf scans instead)
+    if (col->has_range_index && !col->is_raw && d.range_index_size > 12 && !range_dir.empty() &&
+        range_stageable) {
+      const uint8_t* ri = static_cast<const uint8_t*>(d.range_index);
       col->d_range.alloc(d.range_index_size + 16, ctx->device);  // + the padding k_range_slices' paired loads read
       PH_HIP_CHECK(hipMemcpyAsync(col->d_range.ptr, ri, d.range_index_size, hipMemcpyHostToDevice, st));
       col->d_range_dir.alloc(sizeof(int32_t) * std::max<size_t>(1, range_dir.size()), ctx->device);
