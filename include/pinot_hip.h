@@ -19,6 +19,10 @@
  *       ServerQueryExecutorV1Impl.java:369-376) for the filter -> aggregation / group-by shapes:
  *       FilterPlanNode.run (:83-114), AggregationPlanNode.run (:75), GroupByPlanNode.run (:57),
  *       GroupByCombineOperator.mergeResults (:223-252).
+ *   ph_filter_execute
+ *       FilterPlanNode.run (pinot-core/.../plan/FilterPlanNode.java:83-114) -> a BaseFilterOperator
+ *       (BaseFilterOperator.java:59-92: getTrues / canOptimizeCount / getNumMatchingDocs), the segment-level plug
+ *       point (PlanMaker.makeSegmentPlanNode, PlanMaker.java:53; FilterOperatorUtils.setImplementation :40).
  *   ph_result_*
  *       GroupByResultsBlock / AggregationResultsBlock contents (GroupByResultsBlock.java:62,86;
  *       AggregationResultsBlock.java:50) and ExecutionStatistics (GroupByOperator.java:143-148).
@@ -301,6 +305,20 @@ int ph_table_set_column_type(ph_ctx* ctx, const char* column, int32_t data_type)
 /* ------------------------------------------------------------------ queries */
 int ph_query_execute(ph_ctx* ctx, const ph_query* query, ph_segment* const* segments, int32_t num_segments,
                      ph_result** out);
+/* Segment-level filter: the drop-in behind FilterPlanNode.run (pinot-core/.../plan/FilterPlanNode.java:83-114), for a
+ * GpuFilterOperator extends BaseFilterOperator (BaseFilterOperator.java:33-112) whose getTrues() returns a
+ * BitmapDocIdSet (BitmapDocIdSet.java:29) and whose canOptimizeCount() / getNumMatchingDocs() (:59-68) answer from the
+ * count, so the reference's own operators above it (selection, projection, the ~80 aggregation functions, filtered
+ * aggregations) run unchanged over the GPU's doc set.  `query` contributes its filter only (filter_nodes, predicates,
+ * filter_root; group-by, aggregations, ordering and trim are ignored); the planning is ph_query_execute's (same leaf
+ * choice, same evaluators).  doc_words: NULL for the count alone, else >= ceil(num_docs / 64) words receiving the
+ * doc bitmap -- bit i of word w is doc 64 w + i, bits past num_docs zero (the long[] layout of
+ * org.roaringbitmap.BitSetUtil.bitmapOf(long[]) / java.util.BitSet.valueOf).  stats (may be NULL): num_docs_scanned
+ * = matching docs, num_entries_scanned_in_filter = the reference's statistic for the segment's filter operator tree
+ * (BlockDocIdSet.getNumEntriesScannedInFilter), num_total_docs, device_ms, scan_kernel.  No filter (filter_root < 0)
+ * is MatchAllFilterOperator: every doc, answered without a launch. */
+int ph_filter_execute(ph_ctx* ctx, const ph_query* query, ph_segment* segment, uint64_t* doc_words, uint64_t num_words,
+                      ph_exec_stats* stats);
 int ph_result_destroy(ph_result* r);
 int ph_result_stats(const ph_result* r, ph_exec_stats* out);
 /* number of result rows: non-empty groups (group-by) or 1 (aggregation-only) */

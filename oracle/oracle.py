@@ -1024,6 +1024,28 @@ def execute(q, segments: Sequence[OracleSegment], num_threads: int = 1, filter_s
     return OracleResult(keys, merged, OracleStats(*stats))
 
 
+def filter_docs(q, seg: OracleSegment):
+    """One segment's filter as FilterPlanNode.run's operator yields it (FilterPlanNode.java:83-114): the matching
+    docs (bool per doc; BaseFilterOperator.getTrues, :92) and the statistic of its iterator tree
+    (BlockDocIdSet.getNumEntriesScannedInFilter, via filter_entries).  No filter: MatchAllFilterOperator."""
+    n = seg.num_docs
+    if q.filter is None:
+        return np.ones(n, bool), 0
+    used = _used_columns(q)
+    col_index = {c: i for i, c in enumerate(used)}
+    merged = _merge_same_column(_plan_filter(q.filter, seg, col_index))
+    docs = _eval_docs(merged, seg, used)
+    return docs, filter_entries(merged, seg, used) + legacy_partial_entries(merged, seg, used)
+
+
+def doc_words(mask: np.ndarray) -> np.ndarray:
+    """A doc mask as the 64-bit words of ph_filter_execute (bit i of word w = doc 64 w + i)."""
+    n = len(mask)
+    padded = np.zeros(((n + 63) // 64) * 64, np.uint8)
+    padded[:n] = mask
+    return np.packbits(padded, bitorder="little").view("<u8").astype(np.uint64)
+
+
 def execute_timed(q, segments: Sequence[OracleSegment], num_threads: int):
     """Single or_execute call over all segments with a pool of num_threads workers (the timed CPU
     baseline).  All segments must share one filter plan shape (true for the bench workloads)."""

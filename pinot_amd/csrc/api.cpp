@@ -1,5 +1,6 @@
 // api.cpp -- extern "C" entry points of libpinot_hip.so (include/pinot_hip.h).  No C++ exception crosses
 // the ABI: every entry point returns a PH_* status and leaves a thread-local message for ph_last_error().
+#include <algorithm>
 #include <cstring>
 #include <new>
 
@@ -259,6 +260,68 @@ int ph_query_execute(ph_ctx* ctx, const ph_query* query, ph_segment* const* segm
       *out = segment_trim_execute(&ctx->c, query, segments, num_segments);  // GroupByOperator segment trim
     else
       *out = query_execute_impl(&ctx->c, query, segments, num_segments, nullptr);
+  });
+}
+
+// Segment-level drop-in (FilterPlanNode.run -> BaseFilterOperator): one segment's filter as a COUNT(*) whose MODE_COUNT
+// scan also writes the doc bitmap (DenseArgs::docset), the statistic computed exactly as for a query
+int ph_filter_execute(ph_ctx* ctx, const ph_query* query, ph_segment* segment, uint64_t* doc_words, uint64_t num_words,
+                      ph_exec_stats* stats) {
+  return guarded([&] {
+    if (!ctx || !query || !segment) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
+    Context* c = segment->ctx;
+    bool mine = false;
+    for (Context* d : ctx->devs) mine = mine || d == c;
+    if (!mine) fail(PH_ERR_INVALID_ARGUMENT, "segment is pinned on another context");
+    const int64_t nd = segment->num_docs;
+    const uint64_t need = (uint64_t)((nd + 63) / 64);
+    if (doc_words && num_words < need) fail(PH_ERR_INVALID_ARGUMENT, "doc_words holds fewer than ceil(num_docs / 64) words");
+    ph_exec_stats st{};
+    st.num_total_docs = nd;
+    st.num_segments_processed = 1;
+    if (query->filter_root < 0) {  // no WHERE clause: MatchAllFilterOperator (FilterPlanNode.java:96-101)
+      if (doc_words) {
+        for (uint64_t w = 0; w < need; ++w) doc_words[w] = ~0ull;
+        if (nd % 64) doc_words[need - 1] = (1ull << (nd % 64)) - 1ull;
+      }
+      st.num_docs_scanned = nd;
+      st.num_segments_matched = nd > 0;
+      st.plan_mode = -2;
+      if (stats) *stats = st;
+      return;
+    }
+    // the filter as a COUNT(*) with no group-by, ordering or trim
+    ph_query q = *query;
+    ph_aggregation cnt{};
+    cnt.type = PH_AGG_COUNT;
+    q.num_group_by = 0;
+    q.group_by = nullptr;
+    q.num_aggregations = 1;
+    q.aggregations = &cnt;
+    q.num_order_by = 0;
+    q.order_by = nullptr;
+    q.min_segment_group_trim_size = -1;
+    ph_segment* segs[1] = {segment};
+    std::unique_ptr<ph_result> r;
+    if (!doc_words) {
+      r.reset(query_execute_impl(c, &q, segs, 1, nullptr));
+    } else {
+      PH_HIP_CHECK(hipSetDevice(c->device));
+      std::unique_ptr<DeviceBuffer> words = c->scratch_acquire(std::max<uint64_t>(1, need) * 8);
+      struct Back {  // the scratch block goes back to the pool on every exit
+        Context* c;
+        std::unique_ptr<DeviceBuffer>& b;
+        ~Back() { c->scratch_release(std::move(b)); }
+      } back{c, words};
+      const int64_t off[1] = {0};
+      FilterDocset fd{words->as<unsigned long long>(), off, (int64_t)need};
+      DenseArgs d{0, nullptr, 0, 0, nullptr};
+      d.docset = &fd;
+      r.reset(query_execute_impl(c, &q, segs, 1, &d));
+      // the call drained its stream before it read the count
+      if (need) PH_HIP_CHECK(hipMemcpy(doc_words, words->ptr, 8 * need, hipMemcpyDeviceToHost));
+    }
+    if (stats) *stats = r->stats;
   });
 }
 

@@ -199,6 +199,10 @@ struct DevSegment {
   const uint8_t* sp_cbase[kSparseBitmaps];
   const int32_t* sp_ctab;  // [65536-doc key][sp_ntot]: the directory index of range t's container of that key, or -1
   int32_t sp_ntot;         // ranges over all leaves (sum of sp_nrng)
+  int32_t pad2;
+  // ph_filter_execute (KParams::docset): the segment's doc bitmap, ceil(num_docs / 64) 64-bit words (bit i of word w =
+  // doc 64 w + i), written by the MODE_COUNT scans; words outside the scanned chunks stay as zeroed by the host
+  uint32_t* docset;
   DevColumn cols[kMaxCols];
   DevValCol vals[kMaxVals];
   DevValCol vals2[kMaxVals];       // second operand of a 2-operand expression term (KParams::val_op)
@@ -321,6 +325,7 @@ struct KParams {
   int32_t group_sparse;           // MODE_GROUP_LDS / GLOBAL: k_group_sparse (selective bitmap ANDs, DevSegment sp_*)
   int32_t group_reg_lanes_log2;   //   log2 of the slots per key (lane l updates slot key * L + (l & (L - 1)))
   int32_t group_reg_cf, group_reg_cg, group_reg_cv;  // 16-byte loads per lane: filter / each group / value stream
+  int32_t docset;                 // MODE_COUNT: every segment's DevSegment::docset receives its doc bitmap
   unsigned long long* ovf_count;  // overflow table (same layout as out_*), merged at the end
   int64_t* ovf_sum;
   int64_t* ovf_min;
@@ -390,6 +395,14 @@ struct DenseArgs {
   // group-by dictionaries in group-by order, in place of the context's table dictionaries (the multi-device combine
   // builds one union over every device's segments, one copy per device)
   const std::vector<std::shared_ptr<GlobalDict>>* dicts = nullptr;
+  // ph_filter_execute: the call is a COUNT(*) whose scan also writes each segment's doc bitmap into `words` (device
+  // memory, zeroed here): segment i's ceil(num_docs / 64) words start at word_off[i]
+  struct FilterDocset* docset = nullptr;
+};
+struct FilterDocset {
+  unsigned long long* words;
+  const int64_t* word_off;
+  int64_t total_words;
 };
 
 // ------------------------------------------------------------------ host-side segment model

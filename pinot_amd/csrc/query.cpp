@@ -54,6 +54,7 @@ struct PNode {
                              // flipped bitmap: a BitmapDocIdSet, not a user NOT)
   bool range_index = false;  // a scan-evaluated RangeIndexBasedFilterOperator leaf: index-based for the statistics
   bool legacy_range = false;  // ... over a legacy version-1 index (its boundary ranges scanned: legacy_partial_entries)
+  bool range_pred = false;    // the leaf of a RANGE predicate (MergeRangeFilterOptimizer merges these under an AND)
   // AND whose children are index-based leaves (sorted, bitmap, range index, ORs / NOTs of them) followed by scan
   // leaves: the reference's AndDocIdSet applies the scans one after another to the index-based result
   // (ScanBasedDocIdIterator.applyAnd), so its filter entries are |D0| + |D0 n S1| + ... (counted on the device)
@@ -67,6 +68,7 @@ struct BitmapLeaf {
   std::vector<int32_t> dict_ids;  // inverted-index leaf: the OR of these dictIds' bitmaps
   bool range = false;             // exact range-index leaf: dictIds [lo, hi] from the bit slices (k_range_slices)
   int64_t lo = 0, hi = -1;
+  bool dead = false;              // merged into another range leaf (MergeRangeFilterOptimizer): never built
 };
 
 struct DictIdSet {
@@ -310,6 +312,7 @@ struct Planner {
       n.scan = false;
       n.col = -1;
       n.op = OP_BITMAP;
+      n.range_pred = p.type == PH_PRED_RANGE;
       n.bitmap_leaf = (int)bitmaps.size();
       bitmaps.push_back(std::move(b));
       return n;
@@ -459,15 +462,41 @@ void leaf_from_bits(PNode& n, const std::vector<uint32_t>& b, int64_t card) {
 }
 
 template <class CardOf>
-void merge_same_column_leaves(PNode& n, const CardOf& card_of) {
+void merge_same_column_leaves(PNode& n, const CardOf& card_of, std::vector<BitmapLeaf>* bms = nullptr) {
   if (n.kind != L_NODE) return;
-  for (auto& k : n.kids) merge_same_column_leaves(k, card_of);
+  for (auto& k : n.kids) merge_same_column_leaves(k, card_of, bms);
   if (n.op != OP_AND && n.op != OP_OR) return;
   if (n.stats_nscan) return;  // its scan children stay separate: each is one applyAnd step of the statistic
   const bool is_and = n.op == OP_AND;
   std::map<int, size_t> first_of;  // column slot -> index of its first scan leaf
+  std::map<const Column*, size_t> first_range;  // column -> index of its first slice-evaluated RANGE leaf
   std::vector<PNode> kids;
   for (auto& k : n.kids) {
+    // RANGE leaves of one column under an AND evaluated from the range index's slices: one leaf over the
+    // intersected dictId interval (MergeRangeFilterOptimizer.java:50-100 merges the predicates before planning, so
+    // the reference builds one RangeIndexBasedFilterOperator, or an EmptyFilterOperator for an empty interval)
+    if (is_and && bms && k.kind == L_NODE && k.op == OP_BITMAP && k.range_pred && (*bms)[k.bitmap_leaf].range) {
+      BitmapLeaf& b = (*bms)[k.bitmap_leaf];
+      auto it = first_range.find(b.col);
+      if (it != first_range.end()) {
+        PNode& a = kids[it->second];
+        if (a.kind == L_NONE) {
+          b.dead = true;
+          continue;
+        }
+        BitmapLeaf& ab = (*bms)[a.bitmap_leaf];
+        ab.lo = std::max(ab.lo, b.lo);
+        ab.hi = std::min(ab.hi, b.hi);
+        b.dead = true;
+        if (ab.hi < ab.lo) {
+          ab.dead = true;
+          a = PNode{};
+          a.kind = L_NONE;
+        }
+        continue;
+      }
+      first_range[b.col] = kids.size();
+    }
     // a legacy range-index leaf merges only with another under an AND (MergeRangeFilterOptimizer: one RANGE,
     // planned once); the other scans merge as before, never with it
     const bool legacy = k.kind == L_NODE && k.legacy_range;
@@ -950,6 +979,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
                               const DenseArgs* dn) {
   const int dop = dn ? dn->op : 0;
   const bool fin = dop == DENSE_FINALIZE;
+  // ph_filter_execute: a COUNT(*) (no group-by) whose MODE_COUNT scan also writes every segment's doc bitmap
+  const FilterDocset* fds = (dn && !dop) ? dn->docset : nullptr;
   using clock = std::chrono::steady_clock;
   const auto t0 = clock::now();
   const bool host_times = getenv("PH_HOST_TIMES") != nullptr;  // per-phase host clock (tuning)
@@ -960,6 +991,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   if (!q) fail(PH_ERR_INVALID_ARGUMENT, "null query");
   if (nseg < 0 || (nseg > 0 && !segs_in)) fail(PH_ERR_INVALID_ARGUMENT, "bad segment list");
   if (q->num_aggregations > kMaxAggs) fail(PH_ERR_UNSUPPORTED, "too many aggregations");
+  if (fds && (q->num_group_by != 0 || q->num_aggregations != 1 || q->aggregations[0].type != PH_AGG_COUNT ||
+              q->filter_root < 0))
+    fail(PH_ERR_INVALID_ARGUMENT, "a filter call is a filtered COUNT(*)");
   if (q->num_group_by > kMaxGroupCols) fail(PH_ERR_UNSUPPORTED, "too many group-by columns");
   PH_HIP_CHECK(hipSetDevice(ctx->device));
   LaneGuard lane(ctx);  // this call's streams, events and staging (concurrent calls use their own)
@@ -1163,6 +1197,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
 
   // ---- per-segment filter plans
   QueryScratch scratch(ctx, st, lane.lane->stream_b);
+  if (fds && fds->total_words > 0) PH_HIP_CHECK(hipMemsetAsync(fds->words, 0, 8 * (size_t)fds->total_words, st));
   std::vector<SegProgram> progs(nseg);
   std::vector<PNode> roots(nseg);
   std::vector<char> seg_live(nseg, 1);
@@ -1192,7 +1227,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     // same-column scan predicates merge first, as the reference's query optimizer merges them before planning
     // (MergeEqInFilterOptimizer: `d_year = 1997 OR d_year = 1998` -> one IN; MergeRangeFilterOptimizer: ranges of
     // one column under an AND), so the statistics below see the reference's operator tree
-    merge_same_column_leaves(root, [&](int slot) { return (int64_t)segs[i]->columns.at(slot_names[slot])->cardinality; });
+    merge_same_column_leaves(
+        root, [&](int slot) { return (int64_t)segs[i]->columns.at(slot_names[slot])->cardinality; }, &pl.bitmaps);
     if (segs[i]->num_docs > 0)
       stats.num_entries_scanned_in_filter += legacy_partial_entries(
           root, [&](int slot) -> const Column& { return *segs[i]->columns.at(slot_names[slot]); });
@@ -1214,7 +1250,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // ---- FastFilteredCountOperator (AggregationPlanNode.java:183-188): COUNT only, and every segment's filter
   // answers getNumMatchingDocs from its index -- a sorted doc range, an inverted-index bitmap (disjoint per
   // dictId in a single-value column) or their NOT -- so no doc is scanned
-  bool fast_count = q->num_group_by == 0 && nagg > 0 && q->filter_root >= 0 && !dop;
+  bool fast_count = q->num_group_by == 0 && nagg > 0 && q->filter_root >= 0 && !dop && !fds;
   for (int k = 0; k < nagg && fast_count; ++k) fast_count = q->aggregations[k].type == PH_AGG_COUNT;
   if (fast_count) {
     std::function<int64_t(const PNode&, int64_t)> count_of = [&](const PNode& n, int64_t docs) -> int64_t {
@@ -1278,7 +1314,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       int max_chunks = 0;
       for (size_t i = 0; i < nl; ++i) {
         const BitmapLeaf& b = pl.bitmaps[i];
-        if (!b.range) continue;
+        if (!b.range || b.dead) continue;
         const Column& col = *b.col;
         const int32_t pw = (int32_t)(woff[i + 1] - woff[i]);
         RangeSliceLeaf L{};
@@ -1362,6 +1398,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       launch_roaring_or(reinterpret_cast<RoaringWork*>(dev), (int)cs.size(), reinterpret_cast<RoaringTarget*>(dev + b1),
                         st);
     }
+    build_range_leaves();  // after the memset: k_range_slices writes every word of its leaves
   };
   stamp("plan");
   // Aggregation-only queries whose every segment is filtered by ONE inverted leaf (EQ / IN) may run k_agg_sparse
@@ -1502,6 +1539,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   kp.log2m = log2m ? log2m : 8;
   kp.num_groups = G;
   kp.num_group_cols = q->num_group_by;
+  kp.docset = fds ? 1 : 0;
   {
     int64_t stride = 1;
     for (int g = 0; g < q->num_group_by; ++g) {
@@ -1827,6 +1865,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     ph_segment* s = segs[i];
     DevSegment d{};
     d.num_docs = s->num_docs;
+    if (fds) d.docset = reinterpret_cast<uint32_t*>(fds->words + fds->word_off[i]);
     const PNode& root = roots[i];
     const size_t si = dsegs.size();
     auto conj_leaf = [&](const PNode& k) {

@@ -60,22 +60,23 @@ __global__ void __launch_bounds__(256) k_range_slices(const RangeSliceLeaf* __re
   }
   __syncthreads();
   for (int i0 = 0; i0 < S; i0 += kBatch) {
-    // straight-line loads (no branch per slice): a slice without a bitmap container reads the payload's first
-    // bytes and discards them; kinds and offsets are wave-uniform (readfirstlane: scalar branches below)
+    // the batch's bitmap-container words, all loads issued before any is used; kinds and offsets are wave-uniform
+    // (readfirstlane), so a slice without a bitmap container is a scalar branch around its load -- it reads nothing
+    // (an index of array / run containers only can be smaller than the 4 * 256 bytes a thread offset spans)
     uint32_t bw[kBatch];
     bool isbm[kBatch];
 #pragma unroll
     for (int b = 0; b < kBatch; ++b) {
       const int i = min(i0 + b, S - 1);
       isbm[b] = i0 + b < S && __builtin_amdgcn_readfirstlane(s_kind[i]) == kRbBitmap;
-      const int32_t off = isbm[b] ? __builtin_amdgcn_readfirstlane(s_off[i]) + 3 + 4 * part * kPartWords : 0;
-      bw[b] = ld_u32_any(L.payload + off + 4 * t);
+      bw[b] = 0;
+      if (isbm[b])
+        bw[b] = ld_u32_any(L.payload + __builtin_amdgcn_readfirstlane(s_off[i]) + 3 + 4 * part * kPartWords + 4 * t);
     }
 #pragma unroll
     for (int b = 0; b < kBatch; ++b) {
       const int i = i0 + b;
       if (i >= S) break;
-      if (!isbm[b]) bw[b] = 0;
       const int kind = __builtin_amdgcn_readfirstlane(s_kind[i]);
       uint32_t zw = bw[b];  // a bitmap container's word; none: no doc of the key has bit i clear
       if (kind == kRbArray || kind == kRbRun) {

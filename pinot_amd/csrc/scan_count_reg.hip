@@ -7,7 +7,9 @@
 
 namespace ph {
 
-template <int C>
+// DS (ph_filter_execute): each lane also stores its run's 32-bit match mask, word t.w0 * 2 + lane of the segment's doc
+// bitmap -- the wave's 64 lanes write 256 contiguous bytes
+template <int C, int DS>
 __global__ void __launch_bounds__(kBlock) k_count_reg(const KParams p) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -52,6 +54,25 @@ __global__ void __launch_bounds__(kBlock) k_count_reg(const KParams p) {
     const int32_t nv = max(0, min(32, t.ndoc - lane * 32));
     const uint32_t flo = t.S->flo, flen = t.S->flen;
     const int fk = t.S->fkind;
+    if constexpr (DS) {
+      uint32_t m = nv >= 32 ? 0xffffffffu : ((1u << nv) - 1u);
+      if (fk == FK_RANGE) {
+        uint32_t pass = 0;
+        reg_decode<C>(pool, t.S->streams[p.f_stream].bits, [&](auto j, uint32_t v) {
+          pass |= ((v - flo) < flen ? 1u : 0u) << decltype(j)::value;
+        });
+        m &= pass;
+      } else if (fk == FK_DOCRANGE) {
+        const int64_t d0 = (int64_t)t.w0 * 64 + lane * 32;
+        const int64_t lo = max<int64_t>(0, (int64_t)flo - d0), hi = min<int64_t>(32, (int64_t)flo + flen - d0);
+        uint32_t dm = 0;
+        if (hi > lo) dm = (hi >= 32 ? 0xffffffffu : ((1u << hi) - 1u)) & ~(lo <= 0 ? 0u : ((1u << lo) - 1u));
+        m &= dm;
+      }
+      cnt += (uint32_t)__builtin_popcount(m);
+      if (nv > 0) t.S->docset[(int64_t)t.w0 * 2 + lane] = m;
+      return;
+    }
     if (fk == FK_RANGE) {
       reg_decode<C>(pool, t.S->streams[p.f_stream].bits, [&](auto j, uint32_t v) {
         cnt += ((v - flo) < flen && (int32_t)decltype(j)::value < nv) ? 1u : 0u;
@@ -200,8 +221,11 @@ void launch_agg_reg(const KParams& p, int grid, hipStream_t s) {
 
 void launch_count_reg(const KParams& p, int grid, hipStream_t s) {
   switch (p.count_reg) {
-#define PH_COUNT_CASE(n) \
-  case n: hipLaunchKernelGGL(k_count_reg<n>, dim3(grid), dim3(kBlock), 0, s, p); break;
+#define PH_COUNT_CASE(n)                                                                                     \
+  case n:                                                                                                    \
+    if (p.docset) hipLaunchKernelGGL((k_count_reg<n, 1>), dim3(grid), dim3(kBlock), 0, s, p);               \
+    else hipLaunchKernelGGL((k_count_reg<n, 0>), dim3(grid), dim3(kBlock), 0, s, p);                        \
+    break;
     PH_COUNT_CASE(1) PH_COUNT_CASE(2) PH_COUNT_CASE(3) PH_COUNT_CASE(4)
     PH_COUNT_CASE(5) PH_COUNT_CASE(6) PH_COUNT_CASE(7) default: PH_COUNT_CASE(8)
 #undef PH_COUNT_CASE

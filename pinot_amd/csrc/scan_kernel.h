@@ -789,6 +789,9 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
     }
     return;
   }
+  // ph_filter_execute: the ballots ARE the segment's doc bitmap words (FilterPlanNode's BitmapDocIdSet); lane q of the
+  // wave stores word u + q of a step, one 8-byte store per word
+  unsigned long long* const dset = MODE == MODE_COUNT ? reinterpret_cast<unsigned long long*>(S->docset) : nullptr;
   int u = 0;
   for (; u + UB <= nvalid; u += UB) {
     bool hit[UB];
@@ -800,7 +803,14 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
       bal[q] = __ballot(hit[q]);
       acc.matched += __popcll(bal[q]);
     }
-    if constexpr (MODE != MODE_COUNT) {
+    if constexpr (MODE == MODE_COUNT) {
+      if (dset) {
+        unsigned long long mine = bal[0];
+#pragma unroll
+        for (int q = 1; q < UB; ++q) mine = lane == q ? bal[q] : mine;
+        if (lane < UB) dset[w0 + u + lane] = mine;
+      }
+    } else {
 #pragma unroll
       for (int q = 0; q < UB; ++q)
         if (bal[q]) aggregate_word(u + q, hit[q], bal[q]);
@@ -810,7 +820,9 @@ __device__ __forceinline__ void process_tile(const KParams& p, SegPtr S, uint8_t
     const bool hit = filter_word(u);
     const unsigned long long bal = __ballot(hit);
     acc.matched += __popcll(bal);
-    if constexpr (MODE != MODE_COUNT) {
+    if constexpr (MODE == MODE_COUNT) {
+      if (dset && lane == 0) dset[w0 + u] = bal;
+    } else {
       if (bal) aggregate_word(u, hit, bal);
     }
   }

@@ -356,6 +356,28 @@ class GpuContext:
                                st.limit_pass, st.scan_kernel, st.num_devices, st.merge_ms, st.finalize_ms)
         return IntermediateResult(key_cols, agg_cols, n, [a.function for a in q.aggregations], stats)
 
+    # ---------------------------------------------------------------- segment-level filter (plug point 2)
+    def filter(self, sql_or_q, segment: PinnedSegment, words: bool = True):
+        """ph_filter_execute: one segment's WHERE clause on the GPU -- what a GpuFilterOperator returns from
+        getTrues() (BaseFilterOperator.java:92).  Returns (doc-bitmap words as uint64 -- bit i of word w is doc
+        64 w + i -- or None when ``words`` is False, matching-doc count, ExecutionStats)."""
+        q = parse_sql(sql_or_q) if isinstance(sql_or_q, str) else sql_or_q
+        qs = _QueryStruct(q)
+        nd = segment.num_docs
+        out = np.zeros(max(1, (nd + 63) // 64), np.uint64) if words else None
+        st = N.ExecStats()
+        N.check(N.lib().ph_filter_execute(self.handle, ctypes.byref(qs.struct), segment.handle,
+                                          out.ctypes.data if words else None, out.size if words else 0,
+                                          ctypes.byref(st)))
+        stats = ExecutionStats(st.num_docs_scanned, st.num_entries_scanned_in_filter,
+                               st.num_entries_scanned_post_filter, st.num_total_docs, st.num_segments_processed,
+                               st.num_segments_matched, bool(st.num_groups_limit_reached),
+                               bool(st.sum_precision_flag), st.device_ms, st.host_ms, st.plan_mode,
+                               st.limit_pass, st.scan_kernel, st.num_devices, st.merge_ms, st.finalize_ms)
+        if words:
+            out = out[:(nd + 63) // 64]
+        return out, int(st.num_docs_scanned), stats
+
     # ---------------------------------------------------------------- dense partials (multi-GPU combine)
     def dense_layout(self, q: QueryContext, segments: Sequence[PinnedSegment]) -> N.DenseLayout:
         """ph_query_dense_layout: the dense partial tables of ``q`` (count, element type, reduce op)."""

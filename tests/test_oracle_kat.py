@@ -373,3 +373,18 @@ def test_kat_filter_entries_reference_iterators():
     cols = {k: v for k, (v, _) in kat_sv.load_columns().items()}
     entries, matches = _and_or_iterator_entries(cols)
     assert 4 * matches == 24516 and 4 * entries == 252256
+
+
+def test_filter_docs_matches_execute():
+    # oracle.filter_docs (the segment-level filter's doc set + statistic, ph_filter_execute's checker) agrees with the
+    # KAT-pinned execute path on the reference's filter
+    from pinot_amd.query import parse_sql
+    from tests import kat_sv
+    seg = O.build_segment("kat", kat_sv.load_columns(), inverted=kat_sv.INVERTED)
+    q = parse_sql("SELECT COUNT(*) FROM testTable" + kat_sv.FILTER)
+    mask, entries = O.filter_docs(q, seg)
+    e = O.execute(q, [seg])
+    assert int(mask.sum()) * 4 == 24516 and entries * 4 == 252256
+    assert int(mask.sum()) == e.stats.num_docs_scanned and entries == e.stats.num_entries_scanned_in_filter
+    w = O.doc_words(mask)
+    assert len(w) == (seg.num_docs + 63) // 64 and int(np.unpackbits(w.view(np.uint8)).sum()) == int(mask.sum())
