@@ -387,7 +387,16 @@ def _plan_filter(f, seg: OracleSegment, col_index: Dict[str, int]):
 def _merge_same_column(node: _Leaf) -> _Leaf:
     """Same-column scan leaves under one AND / OR become one leaf (their match arrays ANDed / ORed), as the
     reference's query optimizer merges them before planning (MergeEqInFilterOptimizer, MergeRangeFilterOptimizer:
-    QueryOptimizer.java:47-49); the statistics then follow the merged tree.  Results are unchanged."""
+    QueryOptimizer.java:47-49); the statistics then follow the merged tree.  Results are unchanged.  A NOT's child is
+    merged too (MergeRangeFilterOptimizer.java:101-103 optimizes NOT operands)."""
+    if node.kind == "not":
+        node.children = [_merge_same_column(node.children[0])]
+        k = node.children[0]
+        if k.kind == "all":
+            return _Leaf("none")
+        if k.kind == "none":
+            return _Leaf("all")
+        return node
     if node.kind not in ("and", "or"):
         return node
     is_and = node.kind == "and"

@@ -34,14 +34,14 @@ struct PartTiles {
   }
 
   // rounds of this workgroup (every wave runs all of them; a wave past its chunk's words gets an empty tile)
-  __device__ int32_t rounds() const {
+  __device__ __forceinline__ int32_t rounds() const {
     constexpr int32_t round_words = kRegWaves * kRegTileWords;
     int32_t n = 0;
     for (int32_t cc = c; cc < c_end; ++cc) n += (chunks[cc].word_end - chunks[cc].word_begin + round_words - 1) / round_words;
     return n;
   }
 
-  __device__ Tile next() {
+  __device__ __forceinline__ Tile next() {
     constexpr int32_t round_words = kRegWaves * kRegTileWords;
     Tile t{nullptr, 0, 0};
     if (c < c_end) {
@@ -61,11 +61,11 @@ struct PartTiles {
   }
 
   // issue the tile's loads (they stay in flight until decode)
-  __device__ void load(const Tile& t, int lane) {
+  __device__ __forceinline__ void load(const Tile& t, int lane) {
     load_keys(t, lane);
     load_value(t, lane);
   }
-  __device__ void load_keys(const Tile& t, int lane) {
+  __device__ __forceinline__ void load_keys(const Tile& t, int lane) {
     const bool tile = t.ndoc > 0;                        // wave-uniform
     const bool lane_live = tile && lane * 32 < t.ndoc;  // this lane's run holds docs of the tile
     const int32_t run0 = t.w0 * 2;
@@ -82,7 +82,7 @@ struct PartTiles {
                    tile ? bytes(gs) : 0, run0, lane, pk[g]);
     }
   }
-  __device__ void load_value(const Tile& t, int lane) {
+  __device__ __forceinline__ void load_value(const Tile& t, int lane) {
     const bool tile = t.ndoc > 0;
     const bool lane_live = tile && lane * 32 < t.ndoc;
     const int32_t run0 = t.w0 * 2;
@@ -99,7 +99,7 @@ struct PartTiles {
   // (the partition key >> klo, or the lane's scratch word P + lane for a missed doc), then the value phase turns each
   // key into its record in place, (key << (32 - klo)) + value offset: the shift drops the partition bits, and kernel B
   // reads the key as record >> (32 - klo) (peak: 48 registers + the loads)
-  __device__ void decode(const Tile& t, int lane, uint32_t (&X)[32], uint32_t (&PB)[16]) const {
+  __device__ __forceinline__ void decode(const Tile& t, int lane, uint32_t (&X)[32], uint32_t (&PB)[16]) const {
     const uint32_t klo = (uint32_t)p.part_klo, rsh = 32u - klo;
     const uint32_t dummy = (uint32_t)p.num_parts + (uint32_t)lane;
     if (t.ndoc <= 0) {

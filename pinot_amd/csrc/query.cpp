@@ -2738,6 +2738,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       kp.part_vbits = kp.part_reg ? 32 - klo : vbits;
       kp.num_parts = (int32_t)P;
       const size_t lds_a = partition_lds_bytes(kp);
+      // (tentative, for the occupancy query; the region-size condition is checked once the capacity is known)
+      kp.part_fixed = kp.part_reg && P <= kRegBlock && kp.part_slot_log2 == 5 && !rec64 &&
+                      getenv("PH_PART_FIXED0") == nullptr;
       int a_cap = 4;  // 8-wave workgroups: <= 4 per CU (32 waves)
       if (kp.part_reg) a_cap = part_reg_blocks_per_cu(kp, q->num_group_by, lds_a);  // 4-wave groups, VGPR-bound
       if (const char* e = getenv("PH_PART_WG_PER_CU")) a_cap = std::max(1, std::min(8, atoi(e)));  // tuning knob
@@ -2787,6 +2790,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         launch_fill_i64(kp.ovf_max, INT64_MIN, G, st);
       }
       kp.part_cap = (int32_t)cap;
+      // k_part_reg's fixed-count flush: thread t owns partition t, 32-slot rings, a workgroup's regions addressable
+      // by one buffer descriptor
+      kp.part_fixed = kp.part_fixed && (double)P * (double)cap * 4.0 < 2147483647.0;
       kp.part_vbase = nvals ? vmin : 0;
       kp.lds_bytes = (int32_t)lds_a;
       PartAggParams bp{};

@@ -21,7 +21,9 @@ namespace ph {
 // append variants, listed flush with per-record "chunk completed" checks): 64.5 VALU + 33 SALU per doc and the VALU
 // busy 62 % of the kernel.  The flush is one thread per partition (part_flush_owner: pending >= 16 sends its whole
 // 64-byte chunks out), so no append keeps a list.
-template <int NG, int HASV, int CK, int CV>
+// FX: P <= kRegBlock partitions with 32-slot rings -- the in-loop flushes are part_flush_fixed (a fixed count of
+// buffer stores per round, so the decode waits for the next tile's loads only)
+template <int NG, int HASV, int CK, int CV, int FX>
 __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
@@ -50,6 +52,12 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
   const uint32_t dummy_slot = P * RS + (uint32_t)lane;  // scratch slot of a record-less lane
   auto t0 = tiles.next();
   tiles.load(t0, lane);
+  if constexpr (FX != 0) {
+    // the same 2 x 8 (empty) flush stores after the first tile's loads as every later tile has after its own: the
+    // decode's waits then count them on every path into the loop (the minimum over paths is what the compiler uses)
+    part_flush_fixed<kRegBlock>(p, smem, matched, 1);
+    part_flush_fixed<kRegBlock>(p, smem, matched, 0);
+  }
   // per lane and doc j of the tile: X[j] = the 32-bit record; PB packs two 16-bit ring-word indices per register
   uint32_t X[32], PB[16];
   for (int32_t it = 0; it < nrounds; ++it) {
@@ -62,7 +70,8 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
     // (r4's single set needed two: flush, barrier, append, barrier)
     auto append_round = [&](auto jb) {
       const int cur = (int)(round & 1);
-      if (round > 0) part_flush_owner<kRegBlock>(p, smem, matched, false, cur ^ 1);
+      if constexpr (FX != 0) part_flush_fixed<kRegBlock>(p, smem, matched, cur ^ 1);  // (round 0: the set is empty)
+      else if (round > 0) part_flush_owner<kRegBlock>(p, smem, matched, false, cur ^ 1);
       uint32_t* pend = pend0 + (size_t)cur * (P + 64);
       uint32_t* slots = slots0 + (size_t)cur * SW;
       // groups of 4: the 4 rank atomics issue back to back, then the 4 stores.  Branch-free and SGPR-free per record:
@@ -104,8 +113,13 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
 
 template <int NG, int HASV, int CK, int CV>
 static void launch_part_reg_k(const KParams& p, int grid, size_t lds, hipStream_t s) {
-  allow_lds(k_part_reg<NG, HASV, CK, CV>, lds);
-  hipLaunchKernelGGL((k_part_reg<NG, HASV, CK, CV>), dim3(grid), dim3(kRegBlock), lds, s, p);
+  if (p.part_fixed) {
+    allow_lds(k_part_reg<NG, HASV, CK, CV, 1>, lds);
+    hipLaunchKernelGGL((k_part_reg<NG, HASV, CK, CV, 1>), dim3(grid), dim3(kRegBlock), lds, s, p);
+  } else {
+    allow_lds(k_part_reg<NG, HASV, CK, CV, 0>, lds);
+    hipLaunchKernelGGL((k_part_reg<NG, HASV, CK, CV, 0>), dim3(grid), dim3(kRegBlock), lds, s, p);
+  }
 }
 
 template <int NG>
@@ -132,11 +146,18 @@ void launch_part_reg(const KParams& p, int ng, int grid, size_t lds, hipStream_t
 int part_reg_blocks_per_cu(const KParams& p, int ng, size_t lds) {
   const void* f = nullptr;
   const bool hasv = p.num_vals > 0;
-#define PH_REG_FN(NG)                                                                                                 \
-  f = p.part_ck == 3 ? (hasv ? (const void*)k_part_reg<NG, 1, 3, 5> : (const void*)k_part_reg<NG, 0, 3, 5>)          \
-                     : (hasv ? (const void*)k_part_reg<NG, 1, 4, 8> : (const void*)k_part_reg<NG, 0, 4, 8>);
+#define PH_REG_FX(NG, FX)                                                                                             \
+  f = p.part_ck == 3 ? (hasv ? (const void*)k_part_reg<NG, 1, 3, 5, FX> : (const void*)k_part_reg<NG, 0, 3, 5, FX>)  \
+                     : (hasv ? (const void*)k_part_reg<NG, 1, 4, 8, FX> : (const void*)k_part_reg<NG, 0, 4, 8, FX>);
+#define PH_REG_FN(NG)   \
+  if (p.part_fixed) {   \
+    PH_REG_FX(NG, 1)    \
+  } else {              \
+    PH_REG_FX(NG, 0)    \
+  }
   if (ng == 1) { PH_REG_FN(1) } else if (ng == 2) { PH_REG_FN(2) } else { PH_REG_FN(3) }
 #undef PH_REG_FN
+#undef PH_REG_FX
   if (lds > 64 * 1024) PH_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int n = 0;
   PH_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, kRegBlock, lds));
