@@ -447,8 +447,12 @@ def main():
         last["res"] = r
         last["kernel"] = r.stats.scan_kernel
         if devices:
-            phases.append({"scan": r.stats.device_ms, "merge": r.stats.merge_ms, "finalize": r.stats.finalize_ms,
-                           "devices": r.stats.num_devices})
+            # the call's wall time split into its phases (scan / merge / finalize wall times, and the rest: planning,
+            # layout and result assembly on the host); scan_device = the longest device's scan kernels
+            phases.append({"scan": r.stats.scan_ms, "scan_device": r.stats.device_ms, "merge": r.stats.merge_ms,
+                           "finalize": r.stats.finalize_ms,
+                           "host": r.stats.host_ms - r.stats.scan_ms - r.stats.merge_ms - r.stats.finalize_ms,
+                           "call": r.stats.host_ms, "devices": r.stats.num_devices})
         return r.stats.device_ms, r.stats.mode
 
     phases = []

@@ -219,6 +219,8 @@ typedef struct {
   int32_t num_devices;                     /* devices whose segments the query scanned (multi-device contexts) */
   double merge_ms;                         /* multi-device: combining the devices' partial tables (RCCL / local) */
   double finalize_ms;                      /* multi-device: turning the merged key shards into the result */
+  double scan_ms;                          /* multi-device: wall time of the devices' scans into their partial tables
+                                              (host_ms - scan_ms - merge_ms - finalize_ms = planning + assembly) */
 } ph_exec_stats;
 
 /* ph_exec_stats.scan_kernel */

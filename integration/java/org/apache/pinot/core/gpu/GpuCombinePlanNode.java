@@ -41,12 +41,12 @@ import org.apache.pinot.segment.spi.AggregationFunctionType;
 public class GpuCombinePlanNode extends CombinePlanNode {
   private final long _ctx;
   private final GpuQuery _query;
-  private final long[] _segments;
+  private final GpuSegmentRegistry.Lease _segments;  // released when the launch is done
   private final List<PlanNode> _segmentPlans;
   private final QueryContext _queryContext;
   private final ExecutorService _executorService;
 
-  public GpuCombinePlanNode(long ctx, GpuQuery query, long[] segments, List<PlanNode> segmentPlans,
+  public GpuCombinePlanNode(long ctx, GpuQuery query, GpuSegmentRegistry.Lease segments, List<PlanNode> segmentPlans,
       QueryContext queryContext, ExecutorService executorService) {
     super(segmentPlans, queryContext, executorService, null);
     _ctx = ctx;
@@ -74,9 +74,11 @@ public class GpuCombinePlanNode extends CombinePlanNode {
       long res;
       try {
         res = PinotHipJni.queryExecute(_ctx, _query._descriptor, _query._strings, _query._numGroupsLimit,
-            _query._endTimeMs, _segments);
+            _query._endTimeMs, _segments.handles());
       } catch (UnsupportedOperationException e) {
         return new CombinePlanNode(_segmentPlans, _queryContext, _executorService, null).run().nextBlock();
+      } finally {
+        _segments.close();  // the result lives in host memory: the segments may be unpinned from here on
       }
       try {
         PinotHipJni.resultStats(res, _stats);

@@ -31,14 +31,23 @@ public class GpuInstancePlanMaker extends InstancePlanMakerImplV2 {
   /** HBM the pinned segments may hold per device, in bytes (default: 240 GB of a 288 GB MI355X). */
   public static final String GPU_HBM_BUDGET_KEY = "pinot.server.query.executor.gpu.hbm.budget";
   public static final long DEFAULT_HBM_BUDGET = 240L << 30;
+  /**
+   * "instance" (default): a query whose whole shape the library takes runs as ONE batched launch over all its
+   * segments (GpuCombinePlanNode); "segment": every pinned segment gets its own GPU plan (GpuSegmentPlanNode) and the
+   * stock combine merges them.  Either way, queries the instance plan does not take get the segment-level GPU plans
+   * (their filters on the GPU, SURVEY 8(b) plug point 2).
+   */
+  public static final String GPU_MODE_KEY = "pinot.server.query.executor.gpu.mode";
   private long _ctx;
   private GpuSegmentRegistry _segments;
   private boolean _enabled;
+  private boolean _instanceMode;
 
   @Override
   public void init(PinotConfiguration queryExecutorConfig) {
     super.init(queryExecutorConfig);
     _enabled = queryExecutorConfig.getProperty(GPU_ENABLE_KEY, true);
+    _instanceMode = !"segment".equals(queryExecutorConfig.getProperty(GPU_MODE_KEY, "instance"));
     if (!_enabled) {
       return;  // the stock plan maker, unchanged
     }
@@ -68,20 +77,35 @@ public class GpuInstancePlanMaker extends InstancePlanMakerImplV2 {
   @Override
   public Plan makeInstancePlan(List<IndexSegment> indexSegments, QueryContext queryContext,
       ExecutorService executorService, ServerMetrics serverMetrics) {
+    GpuQuery q = _enabled && _instanceMode ? GpuQuery.compile(queryContext) : null;
+    GpuSegmentRegistry.Lease lease = q == null ? null : _segments.acquire(indexSegments);
+    if (lease == null) {
+      // the stock instance plan, whose per-segment nodes come from makeSegmentPlanNode below (GPU filters)
+      return super.makeInstancePlan(indexSegments, queryContext, executorService, serverMetrics);
+    }
     // the stock per-segment plan nodes: building them applies the query options (numGroupsLimit, trim sizes,
     // InstancePlanMakerImplV2.applyQueryOptions :166-229, called from makeSegmentPlanNode :254) and they are the
     // CPU fallback if the library declines the query at execution time
     List<PlanNode> segmentPlans = new ArrayList<>(indexSegments.size());
     for (IndexSegment segment : indexSegments) {
-      segmentPlans.add(makeSegmentPlanNode(segment, queryContext));
+      segmentPlans.add(super.makeSegmentPlanNode(segment, queryContext));
     }
-    GpuQuery q = _enabled ? GpuQuery.compile(queryContext) : null;
-    long[] handles = q == null ? null : _segments.handles(indexSegments);
-    if (handles == null) {
-      return super.makeInstancePlan(indexSegments, queryContext, executorService, serverMetrics);
-    }
-    GpuCombinePlanNode combine = new GpuCombinePlanNode(_ctx, q, handles, segmentPlans, queryContext, executorService);
+    GpuCombinePlanNode combine = new GpuCombinePlanNode(_ctx, q, lease, segmentPlans, queryContext, executorService);
     return new GlobalPlanImplV0(
         new InstanceResponsePlanNode(combine, indexSegments, Collections.emptyList(), queryContext));
+  }
+
+  /**
+   * SURVEY 8(b) plug point 2 (PlanMaker.makeSegmentPlanNode, PlanMaker.java:53): the stock node (which applies the
+   * per-segment query rewrites) wrapped in the GPU segment plan -- whole query on the GPU when GpuQuery takes it, else
+   * the GPU filter under the reference's own operators; an unpinned segment keeps the stock node.
+   */
+  @Override
+  public PlanNode makeSegmentPlanNode(IndexSegment indexSegment, QueryContext queryContext) {
+    PlanNode stock = super.makeSegmentPlanNode(indexSegment, queryContext);
+    if (!_enabled) {
+      return stock;
+    }
+    return new GpuSegmentPlanNode(_ctx, _segments, indexSegment, queryContext, stock);
   }
 }

@@ -126,6 +126,37 @@ public final class GpuQuery {
     }
   }
 
+  /**
+   * The descriptor of a WHERE clause alone, for ph_filter_execute (GpuFilterOperator): [numFilterNodes, filterRoot,
+   * numPredicates, 0, 0, nodes..., predicates...]; null when a predicate is outside the GPU path.
+   */
+  public static GpuQuery compileFilter(FilterContext filter, long endTimeMs) {
+    Builder b = new Builder();
+    try {
+      int root = b.filter(filter);
+      List<Integer> d = new ArrayList<>();
+      d.add(b._nodes.size());
+      d.add(root);
+      d.add(b._preds.size());
+      d.add(0);
+      d.add(0);
+      for (int[] n : b._nodes) {
+        for (int x : n) {
+          d.add(x);
+        }
+      }
+      for (int[] p : b._preds) {
+        for (int x : p) {
+          d.add(x);
+        }
+      }
+      return new GpuQuery(d.stream().mapToInt(Integer::intValue).toArray(), b._strings.toArray(new String[0]), 0,
+          endTimeMs);
+    } catch (UnsupportedOperationException e) {
+      return null;
+    }
+  }
+
   private static final class Builder {
     final List<int[]> _nodes = new ArrayList<>();
     final List<int[]> _preds = new ArrayList<>();

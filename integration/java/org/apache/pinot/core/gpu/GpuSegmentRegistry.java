@@ -3,6 +3,7 @@ package org.apache.pinot.core.gpu;
 import java.io.File;
 import java.util.List;
 import java.util.concurrent.ConcurrentHashMap;
+import java.util.concurrent.atomic.AtomicInteger;
 import org.apache.pinot.segment.spi.IndexSegment;
 
 
@@ -17,6 +18,11 @@ import org.apache.pinot.segment.spi.IndexSegment;
  * the old entry (the old copy's bytes are released first when the budget is checked), and the old segment's destroy
  * hook then finds an entry that is not its own and leaves it alone.  The HBM budget is enforced per device
  * (ph_segment_device), since the library places each segment on one device of the context.
+ *
+ * A query holds its segments through a Lease (acquire): every entry is reference-counted -- one reference for the
+ * registry, one per in-flight query -- and ph_segment_unpin runs when the LAST reference goes, so a refresh or a destroy
+ * that removes an entry while a query still runs on its handle only drops the registry's reference (the query's
+ * release then unpins).  A lease cannot be taken on an entry whose last reference is already gone.
  */
 public final class GpuSegmentRegistry {
   private static final class Entry {
@@ -24,12 +30,61 @@ public final class GpuSegmentRegistry {
     final long _handle;
     final long _bytes;
     final int _device;
+    final AtomicInteger _refs = new AtomicInteger(1);  // the registry's own reference
 
     Entry(IndexSegment segment, long handle, long bytes, int device) {
       _segment = segment;
       _handle = handle;
       _bytes = bytes;
       _device = device;
+    }
+
+    boolean retain() {
+      for (;;) {
+        int r = _refs.get();
+        if (r == 0) {
+          return false;  // already released by its last holder: unpinned or about to be
+        }
+        if (_refs.compareAndSet(r, r + 1)) {
+          return true;
+        }
+      }
+    }
+
+    void release() {
+      if (_refs.decrementAndGet() == 0) {
+        PinotHipJni.segmentUnpin(_handle);
+      }
+    }
+  }
+
+  /** The device handles of one query's segments, held until close() (idempotent). */
+  public static final class Lease implements AutoCloseable {
+    private final Entry[] _entries;
+    private final long[] _handles;
+    private boolean _closed;
+
+    Lease(Entry[] entries) {
+      _entries = entries;
+      _handles = new long[entries.length];
+      for (int i = 0; i < entries.length; i++) {
+        _handles[i] = entries[i]._handle;
+      }
+    }
+
+    public long[] handles() {
+      return _handles;
+    }
+
+    @Override
+    public synchronized void close() {
+      if (_closed) {
+        return;
+      }
+      _closed = true;
+      for (Entry e : _entries) {
+        e.release();
+      }
     }
   }
 
@@ -86,10 +141,10 @@ public final class GpuSegmentRegistry {
       }
     }
     if (!admitted) {
-      PinotHipJni.segmentUnpin(handle);  // over the device's budget: CPU path
+      PinotHipJni.segmentUnpin(handle);  // over the device's budget: CPU path (never visible to a query)
     }
     if (old != null) {
-      PinotHipJni.segmentUnpin(old._handle);  // segment refresh: the new copy (or the CPU path) replaces the old one
+      old.release();  // segment refresh: the new copy (or the CPU path) replaces the old one once its queries finish
     }
   }
 
@@ -104,7 +159,7 @@ public final class GpuSegmentRegistry {
       _pinned.remove(segment.getSegmentName());
       _held[e._device] -= e._bytes;
     }
-    PinotHipJni.segmentUnpin(e._handle);
+    e.release();  // unpinned now, or by the last query still holding it
   }
 
   private void dropStale(String name, IndexSegment replacement) {
@@ -117,20 +172,26 @@ public final class GpuSegmentRegistry {
       _pinned.remove(name);
       _held[old._device] -= old._bytes;
     }
-    PinotHipJni.segmentUnpin(old._handle);
+    old.release();
   }
 
-  /** Device handles of the query's segments, or null when one of them is not pinned (as this very IndexSegment). */
-  public long[] handles(List<IndexSegment> segments) {
-    long[] out = new long[segments.size()];
+  /**
+   * A lease on the device handles of the query's segments, or null when one of them is not pinned (as this very
+   * IndexSegment).  The caller closes it when its device calls are done.
+   */
+  public Lease acquire(List<IndexSegment> segments) {
+    Entry[] out = new Entry[segments.size()];
     for (int i = 0; i < out.length; i++) {
       IndexSegment s = segments.get(i);
       Entry e = _pinned.get(s.getSegmentName());
-      if (e == null || e._segment != s) {
+      if (e == null || e._segment != s || !e.retain()) {
+        for (int j = 0; j < i; j++) {
+          out[j].release();
+        }
         return null;
       }
-      out[i] = e._handle;
+      out[i] = e;
     }
-    return out;
+    return new Lease(out);
   }
 }

@@ -39,6 +39,14 @@ public final class PinotHipJni {
   static native long queryExecute(long ctx, int[] descriptor, String[] strings, long numGroupsLimit, long endTimeMs,
       long[] segments);
 
+  /**
+   * ph_filter_execute over one segment (GpuFilterOperator): the WHERE clause of `descriptor` (GpuQuery.compileFilter);
+   * docWords (ceil(numDocs / 64) longs, bit i of word w = doc 64 w + i) receives the doc set, or null for the count
+   * alone; statsOut[0] = matching docs, statsOut[1] = numEntriesScannedInFilter.  Returns the matching docs.
+   */
+  static native long filterExecute(long ctx, int[] descriptor, String[] strings, long endTimeMs, long segment,
+      long[] docWords, long[] statsOut);
+
   static native long resultNumGroups(long result);                                       // ph_result_num_groups
   static native int resultKeyType(long result, int groupByIndex);                        // ph_result_key_type
   static native int resultKeyEntrySize(long result, int groupByIndex);                   // ph_result_key_entry_size

@@ -141,7 +141,114 @@ JNIEXPORT void JNICALL FN(tableSetColumnType)(JNIEnv* env, jclass c, jlong ctx, 
  *    per filter node: type, numChildren, predicate, child...,
  *    per predicate: type, column, numValues, value..., lower, upper, lowerInclusive, upperInclusive,
  *    per group-by column: column,
- *    per aggregation: type, column, log2m, column2, exprOp]                                                      */
+ *    per aggregation: type, column, log2m, column2, exprOp,
+ *    optional: numOrderBy, (kind, index, asc) x numOrderBy, limit, minSegmentGroupTrimSize]
+ * decoded into `q`; the arrays it points into are owned by `b` (query_bufs_free).  Returns 0, or -1 for a malformed
+ * descriptor (every read is bounds-checked). */
+typedef struct {
+  ph_filter_node* nodes;
+  ph_predicate* preds;
+  const char** gby;
+  ph_aggregation* aggs;
+  ph_order_by* order;
+  int32_t* ints;
+  const char** vals;
+} query_bufs;
+
+static void query_bufs_free(query_bufs* b) {
+  free(b->nodes); free(b->preds); free(b->gby); free(b->aggs); free(b->ints); free(b->vals); free(b->order);
+}
+
+static int decode_query(const jint* desc, jsize nd, const char** strs, jsize ns, ph_query* q, query_bufs* b) {
+#define S(i) ((i) >= 0 && (i) < ns ? strs[(i)] : NULL)
+#define NEXT(dst)             \
+  do {                        \
+    if (k >= nd) return -1;   \
+    (dst) = desc[k++];        \
+  } while (0)
+  int k = 0, tmp = 0;
+  memset(q, 0, sizeof *q);
+  memset(b, 0, sizeof *b);
+  NEXT(q->num_filter_nodes);
+  NEXT(q->filter_root);
+  NEXT(q->num_predicates);
+  NEXT(q->num_group_by);
+  NEXT(q->num_aggregations);
+  /* every entity takes at least one descriptor int, so a count beyond nd is malformed */
+  if (q->num_filter_nodes < 0 || q->num_predicates < 0 || q->num_group_by < 0 || q->num_aggregations < 0 ||
+      q->num_filter_nodes > nd || q->num_predicates > nd || q->num_group_by > nd || q->num_aggregations > nd)
+    return -1;
+  b->nodes = (ph_filter_node*)calloc((size_t)q->num_filter_nodes + 1, sizeof(ph_filter_node));
+  b->preds = (ph_predicate*)calloc((size_t)q->num_predicates + 1, sizeof(ph_predicate));
+  b->gby = (const char**)calloc((size_t)q->num_group_by + 1, sizeof(char*));
+  b->aggs = (ph_aggregation*)calloc((size_t)q->num_aggregations + 1, sizeof(ph_aggregation));
+  b->ints = (int32_t*)calloc((size_t)nd + 1, sizeof(int32_t)); /* children lists live here (<= nd entries) */
+  b->vals = (const char**)calloc((size_t)nd + 1, sizeof(char*));
+  if (!b->nodes || !b->preds || !b->gby || !b->aggs || !b->ints || !b->vals) return -1;
+  int ki = 0, kv = 0;
+  for (int i = 0; i < q->num_filter_nodes; ++i) {
+    NEXT(b->nodes[i].type);
+    NEXT(b->nodes[i].num_children);
+    NEXT(b->nodes[i].predicate);
+    if (b->nodes[i].num_children < 0 || b->nodes[i].num_children > nd - k) return -1;
+    b->nodes[i].children = b->ints + ki;
+    for (int j = 0; j < b->nodes[i].num_children; ++j) NEXT(b->ints[ki++]);
+  }
+  for (int i = 0; i < q->num_predicates; ++i) {
+    NEXT(b->preds[i].type);
+    NEXT(tmp);
+    b->preds[i].column = S(tmp);
+    NEXT(b->preds[i].num_values);
+    if (b->preds[i].num_values < 0 || b->preds[i].num_values > nd - k) return -1;
+    b->preds[i].values = b->vals + kv;
+    for (int j = 0; j < b->preds[i].num_values; ++j) {
+      NEXT(tmp);
+      b->vals[kv++] = S(tmp);
+    }
+    NEXT(tmp);
+    b->preds[i].lower = S(tmp);
+    NEXT(tmp);
+    b->preds[i].upper = S(tmp);
+    NEXT(b->preds[i].lower_inclusive);
+    NEXT(b->preds[i].upper_inclusive);
+  }
+  for (int i = 0; i < q->num_group_by; ++i) {
+    NEXT(tmp);
+    b->gby[i] = S(tmp);
+  }
+  for (int i = 0; i < q->num_aggregations; ++i) {
+    NEXT(b->aggs[i].type);
+    NEXT(tmp);
+    b->aggs[i].column = S(tmp);
+    NEXT(b->aggs[i].log2m);
+    NEXT(tmp);
+    b->aggs[i].column2 = S(tmp);
+    NEXT(b->aggs[i].expr_op);
+  }
+  if (k < nd) { /* optional trailing block: ORDER BY + LIMIT + minSegmentGroupTrimSize */
+    NEXT(q->num_order_by);
+    if (q->num_order_by < 0 || q->num_order_by > nd - k) return -1;
+    b->order = (ph_order_by*)calloc((size_t)q->num_order_by + 1, sizeof(ph_order_by));
+    if (!b->order) return -1;
+    for (int i = 0; i < q->num_order_by; ++i) {
+      NEXT(b->order[i].kind);
+      NEXT(b->order[i].index);
+      NEXT(b->order[i].asc);
+    }
+    NEXT(q->limit);
+    NEXT(q->min_segment_group_trim_size);
+    q->order_by = b->order;
+  }
+  /* indices inside the query (children, predicates, root) are range-checked by the library itself */
+  q->filter_nodes = b->nodes;
+  q->predicates = b->preds;
+  q->group_by = b->gby;
+  q->aggregations = b->aggs;
+  return 0;
+#undef NEXT
+#undef S
+}
+
 JNIEXPORT jlong JNICALL FN(queryExecute)(JNIEnv* env, jclass c, jlong ctx, jintArray descArr, jobjectArray strArr,
                                          jlong numGroupsLimit, jlong endTimeMs, jlongArray segArr) {
   const jsize nd = (*env)->GetArrayLength(env, descArr);
@@ -150,131 +257,77 @@ JNIEXPORT jlong JNICALL FN(queryExecute)(JNIEnv* env, jclass c, jlong ctx, jintA
   jint* desc = (*env)->GetIntArrayElements(env, descArr, NULL);
   utf_strings us = {0, NULL, NULL};
   const int strs_ok = utf_strings_get(env, strArr, &us);
-  const jsize ns = us.n;
-  const char** strs = us.strs;
-#define S(i) ((i) >= 0 && (i) < ns ? strs[(i)] : NULL)
-  /* every read of the descriptor is bounds-checked: a malformed one throws IllegalArgumentException */
-#define NEXT(dst)              \
-  do {                         \
-    if (k >= nd) goto bad;     \
-    (dst) = desc[k++];         \
-  } while (0)
-  int k = 0, tmp = 0;
   ph_query q;
-  memset(&q, 0, sizeof q);
-  ph_filter_node* nodes = NULL;
-  ph_predicate* preds = NULL;
-  const char** gby = NULL;
-  ph_aggregation* aggs = NULL;
-  ph_order_by* order = NULL;
-  int32_t* ints = NULL;
-  const char** vals = NULL;
+  query_bufs qb;
+  memset(&qb, 0, sizeof qb);
   ph_result* res = NULL;
   int rc = PH_ERR_INVALID_ARGUMENT;
-  if (!desc || !strs_ok) goto done;
-  NEXT(q.num_filter_nodes);
-  NEXT(q.filter_root);
-  NEXT(q.num_predicates);
-  NEXT(q.num_group_by);
-  NEXT(q.num_aggregations);
-  /* every entity takes at least one descriptor int, so a count beyond nd is malformed */
-  if (q.num_filter_nodes < 0 || q.num_predicates < 0 || q.num_group_by < 0 || q.num_aggregations < 0 ||
-      q.num_filter_nodes > nd || q.num_predicates > nd || q.num_group_by > nd || q.num_aggregations > nd)
-    goto bad;
-  nodes = (ph_filter_node*)calloc((size_t)q.num_filter_nodes + 1, sizeof(ph_filter_node));
-  preds = (ph_predicate*)calloc((size_t)q.num_predicates + 1, sizeof(ph_predicate));
-  gby = (const char**)calloc((size_t)q.num_group_by + 1, sizeof(char*));
-  aggs = (ph_aggregation*)calloc((size_t)q.num_aggregations + 1, sizeof(ph_aggregation));
-  ints = (int32_t*)calloc((size_t)nd + 1, sizeof(int32_t)); /* children lists live here (<= nd entries) */
-  vals = (const char**)calloc((size_t)nd + 1, sizeof(char*));
-  if (!nodes || !preds || !gby || !aggs || !ints || !vals) goto done;
-  {
-    int ki = 0, kv = 0;
-    for (int i = 0; i < q.num_filter_nodes; ++i) {
-      NEXT(nodes[i].type);
-      NEXT(nodes[i].num_children);
-      NEXT(nodes[i].predicate);
-      if (nodes[i].num_children < 0 || nodes[i].num_children > nd - k) goto bad;
-      nodes[i].children = ints + ki;
-      for (int j = 0; j < nodes[i].num_children; ++j) NEXT(ints[ki++]);
-    }
-    for (int i = 0; i < q.num_predicates; ++i) {
-      NEXT(preds[i].type);
-      NEXT(tmp);
-      preds[i].column = S(tmp);
-      NEXT(preds[i].num_values);
-      if (preds[i].num_values < 0 || preds[i].num_values > nd - k) goto bad;
-      preds[i].values = vals + kv;
-      for (int j = 0; j < preds[i].num_values; ++j) {
-        NEXT(tmp);
-        vals[kv++] = S(tmp);
+  if (desc && strs_ok) {
+    if (decode_query(desc, nd, us.strs, us.n, &q, &qb) != 0) {
+      throw_illegal(env, "malformed GPU query descriptor");
+    } else {
+      q.num_groups_limit = numGroupsLimit;
+      q.end_time_ms = endTimeMs;
+      const jsize nseg = (*env)->GetArrayLength(env, segArr);
+      jlong* segs = (*env)->GetLongArrayElements(env, segArr, NULL);
+      ph_segment** sp = (ph_segment**)calloc((size_t)(nseg ? nseg : 1), sizeof(ph_segment*));
+      if (segs && sp) {
+        for (jsize i = 0; i < nseg; ++i) sp[i] = (ph_segment*)PTR(segs[i]);
+        rc = ph_query_execute(PTR(ctx), &q, sp, (int32_t)nseg, &res);
       }
-      NEXT(tmp);
-      preds[i].lower = S(tmp);
-      NEXT(tmp);
-      preds[i].upper = S(tmp);
-      NEXT(preds[i].lower_inclusive);
-      NEXT(preds[i].upper_inclusive);
-    }
-    for (int i = 0; i < q.num_group_by; ++i) {
-      NEXT(tmp);
-      gby[i] = S(tmp);
-    }
-    for (int i = 0; i < q.num_aggregations; ++i) {
-      NEXT(aggs[i].type);
-      NEXT(tmp);
-      aggs[i].column = S(tmp);
-      NEXT(aggs[i].log2m);
-      NEXT(tmp);
-      aggs[i].column2 = S(tmp);
-      NEXT(aggs[i].expr_op);
+      free(sp);
+      if (segs) (*env)->ReleaseLongArrayElements(env, segArr, segs, JNI_ABORT);
     }
   }
-  /* optional trailing block: [numOrderBy, (kind, index, asc) x numOrderBy, limit, minSegmentGroupTrimSize] */
-  if (k < nd) {
-    NEXT(q.num_order_by);
-    if (q.num_order_by < 0 || q.num_order_by > nd - k) goto bad;
-    order = (ph_order_by*)calloc((size_t)q.num_order_by + 1, sizeof(ph_order_by));
-    if (!order) goto bad;
-    for (int i = 0; i < q.num_order_by; ++i) {
-      NEXT(order[i].kind);
-      NEXT(order[i].index);
-      NEXT(order[i].asc);
-    }
-    NEXT(q.limit);
-    NEXT(q.min_segment_group_trim_size);
-    q.order_by = order;
-  }
-  /* indices inside the query (children, predicates, root) are range-checked by ph_query_execute itself */
-  q.filter_nodes = nodes;
-  q.predicates = preds;
-  q.group_by = gby;
-  q.aggregations = aggs;
-  q.num_groups_limit = numGroupsLimit;
-  q.end_time_ms = endTimeMs;
-  {
-    const jsize nseg = (*env)->GetArrayLength(env, segArr);
-    jlong* segs = (*env)->GetLongArrayElements(env, segArr, NULL);
-    ph_segment** sp = (ph_segment**)calloc((size_t)(nseg ? nseg : 1), sizeof(ph_segment*));
-    if (segs && sp) {
-      for (jsize i = 0; i < nseg; ++i) sp[i] = (ph_segment*)PTR(segs[i]);
-      rc = ph_query_execute(PTR(ctx), &q, sp, (int32_t)nseg, &res);
-    }
-    free(sp);
-    if (segs) (*env)->ReleaseLongArrayElements(env, segArr, segs, JNI_ABORT);
-  }
-  goto done;
-bad:
-  throw_illegal(env, "malformed GPU query descriptor");
-done:
-  free(nodes); free(preds); free(gby); free(aggs); free(ints); free(vals); free(order);
+  query_bufs_free(&qb);
   utf_strings_release(env, &us);
   if (desc) (*env)->ReleaseIntArrayElements(env, descArr, desc, JNI_ABORT);
   (*env)->PopLocalFrame(env, NULL);
-#undef NEXT
-#undef S
   if (!(*env)->ExceptionCheck(env)) throw_ph(env, rc);
   return (jlong)(intptr_t)res;
+}
+
+/* ph_filter_execute over one segment (GpuFilterOperator): the doc bitmap straight into the Java long[] (bit i of word
+ * w = doc 64 w + i: the java.util.BitSet / BitSetUtil.bitmapOf layout), or the count alone when docWords is null;
+ * statsOut = {matching docs, numEntriesScannedInFilter} */
+JNIEXPORT jlong JNICALL FN(filterExecute)(JNIEnv* env, jclass c, jlong ctx, jintArray descArr, jobjectArray strArr,
+                                          jlong endTimeMs, jlong segment, jlongArray wordsArr, jlongArray statsArr) {
+  const jsize nd = (*env)->GetArrayLength(env, descArr);
+  const jsize ns0 = strArr ? (*env)->GetArrayLength(env, strArr) : 0;
+  if ((*env)->PushLocalFrame(env, ns0 + 16) != 0) return 0;
+  jint* desc = (*env)->GetIntArrayElements(env, descArr, NULL);
+  utf_strings us = {0, NULL, NULL};
+  const int strs_ok = utf_strings_get(env, strArr, &us);
+  ph_query q;
+  query_bufs qb;
+  memset(&qb, 0, sizeof qb);
+  ph_exec_stats st;
+  memset(&st, 0, sizeof st);
+  int rc = PH_ERR_INVALID_ARGUMENT;
+  if (desc && strs_ok) {
+    if (decode_query(desc, nd, us.strs, us.n, &q, &qb) != 0) {
+      throw_illegal(env, "malformed GPU filter descriptor");
+    } else {
+      q.end_time_ms = endTimeMs;
+      const jsize nw = wordsArr ? (*env)->GetArrayLength(env, wordsArr) : 0;
+      /* critical section: the library writes the words in place (one D2H copy, no JNI copy-back) */
+      jlong* words = wordsArr ? (jlong*)(*env)->GetPrimitiveArrayCritical(env, wordsArr, NULL) : NULL;
+      if (!wordsArr || words) {
+        rc = ph_filter_execute(PTR(ctx), &q, (ph_segment*)PTR(segment), (uint64_t*)words, (uint64_t)nw, &st);
+        if (words) (*env)->ReleasePrimitiveArrayCritical(env, wordsArr, words, 0);
+      }
+    }
+  }
+  query_bufs_free(&qb);
+  utf_strings_release(env, &us);
+  if (desc) (*env)->ReleaseIntArrayElements(env, descArr, desc, JNI_ABORT);
+  (*env)->PopLocalFrame(env, NULL);
+  if ((*env)->ExceptionCheck(env) || throw_ph(env, rc)) return 0;
+  if (statsArr) {
+    const jlong v[2] = {st.num_docs_scanned, st.num_entries_scanned_in_filter};
+    (*env)->SetLongArrayRegion(env, statsArr, 0, 2, v);
+  }
+  return st.num_docs_scanned;
 }
 
 JNIEXPORT jlong JNICALL FN(resultNumGroups)(JNIEnv* env, jclass c, jlong res) { return ph_result_num_groups(PTR(res)); }

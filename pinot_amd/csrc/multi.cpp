@@ -19,6 +19,8 @@
 
 #include <chrono>
 #include <cstring>
+#include <exception>
+#include <map>
 #include <thread>
 
 #include <rccl/rccl.h>
@@ -80,12 +82,74 @@ double ms_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
 
+constexpr size_t kLayoutCacheEntries = 64;
+
+// A device scratch block of one call, back to its context's pool when the call ends (after a throw, only once the
+// device is idle: a collective or copy may still write it)
+struct ScratchHold {
+  Context* c = nullptr;
+  std::unique_ptr<DeviceBuffer> b;
+  ScratchHold() = default;
+  ScratchHold(Context* ctx, size_t n) : c(ctx), b(ctx->scratch_acquire(n)) {}
+  ScratchHold(ScratchHold&&) = default;
+  ScratchHold& operator=(ScratchHold&&) = default;
+  ~ScratchHold() {
+    if (!b) return;
+    if (std::uncaught_exceptions() > 0) {
+      (void)hipSetDevice(c->device);
+      (void)hipDeviceSynchronize();
+    }
+    c->scratch_release(std::move(b));
+  }
+  void* ptr() const { return b->ptr; }
+};
+
+// the layout cache key: what ph_query_dense_layout's answer depends on -- the group-by columns and aggregations, the
+// segments (their column types and dictionaries), and the table dictionaries in force (their ids change when replaced)
+std::string layout_key(ph_ctx* x, const ph_query* q, const std::vector<ph_segment*>& all) {
+  std::string k;
+  auto add = [&](const char* s) {
+    k += s ? s : "\x01";
+    k += '\0';
+  };
+  for (int g = 0; g < q->num_group_by; ++g) {
+    add(q->group_by[g]);
+    for (Context* c : x->devs) {
+      std::lock_guard<std::mutex> lk(c->mu);
+      auto it = c->table_dicts.find(q->group_by[g]);
+      k += std::to_string(it == c->table_dicts.end() ? 0 : it->second->id) + ",";
+    }
+  }
+  k += "|";
+  for (int a = 0; a < q->num_aggregations; ++a) {
+    const ph_aggregation& g = q->aggregations[a];
+    k += std::to_string(g.type) + "," + std::to_string(g.log2m) + "," + std::to_string(g.expr_op) + ",";
+    add(g.column);
+    add(g.column2);
+  }
+  k += "|";
+  for (ph_segment* s : all) k += std::to_string(s->id) + ",";
+  return k;
+}
+
 }  // namespace
+
+// The dense layout of a query shape over a segment set (and the per-device copies of the group-by unions when the
+// devices have no table-level dictionaries): a planning pass over every segment, kept per (shape, segments,
+// dictionaries) so a repeated query plans it once (r5: the layout pass, the unions and the per-query allocations were
+// most of the ~10 ms of host time of a --devices 0,0 config-3 step)
+struct LayoutEntry {
+  ph_dense_layout layout{};
+  bool have_tables = true;
+  std::vector<std::vector<std::shared_ptr<GlobalDict>>> dicts;  // [device][group-by column] (!have_tables)
+};
 
 struct MultiState {
   std::mutex place_mu;          // segment placement
   std::mutex comm_mu;           // communicator creation / use (one collective sequence at a time)
   std::vector<ncclComm_t> comms;  // one per device (distinct ordinals only), created on first use
+  std::mutex layout_mu;
+  std::map<std::string, std::shared_ptr<LayoutEntry>> layouts;  // bounded: cleared at kLayoutCacheEntries
   ~MultiState() {
     if (!comms.empty())
       for (auto c : comms) rccl().destroy(c);
@@ -171,25 +235,38 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
     const int k = active.empty() ? 0 : active[0];
     return query_execute_impl(x->devs[k], q, by[k].data(), (int32_t)by[k].size(), nullptr);
   }
-  // group-by dictionaries: the table-level ones where every device has them, else one union over every device's
-  // segments -- a separate copy per device (their device-side caches live on that device)
-  bool have_tables = true;
-  for (int g = 0; g < q->num_group_by; ++g)
-    for (Context* c : x->devs) {
-      std::lock_guard<std::mutex> lk(c->mu);
-      have_tables &= c->table_dicts.count(q->group_by[g]) > 0;
-    }
-  std::vector<std::vector<std::shared_ptr<GlobalDict>>> dicts(D);
-  if (!have_tables)
-    for (int g = 0; g < q->num_group_by; ++g) {
-      auto u = union_dictionary(q->group_by[g], all);
-      for (int k = 0; k < D; ++k) {
-        auto c = std::make_shared<GlobalDict>();
-        c->dict = u->dict;
-        c->id = next_object_id();
-        dicts[k].push_back(std::move(c));
+  // the layout (and the group-by unions), planned once per query shape and segment set
+  const std::string lkey = layout_key(x, q, all);
+  std::shared_ptr<LayoutEntry> lay;
+  {
+    std::lock_guard<std::mutex> lk(x->multi->layout_mu);
+    auto it = x->multi->layouts.find(lkey);
+    if (it != x->multi->layouts.end()) lay = it->second;
+  }
+  const bool fresh = !lay;
+  if (fresh) {
+    lay = std::make_shared<LayoutEntry>();
+    // group-by dictionaries: the table-level ones where every device has them, else one union over every device's
+    // segments -- a separate copy per device (their device-side caches live on that device)
+    for (int g = 0; g < q->num_group_by; ++g)
+      for (Context* c : x->devs) {
+        std::lock_guard<std::mutex> lk(c->mu);
+        lay->have_tables &= c->table_dicts.count(q->group_by[g]) > 0;
       }
-    }
+    lay->dicts.resize(D);
+    if (!lay->have_tables)
+      for (int g = 0; g < q->num_group_by; ++g) {
+        auto u = union_dictionary(q->group_by[g], all);
+        for (int k = 0; k < D; ++k) {
+          auto c = std::make_shared<GlobalDict>();
+          c->dict = u->dict;
+          c->id = next_object_id();
+          lay->dicts[k].push_back(std::move(c));
+        }
+      }
+  }
+  const bool have_tables = lay->have_tables;
+  std::vector<std::vector<std::shared_ptr<GlobalDict>>>& dicts = lay->dicts;
   auto dense = [&](int k, int op) {
     DenseArgs a{op, nullptr, 0, 0, nullptr};
     if (!have_tables) a.dicts = &dicts[k];
@@ -211,15 +288,21 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
     r->stats.host_ms = ms_since(t0);
     return r;
   };
-  ph_dense_layout L{};
-  try {
-    DenseArgs la = dense(active[0], DENSE_LAYOUT);
-    la.layout = &L;
-    query_execute_impl(x->devs[active[0]], q, by[active[0]].data(), (int32_t)by[active[0]].size(), &la);
-  } catch (const Error& e) {
-    if (e.code != PH_ERR_UNSUPPORTED) throw;
-    return host_merge();
+  if (fresh) {
+    try {
+      DenseArgs la = dense(active[0], DENSE_LAYOUT);
+      la.layout = &lay->layout;
+      query_execute_impl(x->devs[active[0]], q, by[active[0]].data(), (int32_t)by[active[0]].size(), &la);
+    } catch (const Error& e) {
+      if (e.code != PH_ERR_UNSUPPORTED) throw;
+      lay->layout.num_groups = -1;  // remembered: this shape merges by value
+    }
+    std::lock_guard<std::mutex> lk(x->multi->layout_mu);
+    if (x->multi->layouts.size() >= kLayoutCacheEntries) x->multi->layouts.clear();
+    x->multi->layouts[lkey] = lay;
   }
+  const ph_dense_layout& L = lay->layout;
+  if (L.num_groups < 0) return host_merge();
   if (getenv("PH_MULTI_HOST_MERGE")) return host_merge();  // the value-keyed merge, forced (tests)
   const int64_t G = L.num_groups;
   if (G <= 0) return host_merge();
@@ -227,19 +310,21 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
   int64_t S = (G + D - 1) / D;
   S = (S + 63) / 64 * 64;
   const int64_t padded = S * D;
-  // ---- scan: every device fills its tables (identities where it has no segment, and in the padding rows)
-  std::vector<std::vector<std::unique_ptr<DeviceBuffer>>> T(D);
+  // ---- scan: every device fills its tables (identities where it has no segment, and in the padding rows); the
+  // tables come from the devices' scratch pools (no hipMalloc / hipFree per query), and the identity fill of the rows
+  // the scan never writes runs beside the scan on a stream of its own, drained before the merge reads them
+  std::vector<std::vector<ScratchHold>> T(D);
   std::vector<ph_exec_stats> st(D);
   std::vector<int> every(D);
   for (int k = 0; k < D; ++k) every[k] = k;
+  const auto t_plan = clock::now();
   per_device(every, [&](int k) {
     Context& c = *x->devs[k];
     PH_HIP_CHECK(hipSetDevice(c.device));
     std::vector<void*> ptrs;
     for (int t = 0; t < L.num_tables; ++t) {
-      T[k].push_back(std::make_unique<DeviceBuffer>());
-      T[k].back()->alloc((size_t)padded * L.elems_per_group[t] * L.elem_bytes[t], c.device);
-      ptrs.push_back(T[k].back()->ptr);
+      T[k].emplace_back(&c, (size_t)padded * L.elems_per_group[t] * L.elem_bytes[t]);
+      ptrs.push_back(T[k].back().ptr());
     }
     LaneGuard lg(&c);
     const hipStream_t sk = lg.lane->stream;
@@ -249,13 +334,13 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
       launch_fill_identity(static_cast<uint8_t*>(ptrs[t]) + (size_t)live * per * L.elem_bytes[t], (padded - live) * per,
                            L.reduce_op[t], sk);
     }
-    PH_HIP_CHECK(hipStreamSynchronize(sk));
     if (!by[k].empty()) {
       DenseArgs ea = dense(k, DENSE_EXECUTE);
       ea.tables = ptrs.data();
       std::unique_ptr<ph_result> r(query_execute_impl(&c, q, by[k].data(), (int32_t)by[k].size(), &ea));
       st[k] = r->stats;
     }
+    PH_HIP_CHECK(hipStreamSynchronize(sk));
   });
   const auto t_scan = clock::now();
   // ---- merge: a reduce-scatter of every table by key shard, so device k owns the fully merged shard [k S, (k + 1) S)
@@ -268,13 +353,10 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
     for (int b = a + 1; b < D; ++b) distinct &= x->ordinals[a] != x->ordinals[b];
   const bool use_rccl = distinct && x->transport == PH_TRANSPORT_RCCL;
   std::vector<std::pair<int, std::pair<int64_t, int64_t>>> shards;  // (device, [g0, g1)) to finalise
-  std::vector<std::vector<std::unique_ptr<DeviceBuffer>>> R(D);       // reduce-scatter outputs
+  std::vector<std::vector<ScratchHold>> R(D);  // reduce-scatter outputs
   for (int k = 0; k < D; ++k) {
     PH_HIP_CHECK(hipSetDevice(x->ordinals[k]));
-    for (int t = 0; t < L.num_tables; ++t) {
-      R[k].push_back(std::make_unique<DeviceBuffer>());
-      R[k].back()->alloc((size_t)S * L.elems_per_group[t] * L.elem_bytes[t], x->ordinals[k]);
-    }
+    for (int t = 0; t < L.num_tables; ++t) R[k].emplace_back(x->devs[k], (size_t)S * L.elems_per_group[t] * L.elem_bytes[t]);
   }
   if (use_rccl) {
     const Rccl& api = rccl();
@@ -289,7 +371,7 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
     nccl_check(api.group_start(), "ncclGroupStart");
     for (int t = 0; t < L.num_tables; ++t)
       for (int k = 0; k < D; ++k)
-        nccl_check(api.reduce_scatter(T[k][t]->ptr, R[k][t]->ptr, (size_t)S * L.elems_per_group[t],
+        nccl_check(api.reduce_scatter(T[k][t].ptr(), R[k][t].ptr(), (size_t)S * L.elems_per_group[t],
                                       nccl_type(L.reduce_op[t]), nccl_op(L.reduce_op[t]), x->multi->comms[k],
                                       lanes[k]->lane->stream),
                    "ncclReduceScatter");
@@ -304,28 +386,26 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
       PH_HIP_CHECK(hipSetDevice(c.device));
       LaneGuard lg(&c);
       const hipStream_t sk = lg.lane->stream;
+      // one staging block per table (all copies and folds in flight on one stream, drained once at the end)
+      std::vector<ScratchHold> tmp;
       for (int t = 0; t < L.num_tables; ++t) {
         const size_t eb = (size_t)L.elems_per_group[t] * L.elem_bytes[t];
         const size_t bytes = (size_t)S * eb;
-        std::unique_ptr<DeviceBuffer> tmp;
         bool first = true;
         for (int j = 0; j < D; ++j) {
-          const uint8_t* src = static_cast<const uint8_t*>(T[j][t]->ptr) + (size_t)k * S * eb;
+          const uint8_t* src = static_cast<const uint8_t*>(T[j][t].ptr()) + (size_t)k * S * eb;
           if (first) {  // device j's shard k seeds the output (identities where j has no segments)
-            PH_HIP_CHECK(hipMemcpyPeerAsync(R[k][t]->ptr, c.device, src, x->ordinals[j], bytes, sk));
+            PH_HIP_CHECK(hipMemcpyPeerAsync(R[k][t].ptr(), c.device, src, x->ordinals[j], bytes, sk));
             first = false;
             continue;
           }
           if (by[j].empty()) continue;  // identities only
-          if (!tmp) {
-            tmp = std::make_unique<DeviceBuffer>();
-            tmp->alloc(bytes, c.device);
-          }
-          PH_HIP_CHECK(hipMemcpyPeerAsync(tmp->ptr, c.device, src, x->ordinals[j], bytes, sk));
-          launch_reduce_table(R[k][t]->ptr, tmp->ptr, (int64_t)S * L.elems_per_group[t], L.reduce_op[t], sk);
+          tmp.emplace_back(&c, bytes);
+          PH_HIP_CHECK(hipMemcpyPeerAsync(tmp.back().ptr(), c.device, src, x->ordinals[j], bytes, sk));
+          launch_reduce_table(R[k][t].ptr(), tmp.back().ptr(), (int64_t)S * L.elems_per_group[t], L.reduce_op[t], sk);
         }
-        PH_HIP_CHECK(hipStreamSynchronize(sk));  // tmp is reused / freed: the stream drains per table
       }
+      PH_HIP_CHECK(hipStreamSynchronize(sk));
     });
   }
   for (int k = 0; k < D; ++k) {
@@ -341,17 +421,16 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
     int k = shards[i].first;
     const int64_t g0 = shards[i].second.first, g1 = shards[i].second.second;
     std::vector<void*> ptrs;
-    std::vector<std::unique_ptr<DeviceBuffer>> moved;
-    for (int t = 0; t < L.num_tables; ++t) ptrs.push_back(R[k][t]->ptr);
+    std::vector<ScratchHold> moved;
+    for (int t = 0; t < L.num_tables; ++t) ptrs.push_back(R[k][t].ptr());
     if (by[k].empty()) {
       const int to = active[0];
       PH_HIP_CHECK(hipSetDevice(x->ordinals[to]));
       for (int t = 0; t < L.num_tables; ++t) {
         const size_t bytes = (size_t)(g1 - g0) * L.elems_per_group[t] * L.elem_bytes[t];
-        moved.push_back(std::make_unique<DeviceBuffer>());
-        moved.back()->alloc(bytes, x->ordinals[to]);
-        PH_HIP_CHECK(hipMemcpyPeer(moved.back()->ptr, x->ordinals[to], ptrs[t], x->ordinals[k], bytes));
-        ptrs[t] = moved.back()->ptr;
+        moved.emplace_back(x->devs[to], bytes);
+        PH_HIP_CHECK(hipMemcpyPeer(moved.back().ptr(), x->ordinals[to], ptrs[t], x->ordinals[k], bytes));
+        ptrs[t] = moved.back().ptr();
       }
       k = to;
     }
@@ -410,6 +489,7 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
   }
   for (auto& p : parts) s.sum_precision_flag |= p->stats.sum_precision_flag;
   s.num_devices = (int32_t)active.size();
+  s.scan_ms = std::chrono::duration<double, std::milli>(t_scan - t_plan).count();
   s.merge_ms = std::chrono::duration<double, std::milli>(t_merge - t_scan).count();
   s.finalize_ms = std::chrono::duration<double, std::milli>(t_fin - t_merge).count();
   s.host_ms = ms_since(t0);

@@ -318,8 +318,7 @@ struct KParams {
   int32_t part_depth;             // lean kernel A: tiles of loads in flight per wave (1: k_part_scan, 2: k_part_scan2)
   int32_t part_reg;               // kernel A = k_part_reg (register-direct decode; 0: the LDS-staged forms)
   int32_t part_ck, part_cv;       // k_part_reg: 16-byte loads per lane of a filter / key stream, of the value stream
-  int32_t part_fixed;             // k_part_reg: P <= 256, 32-slot rings, regions of a workgroup < 2 GiB -> the fixed-count
-                                  // buffer-store flush (part_flush_fixed)
+  int32_t part_sets;              // k_part_reg: ring sets (2: append and flush overlap; 1: half the LDS, more workgroups)
   int32_t count_reg;              // MODE_COUNT: k_count_reg with this many 16-byte loads per lane (ceil(b / 4)); 0 off
   int32_t agg_reg;                // MODE_AGG: k_agg_reg (register-direct k_agg_lean)
   int32_t agg_reg_cf, agg_reg_cv; //   16-byte loads per lane of the filter / value stream

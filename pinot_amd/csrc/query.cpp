@@ -2737,12 +2737,25 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       // offset: the shift itself drops the partition bits); the LDS-staged forms keep the key's low klo bits masked
       kp.part_vbits = kp.part_reg ? 32 - klo : vbits;
       kp.num_parts = (int32_t)P;
-      const size_t lds_a = partition_lds_bytes(kp);
-      // (tentative, for the occupancy query; the region-size condition is checked once the capacity is known)
-      kp.part_fixed = kp.part_reg && P <= kRegBlock && kp.part_slot_log2 == 5 && !rec64 &&
-                      getenv("PH_PART_FIXED0") == nullptr;
+      kp.part_sets = 2;
+      size_t lds_a = partition_lds_bytes(kp);
       int a_cap = 4;  // 8-wave workgroups: <= 4 per CU (32 waves)
-      if (kp.part_reg) a_cap = part_reg_blocks_per_cu(kp, q->num_group_by, lds_a);  // 4-wave groups, VGPR-bound
+      if (kp.part_reg) {
+        a_cap = part_reg_blocks_per_cu(kp, q->num_group_by, lds_a);  // 4-wave groups, VGPR-bound
+        // one ring set when it lets more workgroups share a CU (the two sets' LDS is what limits them)
+        KParams k1 = kp;
+        k1.part_sets = 1;
+        const size_t lds1 = partition_lds_bytes(k1);
+        const int cap1 = part_reg_blocks_per_cu(k1, q->num_group_by, lds1);
+        const size_t per2 = std::min<size_t>(a_cap, (160 * 1024) / lds_a), per1 = std::min<size_t>(cap1, (160 * 1024) / lds1);
+        int force = 0;
+        if (const char* e = getenv("PH_PART_SETS")) force = atoi(e);  // tuning knob
+        if (force == 1 || (force != 2 && per1 > per2)) {
+          kp = k1;
+          lds_a = lds1;
+          a_cap = cap1;
+        }
+      }
       if (const char* e = getenv("PH_PART_WG_PER_CU")) a_cap = std::max(1, std::min(8, atoi(e)));  // tuning knob
       const int a_per_cu = (int)std::max<size_t>(1, std::min<size_t>(a_cap, (160 * 1024) / lds_a));
       const int grid_a = ctx->num_cus * a_per_cu;
@@ -2792,7 +2805,6 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       kp.part_cap = (int32_t)cap;
       // k_part_reg's fixed-count flush: thread t owns partition t, 32-slot rings, a workgroup's regions addressable
       // by one buffer descriptor
-      kp.part_fixed = kp.part_fixed && (double)P * (double)cap * 4.0 < 2147483647.0;
       kp.part_vbase = nvals ? vmin : 0;
       kp.lds_bytes = (int32_t)lds_a;
       PartAggParams bp{};

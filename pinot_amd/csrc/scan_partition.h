@@ -142,71 +142,4 @@ __device__ __forceinline__ void part_flush_owner(const KParams& p, uint8_t* smem
   }
 }
 
-// k_part_reg's in-loop flush when thread t owns partition t (P <= BLOCK) and rings hold C = 32 records: every wave
-// issues EXACTLY 8 buffer stores per call -- a lane's two possible 64-byte chunks, 4 x 16 bytes each -- whatever its
-// partition holds; a chunk that does not go out gets an offset past the descriptor's range, which the hardware drops
-// without a memory access.  vmcnt counts loads and stores together in issue order, and the compiler can only wait
-// for the next tile's loads (issued before the append rounds) with vmcnt(stores issued after them) when every path
-// issues the same number of stores: with the data-dependent store loops of part_flush_owner the minimum over paths
-// is 0, so the decode's waits were vmcnt(k) counting the loads alone -- every wave waited for its own flush stores
-// before decoding the next tile (r5: kernel A 2.21 ms with the stores, 1.56 ms without).  The stores address the
-// workgroup's regions through one buffer descriptor (partition b's region at byte b * cap * 4; built here, not held
-// across the caller's lambda: a captured descriptor put the kernel's register arrays in scratch).
-template <int BLOCK>
-__device__ __forceinline__ void part_flush_fixed(const KParams& p, uint8_t* smem, unsigned long long& matched, int set) {
-  uint32_t* slots = reinterpret_cast<uint32_t*>(smem + p.pl_slot_off) + (size_t)set * p.part_set_words;
-  uint32_t* pend = reinterpret_cast<uint32_t*>(smem + p.pl_lcnt_off) + (size_t)set * (p.num_parts + 64);
-  uint32_t* gpos = reinterpret_cast<uint32_t*>(smem + p.pl_bcnt_off);
-  const uint32_t cap = (uint32_t)p.part_cap;
-  const uint32_t P = (uint32_t)p.num_parts;
-  const uint64_t span = (uint64_t)P * (uint64_t)cap * 4u;  // < 2^31 (checked by the host)
-  const uint64_t base = (uint64_t)(uintptr_t)p.part_buf + (uint64_t)blockIdx.x * span;
-  // (readfirstlane returns int: each half goes through uint32_t, or a low half >= 2^31 would sign-extend into the high)
-  const uint32_t base_lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)base);
-  const uint32_t base_hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-  const uint32_t nbytes = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)span);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>((uintptr_t)(((uint64_t)base_hi << 32) | (uint64_t)base_lo)), 0, (int)nbytes, 0x00020000);
-  const uint32_t b = threadIdx.x;
-  const bool own = b < P;
-  const uint32_t bb = own ? b : 0u;
-  const uint32_t raw = own ? pend[bb] : 0u;
-  const uint32_t n = min(raw, 32u);  // records beyond C = 32 went to the overflow table
-  const uint32_t out = raw >= 16u ? (n & ~15u) : 0u, left = n - out;
-  const uint32_t g = gpos[bb];
-  uint32_t* ring = slots + (size_t)bb * (uint32_t)p.part_ring_stride;
-  u32x4 q[8];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) q[e] = *reinterpret_cast<const u32x4*>(ring + 4 * e);
-  if (out == 32u) {
-#pragma unroll
-    for (int e = 4; e < 8; ++e) q[e] = *reinterpret_cast<const u32x4*>(ring + 4 * e);
-  }
-  const uint32_t rbase = bb * cap;  // this partition's region, in records from the workgroup's first region
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const uint32_t k = (uint32_t)(e >> 2) * 16u;  // the chunk's first record
-    const bool go = own && k < out && g + k + 16u <= cap;
-    const uint32_t vo = go ? (rbase + g + k + 4u * (uint32_t)(e & 3)) * 4u : 0x80000000u;
-    __builtin_amdgcn_raw_buffer_store_b128(q[e], rs, vo, 0, 0);
-  }
-  if (own && out && g + out > cap) {  // a region full (skewed keys): the chunks that did not fit, record by record
-    for (uint32_t k = 0; k < out; k += 16u)
-      if (g + k + 16u > cap)
-        for (uint32_t e = 0; e < 16u; ++e) part_store<0>(p, b, g + k + e, ring[k + e]);
-  }
-  if (own && out && left) {  // the partial chunk to the front of the ring (whole 16-byte quarters)
-    u32x4 l[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) l[e] = *reinterpret_cast<const u32x4*>(ring + out + 4 * e);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) *reinterpret_cast<u32x4*>(ring + 4 * e) = l[e];
-  }
-  if (own && raw >= 16u) {
-    pend[b] = left;
-    gpos[b] = g + out;
-    matched += raw - n;
-  }
-}
-
 }  // namespace ph

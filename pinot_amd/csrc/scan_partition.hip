@@ -29,7 +29,7 @@ size_t partition_lds_bytes(KParams& p) {
   p.part_ring_stride = p.part_reg ? (1 << cl) + 4 : (1 << cl);
   // + one scratch slot and one scratch word per lane: k_part_scan appends misses there (branch-free); k_part_reg has
   // two ring sets (a round appends to one while the other's completed chunks go out)
-  const int sets = p.part_reg ? 2 : 1;
+  const int sets = p.part_reg ? (p.part_sets == 1 ? 1 : 2) : 1;
   p.part_set_words = (int32_t)((size_t)p.num_parts * p.part_ring_stride + 64);
   place(p.pl_slot_off, (size_t)sets * p.part_set_words * rec);
   // generic kernel: (flushed / CH << 16 | pending) per partition; lean kernel: pending per partition
@@ -414,99 +414,142 @@ __global__ void __launch_bounds__(1024) k_part_agg(const PartAggParams p) {
   constexpr uint32_t SPAN = 64 * PER;             // records per wave-load
   using Rec = typename std::conditional<REC64 != 0, unsigned long long, uint32_t>::type;
   const Rec* buf = reinterpret_cast<const Rec*>(p.part_buf);
-  for (int b0 = wave * RPW; b0 < NR; b0 += nwaves * RPW) {
+  // the wave's steps: regions [b0, b0 + RPW) x record offsets `base` of them; the next step's loads are issued before
+  // this step's atomics, so they are in flight while the LDS work runs (r5: half of kernel B's wave cycles waited)
+  struct Step {
+    int b0;
+    uint32_t base, maxn;
     uint32_t nn[RPW];
-    uint32_t maxn = 0;
+  };
+  auto regions_at = [&](Step& t, int b0) {
+    for (; b0 < NR; b0 += nwaves * RPW) {  // the first group of regions with records
+      t.b0 = b0;
+      t.base = 0;
+      t.maxn = 0;
+#pragma unroll
+      for (int q = 0; q < RPW; ++q) {
+        t.nn[q] = (b0 + q < NR) ? (uint32_t)__builtin_amdgcn_readfirstlane(fill[b0 + q]) : 0u;  // (uniform: SGPRs)
+        t.maxn = t.nn[q] > t.maxn ? t.nn[q] : t.maxn;
+      }
+      if (t.maxn) return;
+    }
+    t.b0 = NR;  // no step left
+  };
+  auto advance = [&](Step& t) {
+    t.base += SPAN;
+    if (t.base >= t.maxn) regions_at(t, t.b0 + nwaves * RPW);
+  };
+  // RPW buffer loads per step on every path (a region's own descriptor; a lane past the region's fill, or a step
+  // past the last, gets an out-of-range offset: zeros, no access), so the compiler's wait for a step's loads can
+  // leave the next step's in flight -- with the loads under branches the minimum over paths was no load at all
+  auto load = [&](const Step& t, u32x4 (&v)[RPW]) {
+    const bool live = t.b0 < NR;
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
-      nn[q] = (b0 + q < NR) ? fill[b0 + q] : 0u;
-      maxn = nn[q] > maxn ? nn[q] : maxn;
+      const uint64_t base = (uint64_t)(uintptr_t)(buf + (live ? ((size_t)(r0 + t.b0 + q) * p.num_parts + part) *
+                                                                    (size_t)p.part_cap : 0));
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)base);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<void*>((uintptr_t)(((uint64_t)hi << 32) | (uint64_t)lo)), 0,
+          __builtin_amdgcn_readfirstlane(p.part_cap * (int)sizeof(Rec)), 0x00020000);
+      const uint32_t i0 = t.base + lane * PER;
+      const uint32_t vo = (live && i0 < t.nn[q]) ? i0 * (uint32_t)sizeof(Rec) : 0x80000000u;
+      v[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, 0, 0));
     }
-    for (uint32_t base = 0; base < maxn; base += SPAN) {
-      u32x4 v[RPW];
+  };
+  auto process = [&](const Step& t, const u32x4 (&v)[RPW]) {
+    const uint32_t base = t.base;
+    const uint32_t* nn = t.nn;
+    // the step's RPW * PER records of this lane: key and value offset; a record past its region's fill goes to
+    // the lane's dummy key KP + lane, so the atomics below run without per-record branches
+    uint32_t rk[RPW * PER], rv[RPW * PER];
 #pragma unroll
-      for (int q = 0; q < RPW; ++q) {
-        const uint32_t i0 = base + lane * PER;
-        if (i0 < nn[q]) {
-          const Rec* src = buf + ((size_t)(r0 + b0 + q) * p.num_parts + part) * (size_t)p.part_cap + i0;
-          v[q] = *reinterpret_cast<const u32x4*>(src);
-        }
-      }
-      // the step's RPW * PER records of this lane: key and value offset; a record past its region's fill goes to
-      // the lane's dummy key KP + lane, so the atomics below run without per-record branches
-      uint32_t rk[RPW * PER], rv[RPW * PER];
+    for (int q = 0; q < RPW; ++q) {
+      const uint32_t i0 = base + lane * PER;
 #pragma unroll
-      for (int q = 0; q < RPW; ++q) {
-        const uint32_t i0 = base + lane * PER;
-#pragma unroll
-        for (int e = 0; e < PER; ++e) {
-          const unsigned long long r = REC64 ? ((unsigned long long)v[q][2 * e + 1] << 32) | v[q][2 * e]
-                                             : (unsigned long long)v[q][e];
-          uint32_t k, x;
-          if (REC64) {
-            k = (uint32_t)(r >> 32);
-            x = (uint32_t)r;
-          } else {
-            k = (uint32_t)r >> p.part_vbits;
-            x = (uint32_t)r & vmask;
-          }
-          rk[q * PER + e] = (i0 + e < nn[q]) ? k : KP + (uint32_t)lane;
-          rv[q * PER + e] = x;
-        }
-      }
-      constexpr int NREC = RPW * PER;
-#pragma unroll
-      for (int i = 0; i < NREC; ++i) {
-        if (p.pack_cs) {
-          atomicAdd(&cs[rk[i]], (1ull << 40) | (unsigned long long)rv[i]);
+      for (int e = 0; e < PER; ++e) {
+        const unsigned long long r = REC64 ? ((unsigned long long)v[q][2 * e + 1] << 32) | v[q][2 * e]
+                                           : (unsigned long long)v[q][e];
+        uint32_t k, x;
+        if (REC64) {
+          k = (uint32_t)(r >> 32);
+          x = (uint32_t)r;
         } else {
-          atomicAdd(&cnt[rk[i]], 1u);
-          if (p.has_sum) atomicAdd(&sum[rk[i]], (unsigned long long)rv[i]);
+          k = (uint32_t)r >> p.part_vbits;
+          x = (uint32_t)r & vmask;
         }
+        rk[q * PER + e] = (i0 + e < nn[q]) ? k : KP + (uint32_t)lane;
+        rv[q * PER + e] = x;
       }
-      if (p.has_min | p.has_max) {
-        if (p.mm_blind) {  // every record issues its MIN / MAX atomics (no return: nothing waits)
+    }
+    constexpr int NREC = RPW * PER;
 #pragma unroll
-          for (int i = 0; i < NREC; ++i) {
-            if (p.has_min) atomicMin(&mm[2 * rk[i]], rv[i]);
-            if (p.has_max) atomicMax(&mm[2 * rk[i] + 1], rv[i]);
-          }
-        } else {
-          // read the step's (min, max) words together; a record that improves one is rare after a key's first few
-          // records (O(log n) of a key's n), but issuing its atomic in the record's own slot made the wave issue one
-          // min and one max instruction for nearly every slot (some lane of 64 needs it: r5 SQ, 5.3 LDS instructions
-          // per record against 2).  The lane's improving records go to a bitmask instead, and the wave issues one
-          // atomicMin / atomicMax round per pending record of its busiest lane.
-          unsigned long long cur[NREC];
+    for (int i = 0; i < NREC; ++i) {
+      if (p.pack_cs) {
+        atomicAdd(&cs[rk[i]], (1ull << 40) | (unsigned long long)rv[i]);
+      } else {
+        atomicAdd(&cnt[rk[i]], 1u);
+        if (p.has_sum) atomicAdd(&sum[rk[i]], (unsigned long long)rv[i]);
+      }
+    }
+    if (p.has_min | p.has_max) {
+      if (p.mm_blind) {  // every record issues its MIN / MAX atomics (no return: nothing waits)
 #pragma unroll
-          for (int i = 0; i < NREC; ++i) cur[i] = *reinterpret_cast<const unsigned long long*>(mm + 2 * rk[i]);
-          uint32_t pmin = 0, pmax = 0;
+        for (int i = 0; i < NREC; ++i) {
+          if (p.has_min) atomicMin(&mm[2 * rk[i]], rv[i]);
+          if (p.has_max) atomicMax(&mm[2 * rk[i] + 1], rv[i]);
+        }
+      } else {
+        // read the step's (min, max) words together; a record that improves one is rare after a key's first few
+        // records (O(log n) of a key's n), but issuing its atomic in the record's own slot made the wave issue one
+        // min and one max instruction for nearly every slot (some lane of 64 needs it: r5 SQ, 5.3 LDS instructions
+        // per record against 2).  The lane's improving records go to a bitmask instead, and the wave issues one
+        // atomicMin / atomicMax round per pending record of its busiest lane.
+        unsigned long long cur[NREC];
 #pragma unroll
-          for (int i = 0; i < NREC; ++i) {
-            if (p.has_min && rv[i] < (uint32_t)cur[i]) pmin |= 1u << i;
-            if (p.has_max && rv[i] > (uint32_t)(cur[i] >> 32)) pmax |= 1u << i;
-          }
-          while (__ballot((pmin | pmax) != 0u)) {
-            const uint32_t pm = pmin ? pmin : pmax;
-            const int i = pm ? __builtin_ctz(pm) : 0;
-            uint32_t key = 0, val = 0;
+        for (int i = 0; i < NREC; ++i) cur[i] = *reinterpret_cast<const unsigned long long*>(mm + 2 * rk[i]);
+        uint32_t pmin = 0, pmax = 0;
 #pragma unroll
-            for (int t = 0; t < NREC; ++t)  // register-indexed select (no dynamic register indexing)
-              if (t == i) {
-                key = rk[t];
-                val = rv[t];
-              }
-            if (pmin) {
-              atomicMin(&mm[2 * key], val);
-              pmin &= pmin - 1u;
-            } else if (pmax) {
-              atomicMax(&mm[2 * key + 1], val);
-              pmax &= pmax - 1u;
+        for (int i = 0; i < NREC; ++i) {
+          if (p.has_min && rv[i] < (uint32_t)cur[i]) pmin |= 1u << i;
+          if (p.has_max && rv[i] > (uint32_t)(cur[i] >> 32)) pmax |= 1u << i;
+        }
+        while (__ballot((pmin | pmax) != 0u)) {
+          const uint32_t pm = pmin ? pmin : pmax;
+          const int i = pm ? __builtin_ctz(pm) : 0;
+          uint32_t key = 0, val = 0;
+#pragma unroll
+          for (int t = 0; t < NREC; ++t)  // register-indexed select (no dynamic register indexing)
+            if (t == i) {
+              key = rk[t];
+              val = rv[t];
             }
+          if (pmin) {
+            atomicMin(&mm[2 * key], val);
+            pmin &= pmin - 1u;
+          } else if (pmax) {
+            atomicMax(&mm[2 * key + 1], val);
+            pmax &= pmax - 1u;
           }
         }
       }
     }
+  };
+  Step ta, tb;
+  u32x4 va[RPW], vb[RPW];
+  regions_at(ta, wave * RPW);
+  load(ta, va);
+  while (ta.b0 < NR) {  // wave-uniform
+    tb = ta;
+    advance(tb);
+    load(tb, vb);
+    process(ta, va);
+    if (tb.b0 >= NR) break;
+    ta = tb;
+    advance(ta);
+    load(ta, va);
+    process(tb, vb);
   }
   __syncthreads();
   const bool shared_range = p.slices > 1;

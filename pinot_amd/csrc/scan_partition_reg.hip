@@ -21,9 +21,11 @@ namespace ph {
 // append variants, listed flush with per-record "chunk completed" checks): 64.5 VALU + 33 SALU per doc and the VALU
 // busy 62 % of the kernel.  The flush is one thread per partition (part_flush_owner: pending >= 16 sends its whole
 // 64-byte chunks out), so no append keeps a list.
-// FX: P <= kRegBlock partitions with 32-slot rings -- the in-loop flushes are part_flush_fixed (a fixed count of
-// buffer stores per round, so the decode waits for the next tile's loads only)
-template <int NG, int HASV, int CK, int CV, int FX>
+// SETS: ring sets.  2 -- a round appends to one set while the owner threads send out the whole chunks the previous
+// round completed in the other (one barrier per round); 1 -- flush, barrier, append, barrier (half the LDS: at
+// config 3's 245 partitions the two sets' 76 KB hold kernel A at 2 workgroups per CU, one set's 41 KB allow the 3 its
+// registers allow)
+template <int NG, int HASV, int CK, int CV, int SETS>
 __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
@@ -37,7 +39,7 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
     uint32_t* gpos = reinterpret_cast<uint32_t*>(smem + p.pl_bcnt_off);
     // the lanes' scratch words start at 2^31 + 64: a scratch rank is then negative as an int, so the overflow test
     // below (0 <= rank - C as an int) never fires for a missed doc, without a per-record partition compare
-    for (int i = threadIdx.x; i < 2 * (p.num_parts + 64); i += kRegBlock)
+    for (int i = threadIdx.x; i < SETS * (p.num_parts + 64); i += kRegBlock)
       pend[i] = (i % (p.num_parts + 64)) < p.num_parts ? 0u : 0x80000040u;
     for (int i = threadIdx.x; i < p.num_parts; i += kRegBlock) gpos[i] = 0;
   }
@@ -52,12 +54,6 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
   const uint32_t dummy_slot = P * RS + (uint32_t)lane;  // scratch slot of a record-less lane
   auto t0 = tiles.next();
   tiles.load(t0, lane);
-  if constexpr (FX != 0) {
-    // the same 2 x 8 (empty) flush stores after the first tile's loads as every later tile has after its own: the
-    // decode's waits then count them on every path into the loop (the minimum over paths is what the compiler uses)
-    part_flush_fixed<kRegBlock>(p, smem, matched, 1);
-    part_flush_fixed<kRegBlock>(p, smem, matched, 0);
-  }
   // per lane and doc j of the tile: X[j] = the 32-bit record; PB packs two 16-bit ring-word indices per register
   uint32_t X[32], PB[16];
   for (int32_t it = 0; it < nrounds; ++it) {
@@ -65,13 +61,17 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
     // ---- the next tile's loads stay in flight through the append rounds
     t0 = tiles.next();
     tiles.load(t0, lane);
-    // ---- two append rounds into alternating ring sets: a round appends 16 records per lane to set `cur` while the
-    // owner threads send out the whole chunks the previous round completed in the other set; one barrier per round
-    // (r4's single set needed two: flush, barrier, append, barrier)
+    // ---- two append rounds of 16 records per lane each
     auto append_round = [&](auto jb) {
-      const int cur = (int)(round & 1);
-      if constexpr (FX != 0) part_flush_fixed<kRegBlock>(p, smem, matched, cur ^ 1);  // (round 0: the set is empty)
-      else if (round > 0) part_flush_owner<kRegBlock>(p, smem, matched, false, cur ^ 1);
+      const int cur = SETS == 2 ? (int)(round & 1) : 0;
+      if constexpr (SETS == 2) {
+        if (round > 0) part_flush_owner<kRegBlock>(p, smem, matched, false, cur ^ 1);
+      } else {
+        if (round > 0) {  // the previous round's appends are complete (its barrier): flush, then append after a barrier
+          part_flush_owner<kRegBlock>(p, smem, matched, false, 0);
+          lds_barrier();
+        }
+      }
       uint32_t* pend = pend0 + (size_t)cur * (P + 64);
       uint32_t* slots = slots0 + (size_t)cur * SW;
       // groups of 4: the 4 rank atomics issue back to back, then the 4 stores.  Branch-free and SGPR-free per record:
@@ -102,23 +102,27 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
     append_round(std::integral_constant<int, 0>{});
     append_round(std::integral_constant<int, 16>{});
   }
-  // the last round's set still holds its whole chunks; every pending record of both sets then goes out (one owner
-  // thread per partition writes both sets' leftovers, then the region count)
-  if (round > 0) part_flush_owner<kRegBlock>(p, smem, matched, false, (int)((round - 1) & 1));
-  lds_barrier();
-  part_flush_owner<kRegBlock>(p, smem, matched, true, (int)(round & 1), false);
-  part_flush_owner<kRegBlock>(p, smem, matched, true, (int)((round - 1) & 1), true);
+  if constexpr (SETS == 2) {
+    // the last round's set still holds its whole chunks; every pending record of both sets then goes out (one owner
+    // thread per partition writes both sets' leftovers, then the region count)
+    if (round > 0) part_flush_owner<kRegBlock>(p, smem, matched, false, (int)((round - 1) & 1));
+    lds_barrier();
+    part_flush_owner<kRegBlock>(p, smem, matched, true, (int)(round & 1), false);
+    part_flush_owner<kRegBlock>(p, smem, matched, true, (int)((round - 1) & 1), true);
+  } else {
+    part_flush_owner<kRegBlock>(p, smem, matched, true, 0, true);  // (the last round ended at a barrier)
+  }
   if (matched && p.matched_total) atomicAdd(p.matched_total, matched);
 }
 
 template <int NG, int HASV, int CK, int CV>
 static void launch_part_reg_k(const KParams& p, int grid, size_t lds, hipStream_t s) {
-  if (p.part_fixed) {
+  if (p.part_sets == 1) {
     allow_lds(k_part_reg<NG, HASV, CK, CV, 1>, lds);
     hipLaunchKernelGGL((k_part_reg<NG, HASV, CK, CV, 1>), dim3(grid), dim3(kRegBlock), lds, s, p);
   } else {
-    allow_lds(k_part_reg<NG, HASV, CK, CV, 0>, lds);
-    hipLaunchKernelGGL((k_part_reg<NG, HASV, CK, CV, 0>), dim3(grid), dim3(kRegBlock), lds, s, p);
+    allow_lds(k_part_reg<NG, HASV, CK, CV, 2>, lds);
+    hipLaunchKernelGGL((k_part_reg<NG, HASV, CK, CV, 2>), dim3(grid), dim3(kRegBlock), lds, s, p);
   }
 }
 
@@ -149,11 +153,11 @@ int part_reg_blocks_per_cu(const KParams& p, int ng, size_t lds) {
 #define PH_REG_FX(NG, FX)                                                                                             \
   f = p.part_ck == 3 ? (hasv ? (const void*)k_part_reg<NG, 1, 3, 5, FX> : (const void*)k_part_reg<NG, 0, 3, 5, FX>)  \
                      : (hasv ? (const void*)k_part_reg<NG, 1, 4, 8, FX> : (const void*)k_part_reg<NG, 0, 4, 8, FX>);
-#define PH_REG_FN(NG)   \
-  if (p.part_fixed) {   \
-    PH_REG_FX(NG, 1)    \
-  } else {              \
-    PH_REG_FX(NG, 0)    \
+#define PH_REG_FN(NG)     \
+  if (p.part_sets == 1) { \
+    PH_REG_FX(NG, 1)      \
+  } else {                \
+    PH_REG_FX(NG, 2)      \
   }
   if (ng == 1) { PH_REG_FN(1) } else if (ng == 2) { PH_REG_FN(2) } else { PH_REG_FN(3) }
 #undef PH_REG_FN

@@ -46,6 +46,7 @@ class ExecutionStats:
     num_devices: int = 0  # multi-device context: devices that scanned segments
     merge_ms: float = 0.0  # multi-device: partial-table combine (RCCL reduce-scatter / local reduce)
     finalize_ms: float = 0.0  # multi-device: merged key shards -> result
+    scan_ms: float = 0.0  # multi-device: wall time of the devices' scans into their partial tables
 
 
 SCAN_KERNEL_NAMES = {0: "none", 1: "k_scan", 2: "k_agg_lean", 3: "k_agg_sparse", 4: "k_group_lds_lean",
@@ -353,7 +354,8 @@ class GpuContext:
                                st.num_entries_scanned_post_filter, st.num_total_docs, st.num_segments_processed,
                                st.num_segments_matched, bool(st.num_groups_limit_reached),
                                bool(st.sum_precision_flag), st.device_ms, st.host_ms, st.plan_mode,
-                               st.limit_pass, st.scan_kernel, st.num_devices, st.merge_ms, st.finalize_ms)
+                               st.limit_pass, st.scan_kernel, st.num_devices, st.merge_ms, st.finalize_ms,
+                               st.scan_ms)
         return IntermediateResult(key_cols, agg_cols, n, [a.function for a in q.aggregations], stats)
 
     # ---------------------------------------------------------------- segment-level filter (plug point 2)
@@ -373,7 +375,8 @@ class GpuContext:
                                st.num_entries_scanned_post_filter, st.num_total_docs, st.num_segments_processed,
                                st.num_segments_matched, bool(st.num_groups_limit_reached),
                                bool(st.sum_precision_flag), st.device_ms, st.host_ms, st.plan_mode,
-                               st.limit_pass, st.scan_kernel, st.num_devices, st.merge_ms, st.finalize_ms)
+                               st.limit_pass, st.scan_kernel, st.num_devices, st.merge_ms, st.finalize_ms,
+                               st.scan_ms)
         if words:
             out = out[:(nd + 63) // 64]
         return out, int(st.num_docs_scanned), stats

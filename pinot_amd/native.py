@@ -124,7 +124,7 @@ class ExecStats(ctypes.Structure):
                 ("device_ms", ctypes.c_double), ("host_ms", ctypes.c_double), ("plan_mode", ctypes.c_int32),
                 ("limit_pass", ctypes.c_int32),
                 ("scan_kernel", ctypes.c_int32), ("num_devices", ctypes.c_int32),
-                ("merge_ms", ctypes.c_double), ("finalize_ms", ctypes.c_double)]
+                ("merge_ms", ctypes.c_double), ("finalize_ms", ctypes.c_double), ("scan_ms", ctypes.c_double)]
 
 
 # every symbol declared in include/pinot_hip.h
