@@ -235,7 +235,7 @@ enum {
   PH_KERNEL_PART_SCAN = 7,     /* k_scan<MODE_PARTITION> + k_part_agg: partitioned group-by with gathers */
   PH_KERNEL_PART_REG = 8,      /* k_part_reg + k_part_agg: partitioned group-by, register-direct decode */
   PH_KERNEL_COUNT_REG = 9,     /* k_count_reg: COUNT(*) over RANGE / ALL / sorted leaves, register-direct decode */
-  PH_KERNEL_AGG_REG = 10,      /* k_agg_reg: k_agg_lean's aggregation in the register-direct form */
+  /* 10: retired (round 3's k_agg_reg, slower than k_agg_lean everywhere measured; removed in round 6) */
   PH_KERNEL_GROUP_REG = 11,    /* k_group_reg: k_group_lds_lean's group-by in the register-direct form */
   PH_KERNEL_GROUP_SPARSE = 12, /* k_group_sparse: group-by over selective inverted-index ANDs, matched-doc gathers */
   /* 13: retired (round 4's wave-private-ring kernel A, removed in round 5) */
@@ -265,6 +265,20 @@ int32_t ph_ctx_num_devices(const ph_ctx* ctx);
 #define PH_TRANSPORT_RCCL 1
 int ph_ctx_set_multi_transport(ph_ctx* ctx, int32_t transport);
 int ph_ctx_destroy(ph_ctx* ctx);
+/* Plan / kernel-form overrides of a context (tests and tuning sweeps; the library reads no environment).  `name` is
+ * one of the options below; PH_OPTION_UNSET restores the planner's own choice.  Presence-style options act when set
+ * to any value.  PH_ERR_INVALID_ARGUMENT for an unknown name.
+ *   roaring_atomic     inverted-leaf doc bitmaps by the device-atomic build (k_roaring_or) instead of per chunk
+ *   agg_cont / group_cont   0/1: k_agg_sparse / k_group_sparse straight from the roaring containers (group_cont:
+ *                      opt-in, measured slower on the inverted SSB flight)
+ *   agg_sparse / group_sparse  0/1: force the sparse (matched-doc gather) aggregation / group-by plans off / on
+ *   disable_partition, no_group_cache, limit_eager, stat_fuse (off), part_generic, agg_generic, lds_generic,
+ *   count_generic, lds_lean, part_lds, part_flush_first, part_serial: presence -- force the named alternative form
+ *   lds_table_max, tile_words, group_reg_lg, interrupt_chunks, part_klo, part_batch_rows, part_depth, part_sets,
+ *   part_wg_per_cu, part_slices, part_mm_blind, part_ring_log2: the value
+ *   multi_host_merge   presence: a multi-device context merges by group value instead of dense partials */
+#define PH_OPTION_UNSET INT64_MIN
+int ph_ctx_set_option(ph_ctx* ctx, const char* name, int64_t value);
 /* Launch on an external HIP stream (e.g. torch's current stream); NULL restores the context's own. */
 int ph_ctx_set_stream(ph_ctx* ctx, void* hip_stream);
 

@@ -9,6 +9,39 @@
 namespace ph {
 thread_local std::string g_last_error;
 
+const char* const kOptNames[OPT_COUNT] = {
+    "roaring_atomic",
+    "agg_cont",
+    "group_cont",
+    "disable_partition",
+    "lds_table_max",
+    "no_group_cache",
+    "group_sparse",
+    "agg_sparse",
+    "tile_words",
+    "limit_eager",
+    "part_generic",
+    "agg_generic",
+    "lds_generic",
+    "count_generic",
+    "lds_lean",
+    "group_reg_lg",
+    "stat_fuse",
+    "interrupt_chunks",
+    "part_klo",
+    "part_batch_rows",
+    "part_flush_first",
+    "part_depth",
+    "part_lds",
+    "part_sets",
+    "part_wg_per_cu",
+    "part_slices",
+    "part_mm_blind",
+    "part_serial",
+    "part_ring_log2",
+    "multi_host_merge",
+};
+
 void fail(int code, const std::string& msg) { throw Error{code, msg}; }
 
 ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc);
@@ -90,6 +123,18 @@ int ph_ctx_set_multi_transport(ph_ctx* ctx, int32_t transport) {
   return guarded([&] {
     if (!ctx) fail(PH_ERR_INVALID_ARGUMENT, "ctx is null");
     multi_set_transport(ctx, transport);
+  });
+}
+
+int ph_ctx_set_option(ph_ctx* ctx, const char* name, int64_t value) {
+  return guarded([&] {
+    if (!ctx || !name) fail(PH_ERR_INVALID_ARGUMENT, "null argument");
+    for (int o = 0; o < OPT_COUNT; ++o)
+      if (std::strcmp(kOptNames[o], name) == 0) {
+        for (Context* c : ctx->devs) c->opts[o].store(value, std::memory_order_relaxed);
+        return;
+      }
+    fail(PH_ERR_INVALID_ARGUMENT, std::string("unknown option ") + name);
   });
 }
 

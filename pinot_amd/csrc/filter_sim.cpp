@@ -387,16 +387,9 @@ int64_t simulate_filter_entries(const SimNode& root, const std::vector<SimLeaf>&
   return b.entries;
 }
 
-// words per chunk (2, 4 or 8; PH_DFA_CW is a tuning knob): the LDS staging of K x (CW + 1) words per thread sets the
-// waves per CU of k_and_dfa, the per-chunk walks of the other entry types (~4 epochs per chunk) the overhead of small chunks
-int and_dfa_chunk_words() {
-  static const int cw = [] {
-    const char* e = getenv("PH_DFA_CW");
-    const int v = e ? atoi(e) : kDfaChunkWords;
-    return v == 2 || v == 8 ? v : 4;
-  }();
-  return cw;
-}
+// words per chunk (r5 swept 2, 4 and 8: 4 best): the LDS staging of K x (CW + 1) words per thread sets the waves per CU
+// of k_and_dfa, the per-chunk walks of the other entry types (~4 epochs per chunk) the overhead of small chunks
+int and_dfa_chunk_words() { return kDfaChunkWords; }
 
 // The AND-of-scans entries by the device's algorithm (and_walk.h) on the host: chunks of 1 << shift docs (any
 // length: dfa_chunk takes arbitrary bounds), their tables composed in order.

@@ -16,10 +16,6 @@ void launch_scan(const KParams& p, int mode, int ng, int rec64, int grid, size_t
     launch_count_reg(p, grid, s);
     return;
   }
-  if (mode == MODE_AGG && p.agg_reg) {  // register-direct form of k_agg_lean
-    launch_agg_reg(p, grid, s);
-    return;
-  }
   if ((mode == MODE_GROUP_LDS || mode == MODE_GROUP_GLOBAL) && p.group_sparse && !p.first_doc) {
     launch_group_sparse(p, mode, grid, lds, s);  // selective bitmap ANDs: gathers of the matched docs
     return;

@@ -303,7 +303,7 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
   }
   const ph_dense_layout& L = lay->layout;
   if (L.num_groups < 0) return host_merge();
-  if (getenv("PH_MULTI_HOST_MERGE")) return host_merge();  // the value-keyed merge, forced (tests)
+  if (x->c.has(OPT_MULTI_HOST_MERGE)) return host_merge();  // the value-keyed merge, forced (tests)
   const int64_t G = L.num_groups;
   if (G <= 0) return host_merge();
   // shard S of every device: a multiple of 64 groups, D shards covering the padded tables

@@ -320,8 +320,6 @@ struct KParams {
   int32_t part_ck, part_cv;       // k_part_reg: 16-byte loads per lane of a filter / key stream, of the value stream
   int32_t part_sets;              // k_part_reg: ring sets (2: append and flush overlap; 1: half the LDS, more workgroups)
   int32_t count_reg;              // MODE_COUNT: k_count_reg with this many 16-byte loads per lane (ceil(b / 4)); 0 off
-  int32_t agg_reg;                // MODE_AGG: k_agg_reg (register-direct k_agg_lean)
-  int32_t agg_reg_cf, agg_reg_cv; //   16-byte loads per lane of the filter / value stream
   int32_t group_reg;              // MODE_GROUP_LDS: k_group_reg (register-direct, lane-interleaved LDS table)
   int32_t group_sparse;           // MODE_GROUP_LDS / GLOBAL: k_group_sparse (selective bitmap ANDs, DevSegment sp_*)
   int32_t group_reg_lanes_log2;   //   log2 of the slots per key (lane l updates slot key * L + (l & (L - 1)))
@@ -529,6 +527,45 @@ struct Column {
 
 struct Context;
 
+// ------------------------------------------------------------------ per-context options (ph_ctx_set_option)
+// Plan and kernel-form overrides for tests and tuning sweeps; unset (the default) = the planner's own choice.  The
+// product reads no environment: a server process's environment cannot change a query plan.
+enum Opt : int {
+  OPT_ROARING_ATOMIC,
+  OPT_AGG_CONT,
+  OPT_GROUP_CONT,
+  OPT_DISABLE_PARTITION,
+  OPT_LDS_TABLE_MAX,
+  OPT_NO_GROUP_CACHE,
+  OPT_GROUP_SPARSE,
+  OPT_AGG_SPARSE,
+  OPT_TILE_WORDS,
+  OPT_LIMIT_EAGER,
+  OPT_PART_GENERIC,
+  OPT_AGG_GENERIC,
+  OPT_LDS_GENERIC,
+  OPT_COUNT_GENERIC,
+  OPT_LDS_LEAN,
+  OPT_GROUP_REG_LG,
+  OPT_STAT_FUSE,
+  OPT_INTERRUPT_CHUNKS,
+  OPT_PART_KLO,
+  OPT_PART_BATCH_ROWS,
+  OPT_PART_FLUSH_FIRST,
+  OPT_PART_DEPTH,
+  OPT_PART_LDS,
+  OPT_PART_SETS,
+  OPT_PART_WG_PER_CU,
+  OPT_PART_SLICES,
+  OPT_PART_MM_BLIND,
+  OPT_PART_SERIAL,
+  OPT_PART_RING_LOG2,
+  OPT_MULTI_HOST_MERGE,
+  OPT_COUNT
+};
+constexpr int64_t kOptUnset = INT64_MIN;
+extern const char* const kOptNames[OPT_COUNT];
+
 }  // namespace ph
 
 struct ph_segment {
@@ -574,8 +611,14 @@ struct Lane {
 };
 
 struct Context {
+  Context() {
+    for (auto& o : opts) o.store(kOptUnset, std::memory_order_relaxed);
+  }
   int device = 0;
   int num_cus = 256;
+  std::atomic<int64_t> opts[OPT_COUNT];  // ph_ctx_set_option
+  bool has(Opt o) const { return opts[o].load(std::memory_order_relaxed) != kOptUnset; }
+  int64_t opt(Opt o) const { return opts[o].load(std::memory_order_relaxed); }
   std::atomic<hipStream_t> ext_stream{nullptr};  // ph_ctx_set_stream: run calls on the caller's stream
   std::mutex mu;  // guards table_dicts and union_cache (held only around their lookups / inserts)
   std::map<std::string, std::shared_ptr<GlobalDict>> table_dicts;   // ph_table_set_dictionary
@@ -645,11 +688,10 @@ struct LaneGuard {
 void launch_scan(const KParams& p, int mode, int ngroup, int rec64, int grid, size_t lds, hipStream_t s);
 void launch_part_agg(const PartAggParams& p, size_t lds, hipStream_t s);
 size_t part_agg_lds_bytes(const PartAggParams& p);
-size_t partition_lds_bytes(KParams& p);  // fills the pl_* offsets, returns the dynamic LDS size
+size_t partition_lds_bytes(KParams& p, int ring_log2 = 5);  // fills the pl_* offsets, returns the dynamic LDS size
 int part_reg_blocks_per_cu(const KParams& p, int ng, size_t lds);  // k_part_reg occupancy
 void launch_part_reg(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);  // scan_partition_reg.hip
 void launch_count_reg(const KParams& p, int grid, hipStream_t s);                      // scan_count_reg.hip
-void launch_agg_reg(const KParams& p, int grid, hipStream_t s);                        // scan_count_reg.hip
 void launch_group_reg(const KParams& p, int ng, int grid, size_t lds, hipStream_t s);   // scan_group_reg.hip
 void launch_group_sparse(const KParams& p, int mode, int grid, size_t lds, hipStream_t s);  // scan_group_sparse.hip
 struct MergeParams {

@@ -1299,7 +1299,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     // all leaves' bitmaps in one block, each padded to whole 64-doc words + one
     const size_t nl = pl.bitmaps.size();
     std::vector<size_t> woff(nl + 1, 0);
-    bool chunked = getenv("PH_ROARING_ATOMIC") == nullptr;  // PH_ROARING_ATOMIC=1: device-atomic build (tests)
+    bool chunked = !ctx->has(OPT_ROARING_ATOMIC);  // option roaring_atomic: the device-atomic build (tests)
     for (size_t i = 0; i < nl; ++i) {
       woff[i + 1] = woff[i] + (((size_t)pl.bitmaps[i].seg->num_docs + 63) / 64 + 1) * 2;
       const Column& col = *pl.bitmaps[i].col;
@@ -1406,7 +1406,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // of a single-value column have disjoint doc sets, so the leaf's docs are the disjoint union of its ids'
   // containers and no doc bitmap is needed.  The bitmaps are built only if that plan is not taken
   bool cont_defer = q->num_group_by == 0 && !pl.bitmaps.empty() && dop != DENSE_LAYOUT && !fin;
-  if (const char* e = getenv("PH_AGG_CONT")) cont_defer = cont_defer && atoi(e) != 0;  // tuning knob
+  if (ctx->has(OPT_AGG_CONT)) cont_defer = cont_defer && ctx->opt(OPT_AGG_CONT) != 0;
   {
     int live = 0;
     for (int i = 0; i < nseg && cont_defer; ++i) {
@@ -1424,8 +1424,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // Opt-in (PH_GROUP_CONT=1): r5 measured the inverted SSB flight at 15.2 ms of kernels against 10.7 with
   // k_roaring_chunk's bitmaps -- the per-chunk build (container search, byte-wise payload reads, LDS atomics, two
   // barriers) serialises in front of every chunk's gathers, where the separate build runs fully parallel
-  const char* gce = getenv("PH_GROUP_CONT");
-  bool gs_defer = gce && atoi(gce) != 0 && q->num_group_by > 0 && !pl.bitmaps.empty() && dop != DENSE_LAYOUT && !fin;
+  bool gs_defer = ctx->has(OPT_GROUP_CONT) && ctx->opt(OPT_GROUP_CONT) != 0 && q->num_group_by > 0 && !pl.bitmaps.empty() && dop != DENSE_LAYOUT && !fin;
   {
     size_t leaves = 0;
     for (int i = 0; i < nseg && gs_defer; ++i) {
@@ -1695,15 +1694,15 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     const bool part_ok = num_hll == 0 && nvals <= 1 && (nvals == 0 || (val_is_int[0] && !val_exprs[0] && vmax >= vmin &&
                                                                        (uint64_t)(vmax - vmin) < (1ull << 32))) &&
                          G <= ((int64_t)kPartMaxParts << kPartKeysLog2) && !any_limit &&
-                         getenv("PH_DISABLE_PARTITION") == nullptr;
+                         !ctx->has(OPT_DISABLE_PARTITION);
     // LDS-private tables up to 64 KiB; r2 measured 96 KiB tables (one workgroup per CU) slower than the HBM table
     // for selective filters (SSB Q2.1, 7000 keys x COUNT + SUM: 3.9 vs 3.2 ms; Q2.3 3.2 vs 1.6 ms)
     // Dense LDS tables up to 64 KiB (PH_LDS_TABLE_MAX: tuning knob).  r2: routing 32-64 KiB tables to the cached
     // HBM table instead did not speed up SSB Q3.1 / Q4.2 and made an unfiltered 4375-key group-by 22x slower
     // (38.8 vs 1.7 ms: the cache cannot hold every key, the rest pays device atomics)
     size_t lds_table_max = 64 * 1024;
-    if (const char* e = getenv("PH_LDS_TABLE_MAX")) lds_table_max = (size_t)std::max(0, atoi(e));
-    const bool cache_ok = num_hll == 0 && nvals <= 1 && getenv("PH_NO_GROUP_CACHE") == nullptr;
+    if (ctx->has(OPT_LDS_TABLE_MAX)) lds_table_max = (size_t)std::max<int64_t>(0, ctx->opt(OPT_LDS_TABLE_MAX));
+    const bool cache_ok = num_hll == 0 && nvals <= 1 && !ctx->has(OPT_NO_GROUP_CACHE);
     if (off <= (cache_ok ? lds_table_max : (size_t)64 * 1024)) {
       mode = MODE_GROUP_LDS;
       lds_tables = off;
@@ -1831,7 +1830,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       docs += (double)segs[i]->num_docs;
     }
     sparse_plan = ok && docs > 0 && hits * 8 < docs;
-    if (const char* e = getenv("PH_GROUP_SPARSE")) sparse_plan = ok && docs > 0 && atoi(e) != 0;  // tuning knob
+    if (ctx->has(OPT_GROUP_SPARSE)) sparse_plan = ok && docs > 0 && ctx->opt(OPT_GROUP_SPARSE) != 0;
   }
   // k_agg_sparse over ANDs of scan leaves only (register-direct leaves, then gathers of the matched docs' values):
   // aggregation-only queries whose every segment's AND keeps < 1/8 of the docs (same estimate as above)
@@ -1855,7 +1854,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       docs += (double)segs[i]->num_docs;
     }
     agg_conj = ok && docs > 0 && hits * 8 < docs;
-    if (const char* e = getenv("PH_AGG_SPARSE")) agg_conj = ok && docs > 0 && atoi(e) != 0;  // tuning knob
+    if (ctx->has(OPT_AGG_SPARSE)) agg_conj = ok && docs > 0 && ctx->opt(OPT_AGG_SPARSE) != 0;
   }
   std::vector<std::pair<int32_t, int32_t>> dseg_chunks;                // device segment -> its chunk range
   std::vector<int> dseg_src;                                           // device segment -> query segment index
@@ -2048,7 +2047,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     // partition's ring (32 slots) from overflowing
     // (r2 interleaved sweep, config 3: partition tiles of 12 words 3.80-3.82 ms, 8 words 3.89-3.93, 10 words 4.36)
     int tw = mode == MODE_PARTITION ? 12 : ((mode == MODE_GROUP_LDS || kp.gc_slots) ? 16 : kMaxTileWords);
-    if (const char* e = getenv("PH_TILE_WORDS")) tw = std::max(4, std::min(kMaxTileWords, atoi(e)));  // tuning knob
+    if (ctx->has(OPT_TILE_WORDS)) tw = (int)std::max<int64_t>(4, std::min<int64_t>(kMaxTileWords, ctx->opt(OPT_TILE_WORDS)));
     auto loads = [&](int t) {
       int n = 0;
       for (int s = 0; s < kp.nstage; ++s) n += maxbits[s] ? stage_loads(t, maxbits[s]) : 0;
@@ -2094,7 +2093,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // keys can a segment have reached the limit, and only then do the first-seen pass and the truncating rescan run
   // (r2 ran the pass whenever a segment's cardinality product reached the limit: SSB Q3.2-Q4.3, products of
   // 0.4-1.75M keys over a few hundred real groups).  PH_LIMIT_EAGER=1 restores the pass-first order (tests).
-  const bool limit_opt = getenv("PH_LIMIT_EAGER") == nullptr || mode == MODE_GROUP_HASH;
+  const bool limit_opt = !ctx->has(OPT_LIMIT_EAGER) || mode == MODE_GROUP_HASH;
   if (any_limit && q->num_group_by > 0) {
     for (size_t k = 0; k < dsegs.size(); ++k)
       if (seg_limit[dseg_src[k]]) limit_segs.push_back((int)k);
@@ -2131,7 +2130,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // per-segment tile pieces: the 1 KiB wave-loads of a full tile, stream by stream
   for (auto& d : dsegs) fill_tile_pieces(d, kp.nstage, kp.stage_soff, kp.tile_words);
   // the lean kernel A (k_part_scan) covers gather-free tiles with ALL / RANGE / DOCRANGE filter leaves
-  kp.part_fast = !kp.late_prefetch && getenv("PH_PART_GENERIC") == nullptr;
+  kp.part_fast = !kp.late_prefetch && !ctx->has(OPT_PART_GENERIC);
   for (auto& d : dsegs)
     if (d.fkind != FK_ALL && d.fkind != FK_RANGE && d.fkind != FK_DOCRANGE) kp.part_fast = 0;
   // the lean aggregation kernel (k_agg_lean) covers one packed integer value column with ALL / RANGE / DOCRANGE
@@ -2139,7 +2138,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   //   r3: also FK_CONJ ANDs of range leaves (no applyAnd statistic to count) and integer 2-operand value terms of
   //   two packed columns (per-doc int64 fold; SSB Q1.x)
   kp.agg_fast = mode == MODE_AGG && nvals == 1 && num_hll == 0 && val_is_int[0] && !kp.late_prefetch &&
-                getenv("PH_AGG_GENERIC") == nullptr;
+                !ctx->has(OPT_AGG_GENERIC);
   for (auto& d : dsegs) {
     if (!kp.agg_fast) break;  // (val_exprs is empty without value columns)
     bool conj_ok = d.fkind == FK_CONJ && d.conj_nidx == 0;
@@ -2152,7 +2151,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // the lean LDS group-by (k_group_lds_lean): identity remaps, at most one packed integer value column whose
   // offsets from the table-wide minimum fit 32 bits, ALL / RANGE / DOCRANGE leaves
   kp.lds_fast = mode == MODE_GROUP_LDS && num_hll == 0 && nvals <= 1 && !kp.late_prefetch &&
-                getenv("PH_LDS_GENERIC") == nullptr;
+                !ctx->has(OPT_LDS_GENERIC);
   if (nvals == 1)
     kp.lds_fast = kp.lds_fast && val_is_int[0] && !val_exprs[0] && vmax >= vmin && (uint64_t)(vmax - vmin) < (1ull << 32);
   for (auto& d : dsegs)
@@ -2171,7 +2170,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       for (auto& fb : fbitmap_fix) hits += (int64_t)leaf_docs_estimate(pl.bitmaps[fb.second]);
     }
     kp.agg_sparse = (all_bitmap && hits * 8 < docs) || agg_conj;
-    if (const char* e = getenv("PH_AGG_SPARSE")) kp.agg_sparse = (all_bitmap || agg_conj) && atoi(e) != 0;  // tuning knob
+    if (ctx->has(OPT_AGG_SPARSE)) kp.agg_sparse = (all_bitmap || agg_conj) && ctx->opt(OPT_AGG_SPARSE) != 0;
     if (kp.agg_sparse) kp.agg_fast = 0;
     kp.agg_cont = cont_defer && kp.agg_sparse && all_bitmap && !agg_conj;
     if (kp.agg_cont) {
@@ -2200,7 +2199,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     for (int k = 0; d.sp_reg && k < d.sp_nscan; ++k)
       kp.sparse_c = std::max(kp.sparse_c, d.cols[d.sp_slot[k]].bits > 16 ? 8 : d.cols[d.sp_slot[k]].bits > 8 ? 4 : 2);
   // the register-direct COUNT (k_count_reg): every segment a dictId RANGE scan leaf, everything, or a sorted range
-  if (mode == MODE_COUNT && !kp.late_prefetch && getenv("PH_COUNT_GENERIC") == nullptr) {
+  if (mode == MODE_COUNT && !kp.late_prefetch && !ctx->has(OPT_COUNT_GENERIC)) {
     int fb = 1;
     bool ok = true;
     for (auto& d : dsegs) {
@@ -2208,22 +2207,6 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       if (d.fkind == FK_RANGE) fb = std::max(fb, (int)d.streams[kp.f_stream].bits);
     }
     if (ok && fb <= 32) kp.count_reg = (fb + 3) / 4;
-  }
-  // the register-direct aggregation (k_agg_reg): k_agg_lean's shapes with filter streams <= 32 and value streams
-  // <= 26 bits (32-bit tile sums).  Opt-in (PH_AGG_REG=1): r3 measured it slower than the LDS-staged k_agg_lean on
-  // config3-agg (0.90 vs 0.78 ms: 131 VGPRs hold it at 3 waves per SIMD with one tile of loads in flight)
-  if (kp.agg_fast && !val_exprs[0] && getenv("PH_AGG_REG") != nullptr) {
-    int fb = 1, vb = 1;
-    for (auto& d : dsegs) {
-      if (d.fkind == FK_CONJ) fb = 64;  // k_agg_reg reads one filter stream
-      if (d.fkind == FK_RANGE) fb = std::max(fb, (int)d.streams[kp.f_stream].bits);
-      vb = std::max(vb, (int)d.streams[kp.v_stream[0]].bits);
-    }
-    if (fb <= 32 && vb <= 26) {
-      kp.agg_reg = 1;
-      kp.agg_reg_cf = (fb + 3) / 4;
-      kp.agg_reg_cv = (vb + 3) / 4;
-    }
   }
   const size_t stage_bytes = (size_t)(mode == MODE_PARTITION ? kPartWaves : kWaves) * kp.stage_stride;
   size_t lds = 0;
@@ -2265,7 +2248,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       // streams <= 32 bits, the packed slot words, and a lane-interleaved table (L slots per key) in <= 40 KiB so
       // that four workgroups share a CU (r3, config3-lds: L = 16 at four workgroups per CU 1.08 ms, L = 32 at
       // three 1.18-1.24 ms -- occupancy beats the 2-way bank sharing of L = 16)
-      if (kp.lds_fast && kp.lds_pack && q->num_group_by <= 2 && getenv("PH_LDS_LEAN") == nullptr) {
+      if (kp.lds_fast && kp.lds_pack && q->num_group_by <= 2 && !ctx->has(OPT_LDS_LEAN)) {
         int fb = 1, gb = 1, vb = 1;
         for (auto& d : dsegs) {
           if (d.fkind == FK_RANGE) fb = std::max(fb, (int)d.streams[kp.f_stream].bits);
@@ -2275,7 +2258,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         const int cf = fb <= 12 ? 3 : 8, cg = gb <= 8 ? 2 : 4, cv = nvals ? (vb <= 16 ? 4 : 8) : 0;
         constexpr size_t kRegTableBytes = 40 * 1024;
         int lg = 5;
-        if (const char* e = getenv("PH_GROUP_REG_LG")) lg = std::max(0, std::min(5, atoi(e)));  // tuning knob
+        if (ctx->has(OPT_GROUP_REG_LG)) lg = (int)std::max<int64_t>(0, std::min<int64_t>(5, ctx->opt(OPT_GROUP_REG_LG)));
         while (lg > 0 && (size_t)(G + 1) * 16 << lg > kRegTableBytes) --lg;  // + the dummy row of missed docs
         if (fb <= 32 && gb <= 16 && vb <= 32 && (size_t)(G + 1) * 16 << lg <= kRegTableBytes &&
             cf + q->num_group_by * cg + cv <= 20) {
@@ -2416,7 +2399,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   for (auto& sb : sbm_fix) dsegs[sb.first / kSparseBitmaps].sp_bm[sb.first % kSparseBitmaps] = bitmap_dev[sb.second];
   // ANDs of scans on the register-direct sparse front end: its leaf masks become the statistic's leaf bitmaps
   // (conj_reg.h conj_leaf_out), one buffer for all of them (their walks run after the scan, on stream b)
-  if ((kp.group_sparse || kp.agg_sparse) && kp.sparse_c > 0 && getenv("PH_STAT_FUSE") == nullptr) {
+  if ((kp.group_sparse || kp.agg_sparse) && kp.sparse_c > 0 && !ctx->has(OPT_STAT_FUSE)) {
     auto same = [](const PNode& a, const PNode& b) {
       return a.col == b.col && a.op == b.op && a.lo == b.lo && a.len == b.len && a.set == b.set;
     };
@@ -2518,10 +2501,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       kp.chunk_end = (int32_t)chunks.size();
       int blocks_per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / std::max<size_t>(lds, 1)));
       if (mode == MODE_GROUP_LDS) blocks_per_cu = std::min(blocks_per_cu, 4);
-      if (kp.count_reg || kp.agg_reg) blocks_per_cu = 4;  // 16 waves per CU, each with two tiles of loads in flight
+      if (kp.count_reg) blocks_per_cu = 4;  // 16 waves per CU, each with two tiles of loads in flight
       const int grid = (int)std::min<int64_t>((int64_t)chunks.size(), (int64_t)ctx->num_cus * blocks_per_cu);
       stats.scan_kernel = kp.count_reg  ? PH_KERNEL_COUNT_REG
-                          : kp.agg_reg    ? PH_KERNEL_AGG_REG
                           : kp.agg_cont   ? PH_KERNEL_AGG_CONTAINERS
                           : kp.agg_sparse ? PH_KERNEL_AGG_SPARSE
                           : kp.agg_fast  ? PH_KERNEL_AGG_LEAN
@@ -2535,7 +2517,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       // an interruptible call scans in batches of kInterruptChunks chunks and checks between them
       const int32_t nchunks = (int32_t)chunks.size();
       int32_t step = interruptible ? kInterruptChunks : nchunks;
-      if (const char* e = getenv("PH_INTERRUPT_CHUNKS")) if (interruptible) step = std::max(1, atoi(e));  // tests
+      if (ctx->has(OPT_INTERRUPT_CHUNKS) && interruptible) step = (int32_t)std::max<int64_t>(1, ctx->opt(OPT_INTERRUPT_CHUNKS));
       auto run_scan = [&](KParams kx) {
         for (int32_t cb = 0; cb < nchunks; cb += step) {
           kx.chunk_begin = cb;
@@ -2682,14 +2664,14 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       const bool has_sum = nvals && (val_ops[0] & 1), has_min = nvals && (val_ops[0] & 2),
                  has_max = nvals && (val_ops[0] & 4);
       int klo = kPartKeysLog2;
-      if (const char* e = getenv("PH_PART_KLO")) klo = std::max(8, std::min(13, atoi(e)));  // tuning knob (13: kernel B table 128 KiB)
+      if (ctx->has(OPT_PART_KLO)) klo = (int)std::max<int64_t>(8, std::min<int64_t>(13, ctx->opt(OPT_PART_KLO)));  // (13: kernel B table 128 KiB)
       while (klo > 8 && (G >> (klo - 1)) < 256) --klo;  // small key spaces: more partitions, more workgroups
       const int64_t P = (G + (int64_t(1) << klo) - 1) >> klo;
       if (P > kPartMaxParts) fail(PH_ERR_UNSUPPORTED, "partitioned group-by too large");
       const int vbits = nvals ? std::max(1, bits_for_range((uint64_t)(vmax - vmin))) : 0;
       rec64 = (klo + vbits > 32) ? 1 : 0;
       int64_t batch_rows = int64_t(1) << 31;  // one batch: launch tails of many short batches cost more than MALL reuse saves
-      if (const char* e = getenv("PH_PART_BATCH_ROWS")) batch_rows = std::max<int64_t>(1 << 16, atoll(e));
+      if (ctx->has(OPT_PART_BATCH_ROWS)) batch_rows = std::max<int64_t>(1 << 16, ctx->opt(OPT_PART_BATCH_ROWS));
       if (interruptible) batch_rows = std::min<int64_t>(batch_rows, (int64_t)kInterruptChunks * kChunkWords * 64);
       // batches: contiguous chunk ranges of ~batch_rows docs
       std::vector<std::pair<int32_t, int32_t>> batches;
@@ -2710,13 +2692,13 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       kp.part_klo = klo;
       // the next tile's loads go out before the flush (r2: 3.78 vs 4.39 ms on one box); PH_PART_FLUSH_FIRST
       // restores the r1 order
-      kp.part_load_first = getenv("PH_PART_FLUSH_FIRST") == nullptr;
+      kp.part_load_first = !ctx->has(OPT_PART_FLUSH_FIRST);
       kp.part_depth = 1;
-      if (const char* e = getenv("PH_PART_DEPTH")) kp.part_depth = atoi(e) == 2 ? 2 : 1;  // tuning knob
+      if (ctx->has(OPT_PART_DEPTH)) kp.part_depth = ctx->opt(OPT_PART_DEPTH) == 2 ? 2 : 1;
       // register-direct kernel A (k_part_reg): 32-bit records, <= 3 key columns, filter / key streams <= 16 bits
       // and a value stream <= 32 bits (the lane's dwords of a stream are one register window of 4 * CK / 4 * CV)
       kp.part_reg = 0;
-      if (kp.part_fast && !rec64 && q->num_group_by <= 3 && getenv("PH_PART_LDS") == nullptr && kp.part_depth == 1) {
+      if (kp.part_fast && !rec64 && q->num_group_by <= 3 && !ctx->has(OPT_PART_LDS) && kp.part_depth == 1) {
         int kb = 1, vb = 1;
         for (auto& d : dsegs) {
           if (d.fkind == FK_RANGE) kb = std::max(kb, (int)d.streams[kp.f_stream].bits);
@@ -2738,25 +2720,26 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       kp.part_vbits = kp.part_reg ? 32 - klo : vbits;
       kp.num_parts = (int32_t)P;
       kp.part_sets = 2;
-      size_t lds_a = partition_lds_bytes(kp);
+      const int ring_log2 = ctx->has(OPT_PART_RING_LOG2) ? (int)ctx->opt(OPT_PART_RING_LOG2) : 5;
+      size_t lds_a = partition_lds_bytes(kp, ring_log2);
       int a_cap = 4;  // 8-wave workgroups: <= 4 per CU (32 waves)
       if (kp.part_reg) {
         a_cap = part_reg_blocks_per_cu(kp, q->num_group_by, lds_a);  // 4-wave groups, VGPR-bound
         // one ring set when it lets more workgroups share a CU (the two sets' LDS is what limits them)
         KParams k1 = kp;
         k1.part_sets = 1;
-        const size_t lds1 = partition_lds_bytes(k1);
+        const size_t lds1 = partition_lds_bytes(k1, ring_log2);
         const int cap1 = part_reg_blocks_per_cu(k1, q->num_group_by, lds1);
         const size_t per2 = std::min<size_t>(a_cap, (160 * 1024) / lds_a), per1 = std::min<size_t>(cap1, (160 * 1024) / lds1);
         int force = 0;
-        if (const char* e = getenv("PH_PART_SETS")) force = atoi(e);  // tuning knob
+        if (ctx->has(OPT_PART_SETS)) force = (int)ctx->opt(OPT_PART_SETS);
         if (force == 1 || (force != 2 && per1 > per2)) {
           kp = k1;
           lds_a = lds1;
           a_cap = cap1;
         }
       }
-      if (const char* e = getenv("PH_PART_WG_PER_CU")) a_cap = std::max(1, std::min(8, atoi(e)));  // tuning knob
+      if (ctx->has(OPT_PART_WG_PER_CU)) a_cap = (int)std::max<int64_t>(1, std::min<int64_t>(8, ctx->opt(OPT_PART_WG_PER_CU)));
       const int a_per_cu = (int)std::max<size_t>(1, std::min<size_t>(a_cap, (160 * 1024) / lds_a));
       const int grid_a = ctx->num_cus * a_per_cu;
       int max_batch_chunks = 0;
@@ -2826,14 +2809,14 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       // kernel B slices: about one (partition, slice) workgroup per CU; a single slice owns its key range (no
       // device atomics in the merge).  r2 sweep, config 3 (P = 245): 1 slice 3.89, 2 slices 3.90, 3 slices 3.99 ms
       int slices = (int)std::max<int64_t>(1, std::min<int64_t>(8, (int64_t)ctx->num_cus / P));
-      if (const char* e = getenv("PH_PART_SLICES")) slices = std::max(1, std::min(16, atoi(e)));  // tuning knob
+      if (ctx->has(OPT_PART_SLICES)) slices = (int)std::max<int64_t>(1, std::min<int64_t>(16, ctx->opt(OPT_PART_SLICES)));
       bp.slices = slices;
-      bp.mm_blind = getenv("PH_PART_MM_BLIND") ? atoi(getenv("PH_PART_MM_BLIND")) : 0;  // tuning knob
+      bp.mm_blind = ctx->has(OPT_PART_MM_BLIND) ? (int)ctx->opt(OPT_PART_MM_BLIND) : 0;
       bp.regions = grid_a;
       const size_t lds_b = part_agg_lds_bytes(bp);
       Lane& L = *lane.lane;
       // PH_PART_SERIAL=1 runs kernel B on the scan stream (profiling each kernel without overlap)
-      hipStream_t sb = getenv("PH_PART_SERIAL") ? st : L.stream_b;
+      hipStream_t sb = ctx->has(OPT_PART_SERIAL) ? st : L.stream_b;
       PH_HIP_CHECK(hipEventRecord(L.ev_start, st));
       for (size_t b = 0; b < batches.size(); ++b) {
         if (interruptible && b > 0) {

@@ -101,124 +101,6 @@ __global__ void __launch_bounds__(kBlock) k_count_reg(const KParams p) {
   if (lane == 0 && tot) atomicAdd(&p.out_count[0], (unsigned long long)tot);
 }
 
-// k_agg_reg: the register-direct form of k_agg_lean (AggregationOperator over COUNT / SUM / MIN / MAX of one packed
-// integer column, RANGE / ALL / DOCRANGE leaves): per tile the filter stream decodes into a 32-bit per-lane match
-// mask, then the value stream's offsets fold into 32-bit tile accumulators (offsets < 2^26, 32 per lane per tile),
-// and the 64-bit results form once per tile (SUM = offsets + matches * base).
-template <int CF, int CV>
-__global__ void __launch_bounds__(kBlock) k_agg_reg(const KParams p) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  SegPtr segs = (SegPtr)p.segs;
-  const PH_CONST Chunk* chunks = (const PH_CONST Chunk*)p.chunks;
-  constexpr int32_t TW = kRegTileWords;
-  constexpr int32_t round_words = kWaves * TW;
-  const int64_t nch = p.chunk_end - p.chunk_begin;
-  int32_t c = p.chunk_begin + (int32_t)(nch * blockIdx.x / gridDim.x), r = 0;
-  const int32_t c_end = p.chunk_begin + (int32_t)(nch * (blockIdx.x + 1) / gridDim.x);
-  struct Tile {
-    SegPtr S;
-    int32_t w0, ndoc;
-  };
-  auto next_tile = [&]() {
-    Tile t{nullptr, 0, 0};
-    if (c < c_end) {
-      const int32_t cbeg = chunks[c].word_begin, cend = chunks[c].word_end;
-      t.S = segs + chunks[c].seg;
-      t.w0 = cbeg + r * round_words + wave * TW;
-      const int32_t nw = min(TW, cend - t.w0);
-      t.ndoc = nw > 0 ? min(nw * 64, t.S->num_docs - t.w0 * 64) : 0;
-      if (cbeg + (r + 1) * round_words < cend) {
-        ++r;
-      } else {
-        ++c;
-        r = 0;
-      }
-    }
-    return t;
-  };
-  struct Pool {
-    u32x4 f[CF], v[CV];
-  };
-  auto load = [&](const Tile& t, Pool& pl) {
-    const bool tile = t.ndoc > 0;
-    const bool live = tile && lane * 32 < t.ndoc;
-    const bool rng = tile && t.S->fkind == FK_RANGE;
-    const int fs = p.f_stream, vs = p.v_stream[0];
-    reg_load<CF>(rng, live, rng ? t.S->streams[fs].fwd : nullptr, rng ? t.S->streams[fs].bits : 0,
-                 rng ? ((int64_t)t.S->num_docs * t.S->streams[fs].bits + 7) / 8 : 0, t.w0 * 2, lane, pl.f);
-    reg_load<CV>(tile, live, tile ? t.S->streams[vs].fwd : nullptr, tile ? t.S->streams[vs].bits : 0,
-                 tile ? ((int64_t)t.S->num_docs * t.S->streams[vs].bits + 7) / 8 : 0, t.w0 * 2, lane, pl.v);
-  };
-  int64_t asum = 0, amin = INT64_MAX, amax = INT64_MIN;
-  unsigned long long matched = 0;  // per lane
-  // one register set: a tile's streams are unpacked (filter -> match mask, values -> 32 offsets), then the next
-  // tile's loads are issued and stay in flight under this tile's folds (r3: two register sets with the fold inside
-  // the per-width switch spilled to scratch or ran 4.6x slower than k_agg_lean)
-  Pool pl;
-  Tile t = next_tile();
-  load(t, pl);
-  while (t.S != nullptr) {  // wave-uniform
-    const int32_t nv = max(0, min(32, t.ndoc - lane * 32));
-    const uint32_t flo = t.S->flo, flen = t.S->flen;
-    const int fk = t.S->fkind;
-    uint32_t m = (t.ndoc <= 0) ? 0u : nv >= 32 ? 0xffffffffu : ((1u << nv) - 1u);  // docs of this lane's run that match
-    uint32_t tmp[32];
-    if (fk == FK_RANGE) {
-      reg_unpack<CF>(pl.f, t.S->streams[p.f_stream].bits, tmp);
-      uint32_t pass = 0;
-#pragma unroll
-      for (int j = 0; j < 32; ++j) pass |= ((tmp[j] - flo) < flen ? 1u : 0u) << j;
-      m &= pass;
-    } else if (fk == FK_DOCRANGE) {
-      const int64_t d0 = (int64_t)t.w0 * 64 + lane * 32;
-      const int64_t lo = max<int64_t>(0, (int64_t)flo - d0), hi = min<int64_t>(32, (int64_t)flo + flen - d0);
-      uint32_t dm = 0;
-      if (hi > lo) dm = (hi >= 32 ? 0xffffffffu : ((1u << hi) - 1u)) & ~(lo >= 32 ? 0xffffffffu : ((1u << lo) - 1u));
-      m &= dm;
-    }
-    reg_unpack<CV>(pl.v, t.S->streams[p.v_stream[0]].bits, tmp);
-    const int64_t base = t.S->vals[0].base;
-    t = next_tile();
-    load(t, pl);
-    uint32_t tsum = 0, tmin = 0xffffffffu, tmax = 0;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const bool h = (m >> j) & 1u;
-      tsum += h ? tmp[j] : 0u;
-      tmin = min(tmin, h ? tmp[j] : 0xffffffffu);
-      tmax = max(tmax, h ? tmp[j] : 0u);
-    }
-    const uint32_t n = (uint32_t)__builtin_popcount(m);
-    matched += n;
-    asum += (int64_t)tsum + base * (int64_t)n;
-    if (n) {
-      amin = min(amin, base + (int64_t)tmin);
-      amax = max(amax, base + (int64_t)tmax);
-    }
-  }
-  const int64_t si = wave_sum_i64(asum);
-  const int64_t mn = wave_min_i64(amin);
-  const int64_t mx = wave_max_i64(amax);
-  const int64_t mt = wave_sum_i64((int64_t)matched);
-  if (lane == 0) {
-    if (mt) atomicAdd(&p.out_count[0], (unsigned long long)mt);
-    const int ops = p.val_ops[0];
-    if (ops & OPS_SUM) atomicAdd(reinterpret_cast<unsigned long long*>(p.out_sum[0]), (unsigned long long)si);
-    if ((ops & OPS_MIN) && mn != INT64_MAX) atomicMin(reinterpret_cast<long long*>(p.out_min[0]), (long long)mn);
-    if ((ops & OPS_MAX) && mx != INT64_MIN) atomicMax(reinterpret_cast<long long*>(p.out_max[0]), (long long)mx);
-  }
-}
-
-void launch_agg_reg(const KParams& p, int grid, hipStream_t s) {
-  // filter windows of 4 / 8 loads, value windows of 4 / 7 (value offsets < 2^26)
-  if (p.agg_reg_cf <= 4 && p.agg_reg_cv <= 4) hipLaunchKernelGGL((k_agg_reg<4, 4>), dim3(grid), dim3(kBlock), 0, s, p);
-  else if (p.agg_reg_cf <= 4) hipLaunchKernelGGL((k_agg_reg<4, 7>), dim3(grid), dim3(kBlock), 0, s, p);
-  else if (p.agg_reg_cv <= 4) hipLaunchKernelGGL((k_agg_reg<8, 4>), dim3(grid), dim3(kBlock), 0, s, p);
-  else hipLaunchKernelGGL((k_agg_reg<8, 7>), dim3(grid), dim3(kBlock), 0, s, p);
-  PH_HIP_CHECK(hipGetLastError());
-}
-
 void launch_count_reg(const KParams& p, int grid, hipStream_t s) {
   switch (p.count_reg) {
 #define PH_COUNT_CASE(n)                                                                                     \

@@ -4,7 +4,7 @@
 
 namespace ph {
 
-size_t partition_lds_bytes(KParams& p) {
+size_t partition_lds_bytes(KParams& p, int ring_log2) {
   const size_t rec = p.part_vbits + p.part_klo > 32 ? 8 : 4;
   size_t o = 0;
   auto place = [&](int32_t& dst, size_t bytes) {
@@ -16,8 +16,7 @@ size_t partition_lds_bytes(KParams& p) {
   p.stage_off = stage_off;
   // ring slots per partition: a whole 64-byte chunk of leftovers (< 16 records) plus one round's appends
   // (~ round records / P, Poisson) must fit or records take the overflow-table path
-  int cl = 5;
-  if (const char* e = getenv("PH_PART_RING_LOG2")) cl = std::max(3, std::min(7, atoi(e)));  // tuning knob (<= 7: a partition's flush lanes stay in one wave)
+  int cl = std::max(3, std::min(7, ring_log2));  // (<= 7: a partition's flush lanes stay in one wave)
   while (cl > 4 && (size_t)(p.num_parts << cl) * rec > 48 * 1024) --cl;
   // the lean kernel's flush moves a partition's records with 16 lanes, one 16-byte quarter each
   if (p.part_fast) cl = std::min(cl, rec == 4 ? 6 : 5);

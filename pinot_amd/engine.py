@@ -52,7 +52,7 @@ class ExecutionStats:
 SCAN_KERNEL_NAMES = {0: "none", 1: "k_scan", 2: "k_agg_lean", 3: "k_agg_sparse", 4: "k_group_lds_lean",
                      5: "k_part_scan + k_part_agg", 6: "k_part_scan2 + k_part_agg",
                      7: "k_scan<MODE_PARTITION> + k_part_agg", 8: "k_part_reg + k_part_agg",
-                     9: "k_count_reg", 10: "k_agg_reg",
+                     9: "k_count_reg",
                      11: "k_group_reg", 12: "k_group_sparse", 14: "k_agg_sparse over roaring containers",
                      15: "k_group_sparse over roaring containers"}
 
@@ -197,6 +197,17 @@ class _ResultHandle:
             pass
 
 
+# ph_ctx_set_option names (include/pinot_hip.h).  The library reads no environment; this harness (tests, bench, tools)
+# maps PH_<NAME> environment variables onto the options of a context before each of its calls, so a test forces a
+# kernel form with monkeypatch.setenv("PH_PART_SETS", "1").
+OPTION_NAMES = ("roaring_atomic", "agg_cont", "group_cont", "disable_partition", "lds_table_max", "no_group_cache",
+                "group_sparse", "agg_sparse", "tile_words", "limit_eager", "part_generic", "agg_generic",
+                "lds_generic", "count_generic", "lds_lean", "group_reg_lg", "stat_fuse", "interrupt_chunks",
+                "part_klo", "part_batch_rows", "part_flush_first", "part_depth", "part_lds", "part_sets",
+                "part_wg_per_cu", "part_slices", "part_mm_blind", "part_serial", "part_ring_log2", "multi_host_merge")
+OPTION_UNSET = -(1 << 63)
+
+
 class GpuContext:
     """One context per GPU (ph_ctx), or over a set of GPUs of the node (``devices``: ph_ctx_create_multi -- segments
     placed by pinned rows, the devices' partial results merged inside the library; a repeated ordinal is a logical
@@ -222,6 +233,7 @@ class GpuContext:
                     N.check(rc)
         self.handle = h
         self.device = device
+        self._env_options = {}  # options this harness set from PH_* environment variables
         # segments and results of this context: released before it (ph_ctx_destroy contract)
         self._segments = weakref.WeakSet()
         self._results = weakref.WeakSet()
@@ -240,6 +252,22 @@ class GpuContext:
             self.close()
         except Exception:
             pass
+
+    def set_option(self, name: str, value=1):
+        """ph_ctx_set_option (None: back to the planner's choice)."""
+        N.check(N.lib().ph_ctx_set_option(self.handle, name.encode(), OPTION_UNSET if value is None else int(value)))
+
+    def _sync_env_options(self):
+        import os
+        want = {}
+        for name in OPTION_NAMES:
+            v = os.environ.get("PH_" + name.upper())
+            if v is not None:
+                want[name] = int(v) if v.lstrip("-").isdigit() else 1
+        for name in set(self._env_options) | set(want):
+            if self._env_options.get(name) != want.get(name):
+                self.set_option(name, want.get(name))
+        self._env_options = want
 
     def set_stream(self, stream_ptr: int):
         N.check(N.lib().ph_ctx_set_stream(self.handle, ctypes.c_void_p(stream_ptr)))
@@ -286,6 +314,7 @@ class GpuContext:
         """copy=False returns zero-copy views of the result's pinned columns; they stay valid while the
         returned IntermediateResult is alive.  ``interrupt``: optional ctypes.c_int32; setting it non-zero from
         another thread cancels the call (CancelledError)."""
+        self._sync_env_options()
         qs = _QueryStruct(q, interrupt)
         segs = (ctypes.c_void_p * max(1, len(segments)))(*[s.handle for s in segments])
         r = ctypes.c_void_p()
@@ -300,6 +329,7 @@ class GpuContext:
     def execute_datatable(self, q: QueryContext, segments: Sequence[PinnedSegment], extra=None) -> bytes:
         """The query's server response: ph_query_execute then ph_result_datatable (DataTable V4 bytes, as
         InstanceResponseBlock.toDataTable).  ``extra``: metadata entries appended to the results metadata."""
+        self._sync_env_options()
         qs = _QueryStruct(q)
         segs = (ctypes.c_void_p * max(1, len(segments)))(*[s.handle for s in segments])
         r = ctypes.c_void_p()
@@ -364,6 +394,7 @@ class GpuContext:
         getTrues() (BaseFilterOperator.java:92).  Returns (doc-bitmap words as uint64 -- bit i of word w is doc
         64 w + i -- or None when ``words`` is False, matching-doc count, ExecutionStats)."""
         q = parse_sql(sql_or_q) if isinstance(sql_or_q, str) else sql_or_q
+        self._sync_env_options()
         qs = _QueryStruct(q)
         nd = segment.num_docs
         out = np.zeros(max(1, (nd + 63) // 64), np.uint64) if words else None
@@ -384,6 +415,7 @@ class GpuContext:
     # ---------------------------------------------------------------- dense partials (multi-GPU combine)
     def dense_layout(self, q: QueryContext, segments: Sequence[PinnedSegment]) -> N.DenseLayout:
         """ph_query_dense_layout: the dense partial tables of ``q`` (count, element type, reduce op)."""
+        self._sync_env_options()
         qs = _QueryStruct(q)
         segs = (ctypes.c_void_p * max(1, len(segments)))(*[s.handle for s in segments])
         lay = N.DenseLayout()
@@ -393,6 +425,7 @@ class GpuContext:
 
     def execute_dense(self, q: QueryContext, segments: Sequence[PinnedSegment], table_ptrs: Sequence[int]):
         """ph_query_execute_dense into caller-owned device tables (device pointers, layout order)."""
+        self._sync_env_options()
         qs = _QueryStruct(q)
         segs = (ctypes.c_void_p * max(1, len(segments)))(*[s.handle for s in segments])
         tabs = (ctypes.c_void_p * max(1, len(table_ptrs)))(*table_ptrs)
@@ -404,6 +437,7 @@ class GpuContext:
     def dense_finalize(self, q: QueryContext, segments: Sequence[PinnedSegment], table_ptrs: Sequence[int],
                        group_begin: int, group_end: int, copy: bool = True) -> IntermediateResult:
         """ph_dense_finalize of key shard [group_begin, group_end) (pointers to the shard's first group)."""
+        self._sync_env_options()
         qs = _QueryStruct(q)
         segs = (ctypes.c_void_p * max(1, len(segments)))(*[s.handle for s in segments])
         tabs = (ctypes.c_void_p * max(1, len(table_ptrs)))(*table_ptrs)

@@ -130,7 +130,7 @@ class ExecStats(ctypes.Structure):
 # every symbol declared in include/pinot_hip.h
 EXPORTED_SYMBOLS = (
     "ph_ctx_create", "ph_ctx_create_multi", "ph_ctx_num_devices", "ph_ctx_set_multi_transport", "ph_segment_device", "ph_ctx_destroy",
-    "ph_ctx_set_stream", "ph_segment_pin", "ph_segment_check", "ph_segment_load_dir", "ph_filter_execute",
+    "ph_ctx_set_stream", "ph_ctx_set_option", "ph_segment_pin", "ph_segment_check", "ph_segment_load_dir", "ph_filter_execute",
     "ph_segment_unpin",
     "ph_segment_device_bytes", "ph_segment_num_docs", "ph_table_set_dictionary", "ph_table_set_column_type", "ph_query_execute",
     "ph_result_destroy", "ph_result_stats", "ph_result_num_groups", "ph_result_key_entry_size", "ph_result_key_type",
@@ -178,6 +178,7 @@ def lib():
         "ph_segment_device": ([vp], i32),
         "ph_ctx_destroy": ([vp], ctypes.c_int),
         "ph_ctx_set_stream": ([vp, vp], ctypes.c_int),
+        "ph_ctx_set_option": ([vp, ctypes.c_char_p, i64], ctypes.c_int),
         "ph_segment_pin": ([vp, ctypes.POINTER(SegmentDesc), ctypes.POINTER(vp)], ctypes.c_int),
         "ph_segment_check": ([ctypes.POINTER(SegmentDesc)], ctypes.c_int),
         "ph_segment_unpin": ([vp], ctypes.c_int),

@@ -2,12 +2,12 @@
 against the oracle, each query asserting which kernel ran (ph_exec_stats.scan_kernel):
 
   k_count_reg         COUNT(*) over the filter stream, register-direct decode (filter streams of 1..24 bits)
-  k_agg_reg           aggregation only, register-direct (value streams of 1..26 bits)
   k_agg_lean          aggregation only, one packed integer column (value streams of 1..26 bits)
   k_group_reg         LDS group table, register-direct decode, lane-interleaved slots (value streams of 1..31 bits;
                       32 slots per key for 37 keys, 4 for 740 keys, COUNT-only)
   k_group_lds_lean    LDS-private group table (value streams of 1..31 bits)
-  k_part_reg          partitioned group-by, register-direct decode (filter streams <= 16 bits; 32-bit records)
+  k_part_reg          partitioned group-by, register-direct decode (filter streams <= 16 bits; 32-bit records), with
+                      one and with two ring sets (part_sets)
   k_part_scan(2)      partitioned group-by, 90 000 keys (value streams of 1..31 bits; 32- and 64-bit records)
 
 The aggregated column's frame-of-reference stream is `w` bits wide (values base + [0, 2^w - 1], both extremes
@@ -27,7 +27,7 @@ from tests.seeds import seed_of
 pytestmark = pytest.mark.gpu
 
 PH_KERNEL_AGG_LEAN, PH_KERNEL_GROUP_LDS_LEAN, PH_KERNEL_PART_LEAN, PH_KERNEL_PART_LEAN2, PH_KERNEL_PART_REG = 2, 4, 5, 6, 8
-PH_KERNEL_COUNT_REG, PH_KERNEL_AGG_REG, PH_KERNEL_GROUP_REG = 9, 10, 11
+PH_KERNEL_COUNT_REG, PH_KERNEL_GROUP_REG = 9, 11
 
 
 @pytest.fixture(scope="module")
@@ -93,9 +93,6 @@ def test_lean_kernels_every_width(ctx, w, monkeypatch):
     # k_agg_lean: 32-bit tile sums need value offsets below 2^26; wider streams run k_scan<MODE_AGG>
     agg = f"SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where}"
     _check(ctx, gpu, ora, agg, PH_KERNEL_AGG_LEAN if w <= 26 else 1)  # the LDS-staged k_agg_lean (default)
-    monkeypatch.setenv("PH_AGG_REG", "1")
-    _check(ctx, gpu, ora, agg, PH_KERNEL_AGG_REG if w <= 26 else 1)  # register-direct k_agg_reg (opt-in)
-    monkeypatch.delenv("PH_AGG_REG")
     grp = f"SELECT g, COUNT(*), SUM(m), MIN(m), MAX(m) FROM t{where} GROUP BY g ORDER BY g LIMIT 100"
     # k_group_reg keeps COUNT << 40 | SUM in one slot word: value ranges that could carry past 2^40 inside one
     # workgroup (w >= 29 here) run k_group_lds_lean's unpacked table
@@ -111,9 +108,13 @@ def test_lean_kernels_every_width(ctx, w, monkeypatch):
             f"GROUP BY g1, g2 ORDER BY g1, g2 LIMIT 200000")
     # k_part_reg decodes from registers (its own per-width switch): filter / key streams <= 16 bits
     _check(ctx, gpu, ora, part, PH_KERNEL_PART_REG if min(w, 24) <= 16 else PH_KERNEL_PART_LEAN)
-    monkeypatch.setenv("PH_PART_RING_LOG2", "4")  # 16-slot rings: skewed rounds take the overflow path
-    _check(ctx, gpu, ora, part, PH_KERNEL_PART_REG if min(w, 24) <= 16 else PH_KERNEL_PART_LEAN)
-    monkeypatch.delenv("PH_PART_RING_LOG2")
+    for sets in ("1", "2"):  # one ring set (flush, barrier, append, barrier) / two (append beside the flush)
+        monkeypatch.setenv("PH_PART_SETS", sets)
+        _check(ctx, gpu, ora, part, PH_KERNEL_PART_REG if min(w, 24) <= 16 else PH_KERNEL_PART_LEAN)
+        monkeypatch.setenv("PH_PART_RING_LOG2", "4")  # 16-slot rings: skewed rounds take the overflow path
+        _check(ctx, gpu, ora, part, PH_KERNEL_PART_REG if min(w, 24) <= 16 else PH_KERNEL_PART_LEAN)
+        monkeypatch.delenv("PH_PART_RING_LOG2")
+    monkeypatch.delenv("PH_PART_SETS")
     monkeypatch.setenv("PH_PART_LDS", "1")  # the LDS-staged forms
     _check(ctx, gpu, ora, part, PH_KERNEL_PART_LEAN)
     monkeypatch.setenv("PH_PART_DEPTH", "2")
