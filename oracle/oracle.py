@@ -784,7 +784,7 @@ def _or_set(makers, n):
     return make
 
 
-_PRIORITY = {"sorted": 0, "range": 200, "legacy": 200, "and": 300, "or": 400, "scan": 500, "inverted": 10000}
+_PRIORITY = {"sorted": 0, "bitmap": 100, "range": 200, "legacy": 200, "and": 300, "or": 400, "scan": 500, "inverted": 10000}
 
 
 def _priority(node: _Leaf) -> int:
