@@ -188,6 +188,8 @@ typedef struct {
   const struct ph_order_by* order_by;
   int32_t limit;                      /* the query's LIMIT */
   int32_t min_segment_group_trim_size;
+  /* query option skipStarTree (QueryContext.isSkipStarTree): 1 = never answer from a segment's star-tree */
+  int32_t skip_star_tree;
 } ph_query;
 
 /* one ORDER BY expression: a group-by column (index into group_by) or an aggregation (index into aggregations) */
@@ -221,6 +223,8 @@ typedef struct {
   double finalize_ms;                      /* multi-device: turning the merged key shards into the result */
   double scan_ms;                          /* multi-device: wall time of the devices' scans into their partial tables
                                               (host_ms - scan_ms - merge_ms - finalize_ms = planning + assembly) */
+  int64_t num_segments_star_tree;          /* segments answered from a star-tree (GroupByPlanNode :77-99,
+                                              AggregationPlanNode :122-141) */
 } ph_exec_stats;
 
 /* ph_exec_stats.scan_kernel */
@@ -306,6 +310,36 @@ int ph_segment_unpin(ph_segment* seg);
 int64_t ph_segment_device_bytes(const ph_segment* seg);
 int32_t ph_segment_num_docs(const ph_segment* seg);
 int32_t ph_segment_device(const ph_segment* seg);  /* index into the context's device set */
+
+/* Star-tree index of a pinned segment (StarTreeV2: StarTreeIndexContainer / StarTreeLoaderUtils.loadStarTreeV2,
+ * pinot-segment-local/.../startree/v2/store/StarTreeLoaderUtils.java): the buffers of one star-tree in
+ * star_tree_index as star_tree_index_map names them.  The records are pinned beside the segment (the dimensions with
+ * the segment's own dictionaries, the function-column pair columns as raw columns); a later query whose aggregations
+ * are all pairs of the tree, whose filter is an AND of per-column predicates (ORs on one column) over tree dimensions
+ * and whose group-by columns are tree dimensions is answered from it, as GroupByPlanNode.java:77-99 /
+ * AggregationPlanNode.java:122-141 choose it: StarTreeFilterOperator's traversal on the host
+ * (StarTreeFilterOperator.java:207-358) gives the star-tree documents, the remaining predicates and the
+ * aggregation over the pair columns run in the same kernels as any query (COUNT sums count__*, SUM / MIN / MAX read
+ * sum__ / min__ / max__).  A pair of another function (e.g. distinctCountHLL__c) is recorded: a query it would serve
+ * is PH_ERR_UNSUPPORTED (CPU plan). */
+typedef struct {
+  const void* tree;             /* the STAR_TREE buffer (OffHeapStarTree.java:45-83 format, little-endian) */
+  uint64_t tree_size;
+  int32_t num_docs;             /* startree.v2.<i>.total.docs */
+  int32_t num_dimensions;       /* must equal the tree's dimensions (split order) */
+  const char* const* dimensions;
+  const void* const* dimension_forward_index;  /* <dim>.FORWARD_INDEX: fixed-bit dictIds at the column's bit width */
+  const uint64_t* dimension_forward_index_size;
+  int32_t num_metrics;          /* startree.v2.<i>.function.column.pairs ("count__*", "sum__col", ...) */
+  const char* const* metrics;
+  const void* const* metric_forward_index;     /* <pair>.FORWARD_INDEX raw forward index (LONG count, DOUBLE others);
+                                                  NULL for a pair of another function */
+  const uint64_t* metric_forward_index_size;
+} ph_star_tree_desc;
+int ph_segment_add_star_tree(ph_segment* seg, const ph_star_tree_desc* desc);
+int32_t ph_segment_num_star_trees(const ph_segment* seg);
+/* Host-only parse of a STAR_TREE buffer (OffHeapStarTree's checks: magic, version, header size, node count). */
+int ph_star_tree_check(const void* tree, uint64_t tree_size, int32_t* num_nodes, int32_t* num_dimensions);
 
 /* Table-level sorted value union for a column (group keys share ids across segments and GPUs).
  * Optional: without it the union of the queried segments' dictionaries is used. */

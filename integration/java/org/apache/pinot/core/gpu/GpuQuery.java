@@ -92,8 +92,9 @@ public final class GpuQuery {
           d.add(x);
         }
       }
-      // [numOrderBy, (kind, index, asc)..., limit, minSegmentGroupTrimSize]: segment group trim
-      // (GroupByOperator.java:114-130) runs in the library (ph_query.min_segment_group_trim_size)
+      // [numOrderBy, (kind, index, asc)..., limit, minSegmentGroupTrimSize, skipStarTree]: segment group trim
+      // (GroupByOperator.java:114-130) runs in the library (ph_query.min_segment_group_trim_size); a segment's
+      // star-tree is taken there unless the skipStarTree query option is set (ph_query.skip_star_tree)
       List<OrderByExpressionContext> orderBy = ctx.getOrderByExpressions();
       List<int[]> order = new ArrayList<>();
       if (orderBy != null && ctx.getGroupByExpressions() != null) {
@@ -119,6 +120,7 @@ public final class GpuQuery {
       }
       d.add(ctx.getLimit());
       d.add(ctx.getMinSegmentGroupTrimSize());
+      d.add(ctx.isSkipStarTree() ? 1 : 0);
       int[] desc = d.stream().mapToInt(Integer::intValue).toArray();
       return new GpuQuery(desc, b._strings.toArray(new String[0]), ctx.getNumGroupsLimit(), ctx.getEndTimeMs());
     } catch (UnsupportedOperationException e) {

@@ -225,7 +225,7 @@ static int decode_query(const jint* desc, jsize nd, const char** strs, jsize ns,
     b->aggs[i].column2 = S(tmp);
     NEXT(b->aggs[i].expr_op);
   }
-  if (k < nd) { /* optional trailing block: ORDER BY + LIMIT + minSegmentGroupTrimSize */
+  if (k < nd) { /* optional trailing block: ORDER BY + LIMIT + minSegmentGroupTrimSize [+ skipStarTree] */
     NEXT(q->num_order_by);
     if (q->num_order_by < 0 || q->num_order_by > nd - k) return -1;
     b->order = (ph_order_by*)calloc((size_t)q->num_order_by + 1, sizeof(ph_order_by));
@@ -238,6 +238,7 @@ static int decode_query(const jint* desc, jsize nd, const char** strs, jsize ns,
     NEXT(q->limit);
     NEXT(q->min_segment_group_trim_size);
     q->order_by = b->order;
+    if (k < nd) NEXT(q->skip_star_tree); /* QueryContext.isSkipStarTree() */
   }
   /* indices inside the query (children, predicates, root) are range-checked by the library itself */
   q->filter_nodes = b->nodes;

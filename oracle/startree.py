@@ -28,6 +28,14 @@ ALL = -1
 
 
 @dataclass
+class _F:
+    """A filter node (FilterContext shape: type, children, predicate)."""
+    type: str
+    children: tuple = ()
+    predicate: object = None
+
+
+@dataclass
 class Tree:
     dimensions: List[str]
     nodes: np.ndarray  # [num_nodes, 7]: dim, value, start, end, aggregated doc, first child, last child
@@ -283,33 +291,36 @@ def execute(q, seg, st: StarTreeData, pairs, evals):
         return {}, (0, 0, 0, seg.num_docs)
     d0, rem = tr
     # the AND StarTreeFilterOperator builds (:165-198): [BitmapBasedFilterOperator of d0] + per remaining column (its
-    # HashSet order) one operator per composite -- a scan leaf, or an OR of scan leaves -- through
-    # FilterOperatorUtils.getAndFilterOperator (priorities: bitmap 100, OR 400, scan 500; stable sort)
+    # HashSet order) one operator per composite -- a scan leaf, or an OR of scan leaves -- over the star-tree's
+    # dimension columns (forward index + dictionary only: scans), through FilterOperatorUtils.getAndFilterOperator
+    # (priorities: bitmap 100, OR 400, scan 500; stable), after the query optimizer's same-column merges
+    view = O.OracleSegment("startree", st.num_docs)
+    for d in st.tree.dimensions:
+        pc = seg.columns[d]
+        view.columns[d] = O.OracleColumn(d, pc.data_type, pc.dictionary, pc.bits, False,
+                                         fwd=O.fixed_bit_pack(st.dim_ids[d].astype(np.int64), pc.bits))
+    used = list(rem)
+    col_index = {c: i for i, c in enumerate(used)}
+    comps = []
+    for col in rem:
+        for comp in evals[col]:
+            leaves = [_F("PREDICATE", (), p) for p, _ in comp]
+            comps.append(leaves[0] if len(leaves) == 1 else _F("OR", tuple(leaves)))
     mask = np.zeros(st.num_docs, bool)
     mask[d0] = True
-    root = O._Leaf("and")
-    b = O._Leaf("leaf")
-    b.ikind, b.docs = "bitmap", mask.copy()
-    root.children.append(b)
-    for col in rem:
-        ids = st.dim_ids[col]
-        for comp in evals[col]:
-            leaves = []
-            for _, m in comp:
-                lf = O._Leaf("leaf", is_scan=True)
-                lf.ikind, lf.docs = "scan", m[ids].astype(bool)
-                leaves.append(lf)
-            if len(leaves) == 1:
-                root.children.append(leaves[0])
-            else:
-                o = O._Leaf("or")
-                o.children = leaves
-                root.children.append(o)
-            m_any = np.logical_or.reduce([lf.docs for lf in leaves])
-            mask &= m_any
     entries = 0
-    if len(root.children) > 1:
-        entries = O.filter_entries_of(root, st.num_docs, lambda nd: nd.docs)
+    if comps:
+        rest = O._merge_same_column(O._plan_filter(_F("AND", tuple(comps)), view, col_index))
+        if rest.kind == "none":
+            mask[:] = False
+        elif rest.kind != "all":
+            mask &= O._eval_docs(rest, view, used)
+            root = O._Leaf("and")
+            b0 = O._Leaf("leaf")
+            b0.ikind, b0.docs = "bitmap", np.isin(np.arange(st.num_docs), d0)
+            root.children = [b0] + (rest.children if rest.kind == "and" else [rest])
+            entries = O.filter_entries_of(
+                root, st.num_docs, lambda nd: nd.docs if hasattr(nd, "docs") else O._eval_docs(nd, view, used))
     docs = np.nonzero(mask)[0]
     groups: Dict[tuple, list] = {}
     gids = [st.dim_ids[g] for g in q.group_by]
@@ -330,3 +341,89 @@ def execute(q, seg, st: StarTreeData, pairs, evals):
             else:
                 row[j] = float(v) if row[j] is None else max(row[j], float(v))
     return groups, (len(docs), int(entries), len(docs) * nproj, seg.num_docs)
+
+
+def execute_with_star_trees(q, segments):
+    """A query over [(OracleSegment, StarTreeData or None)]: each segment through its star-tree when the plan node
+    takes it (fit), else through oracle.execute; per-group results merged as the combine does (COUNT / SUM add, MIN /
+    MAX), statistics summed.  Returns (keys, aggs, stats dict, segments served by a star-tree)."""
+    merged: Dict[tuple, list] = {}
+    order: List[tuple] = []
+    stats = dict(num_docs_scanned=0, num_entries_scanned_in_filter=0, num_entries_scanned_post_filter=0,
+                 num_total_docs=0)
+    served = 0
+
+    def fold(key, row):
+        cur = merged.get(key)
+        if cur is None:
+            merged[key] = list(row)
+            order.append(key)
+            return
+        for j, a in enumerate(q.aggregations):
+            if row[j] is None:
+                continue
+            if cur[j] is None:
+                cur[j] = row[j]
+            elif a.function in ("COUNT", "SUM"):
+                cur[j] = cur[j] + row[j]
+            elif a.function == "MIN":
+                cur[j] = min(cur[j], row[j])
+            else:
+                cur[j] = max(cur[j], row[j])
+    for seg, st in segments:
+        f = fit(q, seg, st) if st is not None else None
+        if q.group_by == [] and f is not None:
+            # AggregationPlanNode: FastFilteredCount (COUNT only over an index-countable filter) and the
+            # metadata plan (no filter; COUNT / MIN / MAX only) take the segment before the star-tree
+            fns = {a.function for a in q.aggregations}
+            if q.filter is None and "SUM" not in fns:
+                f = None
+            elif fns == {"COUNT"} and q.filter is not None and _index_countable(q, seg):
+                f = None
+        if f is None:
+            r = O.execute(q, [seg])
+            for key, row in zip(r.keys, r.aggs):
+                fold(key, row)
+            stats["num_docs_scanned"] += r.stats.num_docs_scanned
+            stats["num_entries_scanned_in_filter"] += r.stats.num_entries_scanned_in_filter
+            stats["num_entries_scanned_post_filter"] += r.stats.num_entries_scanned_post_filter
+            stats["num_total_docs"] += r.stats.num_total_docs
+            continue
+        served += 1
+        groups, (docs, ent, post, total) = execute(q, seg, st, *f)
+        for key, row in groups.items():
+            fold(key, row)
+        stats["num_docs_scanned"] += docs
+        stats["num_entries_scanned_in_filter"] += ent
+        stats["num_entries_scanned_post_filter"] += post
+        stats["num_total_docs"] += total
+    if not q.group_by and not merged:
+        merged[()] = [0 if a.function == "COUNT" else None for a in q.aggregations]
+        order.append(())
+    keys = order
+    aggs = []
+    for k in keys:
+        row = []
+        for j, a in enumerate(q.aggregations):
+            v = merged[k][j]
+            if v is None:  # an aggregation over no docs: the reference's default (SUM 0, MIN +inf, MAX -inf)
+                v = {"COUNT": 0, "SUM": 0.0, "MIN": float("inf"), "MAX": float("-inf")}[a.function]
+            row.append(v)
+        aggs.append(row)
+    return keys, aggs, stats, served
+
+
+def _index_countable(q, seg) -> bool:
+    """FastFilteredCountOperator's canOptimizeCount on the segment's own filter: sorted / inverted leaves and NOTs of
+    them only (no scan, AND or OR)."""
+    root = O._merge_same_column(O._plan_filter(q.filter, seg, {c: i for i, c in enumerate(seg.columns)}))
+
+    def ok(n):
+        if n.kind in ("all", "none"):
+            return True
+        if n.kind == "leaf":
+            return getattr(n, "ikind", "") in ("sorted", "inverted")
+        if n.kind == "not":
+            return ok(n.children[0])
+        return False
+    return ok(root)

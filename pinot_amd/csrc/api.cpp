@@ -96,6 +96,35 @@ static ph_segment* pin_placed(ph_ctx* ctx, int64_t rows, F&& pin) {
   return s;
 }
 
+namespace ph {
+// drops what the context cached for a segment: its remaps to table / union dictionaries and the unions that include
+// it (never hit again: a re-pinned segment gets a new id)
+void star_tree_forget(Context& c, ph_segment* seg) {
+  std::lock_guard<std::mutex> lk(c.mu);
+  for (auto& kv : c.table_dicts) {
+    std::lock_guard<std::mutex> gl(kv.second->mu);
+    kv.second->remaps.erase(seg->id);
+  }
+  const std::string tag = std::to_string(seg->id) + ",";
+  auto holds = [&](const std::string& key) {
+    const size_t h = key.find('#');
+    for (size_t p = key.find(tag, h); p != std::string::npos; p = key.find(tag, p + 1))
+      if (key[p - 1] == '#' || key[p - 1] == ',') return true;
+    return false;
+  };
+  for (auto it = c.union_order.begin(); it != c.union_order.end();) {
+    if (holds(*it)) {
+      c.union_cache.erase(*it);
+      it = c.union_order.erase(it);
+    } else {
+      ++it;
+    }
+  }
+}
+void star_tree_add_impl(ph_segment* seg, const ph_star_tree_desc* d);
+void star_tree_check_impl(const void* tree, uint64_t size, int32_t* num_nodes, int32_t* num_dimensions);
+}  // namespace ph
+
 extern "C" {
 
 const char* ph_last_error(void) { return g_last_error.c_str(); }
@@ -179,38 +208,30 @@ int ph_segment_check(const ph_segment_desc* desc) {
   return guarded([&] { segment_check_impl(desc); });
 }
 
+
 int ph_segment_unpin(ph_segment* seg) {
   return guarded([&] {
     if (!seg) return;
     (void)hipSetDevice(seg->ctx->device);
     ph::Context& c = *seg->ctx;
-    {
-      // the segment's remaps to table / union dictionaries, and the unions that include it (never hit again:
-      // a re-pinned segment gets a new id)
-      std::lock_guard<std::mutex> lk(c.mu);
-      for (auto& kv : c.table_dicts) {
-        std::lock_guard<std::mutex> gl(kv.second->mu);
-        kv.second->remaps.erase(seg->id);
-      }
-      const std::string tag = std::to_string(seg->id) + ",";
-      auto holds = [&](const std::string& key) {
-        const size_t h = key.find('#');
-        for (size_t p = key.find(tag, h); p != std::string::npos; p = key.find(tag, p + 1))
-          if (key[p - 1] == '#' || key[p - 1] == ',') return true;
-        return false;
-      };
-      for (auto it = c.union_order.begin(); it != c.union_order.end();) {
-        if (holds(*it)) {
-          c.union_cache.erase(*it);
-          it = c.union_order.erase(it);
-        } else {
-          ++it;
-        }
-      }
-    }
+    ph::star_tree_forget(c, seg);  // (its star-tree views forget theirs as they are freed)
     c.pinned_rows -= seg->num_docs;
     delete seg;  // hipFree waits for work in flight on the buffers
   });
+}
+
+int ph_segment_add_star_tree(ph_segment* seg, const ph_star_tree_desc* desc) {
+  return guarded([&] {
+    if (!seg) fail(PH_ERR_INVALID_ARGUMENT, "null segment");
+    PH_HIP_CHECK(hipSetDevice(seg->ctx->device));
+    ph::star_tree_add_impl(seg, desc);
+  });
+}
+
+int32_t ph_segment_num_star_trees(const ph_segment* seg) { return seg ? (int32_t)seg->star_trees.size() : -1; }
+
+int ph_star_tree_check(const void* tree, uint64_t tree_size, int32_t* num_nodes, int32_t* num_dimensions) {
+  return guarded([&] { ph::star_tree_check_impl(tree, tree_size, num_nodes, num_dimensions); });
 }
 
 int64_t ph_segment_device_bytes(const ph_segment* seg) {
@@ -346,6 +367,7 @@ int ph_filter_execute(ph_ctx* ctx, const ph_query* query, ph_segment* segment, u
     q.num_order_by = 0;
     q.order_by = nullptr;
     q.min_segment_group_trim_size = -1;
+    q.skip_star_tree = 1;  // FilterPlanNode's operator is over the segment's own documents
     ph_segment* segs[1] = {segment};
     std::unique_ptr<ph_result> r;
     if (!doc_words) {

@@ -231,6 +231,7 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
   std::vector<int> active;
   for (int k = 0; k < D; ++k)
     if (!by[k].empty()) active.push_back(k);
+  // segments a star-tree serves are answered from their views (startree.cpp), per device, merged by value
   if (active.size() <= 1) {
     const int k = active.empty() ? 0 : active[0];
     return query_execute_impl(x->devs[k], q, by[k].data(), (int32_t)by[k].size(), nullptr);
@@ -288,6 +289,7 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
     r->stats.host_ms = ms_since(t0);
     return r;
   };
+  if (star_tree_serves_any(q, all.data(), (int32_t)all.size())) return host_merge();
   if (fresh) {
     try {
       DenseArgs la = dense(active[0], DENSE_LAYOUT);

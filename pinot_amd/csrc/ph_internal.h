@@ -20,6 +20,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -397,6 +398,18 @@ struct DenseArgs {
   // ph_filter_execute: the call is a COUNT(*) whose scan also writes each segment's doc bitmap into `words` (device
   // memory, zeroed here): segment i's ceil(num_docs / 64) words start at word_off[i]
   struct FilterDocset* docset = nullptr;
+  // star-tree views in this call (startree.cpp): a view's filter is its traversal's documents AND the remaining
+  // predicates, not the query's filter tree
+  const std::map<const ph_segment*, struct StarSegPlan>* star = nullptr;
+};
+// One star-tree view of a query (StarTreeFilterOperator.getFilterOperator, StarTreeFilterOperator.java:157-199): the
+// star-tree documents the traversal matched (sorted, disjoint, inclusive (start, end) pairs), the remaining predicate
+// columns' composites in the order the AND receives them (each a list of predicate indices ORed), and whether a
+// predicate column matched no dictId (EmptyFilterOperator).
+struct StarSegPlan {
+  std::vector<int32_t> ranges;
+  std::vector<std::vector<int32_t>> composites;
+  bool empty = false;
 };
 struct FilterDocset {
   unsigned long long* words;
@@ -568,6 +581,9 @@ extern const char* const kOptNames[OPT_COUNT];
 
 }  // namespace ph
 
+namespace ph {
+struct StarTree;
+}
 struct ph_segment {
   ph::Context* ctx = nullptr;
   std::string name;
@@ -575,7 +591,25 @@ struct ph_segment {
   int64_t device_bytes = 0;
   uint64_t id = 0;
   std::map<std::string, std::unique_ptr<ph::Column>> columns;
+  std::vector<std::unique_ptr<ph::StarTree>> star_trees;  // ph_segment_add_star_tree (startree.cpp)
+  int32_t parent_docs = -1;  // a star-tree view: its segment's total docs (numTotalDocs of a star-tree plan)
+  ~ph_segment();
 };
+
+namespace ph {
+// A star-tree of a pinned segment (StarTreeV2): the tree on the host (OffHeapStarTree nodes, 7 ints each: dimension,
+// value, start, end, aggregated doc, first child, last child) and its records pinned as a segment of their own -- the
+// split-order dimensions with the segment's dictionaries, the count / sum / min / max pair columns as raw columns
+struct StarTree {
+  std::vector<std::string> dims;
+  std::vector<int32_t> nodes;
+  int32_t num_nodes = 0;
+  std::vector<std::string> pairs;     // every function-column pair of the tree
+  std::set<std::string> served;       // the pairs pinned in `view` (count / sum / min / max)
+  ph_segment* view = nullptr;         // owned
+  ~StarTree();
+};
+}  // namespace ph
 
 namespace ph {
 
@@ -836,6 +870,17 @@ void raw_forward_index_decode(const uint8_t* buf, uint64_t size, int32_t data_ty
 std::vector<uint8_t> result_to_datatable(const ph_result* r, const ph_query* q, const ph_metadata_entry* extra,
                                          int32_t num_extra);
 void raw_dictionary_encode(int32_t data_type, const void* values, int64_t n, Dictionary* dict, std::vector<int32_t>* ids);
+// star-trees (startree.cpp): a query whose segments a star-tree serves runs over their views and merges with the rest
+// by group value; nullptr when no queried segment takes its star-tree.  `dense_op`: a dense-partials call refuses
+// star-tree segments (PH_ERR_UNSUPPORTED) rather than mixing their tables.
+ph_result* star_tree_execute(Context* ctx, const ph_query* q, ph_segment* const* segs, int32_t nseg, int dense_op);
+bool star_tree_serves_any(const ph_query* q, ph_segment* const* segs, int32_t nseg);
+void star_tree_forget(Context& c, ph_segment* seg);  // api.cpp: drop a view's remaps / unions before it is freed
+// query.cpp helpers the star-tree planner shares with the scan planner: the dictIds a predicate matches on a column
+// (bit per dictId; *always_true / *always_false as the evaluator reports them), and whether a segment's filter is
+// answered by FastFilteredCountOperator (COUNT(*) over an index-countable filter, AggregationPlanNode.java:183-188)
+std::vector<char> predicate_dict_ids(const ph_predicate& p, const Column& c, bool* always_true, bool* always_false);
+bool filter_index_countable(const ph_query* q, ph_segment* seg);
 
 }  // namespace ph
 

@@ -781,6 +781,66 @@ double leaf_docs_estimate(const BitmapLeaf& b) {
   return (double)b.seg->num_docs * (double)(b.hi - b.lo + 1) / (double)std::max<int32_t>(1, b.col->cardinality);
 }
 
+// FastFilteredCountOperator's getNumMatchingDocs from the index alone (AggregationPlanNode.java:183-188): a sorted doc
+// range, an inverted-index bitmap (disjoint per dictId in a single-value column) or their NOT; -1 when the filter
+// needs a scan (AND / OR / scan leaves, range-slice leaves counted from their bitmap)
+int64_t index_count(const PNode& n, const std::vector<BitmapLeaf>& bms, int64_t docs) {
+  if (n.kind == L_ALL) return docs;
+  if (n.kind == L_NONE) return 0;
+  if (n.op == OP_DOCRANGES) {
+    int64_t c = 0;
+    for (size_t r = 0; r + 1 < n.ranges.size(); r += 2) c += (int64_t)n.ranges[r + 1] - n.ranges[r] + 1;
+    return c;
+  }
+  if (n.op == OP_BITMAP) {
+    const BitmapLeaf& b = bms[(size_t)n.bitmap_leaf];
+    if (b.range) return -1;
+    return bitmap_docs(*b.col, b.dict_ids);
+  }
+  if (n.op == OP_NOT && n.kids.size() == 1) {
+    const int64_t c = index_count(n.kids[0], bms, docs);
+    return c < 0 ? -1 : docs - c;
+  }
+  return -1;
+}
+
+// a star-tree view's filter (StarTreeFilterOperator.getFilterOperator, StarTreeFilterOperator.java:157-199): the
+// traversal's documents (a BitmapBasedFilterOperator: index-based, first in the AND) AND each remaining composite --
+// one predicate's leaf, or the OR of its predicates' leaves -- over the view's dimension columns
+PNode star_root(Planner& pl, ph_segment* seg, const StarSegPlan& sp) {
+  PNode none;
+  none.kind = L_NONE;
+  if (sp.empty || sp.ranges.empty()) return none;
+  PNode docs;
+  docs.op = OP_DOCRANGES;
+  docs.ranges = sp.ranges;
+  PNode a;
+  a.op = OP_AND;
+  a.kids.push_back(std::move(docs));
+  for (auto& comp : sp.composites) {
+    PNode k;
+    if (comp.size() == 1) {
+      k = pl.leaf(seg, pl.q->predicates[comp[0]]);
+    } else {
+      k.op = OP_OR;
+      bool all = false;
+      for (int32_t pi : comp) {
+        PNode x = pl.leaf(seg, pl.q->predicates[pi]);
+        if (x.kind == L_ALL) all = true;
+        if (x.kind == L_NODE) k.kids.push_back(std::move(x));
+      }
+      if (all) k.kind = L_ALL;
+      else if (k.kids.empty()) k.kind = L_NONE;
+      else if (k.kids.size() == 1) k = std::move(k.kids[0]);
+    }
+    if (k.kind == L_NONE) return none;
+    if (k.kind == L_ALL) continue;
+    a.kids.push_back(std::move(k));
+  }
+  if (a.kids.size() == 1) return std::move(a.kids[0]);
+  return a;
+}
+
 }  // namespace
 
 namespace {
@@ -975,6 +1035,42 @@ std::shared_ptr<GlobalDict> union_dictionary(const std::string& col, const std::
   return build_union(nullptr, col, segs);
 }
 
+std::vector<char> predicate_dict_ids(const ph_predicate& p, const Column& c, bool* always_true, bool* always_false) {
+  const DictIdSet s = evaluate_predicate(p, c);
+  *always_true = s.always_true;
+  *always_false = s.always_false;
+  std::vector<char> m((size_t)std::max(0, c.cardinality), 0);
+  if (s.always_false) return m;
+  if (s.always_true) {
+    std::fill(m.begin(), m.end(), 1);
+    return m;
+  }
+  if (s.is_range) {
+    for (int64_t i = s.start; i < s.end && i < (int64_t)m.size(); ++i) m[(size_t)i] = 1;
+    return m;
+  }
+  if (s.exclusive) std::fill(m.begin(), m.end(), 1);
+  for (int32_t id : s.ids)
+    if (id >= 0 && id < (int32_t)m.size()) m[(size_t)id] = s.exclusive ? 0 : 1;
+  return m;
+}
+
+bool filter_index_countable(const ph_query* q, ph_segment* seg) {
+  if (q->filter_root < 0) return true;
+  Planner pl;
+  pl.q = q;
+  std::vector<std::string> names;
+  for (int i = 0; i < q->num_predicates; ++i)
+    if (q->predicates[i].column && !pl.slot.count(q->predicates[i].column)) {
+      pl.slot[q->predicates[i].column] = (int)names.size();
+      names.push_back(q->predicates[i].column);
+    }
+  PNode root = pl.build(seg, q->filter_root, 0);
+  merge_same_column_leaves(root, [&](int slot) { return (int64_t)seg->columns.at(names[(size_t)slot])->cardinality; },
+                           &pl.bitmaps);
+  return index_count(root, pl.bitmaps, seg->num_docs) >= 0;
+}
+
 ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const* segs_in, int32_t nseg,
                               const DenseArgs* dn) {
   const int dop = dn ? dn->op : 0;
@@ -995,6 +1091,11 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
               q->filter_root < 0))
     fail(PH_ERR_INVALID_ARGUMENT, "a filter call is a filtered COUNT(*)");
   if (q->num_group_by > kMaxGroupCols) fail(PH_ERR_UNSUPPORTED, "too many group-by columns");
+  // segments a star-tree serves (GroupByPlanNode.java:77-99, AggregationPlanNode.java:122-141): their views, merged
+  // with the rest (startree.cpp)
+  const std::map<const ph_segment*, StarSegPlan>* star = dn ? dn->star : nullptr;
+  if (!star && !fds && !q->skip_star_tree && nseg > 0)
+    if (ph_result* r = star_tree_execute(ctx, q, segs_in, nseg, dop)) return r;
   PH_HIP_CHECK(hipSetDevice(ctx->device));
   LaneGuard lane(ctx);  // this call's streams, events and staging (concurrent calls use their own)
   const hipStream_t st = lane.stream();
@@ -1149,7 +1250,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   // ---- aggregation-only, no filter, metadata-answerable (NonScanBasedAggregationOperator)
   bool non_scan = q->filter_root < 0 && q->num_group_by == 0 && nagg > 0;
   for (int k = 0; k < nagg && non_scan; ++k) non_scan = q->aggregations[k].type != PH_AGG_SUM;
-  if (dop) non_scan = false;  // dense partials always come from the scan
+  if (dop || star) non_scan = false;  // dense partials always come from the scan; a view's filter is its traversal
   res->num_groups = 1;
   auto init_row_results = [&](int64_t rows) {
     res->aggs.resize(nagg);
@@ -1223,7 +1324,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   for (int i = 0; i < nseg && dop != DENSE_LAYOUT && !fin; ++i) {
     PNode root;
     root.kind = L_ALL;
-    if (q->filter_root >= 0) root = pl.build(segs[i], q->filter_root, 0);
+    auto sv = star ? star->find(segs[i]) : decltype(star->end()){};
+    if (star && sv != star->end()) root = star_root(pl, segs[i], sv->second);
+    else if (q->filter_root >= 0) root = pl.build(segs[i], q->filter_root, 0);
     // same-column scan predicates merge first, as the reference's query optimizer merges them before planning
     // (MergeEqInFilterOptimizer: `d_year = 1997 OR d_year = 1998` -> one IN; MergeRangeFilterOptimizer: ranges of
     // one column under an AND), so the statistics below see the reference's operator tree
@@ -1253,25 +1356,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   bool fast_count = q->num_group_by == 0 && nagg > 0 && q->filter_root >= 0 && !dop && !fds;
   for (int k = 0; k < nagg && fast_count; ++k) fast_count = q->aggregations[k].type == PH_AGG_COUNT;
   if (fast_count) {
-    std::function<int64_t(const PNode&, int64_t)> count_of = [&](const PNode& n, int64_t docs) -> int64_t {
-      if (n.kind == L_ALL) return docs;
-      if (n.kind == L_NONE) return 0;
-      if (n.op == OP_DOCRANGES) {
-        int64_t c = 0;
-        for (size_t r = 0; r + 1 < n.ranges.size(); r += 2) c += (int64_t)n.ranges[r + 1] - n.ranges[r] + 1;
-        return c;
-      }
-      if (n.op == OP_BITMAP) {
-        const BitmapLeaf& b = pl.bitmaps[n.bitmap_leaf];
-        if (b.range) return -1;  // counted from its bitmap
-        return bitmap_docs(*b.col, b.dict_ids);
-      }
-      if (n.op == OP_NOT && n.kids.size() == 1) {
-        const int64_t c = count_of(n.kids[0], docs);
-        return c < 0 ? -1 : docs - c;
-      }
-      return -1;  // AND / OR / scan leaves: the scan counts them
-    };
+    auto count_of = [&](const PNode& n, int64_t docs) { return index_count(n, pl.bitmaps, docs); };
     int64_t total = 0;
     for (int i = 0; i < nseg && fast_count; ++i) {
       if (!seg_live[i]) continue;

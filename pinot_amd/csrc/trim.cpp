@@ -120,6 +120,7 @@ class ValueMerge {
     st.num_total_docs += rs.num_total_docs;
     st.num_segments_processed += rs.num_segments_processed;
     st.num_segments_matched += rs.num_segments_matched;
+    st.num_segments_star_tree += rs.num_segments_star_tree;
     st.num_groups_limit_reached |= rs.num_groups_limit_reached;
     st.sum_precision_flag |= rs.sum_precision_flag;
     st.device_ms = add_device_ms ? st.device_ms + rs.device_ms : std::max(st.device_ms, rs.device_ms);

@@ -47,6 +47,7 @@ class ExecutionStats:
     merge_ms: float = 0.0  # multi-device: partial-table combine (RCCL reduce-scatter / local reduce)
     finalize_ms: float = 0.0  # multi-device: merged key shards -> result
     scan_ms: float = 0.0  # multi-device: wall time of the devices' scans into their partial tables
+    num_segments_star_tree: int = 0  # segments answered from a star-tree
 
 
 SCAN_KERNEL_NAMES = {0: "none", 1: "k_scan", 2: "k_agg_lean", 3: "k_agg_sparse", 4: "k_group_lds_lean",
@@ -172,7 +173,8 @@ class _QueryStruct:
         self.struct = N.Query(len(nodes), node_arr, root, len(preds), pred_arr, len(q.group_by), gb,
                               len(q.aggregations), aggs, q.num_groups_limit, end_ms,
                               ctypes.pointer(interrupt) if interrupt is not None else None,
-                              len(obs), ob_arr, int(q.limit), seg_trim)
+                              len(obs), ob_arr, int(q.limit), seg_trim,
+                              int(str(q.options.get("skipStarTree", "false")).lower() == "true"))
 
 
 _KEY_DTYPE = {N.PH_INT: np.int32, N.PH_LONG: np.int64, N.PH_FLOAT: np.float32, N.PH_DOUBLE: np.float64}
@@ -385,7 +387,7 @@ class GpuContext:
                                st.num_segments_matched, bool(st.num_groups_limit_reached),
                                bool(st.sum_precision_flag), st.device_ms, st.host_ms, st.plan_mode,
                                st.limit_pass, st.scan_kernel, st.num_devices, st.merge_ms, st.finalize_ms,
-                               st.scan_ms)
+                               st.scan_ms, st.num_segments_star_tree)
         return IntermediateResult(key_cols, agg_cols, n, [a.function for a in q.aggregations], stats)
 
     # ---------------------------------------------------------------- segment-level filter (plug point 2)
@@ -407,7 +409,7 @@ class GpuContext:
                                st.num_segments_matched, bool(st.num_groups_limit_reached),
                                bool(st.sum_precision_flag), st.device_ms, st.host_ms, st.plan_mode,
                                st.limit_pass, st.scan_kernel, st.num_devices, st.merge_ms, st.finalize_ms,
-                               st.scan_ms)
+                               st.scan_ms, st.num_segments_star_tree)
         if words:
             out = out[:(nd + 63) // 64]
         return out, int(st.num_docs_scanned), stats

@@ -102,7 +102,7 @@ class Query(ctypes.Structure):
                 ("aggregations", ctypes.POINTER(Aggregation)), ("num_groups_limit", ctypes.c_int64),
                 ("end_time_ms", ctypes.c_int64), ("interrupt", ctypes.POINTER(ctypes.c_int32)),
                 ("num_order_by", ctypes.c_int32), ("order_by", ctypes.POINTER(OrderBy)), ("limit", ctypes.c_int32),
-                ("min_segment_group_trim_size", ctypes.c_int32)]
+                ("min_segment_group_trim_size", ctypes.c_int32), ("skip_star_tree", ctypes.c_int32)]
 
 
 PH_MAX_DENSE_TABLES = 16
@@ -124,7 +124,8 @@ class ExecStats(ctypes.Structure):
                 ("device_ms", ctypes.c_double), ("host_ms", ctypes.c_double), ("plan_mode", ctypes.c_int32),
                 ("limit_pass", ctypes.c_int32),
                 ("scan_kernel", ctypes.c_int32), ("num_devices", ctypes.c_int32),
-                ("merge_ms", ctypes.c_double), ("finalize_ms", ctypes.c_double), ("scan_ms", ctypes.c_double)]
+                ("merge_ms", ctypes.c_double), ("finalize_ms", ctypes.c_double), ("scan_ms", ctypes.c_double),
+                ("num_segments_star_tree", ctypes.c_int64)]
 
 
 # every symbol declared in include/pinot_hip.h
@@ -137,7 +138,8 @@ EXPORTED_SYMBOLS = (
     "ph_result_group_keys", "ph_result_aggregation", "ph_result_key_data", "ph_result_aggregation_data",
     "ph_query_dense_layout", "ph_query_execute_dense", "ph_dense_finalize", "ph_fixed_bit_pack",
     "ph_raw_forward_index_read", "ph_index_map_lookup", "ph_result_datatable", "ph_selftest_unpack",
-    "ph_selftest_unpack_staged", "ph_last_error", "ph_version",
+    "ph_selftest_unpack_staged", "ph_last_error", "ph_version", "ph_segment_add_star_tree", "ph_segment_num_star_trees",
+    "ph_star_tree_check",
 )
 
 _lib = None
@@ -214,6 +216,9 @@ def lib():
                                  ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
         "ph_selftest_unpack": ([vp, vp, ctypes.c_uint64, i64, i32, vp], ctypes.c_int),
         "ph_selftest_unpack_staged": ([vp, vp, ctypes.c_uint64, i64, i32, i32, vp], ctypes.c_int),
+        "ph_segment_add_star_tree": ([vp, vp], ctypes.c_int),
+        "ph_segment_num_star_trees": ([vp], i32),
+        "ph_star_tree_check": ([vp, ctypes.c_uint64, ctypes.POINTER(i32), ctypes.POINTER(i32)], ctypes.c_int),
         "ph_last_error": ([], ctypes.c_char_p),
         "ph_version": ([], ctypes.c_char_p),
     }

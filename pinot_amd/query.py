@@ -358,7 +358,8 @@ def parse_sql(sql: str) -> QueryContext:
     while p.accept("kw", "SET"):
         key = p.ident()
         p.expect("op", "=")
-        q.options[key] = p.literal()
+        # (QueryOptionsUtils reads boolean options such as skipStarTree=true as strings)
+        q.options[key] = p.ident() if p.peek()[0] == "id" else p.literal()
         p.accept("op", ";")
     p.expect("kw", "SELECT")
     while True:
