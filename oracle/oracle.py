@@ -166,6 +166,8 @@ class OracleColumn:
     # a legacy version-1 range index (RangeIndexReaderImpl, inexact) over dictIds: its range starts + the last
     # range's end (inclusive), as RangeIndexCreator's header holds them
     legacy_ranges: Optional[np.ndarray] = None
+    # ... over a raw (no-dictionary) column's values: (stored type, range starts + the last range's end as values)
+    legacy_raw: Optional[tuple] = None
     fwd: Optional[np.ndarray] = None      # packed big-endian fixed-bit bytes (unsorted)
     sorted_ranges: Optional[np.ndarray] = None  # int32 [card, 2]
 
@@ -206,8 +208,8 @@ def build_column(name: str, values: np.ndarray, data_type: str, inverted: bool =
 
 
 def build_segment(name: str, columns: Dict[str, tuple], inverted: Sequence[str] = (),
-                  range_index: Sequence[str] = (), legacy_ranges: Optional[Dict[str, np.ndarray]] = None
-                  ) -> OracleSegment:
+                  range_index: Sequence[str] = (), legacy_ranges: Optional[Dict[str, np.ndarray]] = None,
+                  legacy_raw: Optional[Dict[str, np.ndarray]] = None) -> OracleSegment:
     """columns: name -> (values, data_type); legacy_ranges: name -> a version-1 range index's dictId range starts
     followed by the last range's end"""
     n = None
@@ -217,6 +219,8 @@ def build_segment(name: str, columns: Dict[str, tuple], inverted: Sequence[str] 
         col.has_range_index = c in range_index
         if legacy_ranges and c in legacy_ranges:
             col.legacy_ranges = np.asarray(legacy_ranges[c], np.int64)
+        if legacy_raw and c in legacy_raw:  # a raw column's version-1 index: its range starts + last end (values)
+            col.legacy_raw = (dt, np.asarray(legacy_raw[c]))
         seg.columns[c] = col
         n = len(vals) if n is None else n
         assert n == len(vals)
@@ -314,6 +318,29 @@ class _Leaf:
         self.children = []
 
 
+def raw_inclusive_bounds(p, data_type: str):
+    """A raw column's RANGE bounds as its raw-value evaluator holds them (RangePredicateEvaluatorFactory.java:70-92,
+    :314-499): unbounded = the type's inclusive min / max (infinities for reals), an exclusive bound moved by one
+    (INT wraps at 32 bits) or by Math.nextUp / nextDown (float32 steps for FLOAT)."""
+    lu, hu = p.lower == "*", p.upper == "*"
+    li, hi_inc = lu or p.lower_inclusive, hu or p.upper_inclusive
+    if data_type in ("INT", "LONG"):
+        bits = 32 if data_type == "INT" else 64
+        mn, mx = -(1 << (bits - 1)), (1 << (bits - 1)) - 1
+        wrap = lambda v: ((v - mn) % (1 << bits)) + mn  # noqa: E731
+        a = mn if lu else int(p.lower)
+        b = mx if hu else int(p.upper)
+        return (a if li else wrap(a + 1)), (b if hi_inc else wrap(b - 1))
+    f32 = data_type == "FLOAT"
+    a = -np.inf if lu else (float(np.float32(float(p.lower))) if f32 else float(p.lower))
+    b = np.inf if hu else (float(np.float32(float(p.upper))) if f32 else float(p.upper))
+    if not li:
+        a = float(np.nextafter(np.float32(a), np.float32(np.inf))) if f32 else float(np.nextafter(a, np.inf))
+    if not hi_inc:
+        b = float(np.nextafter(np.float32(b), np.float32(-np.inf))) if f32 else float(np.nextafter(b, -np.inf))
+    return a, b
+
+
 def _plan_filter(f, seg: OracleSegment, col_index: Dict[str, int]):
     """FilterPlanNode.constructPhysicalOperator simplification rules."""
     if f.type == "PREDICATE":
@@ -333,7 +360,7 @@ def _plan_filter(f, seg: OracleSegment, col_index: Dict[str, int]):
             is_scan, ikind = False, "inverted"
         elif col.has_range_index and p.TYPE in ("RANGE", "EQ"):
             is_scan, ikind = False, "range"
-        elif col.legacy_ranges is not None and p.TYPE == "RANGE":
+        elif (col.legacy_ranges is not None or col.legacy_raw is not None) and p.TYPE == "RANGE":
             # an inexact index evaluates RANGE only (RangeIndexBasedFilterOperator.canEvaluate :56-61): a
             # BitmapDocIdSet of the exact docs, whose entries are the partial ranges' scan (:82-107)
             is_scan, ikind = False, "legacy"
@@ -341,6 +368,8 @@ def _plan_filter(f, seg: OracleSegment, col_index: Dict[str, int]):
             is_scan, ikind = True, "scan"
         leaf = _Leaf("leaf", col_index[p.column], match, is_scan)
         leaf.ikind = ikind
+        if ikind == "legacy" and col.legacy_raw is not None:
+            leaf.raw_bounds = raw_inclusive_bounds(p, col.legacy_raw[0])
         return leaf
     if f.type == "AND":
         kids = []
@@ -409,6 +438,8 @@ def _merge_same_column(node: _Leaf) -> _Leaf:
                 a = out[j]
                 out[j] = _Leaf("leaf", a.col_index, (a.match & k.match).astype(a.match.dtype), False)
                 out[j].ikind = "legacy"
+                if hasattr(a, "raw_bounds"):  # MergeRangeFilterOptimizer: the intersected raw bounds
+                    out[j].raw_bounds = (max(a.raw_bounds[0], k.raw_bounds[0]), min(a.raw_bounds[1], k.raw_bounds[1]))
                 continue
             first[("legacy", k.col_index)] = len(out)
         if k.kind == "leaf" and k.is_scan:
@@ -814,9 +845,13 @@ def legacy_partial_entries(root: _Leaf, seg: OracleSegment, used: list) -> int:
     if root.kind != "leaf" or getattr(root, "ikind", "") != "legacy":
         return 0
     col = seg.columns[used[root.col_index]]
-    ids = np.flatnonzero(root.match)
-    lo, hi = int(ids[0]), int(ids[-1])
-    starts, last_end = col.legacy_ranges[:-1], int(col.legacy_ranges[-1])
+    if col.legacy_raw is not None:  # over raw values: the predicate's inclusive raw bounds
+        lo, hi = root.raw_bounds
+        starts, last_end = col.legacy_raw[1][:-1], col.legacy_raw[1][-1]
+    else:
+        ids = np.flatnonzero(root.match)
+        lo, hi = int(ids[0]), int(ids[-1])
+        starts, last_end = col.legacy_ranges[:-1], int(col.legacy_ranges[-1])
 
     def find(v):
         for i, st in enumerate(starts):
@@ -826,11 +861,13 @@ def legacy_partial_entries(root: _Leaf, seg: OracleSegment, used: list) -> int:
 
     a, b = find(lo), find(hi)
     rids = {r for r in (a, b) if 0 <= r < len(starts)}
-    dict_ids = _doc_ids(col, seg.num_docs)
+    vals = _doc_ids(col, seg.num_docs)
+    if col.legacy_raw is not None:  # the docs' raw values (the index ranges hold values, not dictIds)
+        vals = col.dictionary[vals]
     total = 0
     for r in rids:
-        end = int(starts[r + 1]) if r + 1 < len(starts) else last_end + 1
-        total += int(((dict_ids >= starts[r]) & (dict_ids < end)).sum())
+        inside = (vals >= starts[r]) & ((vals < starts[r + 1]) if r + 1 < len(starts) else (vals <= last_end))
+        total += int(inside.sum())
     return total
 
 

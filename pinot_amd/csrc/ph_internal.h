@@ -517,6 +517,12 @@ struct Column {
   bool legacy_range = false;
   std::vector<int64_t> legacy_starts, legacy_cards;
   int64_t legacy_last_end = 0;
+  // ... or over a raw column's values (legacy_raw; RangeIndexCreator of the stored type): INT / LONG starts in
+  // legacy_starts, FLOAT / DOUBLE in legacy_rstarts; a RANGE leaf's boundary ranges come from the predicate's raw
+  // inclusive bounds (RangeIndexBasedFilterOperator.getPartiallyMatchingDocIds :143-166)
+  bool legacy_raw = false;
+  std::vector<double> legacy_rstarts;
+  double legacy_rlast_end = 0.0;
   Dictionary dict;
   std::vector<int32_t> sorted_ranges;  // [card][2] (sorted columns)
   std::vector<uint8_t> inverted;       // host copy of the inverted index (offsets + roaring blobs)
@@ -752,6 +758,9 @@ void build_bitmap_directory(Column& c);  // at pin, from c.inverted
 // at pin: the (key, slice) container directory of an exact range index's RangeBitmap (after Pinot's 12-byte header)
 void parse_legacy_range_index(const uint8_t* b, uint64_t size, std::vector<int64_t>* starts, int64_t* last_end,
                               std::vector<int64_t>* cards);
+void parse_legacy_range_index_typed(const uint8_t* b, uint64_t size, std::string* type, std::vector<int64_t>* starts,
+                                    int64_t* last_end, std::vector<double>* rstarts, double* rlast_end,
+                                    std::vector<int64_t>* cards);
 std::vector<int32_t> parse_range_bitmap(const uint8_t* b, uint64_t size, int64_t num_docs, int32_t* nkeys,
                                         int32_t* nslices, bool* stageable);
 // (column, index id) -> (startOffset, size) of a V3 index_map file (loader.cpp)

@@ -54,6 +54,9 @@ struct PNode {
                              // flipped bitmap: a BitmapDocIdSet, not a user NOT)
   bool range_index = false;  // a scan-evaluated RangeIndexBasedFilterOperator leaf: index-based for the statistics
   bool legacy_range = false;  // ... over a legacy version-1 index (its boundary ranges scanned: legacy_partial_entries)
+  bool legacy_raw = false;    // ... whose index is over raw values: the predicate's inclusive raw bounds
+  int64_t rlo_i = 0, rhi_i = 0;
+  double rlo_d = 0, rhi_d = 0;
   bool range_pred = false;    // the leaf of a RANGE predicate (MergeRangeFilterOptimizer merges these under an AND)
   // AND whose children are index-based leaves (sorted, bitmap, range index, ORs / NOTs of them) followed by scan
   // leaves: the reference's AndDocIdSet applies the scans one after another to the index-based result
@@ -255,6 +258,41 @@ std::vector<int32_t> sorted_doc_ranges(const Column& c, const DictIdSet& s) {
   return out;
 }
 
+// A raw column's RANGE bounds as its raw-value evaluator holds them (RangePredicateEvaluatorFactory.java:70-92,
+// :314-499): unbounded = the type's inclusive min / max (NEGATIVE / POSITIVE_INFINITY for reals), an exclusive bound
+// moved by one (INT / LONG, int32 wrap-around for INT) or by Math.nextUp / nextDown (FLOAT / DOUBLE)
+void raw_inclusive_bounds(const ph_predicate& p, int32_t type, int64_t* lo_i, int64_t* hi_i, double* lo_d, double* hi_d) {
+  const std::string lo = lit(p.lower), hi = lit(p.upper);
+  const bool lu = !p.lower || lo == "*", hu = !p.upper || hi == "*";
+  const bool li = lu || p.lower_inclusive, hi_inc = hu || p.upper_inclusive;
+  auto parse_i = [&](const std::string& v) {
+    char* e = nullptr;
+    const long long x = strtoll(v.c_str(), &e, 10);
+    if (e == v.c_str() || *e) fail(PH_ERR_BAD_QUERY, "not an integer: " + v);
+    return (int64_t)x;
+  };
+  auto parse_d = [&](const std::string& v) {
+    char* e = nullptr;
+    const double x = type == PH_FLOAT ? (double)strtof(v.c_str(), &e) : strtod(v.c_str(), &e);
+    if (e == v.c_str()) fail(PH_ERR_BAD_QUERY, "not a number: " + v);
+    return x;
+  };
+  if (type == PH_INT || type == PH_LONG) {
+    const int64_t mn = type == PH_INT ? INT32_MIN : INT64_MIN, mx = type == PH_INT ? INT32_MAX : INT64_MAX;
+    int64_t a = lu ? mn : parse_i(lo), b = hu ? mx : parse_i(hi);
+    if (!li) a = type == PH_INT ? (int64_t)(int32_t)((uint32_t)a + 1u) : (int64_t)((uint64_t)a + 1u);
+    if (!hi_inc) b = type == PH_INT ? (int64_t)(int32_t)((uint32_t)b - 1u) : (int64_t)((uint64_t)b - 1u);
+    *lo_i = a;
+    *hi_i = b;
+  } else {
+    double a = lu ? -INFINITY : parse_d(lo), b = hu ? INFINITY : parse_d(hi);
+    if (!li) a = type == PH_FLOAT ? (double)nextafterf((float)a, INFINITY) : nextafter(a, INFINITY);
+    if (!hi_inc) b = type == PH_FLOAT ? (double)nextafterf((float)b, -INFINITY) : nextafter(b, -INFINITY);
+    *lo_d = a;
+    *hi_d = b;
+  }
+}
+
 struct Planner {
   const ph_query* q;
   std::map<std::string, int> slot;
@@ -320,10 +358,13 @@ struct Planner {
     // a legacy version-1 range index evaluates RANGE only (RangeIndexBasedFilterOperator.canEvaluate :56-61): a
     // BitmapDocIdSet of the exact docs (scanned from the dictIds here) whose entries are the scan of its boundary
     // ranges (evaluateLegacyRangeFilter :82-107), added per segment by legacy_partial_entries
-    if (c.has_inexact_range_index && p.type == PH_PRED_RANGE) {
-      if (!c.legacy_range) fail(PH_ERR_UNSUPPORTED, "column " + c.name + ": a version-1 range index over raw values");
+    if (c.has_inexact_range_index && p.type == PH_PRED_RANGE && (c.legacy_range || c.legacy_raw)) {
       n.range_index = true;
       n.legacy_range = true;
+      if (c.legacy_raw) {
+        n.legacy_raw = true;
+        raw_inclusive_bounds(p, c.data_type, &n.rlo_i, &n.rhi_i, &n.rlo_d, &n.rhi_d);
+      }
     }
     if (s.is_range) {
       n.op = OP_RANGE;
@@ -508,7 +549,15 @@ void merge_same_column_leaves(PNode& n, const CardOf& card_of, std::vector<Bitma
         const int64_t card = card_of(k.col);
         std::vector<uint32_t> x = leaf_bits(a, card), y = leaf_bits(k, card);
         for (size_t w = 0; w < x.size(); ++w) x[w] = is_and ? (x[w] & y[w]) : (x[w] | y[w]);
+        const PNode ka = a;
         leaf_from_bits(a, x, card);
+        if (legacy && ka.legacy_raw && a.kind == L_NODE) {  // the merged RANGE's raw bounds (MergeRangeFilterOptimizer)
+          a.range_index = a.legacy_range = a.legacy_raw = true;
+          a.rlo_i = std::max(ka.rlo_i, k.rlo_i);
+          a.rhi_i = std::min(ka.rhi_i, k.rhi_i);
+          a.rlo_d = std::max(ka.rlo_d, k.rlo_d);
+          a.rhi_d = std::min(ka.rhi_d, k.rhi_d);
+        }
         continue;
       }
       first_of[key] = kids.size();
@@ -738,6 +787,13 @@ int64_t legacy_range_id(const Column& c, int64_t v) {
     if (v < c.legacy_starts[i]) return (int64_t)i - 1;
   return v <= c.legacy_last_end ? (int64_t)c.legacy_starts.size() - 1 : (int64_t)c.legacy_starts.size();
 }
+// RangeIndexReaderImpl.findRangeId(double / float) (:257-273): reals compared in the index's type (a float widened to
+// double keeps its order)
+int64_t legacy_range_id_real(const Column& c, double v) {
+  for (size_t i = 0; i < c.legacy_rstarts.size(); ++i)
+    if (v < c.legacy_rstarts[i]) return (int64_t)i - 1;
+  return v <= c.legacy_rlast_end ? (int64_t)c.legacy_rstarts.size() - 1 : (int64_t)c.legacy_rstarts.size();
+}
 
 // the legacy range-index leaves' boundary-range scans of one segment's (merged) tree: getPartialMatchesInRange
 // (RangeIndexReaderImpl.java:300-308) of the leaf's inclusive dictId bounds, counted by ScanBasedDocIdIterator.applyAnd
@@ -749,6 +805,15 @@ int64_t legacy_partial_entries(const PNode& n, const ColOf& col_of) {
   for (auto& k : n.kids) e += legacy_partial_entries(k, col_of);
   if (!n.legacy_range || !n.kids.empty()) return e;
   const Column& c = col_of(n.col);
+  if (n.legacy_raw) {  // over raw values: the predicate's inclusive raw bounds
+    const int64_t R = (int64_t)c.legacy_cards.size();
+    const bool real = c.data_type == PH_FLOAT || c.data_type == PH_DOUBLE;
+    const int64_t a = real ? legacy_range_id_real(c, n.rlo_d) : legacy_range_id(c, n.rlo_i);
+    const int64_t b = real ? legacy_range_id_real(c, n.rhi_d) : legacy_range_id(c, n.rhi_i);
+    if (a >= 0 && a < R) e += c.legacy_cards[a];
+    if (b >= 0 && b < R && b != a) e += c.legacy_cards[b];
+    return e;
+  }
   int64_t lo = -1, hi = -1;
   if (n.op == OP_RANGE) {
     lo = n.lo;

@@ -120,25 +120,45 @@ void build_bitmap_directory(Column& c) {
 // R + 1 values (the ranges' first values, then the last range's end), R + 1 int64 BE absolute offsets of the ranges'
 // portable roaring bitmaps.  Kept: the starts, the end and each range's doc count -- the leaf's doc set is exact
 // from the dictIds; its statistic is the docs of its boundary ranges (getPartialMatchesInRange :300-308)
-void parse_legacy_range_index(const uint8_t* b, uint64_t size, std::vector<int64_t>* starts, int64_t* last_end,
-                              std::vector<int64_t>* cards) {
+void parse_legacy_range_index_typed(const uint8_t* b, uint64_t size, std::string* type, std::vector<int64_t>* starts,
+                                    int64_t* last_end, std::vector<double>* rstarts, double* rlast_end,
+                                    std::vector<int64_t>* cards) {
   auto need = [&](uint64_t at) {
     if (at > size) fail(PH_ERR_INVALID_ARGUMENT, "legacy range index: truncated");
   };
   need(8);
   const uint32_t tl = be32u(b + 4);
   need(8 + (uint64_t)tl + 4);
-  const std::string type(reinterpret_cast<const char*>(b + 8), tl);
-  if (type != "INT") fail(PH_ERR_UNSUPPORTED, "legacy range index over " + type + " values");
+  type->assign(reinterpret_cast<const char*>(b + 8), tl);
+  const int w = *type == "INT" || *type == "FLOAT" ? 4 : (*type == "LONG" || *type == "DOUBLE" ? 8 : 0);
+  if (!w) fail(PH_ERR_UNSUPPORTED, "legacy range index over " + *type + " values");
   uint64_t at = 8 + tl;
   const uint32_t R = be32u(b + at);
   at += 4;
   if (R == 0 || R > (1u << 24)) fail(PH_ERR_INVALID_ARGUMENT, "legacy range index: bad range count");
-  need(at + 4ull * (R + 1) + 8ull * (R + 1));
+  need(at + (uint64_t)w * (R + 1) + 8ull * (R + 1));
+  // the R + 1 values in the index's type (DataType.size(): 4 for INT / FLOAT, 8 for LONG / DOUBLE)
+  auto value = [&](uint32_t r, int64_t* iv, double* dv) {
+    const uint8_t* q = b + at + (uint64_t)w * r;
+    const uint64_t u = w == 4 ? (uint64_t)be32u(q) : ((uint64_t)be32u(q) << 32) | be32u(q + 4);
+    if (*type == "INT") *iv = (int32_t)(uint32_t)u;
+    else if (*type == "LONG") *iv = (int64_t)u;
+    else if (*type == "FLOAT") {
+      const uint32_t x = (uint32_t)u;
+      float f;
+      memcpy(&f, &x, 4);
+      *dv = f;
+    } else {
+      memcpy(dv, &u, 8);
+    }
+  };
   starts->assign(R, 0);
-  for (uint32_t r = 0; r < R; ++r) (*starts)[r] = (int32_t)be32u(b + at + 4ull * r);
-  *last_end = (int32_t)be32u(b + at + 4ull * R);
-  at += 4ull * (R + 1);
+  rstarts->assign(R, 0.0);
+  for (uint32_t r = 0; r < R; ++r) value(r, &(*starts)[r], &(*rstarts)[r]);
+  *last_end = 0;
+  *rlast_end = 0.0;
+  value(R, last_end, rlast_end);
+  at += (uint64_t)w * (R + 1);
   auto off = [&](uint32_t r) {
     return ((uint64_t)be32u(b + at + 8ull * r) << 32) | be32u(b + at + 8ull * r + 4);
   };
@@ -161,6 +181,16 @@ void parse_legacy_range_index(const uint8_t* b, uint64_t size, std::vector<int64
     }
     (*cards)[r] = docs;
   }
+}
+
+// a dictionary column's index is over dictIds ("INT")
+void parse_legacy_range_index(const uint8_t* b, uint64_t size, std::vector<int64_t>* starts, int64_t* last_end,
+                              std::vector<int64_t>* cards) {
+  std::string type;
+  std::vector<double> rs;
+  double rl = 0;
+  parse_legacy_range_index_typed(b, size, &type, starts, last_end, &rs, &rl, cards);
+  if (type != "INT") fail(PH_ERR_UNSUPPORTED, "legacy range index over " + type + " values on a dictionary column");
 }
 
 // RoaringBitmap's RangeBitmap as BitSlicedRangeIndexCreator.seal writes it after its header (int32 BE version 2,

@@ -510,6 +510,15 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
       if (version == 1 && !col->is_raw) {
         parse_legacy_range_index(h, d.range_index_size, &col->legacy_starts, &col->legacy_last_end, &col->legacy_cards);
         col->legacy_range = true;
+      } else if (version == 1) {  // over the raw values, in the column's stored type
+        std::string type;
+        parse_legacy_range_index_typed(h, d.range_index_size, &type, &col->legacy_starts, &col->legacy_last_end,
+                                       &col->legacy_rstarts, &col->legacy_rlast_end, &col->legacy_cards);
+        static const char* const kTypeNames[] = {"INT", "LONG", "FLOAT", "DOUBLE", "STRING"};
+        if (d.data_type < PH_INT || d.data_type > PH_DOUBLE || type != kTypeNames[d.data_type])
+          fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": legacy range index of type " + type +
+                                            " on a column of another stored type");
+        col->legacy_raw = true;
       }
     }
     const uint8_t* fwd = static_cast<const uint8_t*>(d.forward_index);

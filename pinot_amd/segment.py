@@ -194,13 +194,18 @@ def range_index_bytes(values: np.ndarray, max_value: int, min_value: int = 0) ->
     return np.concatenate([range_index_header(min_value), np.frombuffer(body, np.uint8)])
 
 
-def legacy_range_index_bytes(ids: np.ndarray, num_ranges: int = 20) -> tuple:
-    """A legacy version-1 range index over dictIds as RangeIndexCreator.seal lays it out (RangeIndexCreator.java:
-    283-380): ranges of about ceil(n / num_ranges) sorted values that never split a value, then int32 BE version 1,
-    the type name "INT", the range count, the ranges' first values + the last range's end, (R + 1) int64 BE absolute
-    offsets and each range's doc bitmap (portable roaring).  -> (bytes, starts + [last end]) -- the second for the
-    oracle."""
-    ids = np.asarray(ids, np.int64)
+def legacy_range_index_bytes(ids: np.ndarray, num_ranges: int = 20, value_type: str = "INT") -> tuple:
+    """A legacy version-1 range index as RangeIndexCreator.seal lays it out (RangeIndexCreator.java:283-410): ranges of
+    about ceil(n / num_ranges) sorted values that never split a value, then int32 BE version 1, the value type's name,
+    the range count, the ranges' first values + the last range's end (in the value type: int32 / int64 / float32 /
+    float64 BE), (R + 1) int64 BE absolute offsets and each range's doc bitmap (portable roaring).  ``ids``: the
+    dictIds of a dictionary column (value_type "INT"), or the raw values of a no-dictionary column of that type.
+    -> (bytes, starts + [last end]) -- the second for the oracle."""
+    dt = {"INT": (">i4", np.int64), "LONG": (">i8", np.int64), "FLOAT": (">f4", np.float64),
+          "DOUBLE": (">f8", np.float64)}[value_type]
+    ids = np.asarray(ids)
+    ids = ids.astype(np.float32 if value_type == "FLOAT" else np.float64) if value_type in ("FLOAT", "DOUBLE") \
+        else ids.astype(np.int64)
     n = int(ids.size)
     order = np.argsort(ids, kind="stable")
     sv = ids[order]
@@ -217,15 +222,16 @@ def legacy_range_index_bytes(ids: np.ndarray, num_ranges: int = 20) -> tuple:
     ranges.append((start, n - 1))
     bitmaps = [roaring_serialize(np.sort(order[a:b + 1]).astype(np.uint32)) for a, b in ranges]
     R = len(ranges)
-    head = struct.pack(">ii", 1, 3) + b"INT" + struct.pack(">i", R)
-    head += np.array([sv[a] for a, _ in ranges] + [sv[-1]], ">i4").tobytes()
+    name = value_type.encode()
+    head = struct.pack(">ii", 1, len(name)) + name + struct.pack(">i", R)
+    head += np.array([sv[a] for a, _ in ranges] + [sv[-1]], dt[0]).tobytes()
     off = len(head) + 8 * (R + 1)
     offs = [off]
     for bm in bitmaps:
         off += len(bm)
         offs.append(off)
     blob = head + np.array(offs, ">i8").tobytes() + b"".join(bitmaps)
-    return np.frombuffer(blob, np.uint8).copy(), np.array([sv[a] for a, _ in ranges] + [sv[-1]], np.int64)
+    return np.frombuffer(blob, np.uint8).copy(), np.array([sv[a] for a, _ in ranges] + [sv[-1]], dt[1])
 
 
 @dataclass

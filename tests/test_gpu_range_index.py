@@ -114,6 +114,56 @@ def test_legacy_range_index(ctx, nr):
     assert 0 < r.stats.num_entries_scanned_in_filter < sum(len(t["r"][0]) for t in tables)
 
 
+RAW_LEGACY_SQL = [
+    "SELECT COUNT(*), SUM(m) FROM t WHERE r BETWEEN {a} AND {b}",
+    "SELECT COUNT(*) FROM t WHERE r > {a}",                              # exclusive lower bound: lo + 1 / nextUp
+    "SELECT COUNT(*), MIN(m) FROM t WHERE r < {b}",                      # unbounded lower: the type's minimum
+    "SELECT COUNT(*) FROM t WHERE r >= {x}",                             # a bound equal to a range start
+    "SELECT COUNT(*) FROM t WHERE r > {x}",                              # ... exclusive: the range before it
+    "SELECT COUNT(*), MAX(m) FROM t WHERE r > {a} AND r <= {b}",         # merged into one RANGE (raw bounds)
+    "SELECT g, COUNT(*), SUM(m) FROM t WHERE r < {b} AND f < 300 GROUP BY g ORDER BY g LIMIT 100",
+    "SELECT COUNT(*), SUM(m) FROM t WHERE r < {a} OR f BETWEEN 10 AND 20",
+    "SELECT COUNT(*) FROM t WHERE NOT r BETWEEN {a} AND {b}",
+    "SELECT COUNT(*) FROM t WHERE r = {x}",                              # EQ: an inexact index cannot (scan)
+]
+
+
+@pytest.mark.parametrize("dtype", ["INT", "LONG", "FLOAT", "DOUBLE"])
+def test_legacy_range_index_raw(ctx, dtype):
+    # a legacy version-1 index over a raw (no-dictionary) column's values (RangeIndexCreator of the stored type,
+    # RangeIndexReaderImpl.findRangeId over typed starts): RANGE leaves are index-based with the exact doc set and
+    # scan the docs of the ranges holding the predicate's raw inclusive bounds
+    # (RangeIndexBasedFilterOperator.getPartiallyMatchingDocIds :143-166 with the raw evaluators' bounds)
+    from pinot_amd.segment import legacy_range_index_bytes
+    rng = np.random.default_rng(hash(dtype) % 1000)
+    segs, osegs = [], []
+    starts = None
+    for i, n in enumerate((60_000, 33_331)):
+        t = _cols(n, 40 + i)
+        v = rng.integers(-5000, 5000, n)
+        if dtype == "FLOAT":
+            v = (v / 8.0).astype(np.float32)
+        elif dtype == "DOUBLE":
+            v = v / 16.0
+        elif dtype == "LONG":
+            v = v.astype(np.int64) * 1_000_000_007
+        t["r"] = (v.astype({"INT": np.int32, "LONG": np.int64, "FLOAT": np.float32, "DOUBLE": np.float64}[dtype]),
+                  dtype)
+        buf = create_segment(f"lr{i}", t, raw=("r",))
+        blob, ranges = legacy_range_index_bytes(t["r"][0], 13 + 4 * i, dtype)
+        buf.columns["r"].range_index = blob
+        segs.append(ctx.pin(buf))
+        osegs.append(O.build_segment(f"lr{i}", t, legacy_raw={"r": ranges}))
+        starts = ranges
+    lit = (lambda x: repr(float(x))) if dtype in ("FLOAT", "DOUBLE") else (lambda x: str(int(x)))
+    vals = np.sort(np.unique(np.concatenate([o.columns["r"].dictionary for o in osegs])))
+    a, b, x = vals[len(vals) // 5], vals[3 * len(vals) // 5], starts[len(starts) // 2]
+    for sql in RAW_LEGACY_SQL:
+        _check(ctx, segs, osegs, sql.format(a=lit(a), b=lit(b), x=lit(x)), None)
+    r = ctx.execute(parse_sql(f"SELECT COUNT(*) FROM t WHERE r BETWEEN {lit(a)} AND {lit(b)}"), segs)
+    assert 0 < r.stats.num_entries_scanned_in_filter < sum(s.num_docs for s in segs)
+
+
 SLICE_SQL = [
     "SELECT COUNT(*), SUM(m) FROM t WHERE k BETWEEN 0 AND 1022",        # skewed: array containers
     "SELECT COUNT(*), MIN(m) FROM t WHERE k = 1023",

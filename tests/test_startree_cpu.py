@@ -185,3 +185,18 @@ def test_star_tree_not_fit():
         assert S.fit(q, oseg, osd) is None or sql == "SELECT MAX(m) FROM t"
         _, _, _, served = S.execute_with_star_trees(q, [(oseg, osd)])
         assert served == 0, sql
+
+
+def test_raw_inclusive_bounds():
+    # RangePredicateEvaluatorFactory's raw evaluators (:70-92, :314-499): unbounded = inclusive type min / max, an
+    # exclusive bound moved by one (INT wraps) or by Math.nextUp / nextDown in the column's own precision
+    from pinot_amd.query import parse_sql as P
+    def b(where, t):
+        return O.raw_inclusive_bounds(P("SELECT COUNT(*) FROM t WHERE " + where).filter.predicate, t)
+    assert b("r > 5", "INT") == (6, 2 ** 31 - 1)
+    assert b("r <= 5", "LONG") == (-2 ** 63, 5)
+    assert b("r < -2147483648", "INT") == (-2 ** 31, 2 ** 31 - 1)  # (-2^31) - 1 wraps, as Java int arithmetic
+    lo, hi = b("r > 1.5", "FLOAT")
+    assert lo == float(np.nextafter(np.float32(1.5), np.float32(np.inf))) and hi == np.inf
+    lo, hi = b("r BETWEEN 0.1 AND 0.2", "DOUBLE")
+    assert (lo, hi) == (0.1, 0.2)
