@@ -457,20 +457,33 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
   out->num_groups = total;
   out->keys.resize(f.keys.size());
   out->aggs.resize(f.aggs.size());
+  // the shards' columns back to back in pinned blocks of the first context's pool (already mapped: no page faults on
+  // a fresh 40 MB host allocation, no zero fill), copied by a few threads in 4 MiB pieces
+  out->ctx = &x->c;
+  struct Piece {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t n;
+  };
+  std::vector<Piece> pieces;
   auto concat = [&](std::vector<ResultBuf> ph_result::*field, size_t i) {
     size_t bytes = 0;
     for (auto& p : parts) bytes += ((*p).*field)[i].size();
     ResultBuf& dst = (out.get()->*field)[i];
-    dst.assign(bytes, 0);
+    if (bytes == 0) return;
+    dst.pinned = x->c.pinned_acquire(bytes, &dst.cap);
+    dst.n = bytes;
     size_t o = 0;
     for (auto& p : parts) {
       const ResultBuf& src = ((*p).*field)[i];
-      if (src.size()) std::memcpy(dst.data() + o, src.data(), src.size());
+      for (size_t a = 0; a < src.size(); a += (size_t)4 << 20)
+        pieces.push_back({dst.data() + o + a, src.data() + a, std::min<size_t>((size_t)4 << 20, src.size() - a)});
       o += src.size();
     }
   };
   for (size_t i = 0; i < f.keys.size(); ++i) concat(&ph_result::keys, i);
   for (size_t i = 0; i < f.aggs.size(); ++i) concat(&ph_result::aggs, i);
+  pool_run(pieces.size(), 8, [&](size_t t) { std::memcpy(pieces[t].dst, pieces[t].src, pieces[t].n); });
   ph_exec_stats& s = out->stats;
   for (auto& p : parts) {  // matched docs from the merged COUNT table, shard by shard (as ph_dense_finalize)
     s.num_docs_scanned += p->stats.num_docs_scanned;

@@ -5,6 +5,9 @@
 
 namespace ph {
 
+// records whose ring-rank atomics issue back to back before their stores (the stores need the ranks)
+constexpr int kAppendGroup = 8;
+
 // ------------------------------------------------------------------ kernel A, register-direct form (k_part_reg)
 // The LDS-staged forms (scan_partition.hip) stage every stream through LDS and decode each value with a ds_read2
 // (4 streams x 64 docs = 16+ LDS cycles per word, ~35 VALU per word): at config 3 they are LDS- and issue-bound at
@@ -74,24 +77,24 @@ __global__ void __launch_bounds__(kRegBlock) k_part_reg(const KParams p) {
       }
       uint32_t* pend = pend0 + (size_t)cur * (P + 64);
       uint32_t* slots = slots0 + (size_t)cur * SW;
-      // groups of 4: the 4 rank atomics issue back to back, then the 4 stores.  Branch-free and SGPR-free per record:
+      // groups of kAppendGroup: the group's rank atomics issue back to back, then its stores.  Branch-free and SGPR-free per record:
       // slot = min(b * RS + min(rank, C), scratch slot) -- a real partition's ring slot (rank C: the ring's padding
       // quarter, for a record that overflows), a missed doc's scratch slot; a full ring (skewed round) shows as
       // 0 <= (int)(rank - C) (scratch ranks are negative), ORed over the group into one sign test
-      static_for<0, 4>([&](auto u) {
-        constexpr int J0 = decltype(jb)::value + 4 * decltype(u)::value;
-        uint32_t b[4], w[4];
-        static_for<0, 4>([&](auto q) {
+      static_for<0, 16 / kAppendGroup>([&](auto u) {
+        constexpr int J0 = decltype(jb)::value + kAppendGroup * decltype(u)::value;
+        uint32_t b[kAppendGroup], w[kAppendGroup];
+        static_for<0, kAppendGroup>([&](auto q) {
           b[q] = part_of<J0 + decltype(q)::value>(PB);
           w[q] = atomicAdd(&pend[b[q]], 1u);
         });
         uint32_t neg = 0xffffffffu;  // bit 31 stays set while no record overflowed
-        static_for<0, 4>([&](auto q) {
+        static_for<0, kAppendGroup>([&](auto q) {
           neg &= w[q] - C;
           slots[min(__umul24(b[q], RS) + min(w[q], C), dummy_slot)] = X[J0 + decltype(q)::value];
         });
         if (__builtin_expect(__ballot((int32_t)neg >= 0) != 0ull, 0)) {
-          static_for<0, 4>([&](auto q) {
+          static_for<0, kAppendGroup>([&](auto q) {
             if ((int32_t)(w[q] - C) >= 0) part_overflow<0>(p, b[q], X[J0 + decltype(q)::value]);
           });
         }
