@@ -84,7 +84,11 @@ std::map<std::string, std::string> read_properties(const std::string& path) {
       }
     }
     if (sep == std::string::npos) continue;
-    kv[unescape(trim(t.substr(0, sep)))] = unescape(trim(t.substr(sep + 1)));
+    // a repeated key is a list (commons-configuration: startree.v2.<i>.split.order, .function.column.pairs)
+    const std::string key = unescape(trim(t.substr(0, sep))), val = unescape(trim(t.substr(sep + 1)));
+    auto it = kv.find(key);
+    if (it == kv.end()) kv[key] = val;
+    else it->second += "," + val;
   }
   return kv;
 }
@@ -191,6 +195,8 @@ int64_t segment_dir_num_docs(const char* dir_c) {
     return 0;
   }
 }
+
+void star_tree_add_impl(ph_segment* seg, const ph_star_tree_desc* d);  // startree.cpp
 
 ph_segment* segment_load_dir_impl(Context* ctx, const char* dir_c, const char* const* want, int32_t nwant) {
   if (!dir_c) fail(PH_ERR_INVALID_ARGUMENT, "null segment directory");
@@ -329,7 +335,89 @@ ph_segment* segment_load_dir_impl(Context* ctx, const char* dir_c, const char* c
   sd.num_docs = (int32_t)num_docs;
   sd.num_columns = (int32_t)descs.size();
   sd.columns = descs.data();
-  return segment_pin_impl(ctx, &sd);  // copies the mapped bytes into HBM; the mappings close on return
+  ph_segment* seg = segment_pin_impl(ctx, &sd);  // copies the mapped bytes into HBM; the mappings close on return
+  // star-trees (StarTreeLoaderUtils.loadStarTreeV2, StarTreeIndexContainer): star_tree_index holds every tree's
+  // buffers, star_tree_index_map names them "<i>.<column>.<STAR_TREE | FORWARD_INDEX>.<OFFSET | SIZE>" (column "null"
+  // for the tree itself), metadata.properties describes tree i under startree.v2.<i>.*.  A tree whose dimensions are
+  // not all pinned (an explicit column list) cannot serve a query and is skipped.
+  try {
+    if (file_exists(dir + "/star_tree_index_map") && get("startree.v2.count")) {
+      const int64_t ntrees = to_i64(*get("startree.v2.count"), "startree.v2.count", 0, 64);
+      auto smap = read_properties(dir + "/star_tree_index_map");
+      auto blob = map_file(dir + "/star_tree_index", true);
+      auto list = [&](const std::string& k) {
+        std::vector<std::string> out;
+        const std::string* v = get(k);
+        if (!v) fail(PH_ERR_INVALID_ARGUMENT, "metadata.properties without " + k);
+        size_t a = 0;
+        while (a <= v->size()) {
+          size_t b = v->find(',', a);
+          if (b == std::string::npos) b = v->size();
+          std::string x = v->substr(a, b - a);
+          while (!x.empty() && x.front() == ' ') x.erase(0, 1);
+          while (!x.empty() && x.back() == ' ') x.pop_back();
+          if (!x.empty()) out.push_back(x);
+          a = b + 1;
+        }
+        return out;
+      };
+      auto buffer = [&](int64_t i, const std::string& col, const char* type, const void** ptr, uint64_t* size) {
+        const std::string k = std::to_string(i) + "." + col + "." + type;
+        auto o = smap.find(k + ".OFFSET"), n = smap.find(k + ".SIZE");
+        if (o == smap.end() || n == smap.end()) fail(PH_ERR_INVALID_ARGUMENT, "star_tree_index_map without " + k);
+        const int64_t off = to_i64(o->second, k, 0, INT64_MAX), sz = to_i64(n->second, k, 0, INT64_MAX);
+        if ((uint64_t)off > blob->n || (uint64_t)sz > blob->n - (uint64_t)off)
+          fail(PH_ERR_INVALID_ARGUMENT, "star_tree_index_map entry out of star_tree_index: " + k);
+        *ptr = static_cast<const uint8_t*>(blob->p) + off;
+        *size = (uint64_t)sz;
+      };
+      for (int64_t i = 0; i < ntrees; ++i) {
+        const std::string pre = "startree.v2." + std::to_string(i) + ".";
+        const std::vector<std::string> dims = list(pre + "split.order"), pairs = list(pre + "function.column.pairs");
+        bool pinned = true;
+        for (auto& d : dims) pinned = pinned && seg->columns.count(d) > 0;
+        if (!pinned) continue;
+        ph_star_tree_desc t{};
+        buffer(i, "null", "STAR_TREE", &t.tree, &t.tree_size);
+        t.num_docs = (int32_t)to_i64(get(pre + "total.docs") ? *get(pre + "total.docs") : std::string(),
+                                     pre + "total.docs", 0, INT32_MAX);
+        std::vector<const char*> dn, pn;
+        std::vector<const void*> dp, pp;
+        std::vector<uint64_t> ds, ps;
+        for (auto& d : dims) {
+          const void* ptr = nullptr;
+          uint64_t size = 0;
+          buffer(i, d, "FORWARD_INDEX", &ptr, &size);
+          dn.push_back(d.c_str());
+          dp.push_back(ptr);
+          ds.push_back(size);
+        }
+        for (auto& pr : pairs) {
+          const void* ptr = nullptr;
+          uint64_t size = 0;
+          const std::string k = std::to_string(i) + "." + pr + ".FORWARD_INDEX.OFFSET";
+          if (smap.count(k)) buffer(i, pr, "FORWARD_INDEX", &ptr, &size);
+          pn.push_back(pr.c_str());
+          pp.push_back(ptr);
+          ps.push_back(size);
+        }
+        t.num_dimensions = (int32_t)dims.size();
+        t.dimensions = dn.data();
+        t.dimension_forward_index = dp.data();
+        t.dimension_forward_index_size = ds.data();
+        t.num_metrics = (int32_t)pairs.size();
+        t.metrics = pn.data();
+        t.metric_forward_index = pp.data();
+        t.metric_forward_index_size = ps.data();
+        star_tree_add_impl(seg, &t);
+      }
+    }
+  } catch (...) {
+    ctx->pinned_rows -= seg->num_docs;
+    delete seg;
+    throw;
+  }
+  return seg;
 }
 
 }  // namespace ph

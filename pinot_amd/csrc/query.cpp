@@ -2875,7 +2875,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       int a_cap = 4;  // 8-wave workgroups: <= 4 per CU (32 waves)
       if (kp.part_reg) {
         a_cap = part_reg_blocks_per_cu(kp, q->num_group_by, lds_a);  // 4-wave groups, VGPR-bound
-        // one ring set when it lets more workgroups share a CU (the two sets' LDS is what limits them)
+        // one ring set only when two sets would leave a single workgroup per CU
         KParams k1 = kp;
         k1.part_sets = 1;
         const size_t lds1 = partition_lds_bytes(k1, ring_log2);
@@ -2883,7 +2883,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         const size_t per2 = std::min<size_t>(a_cap, (160 * 1024) / lds_a), per1 = std::min<size_t>(cap1, (160 * 1024) / lds1);
         int force = 0;
         if (ctx->has(OPT_PART_SETS)) force = (int)ctx->opt(OPT_PART_SETS);
-        if (force == 1 || (force != 2 && per1 > per2)) {
+        // r6 (config 3): two sets at 2 workgroups per CU 2.69-2.73 ms against one set at 3 per CU 2.71-2.76: two sets
+        // unless they leave one workgroup per CU
+        if (force == 1 || (force != 2 && per2 < 2 && per1 > per2)) {
           kp = k1;
           lds_a = lds1;
           a_cap = cap1;

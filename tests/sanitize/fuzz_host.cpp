@@ -40,7 +40,11 @@ ph_segment* segment_pin_impl(Context*, const ph_segment_desc* d) {
   (void)acc;
   fail(PH_ERR_DEVICE, "harness: pin reached");
 }
+// (the pin never returns here, so the loader's star-tree step is not reached; these satisfy the link)
+void star_tree_add_impl(ph_segment*, const ph_star_tree_desc*) { fail(PH_ERR_DEVICE, "harness: star-tree reached"); }
+StarTree::~StarTree() {}
 }  // namespace ph
+ph_segment::~ph_segment() = default;
 
 namespace {
 

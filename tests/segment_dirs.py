@@ -66,6 +66,32 @@ def write_v3(seg, path, extra_meta=None):
     open(os.path.join(d, "columns.psf"), "wb").write(bytes(blob))
 
 
+def write_star_trees(path, trees):
+    """StarTreeIndexCombiner's layout beside a V3 segment (pinot-segment-local/.../startree/v2/builder/
+    StarTreeIndexCombiner.java, StarTreeIndexMapUtils): every tree's buffers back to back in v3/star_tree_index (no
+    magic), v3/star_tree_index_map keys "<i>.<column>.<STAR_TREE | FORWARD_INDEX>.<OFFSET | SIZE>" (column "null" for
+    the tree), and the trees' metadata appended to v3/metadata.properties (repeated keys are lists, as the reference's
+    own fixture writes split.order and function.column.pairs)."""
+    d = os.path.join(path, "v3")
+    blob, imap, meta, off = bytearray(), [], [f"startree.v2.count = {len(trees)}"], 0
+    for i, st in enumerate(trees):
+        parts = [("null", "STAR_TREE", st.tree)] + [(c, "FORWARD_INDEX", st.dim_fwd[c]) for c in st.dimensions] + \
+                [(m, "FORWARD_INDEX", st.metric_fwd[m]) for m in st.pairs]
+        for col, kind, payload in parts:
+            b = np.ascontiguousarray(payload, np.uint8).tobytes()
+            imap += [f"{i}.{col}.{kind}.OFFSET = {off}", f"{i}.{col}.{kind}.SIZE = {len(b)}"]
+            blob += b
+            off += len(b)
+        meta.append(f"startree.v2.{i}.total.docs = {st.num_docs}")
+        meta += [f"startree.v2.{i}.split.order = {x}" for x in st.dimensions]
+        meta += [f"startree.v2.{i}.function.column.pairs = {x}" for x in st.pairs]
+        meta.append(f"startree.v2.{i}.max.leaf.records = {st.max_leaf_records}")
+    open(os.path.join(d, "star_tree_index"), "wb").write(bytes(blob))
+    open(os.path.join(d, "star_tree_index_map"), "w").write("\n".join(imap) + "\n")
+    with open(os.path.join(d, "metadata.properties"), "a") as f:
+        f.write("\n".join(meta) + "\n")
+
+
 def write_v1(seg, path):
     os.makedirs(path, exist_ok=True)
     open(os.path.join(path, "metadata.properties"), "w").write(_metadata(seg))

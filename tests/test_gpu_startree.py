@@ -128,3 +128,20 @@ def test_filter_execute_ignores_star_tree(ctx):
     words, cnt, st = ctx.filter(q, gpu[0])
     mask, _ = O.filter_docs(q, ora[0][0])
     assert cnt == int(mask.sum()) and st.num_total_docs == 5000
+
+
+def test_star_tree_from_segment_directory(ctx, tmp_path):
+    # ph_segment_load_dir reads v3/star_tree_index + star_tree_index_map + the startree.v2.* metadata
+    # (StarTreeLoaderUtils.loadStarTreeV2) and takes the tree like a pinned one
+    from tests import segment_dirs as SD
+    rng = np.random.default_rng(91)
+    cols = star_table(rng, 7000)
+    seg, st, oseg, osd = make_star(cols, name="sd", max_leaf=5)
+    path = str(tmp_path / "st")
+    SD.write_v3(seg, path)
+    SD.write_star_trees(path, [st])
+    loaded = ctx.load_segment_dir(path)
+    from pinot_amd import native as N
+    assert N.lib().ph_segment_num_star_trees(loaded.handle) == 1
+    for sql in STAR_QUERIES:
+        _check(ctx, [loaded], [(oseg, osd)], sql)
