@@ -407,13 +407,46 @@ int64_t and_walk_entries_host(const uint64_t* bits, int k, int64_t num_docs, int
     uint8_t x[K + 1];
     auto get = [&](int i, int64_t w) -> unsigned long long { return bits[(int64_t)i * nwords + w]; };
     dfa_chunk<K>(k, c0, c1, get, d, x);
-    total += d[e];
+    total += (unsigned long long)(int64_t)(int32_t)d[e];
+    e = x[e];
+  }
+  return num_docs - 1 + (int64_t)total + (e == 0 ? 1 : 0);
+}
+
+// The same entries through k_and_dfa_reg's word tables (dfa_word, scans past k filled with all-ones words up to K)
+template <int K>
+static int64_t and_walk_entries_words(const uint64_t* bits, int k, int64_t num_docs) {
+  const int64_t nwords = (num_docs + 63) / 64;
+  unsigned long long total = 0;
+  int e = 0;
+  for (int64_t w = 0; w < nwords; ++w) {
+    const int32_t c1 = (int32_t)std::min<int64_t>(64, num_docs - w * 64);
+    unsigned long long W[K];
+    for (int i = 0; i < K; ++i)
+      W[i] = i < k ? bits[(int64_t)i * nwords + w] & (c1 < 64 ? (1ull << c1) - 1ull : ~0ull) : ~0ull;
+    uint32_t d[K + 1];
+    uint8_t x[K + 1];
+    dfa_word<K>(k, W, c1, d, x);
+    total += (unsigned long long)(int64_t)(int32_t)d[e];  // a word's sum is < 0 only for k = 1
     e = x[e];
   }
   return num_docs - 1 + (int64_t)total + (e == 0 ? 1 : 0);
 }
 
 }  // namespace ph
+
+// test hook: the AND-of-scans entries by k_and_dfa_reg's per-word tables on the host, with `width` (k..4) scans
+extern "C" int64_t phx_and_walk_entries_words(const uint64_t* bits, int32_t k, int64_t num_docs, int32_t width) {
+  using namespace ph;
+  if (num_docs <= 0) return 0;
+  if (k < 1 || k > width || width > 4) return -1;
+  switch (width) {
+    case 1:
+    case 2: return and_walk_entries_words<2>(bits, k, num_docs);
+    case 3: return and_walk_entries_words<3>(bits, k, num_docs);
+    default: return and_walk_entries_words<4>(bits, k, num_docs);
+  }
+}
 
 // test hooks (not part of the product boundary, include/pinot_hip.h).  k_and_dfa's chunk tables composed on the host
 // over k leaf bitmaps (leaf-major), so the CPU tests check the automaton against the simulator

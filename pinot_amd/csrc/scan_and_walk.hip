@@ -13,6 +13,45 @@
 
 namespace ph {
 
+// the workgroup's chunk tables composed in a tree (LDS), thread 0 storing the workgroup's table
+template <int K, int BLOCK>
+__device__ __forceinline__ void dfa_group_compose(const AndWalkJob& J, int64_t g, uint32_t (&d)[K + 1],
+                                                  uint8_t (&x)[K + 1], unsigned char* smem) {
+  uint32_t* td = reinterpret_cast<uint32_t*>(smem);                              // [BLOCK][K + 1]
+  uint8_t* tx = reinterpret_cast<uint8_t*>(smem + (size_t)BLOCK * (K + 1) * 4);  // [BLOCK][K + 1]
+  for (int s = 1; s < BLOCK; s <<= 1) {
+#pragma unroll
+    for (int e = 0; e <= K; ++e) {
+      td[threadIdx.x * (K + 1) + e] = d[e];
+      tx[threadIdx.x * (K + 1) + e] = x[e];
+    }
+    __syncthreads();
+    if ((threadIdx.x & (2 * s - 1)) == 0) {
+      uint32_t bd[K + 1];
+      uint8_t bx[K + 1];
+#pragma unroll
+      for (int e = 0; e <= K; ++e) {
+        bd[e] = td[(threadIdx.x + s) * (K + 1) + e];
+        bx[e] = tx[(threadIdx.x + s) * (K + 1) + e];
+      }
+      uint32_t od[K + 1];
+      uint8_t ox[K + 1];
+      dfa_compose<K>(K, d, x, bd, bx, od, ox);
+#pragma unroll
+      for (int e = 0; e <= K; ++e) {
+        d[e] = od[e];
+        x[e] = ox[e];
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    for (int e = 0; e <= J.k; ++e) {
+      J.gdelta[(int64_t)e * J.ngroups + g] = d[e];
+      J.gexit[(int64_t)e * J.ngroups + g] = x[e];
+    }
+}
+
 template <int K, int BLOCK, int CW>
 __global__ void __launch_bounds__(BLOCK) k_and_dfa(const AndWalkJob* __restrict__ jobs) {
   constexpr int ST = CW + 1;  // chunk words in LDS with one word of padding (bank spread)
@@ -49,39 +88,70 @@ __global__ void __launch_bounds__(BLOCK) k_and_dfa(const AndWalkJob* __restrict_
     }
   }
   __syncthreads();  // the words are consumed: their LDS holds the tables now
-  uint32_t* td = reinterpret_cast<uint32_t*>(smem);                      // [BLOCK][K + 1]
-  uint8_t* tx = reinterpret_cast<uint8_t*>(smem + (size_t)BLOCK * (K + 1) * 4);  // [BLOCK][K + 1]
-  for (int s = 1; s < BLOCK; s <<= 1) {
+  dfa_group_compose<K, BLOCK>(J, g, d, x, smem);
+}
+
+// ANDs of <= 4 scans (every SSB query; r6): one thread per chunk of CW words, the chunk's k x CW words loaded straight
+// into registers (consecutive lanes read consecutive 8 * CW-byte runs), each word's table from dfa_word (walks inside
+// registers only) composed in order into the chunk's table, then the workgroup tree.  K = the launch's widest AND
+// (2..4): narrower jobs fill with all-ones scans.
+template <int K, int BLOCK, int CW>
+__global__ void __launch_bounds__(BLOCK) k_and_dfa_reg(const AndWalkJob* __restrict__ jobs) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const AndWalkJob& J = jobs[blockIdx.y];
+  const int64_t g = blockIdx.x;
+  if (g >= J.ngroups) return;  // uniform over the workgroup
+  const int k = J.k;
+  const int64_t N = J.ndocs, nwords = J.nwords;
+  const int64_t c = g * BLOCK + threadIdx.x;
+  uint32_t d[K + 1];
+  uint8_t x[K + 1];
 #pragma unroll
-    for (int e = 0; e <= K; ++e) {
-      td[threadIdx.x * (K + 1) + e] = d[e];
-      tx[threadIdx.x * (K + 1) + e] = x[e];
-    }
-    __syncthreads();
-    if ((threadIdx.x & (2 * s - 1)) == 0) {
-      uint32_t bd[K + 1];
-      uint8_t bx[K + 1];
-#pragma unroll
-      for (int e = 0; e <= K; ++e) {
-        bd[e] = td[(threadIdx.x + s) * (K + 1) + e];
-        bx[e] = tx[(threadIdx.x + s) * (K + 1) + e];
-      }
-      uint32_t od[K + 1];
-      uint8_t ox[K + 1];
-      dfa_compose<K>(K, d, x, bd, bx, od, ox);
-#pragma unroll
-      for (int e = 0; e <= K; ++e) {
-        d[e] = od[e];
-        x[e] = ox[e];
-      }
-    }
-    __syncthreads();
+  for (int e = 0; e <= K; ++e) {
+    d[e] = 0;
+    x[e] = (uint8_t)e;
   }
-  if (threadIdx.x == 0)
-    for (int e = 0; e <= k; ++e) {
-      J.gdelta[(int64_t)e * J.ngroups + g] = d[e];
-      J.gexit[(int64_t)e * J.ngroups + g] = x[e];
+  if (c < J.nchunks) {
+    unsigned long long Wall[K][CW];
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+#pragma unroll
+      for (int q = 0; q < CW; ++q) {
+        const int64_t w = c * CW + q;
+        Wall[i][q] = i >= k ? ~0ull : (w < nwords ? J.bits[(int64_t)i * nwords + w] : 0ull);
+      }
+#pragma unroll
+    for (int q = 0; q < CW; ++q) {
+      const int64_t c0 = (c * CW + q) * 64;
+      if (c0 < N) {  // (lanes differ only in the job's last chunk)
+        const int32_t c1 = N - c0 < 64 ? (int32_t)(N - c0) : 64;
+        unsigned long long Wq[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+          Wq[i] = (c1 < 64 && i < k) ? Wall[i][q] & ((1ull << c1) - 1ull) : Wall[i][q];
+        uint32_t wd[K + 1];
+        uint8_t wx[K + 1];
+        dfa_word<K>(k, Wq, c1, wd, wx);
+        if (q == 0) {
+#pragma unroll
+          for (int e = 0; e <= K; ++e) {
+            d[e] = wd[e];
+            x[e] = wx[e];
+          }
+        } else {
+          uint32_t od[K + 1];
+          uint8_t ox[K + 1];
+          dfa_compose<K>(K, d, x, wd, wx, od, ox);
+#pragma unroll
+          for (int e = 0; e <= K; ++e) {
+            d[e] = od[e];
+            x[e] = ox[e];
+          }
+        }
+      }
     }
+  }
+  dfa_group_compose<K, BLOCK>(J, g, d, x, smem);
 }
 
 // one wave per job: lane l composes its slice of the workgroup tables for every entry type (the k + 1 chains' loads
@@ -106,7 +176,7 @@ __global__ void __launch_bounds__(64) k_and_compose(const AndWalkJob* __restrict
 #pragma unroll
     for (int e = 0; e <= K; ++e)
       if (e <= k) {
-        acc[e] += J.gdelta[(int64_t)t[e] * G + g];
+        acc[e] += (unsigned long long)(int64_t)(int32_t)J.gdelta[(int64_t)t[e] * G + g];  // (< 0 only for k = 1)
         t[e] = J.gexit[(int64_t)t[e] * G + g];
       }
   }
@@ -155,7 +225,19 @@ void launch_and_walk(const AndWalkJob* jobs, int32_t njobs, int64_t max_groups, 
   if (njobs <= 0 || max_groups <= 0) return;
   if (max_k > kMaxFbProgs) fail(PH_ERR_DEVICE, "AND walk wider than kMaxFbProgs scans");
   // the widest AND of the launch picks the register set (ST_SCANAND: at most kMaxFbProgs scans); LDS = K x 18 KiB
-  if (max_k <= 4) launch_dfa<4, 128>(jobs, njobs, max_groups, s);
+  if (max_k <= 4 && and_dfa_chunk_words() == 4) {
+    constexpr size_t lds = (size_t)128 * 5 * 5;
+    if (max_k <= 2) {
+      allow_lds(k_and_dfa_reg<2, 128, 4>, lds);
+      hipLaunchKernelGGL((k_and_dfa_reg<2, 128, 4>), dim3((unsigned)max_groups, (unsigned)njobs), dim3(128), lds, s, jobs);
+    } else if (max_k == 3) {
+      allow_lds(k_and_dfa_reg<3, 128, 4>, lds);
+      hipLaunchKernelGGL((k_and_dfa_reg<3, 128, 4>), dim3((unsigned)max_groups, (unsigned)njobs), dim3(128), lds, s, jobs);
+    } else {
+      allow_lds(k_and_dfa_reg<4, 128, 4>, lds);
+      hipLaunchKernelGGL((k_and_dfa_reg<4, 128, 4>), dim3((unsigned)max_groups, (unsigned)njobs), dim3(128), lds, s, jobs);
+    }
+  } else if (max_k <= 4) launch_dfa<4, 128>(jobs, njobs, max_groups, s);
   else if (max_k <= 8) launch_dfa<8, 128>(jobs, njobs, max_groups, s);
   else launch_dfa<kMaxFbProgs, 64>(jobs, njobs, max_groups, s);
   PH_HIP_CHECK(hipGetLastError());

@@ -199,3 +199,38 @@ def test_and_walk_at_bench_densities():
         exp = _native_sim(root, leaves, docs, n)
         assert _walk(docs, n, 9) == exp, dens
         assert _walk(docs, n, 6) == exp, dens
+
+
+def _walk_words(docs, n, width):
+    f = N.lib().phx_and_walk_entries_words
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int32]
+    bits = np.concatenate([_bitmap(d, n) for d in docs])
+    return f(bits.ctypes.data, len(docs), n, width)
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_and_walk_word_tables(seed):
+    # k_and_dfa_reg's per-word tables (dfa_word: the type -1 walk's candidates as a mask, the other entry types
+    # joining it through the epoch-sum bit planes), narrower ANDs padded with all-ones scans up to `width`
+    rng = np.random.default_rng(4000 + seed)
+    n = int(rng.choice([1, 2, 63, 64, 65, 127, 4097, 20_000, 70_001]))
+    k = int(rng.integers(1, 5))
+    dens = rng.choice([0.003, 0.02, 0.15, 0.5, 0.9, 1.0], size=k)
+    docs = [rng.random(n) < d for d in dens]
+    root, leaves = _scan_and(k)
+    exp = _native_sim(root, leaves, docs, n) if k > 1 else _walk(docs, n, 62)
+    for width in range(max(2, k), 5):
+        assert _walk_words(docs, n, width) == exp, (seed, k, width)
+
+
+def test_and_walk_word_tables_at_bench_densities():
+    rng = np.random.default_rng(8)
+    n = 100_000
+    for dens in ([1 / 7, 3 / 11, 0.48], [1 / 84, 3 / 11, 0.2], [2 / 250, 2 / 250, 6 / 7], [1 / 25, 1 / 5],
+                 [1 / 5, 1 / 5, 2 / 7, 2 / 5], [1.0, 1.0, 1.0, 1.0], [0.0, 1.0], [1.0, 0.0, 0.5]):
+        docs = [rng.random(n) < d for d in dens]
+        root, leaves = _scan_and(len(dens))
+        exp = _native_sim(root, leaves, docs, n)
+        assert _walk_words(docs, n, len(dens)) == exp, dens
+        assert _walk_words(docs, n, 4) == exp, dens
