@@ -1361,6 +1361,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     return res.release();
   }
 
+  stamp("pre-plan");
   // ---- per-segment filter plans
   QueryScratch scratch(ctx, st, lane.lane->stream_b);
   if (fds && fds->total_words > 0) PH_HIP_CHECK(hipMemsetAsync(fds->words, 0, 8 * (size_t)fds->total_words, st));
@@ -1681,6 +1682,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     return nullptr;
   }
 
+  stamp("keys");
   // ---- kernel parameters
   KParams kp{};
   kp.num_vals = nvals;
@@ -1818,6 +1820,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     stats.plan_mode = mode;
     res->mode = mode;
   } else {
+  stamp("kparams");
   // ---- mode selection (LDS table offsets are relative to the end of the staging areas, fixed below)
   size_t lds_tables = 16;
   int rec64 = 0;
@@ -1905,6 +1908,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
   }
 
+  stamp("mode");
   // ---- outputs (dense execute: the caller's tables, initialised here)
   auto out_table = [&](int& t, size_t bytes) -> void* {
     if (dop == DENSE_EXECUTE) return dn->tables[t++];
@@ -1936,6 +1940,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   };
   init_tables();
 
+  stamp("outputs");
   // ---- device segment table, programs, chunks
   std::vector<DevSegment> dsegs;
   std::vector<std::vector<PNode>> sp_nodes;  // per DevSegment: its sparse scan leaves (SparseShape::scans)
@@ -2186,6 +2191,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       dseg_chunks.back().second = (int32_t)chunks.size();
     }
   }
+  stamp("segtable");
   // ---- per-wave staging layout: one span per staged stream, sized by its widest segment; the tile is the
   // largest (<= 32 words) whose spans fit the kernel's prefetch register pool
   {
@@ -2308,6 +2314,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if ((d.fkind != FK_ALL && d.fkind != FK_RANGE && d.fkind != FK_DOCRANGE) ||
         (nvals == 1 && d.vals[0].kind != VK_PACKED))
       kp.lds_fast = 0;
+  stamp("staging");
   // selective inverted-index leaves (k_agg_sparse): every segment's filter is one bitmap leaf and together they
   // match < 1/8 of the docs -> gather the matched docs' values instead of streaming the columns
   {
@@ -2342,6 +2349,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
     }
   }
+  stamp("sparse");
   // the register-direct leaves' loads per lane (conj_reg.h): by the widest scan column of an sp_reg segment
   // (2: every leaf <= 8 bits, all loads hoisted; 0: no segment has register-direct leaves)
   kp.sparse_c = 0;
