@@ -1,6 +1,10 @@
 // kernels.hip -- gfx950 kernels of libpinot_hip.so outside the scan template: the launch dispatcher, value
 // re-encoding, result compaction, self-tests, HLL tables and the roaring OR (the scan kernel itself is
 // scan_kernel.h, instantiated per plan mode by scan_*.hip).
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "scan_kernel.h"
 
 namespace ph {
@@ -66,6 +70,18 @@ void launch_encode_values(const uint32_t* fwd, int32_t bits, const int64_t* tabl
   PH_HIP_CHECK(hipGetLastError());  // a failure left by an earlier unchecked call is reported as such, not as ours
   hipLaunchKernelGGL(k_encode_values, dim3(grid), dim3(256), 0, s, fwd, bits, table, base, vbits, n, out, nwords);
   PH_HIP_CHECK(hipGetLastError());
+}
+
+void allow_lds_raw(const void* kernel, size_t lds) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, size_t> set;  // the largest dynamic LDS set per (kernel, device)
+  int dev = 0;
+  PH_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  size_t& cur = set[{kernel, dev}];
+  if (cur >= lds) return;
+  PH_HIP_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  cur = lds;
 }
 
 // ------------------------------------------------------------------ result compaction

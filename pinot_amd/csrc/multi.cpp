@@ -434,6 +434,10 @@ ph_result* multi_execute(ph_ctx* x, const ph_query* q, ph_segment* const* segs, 
         PH_HIP_CHECK(hipMemcpyPeer(moved.back().ptr(), x->ordinals[to], ptrs[t], x->ordinals[k], bytes));
         ptrs[t] = moved.back().ptr();
       }
+      // a device-to-device copy may return before it lands, and the finalize below runs on a non-blocking lane
+      // stream that does not order after the null stream: wait for the copies (r6: the first rows of a moved shard
+      // were intermittently read stale)
+      PH_HIP_CHECK(hipStreamSynchronize(nullptr));
       k = to;
     }
     PH_HIP_CHECK(hipSetDevice(x->ordinals[k]));

@@ -184,15 +184,18 @@ DictIdSet evaluate_predicate(const ph_predicate& p, const Column& c) {
     }
     case PH_PRED_IN:
     case PH_PRED_NOT_IN: {
-      std::set<int32_t> ids;
+      std::vector<int32_t> ids;  // sorted, distinct
+      ids.reserve((size_t)std::max(0, p.num_values));
       for (int i = 0; i < p.num_values; ++i) {
         int64_t id = d.index_of(lit(p.values[i]));
-        if (id >= 0) ids.insert((int32_t)id);
+        if (id >= 0) ids.push_back((int32_t)id);
       }
+      std::sort(ids.begin(), ids.end());
+      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
       if (p.type == PH_PRED_IN) {
         if (ids.empty()) { r.always_false = true; return r; }
         if ((int64_t)ids.size() == card) { r.always_true = true; return r; }
-        r.ids.assign(ids.begin(), ids.end());
+        r.ids = std::move(ids);
         if (r.ids.back() - r.ids.front() + 1 == (int32_t)r.ids.size()) {
           r.is_range = true;
           r.start = r.ids.front();
@@ -203,7 +206,7 @@ DictIdSet evaluate_predicate(const ph_predicate& p, const Column& c) {
       if (ids.empty()) { r.always_true = true; return r; }
       if ((int64_t)ids.size() == card) { r.always_false = true; return r; }
       r.exclusive = true;
-      r.ids.assign(ids.begin(), ids.end());
+      r.ids = std::move(ids);
       return r;
     }
     case PH_PRED_RANGE: {
@@ -1387,12 +1390,21 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
            (n.op == OP_RANGE || (n.op == OP_SET && n.set.size() <= (size_t)kLeafSetWords));
   };
   std::vector<StatSeg> stat_segs;
+  pl.bitmaps.reserve(pl.bitmaps.size() + (size_t)nseg * 2);
+  double tacc[8] = {};
+  auto tnow = [&]() { return host_times ? clock::now() : clock::time_point{}; };
+  auto tadd = [&](int k, clock::time_point a) {
+    if (host_times) tacc[k] += std::chrono::duration<double, std::milli>(clock::now() - a).count();
+  };
   for (int i = 0; i < nseg && dop != DENSE_LAYOUT && !fin; ++i) {
+    auto ta = tnow();
     PNode root;
     root.kind = L_ALL;
     auto sv = star ? star->find(segs[i]) : decltype(star->end()){};
     if (star && sv != star->end()) root = star_root(pl, segs[i], sv->second);
     else if (q->filter_root >= 0) root = pl.build(segs[i], q->filter_root, 0);
+    tadd(0, ta);
+    ta = tnow();
     // same-column scan predicates merge first, as the reference's query optimizer merges them before planning
     // (MergeEqInFilterOptimizer: `d_year = 1997 OR d_year = 1998` -> one IN; MergeRangeFilterOptimizer: ranges of
     // one column under an AND), so the statistics below see the reference's operator tree
@@ -1401,6 +1413,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     if (segs[i]->num_docs > 0)
       stats.num_entries_scanned_in_filter += legacy_partial_entries(
           root, [&](int slot) -> const Column& { return *segs[i]->columns.at(slot_names[slot]); });
+    tadd(1, ta);
+    ta = tnow();
     const int sk = stat_kind(root);
     if (sk != ST_DEVICE && segs[i]->num_docs > 0) {
       StatSeg ss;
@@ -1414,7 +1428,9 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     else stats.num_entries_scanned_in_filter += (int64_t)segs[i]->num_docs * count_scan_leaves(root);
     if (root.kind == L_NONE || segs[i]->num_docs == 0) seg_live[i] = 0;
     roots[i] = std::move(root);
+    tadd(2, ta);
   }
+  if (host_times) fprintf(stderr, "[ph host]   plans: build %.3f merge+legacy %.3f stat+mark %.3f ms\n", tacc[0], tacc[1], tacc[2]);
 
   // ---- FastFilteredCountOperator (AggregationPlanNode.java:183-188): COUNT only, and every segment's filter
   // answers getNumMatchingDocs from its index -- a sorted doc range, an inverted-index bitmap (disjoint per
@@ -2014,8 +2030,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   std::vector<std::pair<int32_t, int32_t>> dseg_chunks;                // device segment -> its chunk range
   std::vector<int> dseg_src;                                           // device segment -> query segment index
   std::vector<std::pair<int32_t, int32_t>> seg_words;                  // device segment -> [first, end) words to scan
+  for (int k = 0; k < 8; ++k) tacc[k] = 0;
   for (int i = 0; i < nseg; ++i) {
     if (!seg_live[i]) continue;
+    auto tb = tnow();
     ph_segment* s = segs[i];
     DevSegment d{};
     d.num_docs = s->num_docs;
@@ -2100,6 +2118,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         all_insns.insert(all_insns.end(), sp.insns.begin(), sp.insns.end());
       }
     }
+    tadd(3, tb);
+    tb = tnow();
     if (sparse_plan || agg_conj) {
       const SparseShape sh = sparse_shape(root);
       if (sp_nodes.size() <= (size_t)si) sp_nodes.resize((size_t)si + 1);
@@ -2122,6 +2142,8 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         if (leaf.op == OP_SET) sset_fix.push_back({si * kMaxConj + k, leaf.set});
       }
     }
+    tadd(4, tb);
+    tb = tnow();
     for (size_t sl = 0; sl < slot_names.size(); ++sl) {
       Column& c = *s->columns.at(slot_names[sl]);
       DevColumn& dc = d.cols[sl];
@@ -2171,25 +2193,59 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     }
     // chunks cover only the words the filter can match in (SortedIndexBasedFilterOperator: a sorted leaf, alone
     // or under an AND, bounds the docs; r1 staged every stream of the whole segment)
+    tadd(5, tb);
+    tb = tnow();
     const std::pair<int64_t, int64_t> span = doc_span(root, s->num_docs);
     seg_words.push_back({(int32_t)(span.first / 64), (int32_t)((span.second + 63) / 64)});
     dseg_src.push_back(i);
     dsegs.push_back(d);
     stats.num_segments_matched++;
+    tadd(6, tb);
   }
+  if (host_times)
+    fprintf(stderr, "[ph host]   segtable: filter+stat %.3f sparse %.3f columns %.3f span+push %.3f ms\n", tacc[3], tacc[4],
+            tacc[5], tacc[6]);
+  // selective inverted-index leaves (k_agg_sparse): every segment's filter is one bitmap leaf and together they
+  // match < 1/8 of the docs -> gather the matched docs' values instead of streaming the columns.  Decided before the
+  // chunk list: the container form replaces it (r6: config 5's 400 segments built 244K streaming chunks, 0.25 ms of
+  // host time, only to drop them)
+  bool all_bitmap_agg = mode == MODE_AGG && !dsegs.empty();
+  for (int j = 0; j < nvals; ++j) all_bitmap_agg = all_bitmap_agg && !val_exprs[j];
+  for (auto& d : dsegs) all_bitmap_agg = all_bitmap_agg && d.fkind == FK_BITMAP;
+  bool agg_sparse_plan = agg_conj;
   {
+    int64_t docs = 0, hits = 0;
+    if (all_bitmap_agg) {
+      for (auto& d : dsegs) docs += d.num_docs;
+      for (auto& fb : fbitmap_fix) hits += (int64_t)leaf_docs_estimate(pl.bitmaps[fb.second]);
+    }
+    agg_sparse_plan = (all_bitmap_agg && hits * 8 < docs) || agg_conj;
+    if (ctx->has(OPT_AGG_SPARSE)) agg_sparse_plan = (all_bitmap_agg || agg_conj) && ctx->opt(OPT_AGG_SPARSE) != 0;
+  }
+  const bool agg_cont_plan = cont_defer && agg_sparse_plan && all_bitmap_agg && !agg_conj;
+  int64_t chunk_docs_total = 0;  // the streaming chunk list's words x 64 and its widest chunk
+  int32_t chunk_words_max = 0;
+  if (agg_cont_plan) {
+    dseg_chunks.assign(seg_words.size(), {0, 0});
+  } else {
     // chunk size: 16384 docs, smaller when the whole scan has too few chunks to give every CU several (a single
     // 10M-row segment clipped to an 8 % sorted range is ~50 full chunks: latency-bound on 50 workgroups)
     int64_t total_words = 0;
     for (auto& sw : seg_words) total_words += std::max(0, sw.second - sw.first);
     const int32_t cw = (int32_t)std::max<int64_t>(
         32, std::min<int64_t>(kChunkWords, (total_words + 4 * ctx->num_cus - 1) / (4 * ctx->num_cus)));
+    size_t nch = 0;
+    for (auto& sw : seg_words) nch += (size_t)((std::max(0, sw.second - sw.first) + cw - 1) / cw);
+    chunks.reserve(nch);
+    dseg_chunks.reserve(seg_words.size());
     for (size_t si = 0; si < seg_words.size(); ++si) {
       dseg_chunks.push_back({(int32_t)chunks.size(), 0});
       for (int32_t w = seg_words[si].first; w < seg_words[si].second; w += cw)
         chunks.push_back({(int32_t)si, w, std::min(seg_words[si].second, w + cw), 0});
       dseg_chunks.back().second = (int32_t)chunks.size();
     }
+    chunk_docs_total = total_words * 64;
+    chunk_words_max = (int32_t)std::min<int64_t>(cw, total_words);
   }
   stamp("segtable");
   // ---- per-wave staging layout: one span per staged stream, sized by its widest segment; the tile is the
@@ -2315,21 +2371,11 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         (nvals == 1 && d.vals[0].kind != VK_PACKED))
       kp.lds_fast = 0;
   stamp("staging");
-  // selective inverted-index leaves (k_agg_sparse): every segment's filter is one bitmap leaf and together they
-  // match < 1/8 of the docs -> gather the matched docs' values instead of streaming the columns
+  // the k_agg_sparse plan decided above
   {
-    bool all_bitmap = mode == MODE_AGG && !dsegs.empty();
-    for (int j = 0; j < nvals; ++j) all_bitmap = all_bitmap && !val_exprs[j];
-    for (auto& d : dsegs) all_bitmap = all_bitmap && d.fkind == FK_BITMAP;
-    int64_t docs = 0, hits = 0;
-    if (all_bitmap) {
-      for (auto& d : dsegs) docs += d.num_docs;
-      for (auto& fb : fbitmap_fix) hits += (int64_t)leaf_docs_estimate(pl.bitmaps[fb.second]);
-    }
-    kp.agg_sparse = (all_bitmap && hits * 8 < docs) || agg_conj;
-    if (ctx->has(OPT_AGG_SPARSE)) kp.agg_sparse = (all_bitmap || agg_conj) && ctx->opt(OPT_AGG_SPARSE) != 0;
+    kp.agg_sparse = agg_sparse_plan;
     if (kp.agg_sparse) kp.agg_fast = 0;
-    kp.agg_cont = cont_defer && kp.agg_sparse && all_bitmap && !agg_conj;
+    kp.agg_cont = agg_cont_plan;
     if (kp.agg_cont) {
       // chunks = ranges of <= 8 containers of each dictId of each segment's leaf (a wave takes one at a time)
       chunks.clear();
@@ -2630,6 +2676,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     PH_HIP_CHECK(hipMemcpyAsync(d_chunks, stage + b1 + b2, b3, hipMemcpyHostToDevice, st));
     if (b4) PH_HIP_CHECK(hipMemcpyAsync(d_segs_opt, stage + b1 + b2 + b3, b4, hipMemcpyHostToDevice, st));
     PH_HIP_CHECK(hipEventRecord(lane.lane->ev_uploaded, st));  // the statistics pass (stream b) starts here
+    stamp("uploaded");
     // container mode skipped the doc bitmaps; a numGroupsLimit first-seen pass runs the segments' generic programs,
     // which read them: build them then, patch the programs / segment tables and upload them again
     bool late_built = false;
@@ -2834,7 +2881,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       // batches: contiguous chunk ranges of ~batch_rows docs
       std::vector<std::pair<int32_t, int32_t>> batches;
       int64_t max_batch_docs = 0;
-      {
+      if (chunk_docs_total < batch_rows) {  // one batch (config 3: no walk over its 61K chunks)
+        batches.push_back({0, (int32_t)chunks.size()});
+        max_batch_docs = chunk_docs_total;
+      } else {
         int32_t b0 = 0;
         int64_t acc = 0;
         for (int32_t c = 0; c < (int32_t)chunks.size(); ++c) {
@@ -2907,8 +2957,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       // region (partition, workgroup) capacity: a workgroup scans <= ceil(chunks / grid) chunks; uniform keys
       // put 1/P of its docs in each partition; 25 % headroom + 64, rounded to 64 records (16-byte aligned
       // regions).  Skew beyond that spills to the overflow table.
-      int32_t max_chunk_words = 1;
-      for (auto& ch : chunks) max_chunk_words = std::max(max_chunk_words, ch.word_end - ch.word_begin);
+      const int32_t max_chunk_words = std::max<int32_t>(1, chunk_words_max);
       const int64_t wg_docs = (int64_t)((max_batch_chunks + grid_a - 1) / grid_a) * max_chunk_words * 64;
       int64_t cap = (int64_t)((double)wg_docs * 1.25 / (double)P) + 64;
       cap = (cap + 63) / 64 * 64;
@@ -2931,6 +2980,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
         bufs[b] = scratch.alloc<uint8_t>((size_t)P * grid_a * cap * rec_bytes);
         counts[b] = scratch.alloc<uint32_t>((size_t)P * grid_a);
       }
+      stamp("part regions");
       kp.ovf_count = scratch.alloc<unsigned long long>(G);
       PH_HIP_CHECK(hipMemsetAsync(kp.ovf_count, 0, 8 * G, st));
       if (has_sum) {
@@ -2977,6 +3027,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       Lane& L = *lane.lane;
       // PH_PART_SERIAL=1 runs kernel B on the scan stream (profiling each kernel without overlap)
       hipStream_t sb = ctx->has(OPT_PART_SERIAL) ? st : L.stream_b;
+      stamp("part fills");
       PH_HIP_CHECK(hipEventRecord(L.ev_start, st));
       for (size_t b = 0; b < batches.size(); ++b) {
         if (interruptible && b > 0) {

@@ -1082,12 +1082,12 @@ __global__ void __launch_bounds__(MODE == MODE_PARTITION ? kPartBlock : kBlock) 
   }
 }
 
+// kernels that use more than the default 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU); the attribute is set once
+// per (kernel, device) and raised when a launch needs more (the call costs host time on every launch otherwise)
+void allow_lds_raw(const void* kernel, size_t lds);
 template <class K>
 inline void allow_lds(K kernel, size_t lds) {
-  // kernels that use more than the default 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
-  if (lds > 64 * 1024)
-    PH_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  if (lds > 64 * 1024) allow_lds_raw(reinterpret_cast<const void*>(kernel), lds);
 }
 
 template <int MODE, int NG, int REC64>

@@ -1,5 +1,9 @@
 // scan_partition_reg.hip -- kernel A of the partitioned group-by in its register-direct form (k_part_reg); kernel B
 // and the LDS-staged forms are in scan_partition.hip.
+#include <map>
+#include <mutex>
+#include <tuple>
+
 #include "scan_partition.h"
 #include "part_tiles.h"
 
@@ -165,10 +169,25 @@ int part_reg_blocks_per_cu(const KParams& p, int ng, size_t lds) {
   if (ng == 1) { PH_REG_FN(1) } else if (ng == 2) { PH_REG_FN(2) } else { PH_REG_FN(3) }
 #undef PH_REG_FN
 #undef PH_REG_FX
+  // (the occupancy query and the attribute call cost tens of microseconds of host time per query: cached per
+  // (kernel, LDS bytes, device))
+  static std::mutex mu;
+  static std::map<std::tuple<const void*, size_t, int>, int> cache;
+  int dev = 0;
+  PH_HIP_CHECK(hipGetDevice(&dev));
+  const auto key = std::make_tuple(f, lds, dev);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
   if (lds > 64 * 1024) PH_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   int n = 0;
   PH_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, kRegBlock, lds));
-  return std::max(1, n);
+  n = std::max(1, n);
+  std::lock_guard<std::mutex> lk(mu);
+  cache[key] = n;
+  return n;
 }
 
 }  // namespace ph
