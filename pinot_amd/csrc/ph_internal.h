@@ -42,6 +42,13 @@ struct Error {
     if (e_ != hipSuccess) ::ph::fail(PH_ERR_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
+// a host -> device copy that has LANDED when this returns: the library's lanes are non-blocking streams, which do not
+// order after work on the null stream, and a plain hipMemcpy may return once its source is staged
+inline void copy_h2d_sync(void* dst, const void* src, size_t bytes) {
+  PH_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, nullptr));
+  PH_HIP_CHECK(hipStreamSynchronize(nullptr));
+}
+
 // ------------------------------------------------------------------ limits
 constexpr int kMaxCols = 12;      // distinct columns referenced by one query
 constexpr int kMaxAggs = 8;       // aggregation functions per query

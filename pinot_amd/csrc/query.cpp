@@ -982,7 +982,7 @@ const int32_t* segment_remap(Context* ctx, const ph_segment& s, const Column& c,
   if (!identity) {
     buf = std::make_shared<DeviceBuffer>();
     buf->alloc(sizeof(int32_t) * map.size(), ctx->device);
-    PH_HIP_CHECK(hipMemcpy(buf->ptr, map.data(), sizeof(int32_t) * map.size(), hipMemcpyHostToDevice));
+    copy_h2d_sync(buf->ptr, map.data(), sizeof(int32_t) * map.size());
   }
   g.remaps[s.id] = buf;
   return buf ? buf->as<int32_t>() : nullptr;
@@ -998,7 +998,7 @@ const void* global_dict_device_values(Context* ctx, GlobalDict& g) {
     b->alloc(8 * n, ctx->device);
     const void* src = (g.dict.type == PH_INT || g.dict.type == PH_LONG) ? (const void*)g.dict.ints.data()
                                                                         : (const void*)g.dict.reals.data();
-    PH_HIP_CHECK(hipMemcpy(b->ptr, src, 8 * g.dict.size, hipMemcpyHostToDevice));
+    copy_h2d_sync(b->ptr, src, 8 * g.dict.size);
     g.d_values = std::move(b);
   }
   return g.d_values->ptr;
@@ -2691,10 +2691,10 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
       PH_HIP_CHECK(hipStreamSynchronize(st));  // nothing in flight reads the tables while they are replaced
       if (!all_insns.empty())
-        PH_HIP_CHECK(hipMemcpy(d_prog, all_insns.data(), sizeof(FilterInsn) * all_insns.size(), hipMemcpyHostToDevice));
-      PH_HIP_CHECK(hipMemcpy(d_segs, dsegs.data(), sizeof(DevSegment) * dsegs.size(), hipMemcpyHostToDevice));
+        copy_h2d_sync(d_prog, all_insns.data(), sizeof(FilterInsn) * all_insns.size());
+      copy_h2d_sync(d_segs, dsegs.data(), sizeof(DevSegment) * dsegs.size());
       if (d_segs_opt)
-        PH_HIP_CHECK(hipMemcpy(d_segs_opt, dsegs_opt.data(), sizeof(DevSegment) * dsegs_opt.size(), hipMemcpyHostToDevice));
+        copy_h2d_sync(d_segs_opt, dsegs_opt.data(), sizeof(DevSegment) * dsegs_opt.size());
       late_built = true;
     };
     kp.segs = d_segs;
@@ -2782,7 +2782,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
           std::vector<DevSegment> dl = dsegs_opt;
           for (int k : limit_segs) dl[k].keep = keep2;
           DevSegment* d_segs_lim = scratch.alloc<DevSegment>(dl.size());
-          PH_HIP_CHECK(hipMemcpy(d_segs_lim, dl.data(), sizeof(DevSegment) * dl.size(), hipMemcpyHostToDevice));
+          copy_h2d_sync(d_segs_lim, dl.data(), sizeof(DevSegment) * dl.size());
           auto launch_range = [&](KParams kx, int32_t cb, int32_t ce) {
             if (ce <= cb) return;
             kx.chunk_begin = cb;

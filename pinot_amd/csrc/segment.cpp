@@ -467,7 +467,7 @@ void build_hll_table(Context* ctx, Column& c, int log2m, hipStream_t st) {
       const std::string& s = c.dict.strings[i];
       h[i] = hll_entry(murmur_hash_bytes(reinterpret_cast<const uint8_t*>(s.data()), (int32_t)s.size(), -1), log2m);
     }
-    PH_HIP_CHECK(hipMemcpy(t.buf->ptr, h.data(), sizeof(uint32_t) * h.size(), hipMemcpyHostToDevice));
+    copy_h2d_sync(t.buf->ptr, h.data(), sizeof(uint32_t) * h.size());
   } else {
     // INT / LONG -> hashLong((long) value); DOUBLE -> hashLong(doubleToRawLongBits); FLOAT ->
     // hashLong(floatToRawIntBits) (DistinctCountHLLAggregationFunction.java:127-131 offers the Float itself)
