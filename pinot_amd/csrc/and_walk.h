@@ -196,13 +196,15 @@ __host__ __device__ inline void dfa_chunk(int k, int64_t c0, int64_t c1, Get&& g
 // One 64-doc word's table (the device form for ANDs of <= 4 scans, r6): the same automaton with the word as the
 // chunk, so a chunk's table is its words' tables composed in order.  Every walk stays inside the k scans' words in
 // registers (no word switches, no LDS); W[i] for k <= i < K are all-ones fillers (never the first scan without a doc),
-// bits at or past c1 (the docs of the word) are zero.  The type -1 walk marks its candidates in a 64-bit mask and its
-// epochs' (calls - [match]) + 1 in three bit planes, so another type's walk that reaches one of its candidates M takes the rest as the
-// sum of the planes above M (the walks agree after a shared candidate): no candidate history, no joins missed.
+// bits at or past c1 (the docs of the word) are zero.  The type -1 walk only marks its candidates (V) and the epochs
+// whose setter is skipped (S): an epoch's (calls - [match]) is f + 1 - skip, or k - 1 - skip for a match, and f is
+// the number of nested prefix ANDs holding the doc, so the sum of any run of its epochs is a handful of masked
+// popcounts.  Another type's walk that reaches one of its candidates M takes the rest as that sum above M (the walks
+// agree after a shared candidate).
 template <int K>
 __host__ __device__ inline void dfa_word(int k, const unsigned long long (&W)[K], int32_t c1, uint32_t (&delta)[K + 1],
                                          uint8_t (&ext)[K + 1]) {
-  static_assert(K <= 4, "epoch sums are kept in three bit planes");
+  static_assert(K <= 4, "ANDs of at most 4 scans");
   unsigned long long P[K];
   {
     unsigned long long a = ~0ull;
@@ -212,53 +214,59 @@ __host__ __device__ inline void dfa_word(int k, const unsigned long long (&W)[K]
       P[i] = a;
     }
   }
-  // one epoch at M set by scan j: its (calls - [match]), the next candidate (-1: leaves the word) and its setter
-  auto epoch = [&](int32_t M, int j, int32_t& nxt, int& jn) -> uint32_t {
+  // the first scan without doc M (>= k: a match; fillers only add to it past k)
+  auto level = [&](int32_t M) {
     int f = 0;
 #pragma unroll
     for (int i = 0; i < K; ++i) f += (int)((P[i] >> M) & 1ull);
-    const uint32_t skip = j >= 0 ? 1u : 0u;
-    if (f >= k) {  // a match (fillers only add to f past k)
-      nxt = M + 1 < c1 ? M + 1 : -1;
-      jn = -1;
-      return (uint32_t)k - 1u - skip;
-    }
+    return f;
+  };
+  // scan f's next match after M, or -1
+  auto seek = [&](int f, int32_t M) -> int32_t {
     unsigned long long v = 0;
 #pragma unroll
     for (int y = 0; y < K; ++y)
       if (y == f) v = W[y];
     v &= (~0ull << M) << 1;
-    nxt = v ? (int32_t)__builtin_ctzll(v) : -1;
-    jn = f;
-    return (uint32_t)f + 1u - ((skip != 0u && j < f) ? 1u : 0u);
+    return v ? (int32_t)__builtin_ctzll(v) : -1;
   };
-  // type -1: from doc 0 of the word
-  unsigned long long V = 0, C0 = 0, C1 = 0, C2 = 0;
-  uint32_t total = 0;
+  // the type -1 walk from doc 0 of the word
+  unsigned long long V = 0, S = 0;
   uint8_t x0 = 0;
   {
     int32_t M = 0;
     int j = -1;
-    for (;;) {
-      int32_t nxt;
-      int jn;
-      const uint32_t c = epoch(M, j, nxt, jn);
-      total += c;
+    for (;;) {  // (branch-free body: the match and seek successors are both computed, then selected)
+      const int f = level(M);
       const unsigned long long bit = 1ull << M;
-      const uint32_t c1p = c + 1u;  // -1 (a match right after a jump when k = 1) .. k, stored as 0 .. k + 1
       V |= bit;
-      C0 |= (c1p & 1u) ? bit : 0ull;
-      C1 |= (c1p & 2u) ? bit : 0ull;
-      C2 |= (c1p & 4u) ? bit : 0ull;
+      S |= (j >= 0 && j < f) ? bit : 0ull;  // (j < k <= f for a match: skipped whenever a scan set M)
+      const bool match = f >= k;
+      const int32_t sk = seek(match ? 0 : f, M);
+      const int32_t nm = M + 1 < c1 ? M + 1 : -1;
+      const int32_t nxt = match ? nm : sk;
+      j = match ? -1 : f;
       if (nxt < 0) {
-        x0 = (uint8_t)(jn + 1);
+        x0 = (uint8_t)(j + 1);
         break;
       }
       M = nxt;
-      j = jn;
     }
   }
-  delta[0] = total;
+  // the type -1 epochs' sum over the candidates in `sel`: sum of (f + 1) - 2 per match - skips
+  auto run_sum = [&](unsigned long long sel) -> uint32_t {
+    const unsigned long long v = V & sel;
+    uint32_t t = (uint32_t)__builtin_popcountll(v) - (uint32_t)__builtin_popcountll(S & sel);
+    unsigned long long last = 0;
+#pragma unroll
+    for (int i = 0; i < K; ++i)
+      if (i < k) {
+        t += (uint32_t)__builtin_popcountll(v & P[i]);
+        last = P[i];
+      }
+    return t - 2u * (uint32_t)__builtin_popcountll(v & last);
+  };
+  delta[0] = run_sum(~0ull);
   ext[0] = x0;
 #pragma unroll
   for (int e = 0; e < K; ++e) {
@@ -267,15 +275,18 @@ __host__ __device__ inline void dfa_word(int k, const unsigned long long (&W)[K]
     if (e < k && W[e] != 0ull) {  // else the jump passes through the word
       int32_t M = (int32_t)__builtin_ctzll(W[e]);
       int j = e;
-      for (;;) {
-        int32_t nxt;
-        int jn;
-        de += epoch(M, j, nxt, jn);
+      int32_t joined = -1;
+      for (;;) {  // (branch-free body, as the type -1 walk's)
+        const int f = level(M);
+        const uint32_t skip = (j >= 0 && j < f) ? 1u : 0u;
+        const bool match = f >= k;
+        de += (match ? (uint32_t)k - 2u : (uint32_t)f) + 1u - skip;
+        const int32_t sk = seek(match ? 0 : f, M);
+        const int32_t nm = M + 1 < c1 ? M + 1 : -1;
+        const int32_t nxt = match ? nm : sk;
+        const int jn = match ? -1 : f;
         if ((V >> M) & 1ull) {  // a type -1 candidate: its epochs after M follow
-          const unsigned long long hi = (~0ull << M) << 1;
-          de += (uint32_t)__builtin_popcountll(C0 & hi) + 2u * (uint32_t)__builtin_popcountll(C1 & hi) +
-                4u * (uint32_t)__builtin_popcountll(C2 & hi) - (uint32_t)__builtin_popcountll(V & hi);
-          xe = x0;
+          joined = M;
           break;
         }
         if (nxt < 0) {
@@ -284,6 +295,10 @@ __host__ __device__ inline void dfa_word(int k, const unsigned long long (&W)[K]
         }
         M = nxt;
         j = jn;
+      }
+      if (joined >= 0) {
+        de += run_sum((~0ull << joined) << 1);
+        xe = x0;
       }
     }
     delta[e + 1] = de;
