@@ -551,11 +551,16 @@ __device__ __forceinline__ void roaring_or_container(const RoaringContainer& c, 
       if (doc < limit) atomicOr(&bitmap[doc >> 5], 1u << (doc & 31u));
     }
   } else if (c.type == 1) {  // bitmap container: 1024 x uint64 LE = 2048 x uint32 LE
+    // aligned dword loads, funnel-shifted when the payload is not 4-byte aligned (one load per word instead of four
+    // byte loads; the device buffer carries 16 bytes past its end, so the dword after the last one is readable)
+    const uintptr_t pa = reinterpret_cast<uintptr_t>(pay);
+    const uint32_t* A = reinterpret_cast<const uint32_t*>(pa & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(pa & 3u) * 8u;  // (wave-uniform)
     for (int i = lane; i < 2048; i += 64) {
       const uint32_t d0 = hi + 32u * (uint32_t)i;
       if (d0 >= limit) break;
-      const uint8_t* q = pay + 4 * i;
-      uint32_t v = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+      uint32_t v = A[i];
+      if (sh) v = __builtin_amdgcn_alignbit(A[i + 1], v, sh);
       if (limit - d0 < 32u) v &= (1u << (limit - d0)) - 1u;
       if (v) atomicOr(&bitmap[d0 >> 5], v);
     }
@@ -612,6 +617,8 @@ __global__ void __launch_bounds__(256) k_roaring_chunk(const RoaringLeaf* __rest
   for (int r = wave; r < L.ids_count; r += 4) {
     const RoaringRange rg = ranges[L.ids_first + r];
     int found = -1;
+    // a dictId with a container in every chunk has the chunk's at index `chunk` (keys ascend): one load, no search
+    if ((int)chunk < rg.count && L.dir[rg.first + chunk].key == (int)chunk) found = (int)chunk;
     for (int b = 0; b < rg.count && found < 0; b += 256) {
       int key[4];
 #pragma unroll

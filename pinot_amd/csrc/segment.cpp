@@ -596,7 +596,7 @@ ph_segment* segment_pin_impl(Context* ctx, const ph_segment_desc* desc) {
         fail(PH_ERR_INVALID_ARGUMENT, "column " + col->name + ": inverted index too small");
       col->inverted.assign(inv, inv + d.inverted_index_size);
       build_bitmap_directory(*col);
-      col->d_inverted.alloc(d.inverted_index_size, ctx->device);
+      col->d_inverted.alloc(d.inverted_index_size + 16, ctx->device);  // + the dword past a bitmap container's end
       PH_HIP_CHECK(hipMemcpyAsync(col->d_inverted.ptr, inv, d.inverted_index_size, hipMemcpyHostToDevice, st));
       seg->device_bytes += d.inverted_index_size;
       // the container directory too, so a query's inverted leaves upload only (dictId -> container range) items
