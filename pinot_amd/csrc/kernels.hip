@@ -543,10 +543,11 @@ __device__ __forceinline__ uint32_t ld_u16(const uint8_t* b) { return (uint32_t)
 // ORs one container's docs (hi | low 16 bits) below `limit` into `bitmap` (word = doc / 32); `bitmap` is the
 // device doc bitmap (hi = key << 16, limit = num_docs) or a workgroup's LDS chunk (hi = 0, limit = docs in chunk)
 __device__ __forceinline__ void roaring_or_container(const RoaringContainer& c, const uint8_t* __restrict__ base,
-                                                     uint32_t* bitmap, uint32_t hi, uint32_t limit, int lane) {
+                                                     uint32_t* bitmap, uint32_t hi, uint32_t limit, int lane,
+                                                     int nlanes = 64) {
   const uint8_t* pay = base + c.offset;
   if (c.type == 0) {  // array container: card x uint16 LE
-    for (int i = lane; i < c.card; i += 64) {
+    for (int i = lane; i < c.card; i += nlanes) {
       const uint32_t doc = hi | ld_u16(pay + 2 * i);
       if (doc < limit) atomicOr(&bitmap[doc >> 5], 1u << (doc & 31u));
     }
@@ -556,16 +557,18 @@ __device__ __forceinline__ void roaring_or_container(const RoaringContainer& c, 
     const uintptr_t pa = reinterpret_cast<uintptr_t>(pay);
     const uint32_t* A = reinterpret_cast<const uint32_t*>(pa & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)(pa & 3u) * 8u;  // (wave-uniform)
-    for (int i = lane; i < 2048; i += 64) {
+    // the words below `limit` (no early exit inside the loop, so the loads of several iterations overlap)
+    const int nw = limit > hi ? (int)min(2048u, (limit - hi + 31u) >> 5) : 0;
+#pragma unroll 4
+    for (int i = lane; i < nw; i += nlanes) {
       const uint32_t d0 = hi + 32u * (uint32_t)i;
-      if (d0 >= limit) break;
       uint32_t v = A[i];
       if (sh) v = __builtin_amdgcn_alignbit(A[i + 1], v, sh);
       if (limit - d0 < 32u) v &= (1u << (limit - d0)) - 1u;
       if (v) atomicOr(&bitmap[d0 >> 5], v);
     }
   } else {  // run container: uint16 numRuns, then (start, length-1) pairs
-    for (int r = lane; r < c.card; r += 64) {
+    for (int r = lane; r < c.card; r += nlanes) {
       const uint32_t start = hi | ld_u16(pay + 2 + 4 * r);
       const uint32_t end = start + ld_u16(pay + 4 + 4 * r);  // inclusive
       for (uint32_t d = start; d <= end && d < limit;) {
@@ -614,7 +617,11 @@ __global__ void __launch_bounds__(256) k_roaring_chunk(const RoaringLeaf* __rest
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t nd = (uint32_t)L.num_docs, d0 = chunk << 16;
   const uint32_t limit = nd > d0 ? min(nd - d0, 65536u) : 0u;
-  for (int r = wave; r < L.ids_count; r += 4) {
+  // the four waves share the leaf's dictIds: `per` waves OR each container together (a one-dictId leaf -- EQ, most SSB
+  // dimension leaves -- takes the whole workgroup; r5 gave every dictId one wave and left the others idle)
+  const int per = L.ids_count >= 4 ? 1 : 4 / max(1, L.ids_count);
+  const int sub = wave % per;
+  for (int r = wave / per; r < L.ids_count; r += 4 / per) {
     const RoaringRange rg = ranges[L.ids_first + r];
     int found = -1;
     // a dictId with a container in every chunk has the chunk's at index `chunk` (keys ascend): one load, no search
@@ -632,7 +639,7 @@ __global__ void __launch_bounds__(256) k_roaring_chunk(const RoaringLeaf* __rest
         if (m && found < 0) found = b + 64 * q + (int)__ffsll((long long)m) - 1;
       }
     }
-    if (found >= 0) roaring_or_container(L.dir[rg.first + found], L.base, bm, 0u, limit, lane);
+    if (found >= 0) roaring_or_container(L.dir[rg.first + found], L.base, bm, 0u, limit, sub * 64 + lane, per * 64);
   }
   __syncthreads();
   const uint32_t nw = min(2048u, (uint32_t)L.padded_words - w0);
