@@ -280,7 +280,9 @@ int ph_ctx_destroy(ph_ctx* ctx);
  *   count_generic, lds_lean, part_lds, part_flush_first, part_serial: presence -- force the named alternative form
  *   lds_table_max, tile_words, group_reg_lg, interrupt_chunks, part_klo, part_batch_rows, part_depth, part_sets,
  *   part_wg_per_cu, part_slices, part_mm_blind, part_ring_log2: the value
- *   multi_host_merge   presence: a multi-device context merges by group value instead of dense partials */
+ *   multi_host_merge   presence: a multi-device context merges by group value instead of dense partials
+ *   sparse_c           2/4/8: the sparse kernels' register-direct leaf loads (2: every leaf's loads of a step in
+ *                      flight at once, leaves <= 8 bits only; 4 -- the default -- / 8: leaf by leaf, fewer registers) */
 #define PH_OPTION_UNSET INT64_MIN
 int ph_ctx_set_option(ph_ctx* ctx, const char* name, int64_t value);
 /* Launch on an external HIP stream (e.g. torch's current stream); NULL restores the context's own. */

@@ -39,7 +39,8 @@ const char* const kOptNames[OPT_COUNT] = {
     "part_mm_blind",
     "part_serial",
     "part_ring_log2",
-    "multi_host_merge"
+    "multi_host_merge",
+    "sparse_c"
 };
 
 void fail(int code, const std::string& msg) { throw Error{code, msg}; }

@@ -587,6 +587,7 @@ enum Opt : int {
   OPT_PART_SERIAL,
   OPT_PART_RING_LOG2,
   OPT_MULTI_HOST_MERGE,
+  OPT_SPARSE_C,
   OPT_COUNT
 };
 constexpr int64_t kOptUnset = INT64_MIN;

@@ -2402,6 +2402,18 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
   for (auto& d : dsegs)
     for (int k = 0; d.sp_reg && k < d.sp_nscan; ++k)
       kp.sparse_c = std::max(kp.sparse_c, d.cols[d.sp_slot[k]].bits > 16 ? 8 : d.cols[d.sp_slot[k]].bits > 8 ? 4 : 2);
+  // r6: the all-leaves-at-once form (C = 2, every leaf <= 8 bits) holds 185 VGPRs (2 waves per SIMD); leaf by leaf
+  // (C = 4, 139 VGPRs) measured 13.33 vs 13.89 ms of kernels on the scan-dimension SSB flight (Q2.1 1.02 vs 1.16), the
+  // same on Q1.x -- so it is the default; option sparse_c = 2 restores the wide form
+  if (kp.sparse_c == 2) kp.sparse_c = 4;
+  if (kp.sparse_c > 0 && ctx->has(OPT_SPARSE_C)) {
+    const int64_t c = ctx->opt(OPT_SPARSE_C);
+    bool narrow = true;  // the wide form needs every leaf <= 8 bits
+    for (auto& d : dsegs)
+      for (int k = 0; d.sp_reg && k < d.sp_nscan; ++k) narrow = narrow && d.cols[d.sp_slot[k]].bits <= 8;
+    if (c <= 2 && narrow) kp.sparse_c = 2;
+    else kp.sparse_c = std::max(kp.sparse_c, c >= 8 ? 8 : 4);
+  }
   // the register-direct COUNT (k_count_reg): every segment a dictId RANGE scan leaf, everything, or a sorted range
   if (mode == MODE_COUNT && !kp.late_prefetch && !ctx->has(OPT_COUNT_GENERIC)) {
     int fb = 1;

@@ -206,7 +206,8 @@ OPTION_NAMES = ("roaring_atomic", "agg_cont", "group_cont", "disable_partition",
                 "group_sparse", "agg_sparse", "tile_words", "limit_eager", "part_generic", "agg_generic",
                 "lds_generic", "count_generic", "lds_lean", "group_reg_lg", "stat_fuse", "interrupt_chunks",
                 "part_klo", "part_batch_rows", "part_flush_first", "part_depth", "part_lds", "part_sets",
-                "part_wg_per_cu", "part_slices", "part_mm_blind", "part_serial", "part_ring_log2", "multi_host_merge")
+                "part_wg_per_cu", "part_slices", "part_mm_blind", "part_serial", "part_ring_log2", "multi_host_merge",
+                "sparse_c")
 OPTION_UNSET = -(1 << 63)
 
 

@@ -4,7 +4,8 @@ SSB on dictionary-encoded dimensions).  The leaves are decoded 32 docs per lane 
 only the matched docs' keys and values are gathered; results and every statistic (numEntriesScannedInFilter
 included) against the oracle.  Covered: range / IN / NOT IN leaves, sets staged in LDS (<= 8192 ids) and read from HBM
 (larger), leaf columns over 16 bits (32-byte lane loads), 2-operand value terms, segments that end mid-step, and the
-plan picked by the selectivity estimate as well as forced (PH_GROUP_SPARSE / PH_AGG_SPARSE)."""
+plan picked by the selectivity estimate as well as forced (PH_GROUP_SPARSE / PH_AGG_SPARSE), in the default leaf-by-leaf
+load form and the all-leaves-at-once one (PH_SPARSE_C=2, leaves <= 8 bits)."""
 import numpy as np
 import pytest
 
@@ -42,11 +43,13 @@ WHERES = [
 ]
 
 
-@pytest.mark.parametrize("force", [False, True])
+@pytest.mark.parametrize("force", [False, True, "wide"])
 @pytest.mark.parametrize("where", WHERES)
 def test_conj_sparse_group_by(ctx, monkeypatch, where, force):  # noqa: F811
     if force:
         monkeypatch.setenv("PH_GROUP_SPARSE", "1")
+    if force == "wide":
+        monkeypatch.setenv("PH_SPARSE_C", "2")
     rng = np.random.default_rng(seed_of("conj-g" + where))
     tables = [_table(rng, n) for n in SIZES]
     for group in ("g1", "g1, g2", "y, g2"):
@@ -58,11 +61,13 @@ def test_conj_sparse_group_by(ctx, monkeypatch, where, force):  # noqa: F811
                            f"WHERE {where} GROUP BY {group} ORDER BY {group} LIMIT 100000")
 
 
-@pytest.mark.parametrize("force", [False, True])
+@pytest.mark.parametrize("force", [False, True, "wide"])
 @pytest.mark.parametrize("where", WHERES)
 def test_conj_sparse_aggregation(ctx, monkeypatch, where, force):  # noqa: F811
     if force:
         monkeypatch.setenv("PH_AGG_SPARSE", "1")
+    if force == "wide":
+        monkeypatch.setenv("PH_SPARSE_C", "2")
     rng = np.random.default_rng(seed_of("conj-a" + where))
     tables = [_table(rng, n) for n in SIZES]
     for sel in ("SUM(m * p)", "SUM(m - p)", "SUM(m), MIN(m), MAX(m)", "SUM(d), MIN(d), MAX(d)", "SUM(m + d)"):
