@@ -13,27 +13,23 @@
 
 namespace ph {
 
-// the workgroup's chunk tables composed in a tree (LDS), thread 0 storing the workgroup's table
+// the workgroup's chunk tables composed in order, thread 0 storing the workgroup's table: a butterfly of shuffles
+// inside each wave (r6; r5 ran all 7 levels through LDS with a barrier each), then thread 0 over the waves' tables
 template <int K, int BLOCK>
 __device__ __forceinline__ void dfa_group_compose(const AndWalkJob& J, int64_t g, uint32_t (&d)[K + 1],
                                                   uint8_t (&x)[K + 1], unsigned char* smem) {
-  uint32_t* td = reinterpret_cast<uint32_t*>(smem);                              // [BLOCK][K + 1]
-  uint8_t* tx = reinterpret_cast<uint8_t*>(smem + (size_t)BLOCK * (K + 1) * 4);  // [BLOCK][K + 1]
-  for (int s = 1; s < BLOCK; s <<= 1) {
+  constexpr int NW = BLOCK / 64;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    uint32_t bd[K + 1];
+    uint8_t bx[K + 1];
 #pragma unroll
     for (int e = 0; e <= K; ++e) {
-      td[threadIdx.x * (K + 1) + e] = d[e];
-      tx[threadIdx.x * (K + 1) + e] = x[e];
+      bd[e] = (uint32_t)__shfl_down((int)d[e], s, 64);
+      bx[e] = (uint8_t)__shfl_down((int)x[e], s, 64);
     }
-    __syncthreads();
-    if ((threadIdx.x & (2 * s - 1)) == 0) {
-      uint32_t bd[K + 1];
-      uint8_t bx[K + 1];
-#pragma unroll
-      for (int e = 0; e <= K; ++e) {
-        bd[e] = td[(threadIdx.x + s) * (K + 1) + e];
-        bx[e] = tx[(threadIdx.x + s) * (K + 1) + e];
-      }
+    if ((lane & (2 * s - 1)) == 0) {  // lane + s < 64: the next run of lanes, in chunk order
       uint32_t od[K + 1];
       uint8_t ox[K + 1];
       dfa_compose<K>(K, d, x, bd, bx, od, ox);
@@ -43,13 +39,37 @@ __device__ __forceinline__ void dfa_group_compose(const AndWalkJob& J, int64_t g
         x[e] = ox[e];
       }
     }
-    __syncthreads();
   }
-  if (threadIdx.x == 0)
+  uint32_t* td = reinterpret_cast<uint32_t*>(smem);                           // [NW][K + 1]
+  uint8_t* tx = reinterpret_cast<uint8_t*>(smem + (size_t)NW * (K + 1) * 4);  // [NW][K + 1]
+  if (lane == 0)
+#pragma unroll
+    for (int e = 0; e <= K; ++e) {
+      td[wave * (K + 1) + e] = d[e];
+      tx[wave * (K + 1) + e] = x[e];
+    }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < NW; ++w) {
+      uint32_t bd[K + 1], od[K + 1];
+      uint8_t bx[K + 1], ox[K + 1];
+#pragma unroll
+      for (int e = 0; e <= K; ++e) {
+        bd[e] = td[w * (K + 1) + e];
+        bx[e] = tx[w * (K + 1) + e];
+      }
+      dfa_compose<K>(K, d, x, bd, bx, od, ox);
+#pragma unroll
+      for (int e = 0; e <= K; ++e) {
+        d[e] = od[e];
+        x[e] = ox[e];
+      }
+    }
     for (int e = 0; e <= J.k; ++e) {
       J.gdelta[(int64_t)e * J.ngroups + g] = d[e];
       J.gexit[(int64_t)e * J.ngroups + g] = x[e];
     }
+  }
 }
 
 template <int K, int BLOCK, int CW>
