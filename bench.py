@@ -348,7 +348,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=None, help="table rows (sharded across the GPUs); default 1e9, "
                                                            "config1 1e7")
     ap.add_argument("--segment-rows", type=int, default=None, help="default 1e7")
