@@ -2671,17 +2671,20 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     DevSegment* d_segs = scratch.alloc<DevSegment>(dsegs.size());
     DevSegment* d_segs_opt = dsegs_opt.empty() ? nullptr : scratch.alloc<DevSegment>(dsegs_opt.size());
     FilterInsn* d_prog = scratch.alloc<FilterInsn>(std::max<size_t>(1, all_insns.size()));
-    std::vector<Chunk> all_chunks = chunks;  // + the numGroupsLimit pass's chunks (limit segments only)
+    // the chunks + the numGroupsLimit pass's chunks (limit segments only; without them the list uploads as built)
+    std::vector<Chunk> limit_chunks;
     for (int k : limit_segs)
-      all_chunks.insert(all_chunks.end(), chunks.begin() + dseg_chunks[k].first, chunks.begin() + dseg_chunks[k].second);
-    const size_t n_limit_chunks = all_chunks.size() - chunks.size();
-    Chunk* d_chunks = scratch.alloc<Chunk>(all_chunks.size());
+      limit_chunks.insert(limit_chunks.end(), chunks.begin() + dseg_chunks[k].first, chunks.begin() + dseg_chunks[k].second);
+    const size_t n_limit_chunks = limit_chunks.size();
+    const size_t n_all_chunks = chunks.size() + n_limit_chunks;
+    Chunk* d_chunks = scratch.alloc<Chunk>(n_all_chunks);
     const size_t b1 = sizeof(DevSegment) * dsegs.size(), b2 = sizeof(FilterInsn) * all_insns.size(),
-                 b3 = sizeof(Chunk) * all_chunks.size(), b4 = sizeof(DevSegment) * dsegs_opt.size();
+                 b3 = sizeof(Chunk) * n_all_chunks, b4 = sizeof(DevSegment) * dsegs_opt.size();
     uint8_t* stage = static_cast<uint8_t*>(lane.lane->host_staging(b1 + b2 + b3 + b4));
     memcpy(stage, dsegs.data(), b1);
     memcpy(stage + b1, all_insns.data(), b2);
-    memcpy(stage + b1 + b2, all_chunks.data(), b3);
+    if (!chunks.empty()) memcpy(stage + b1 + b2, chunks.data(), sizeof(Chunk) * chunks.size());
+    if (n_limit_chunks) memcpy(stage + b1 + b2 + sizeof(Chunk) * chunks.size(), limit_chunks.data(), sizeof(Chunk) * n_limit_chunks);
     if (b4) memcpy(stage + b1 + b2 + b3, dsegs_opt.data(), b4);
     PH_HIP_CHECK(hipMemcpyAsync(d_segs, stage, b1, hipMemcpyHostToDevice, st));
     if (b2) PH_HIP_CHECK(hipMemcpyAsync(d_prog, stage + b1, b2, hipMemcpyHostToDevice, st));

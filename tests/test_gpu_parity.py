@@ -692,3 +692,17 @@ def test_conj_set_leaf_merged_from_equalities(ctx, where):
     tables = [{"a": (rng.integers(0, 40, n).astype(np.int32), "INT"), "b": (rng.integers(0, 30, n).astype(np.int32), "INT"),
                "m": (rng.integers(-100, 1000, n).astype(np.int32), "INT")} for n in (200_000, 77_777)]
     _both(ctx, tables, f"SELECT a, b, COUNT(*), SUM(m) FROM t WHERE {where} GROUP BY a, b ORDER BY a, b LIMIT 1000")
+
+
+@pytest.mark.parametrize("inverted", [(), ("c",)])
+def test_in_lists_with_repeats_and_absent_values(ctx, inverted):
+    # InPredicateEvaluatorFactory: the literals' dictIds as a set -- repeated literals and literals outside the
+    # dictionary change nothing; NOT IN of every value is alwaysFalse, IN of every value alwaysTrue
+    rng = np.random.default_rng(seed_of("in-repeats"))
+    cols = [{"c": (rng.integers(0, 6, n).astype(np.int32), "INT"), "g": (rng.integers(0, 9, n).astype(np.int32), "INT"),
+             "m": (rng.integers(-100, 100, n).astype(np.int32), "INT")} for n in (3000, 1777)]
+    for where in ("c IN (3, 3, 1, 3, 99)", "c NOT IN (2, 2, -7, 5)", "c IN (0, 1, 2, 3, 4, 5, 5)",
+                  "c NOT IN (0, 1, 2, 3, 4, 5)", "c IN (4, 4) AND g IN (1, 8, 8, 1)", "c IN (77, 78)"):
+        _both(ctx, cols, f"SELECT g, COUNT(*), SUM(m) FROM t WHERE {where} GROUP BY g ORDER BY g LIMIT 100",
+              inverted=inverted)
+        _both(ctx, cols, f"SELECT COUNT(*), MIN(m), MAX(m) FROM t WHERE {where}", inverted=inverted)
