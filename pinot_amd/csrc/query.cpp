@@ -3487,10 +3487,18 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
     res->num_groups = R;
     res->ctx = ctx;
     res->aggs.resize(nagg);
+    // the columns' copies alternate between the two streams of the lane (two copy queues over PCIe) unless the fused
+    // statistic walk still runs on the second one
+    const bool two = !fused_blk;
+    bool used_b = false;
+    int cix = 0;
     auto take = [&](ResultBuf& b, const void* dsrc, size_t bytes) {
       b.pinned = ctx->pinned_acquire(bytes, &b.cap);
       b.n = bytes;
-      if (bytes) PH_HIP_CHECK(hipMemcpyAsync(b.pinned, dsrc, bytes, hipMemcpyDeviceToHost, st));
+      if (!bytes) return;
+      const bool on_b = two && (cix++ & 1);
+      used_b |= on_b;
+      PH_HIP_CHECK(hipMemcpyAsync(b.pinned, dsrc, bytes, hipMemcpyDeviceToHost, on_b ? lane.lane->stream_b : st));
     };
     for (int k = 0; k < nagg; ++k) {
       if (cp.agg_kind[k] == CK_COUNT) take(res->aggs[k], cp.count_out, 8 * (size_t)R);
@@ -3525,6 +3533,7 @@ ph_result* query_execute_impl(Context* ctx, const ph_query* q, ph_segment* const
       }
     }
     PH_HIP_CHECK(hipStreamSynchronize(st));
+    if (used_b) PH_HIP_CHECK(hipStreamSynchronize(lane.lane->stream_b));
     // a finalised key shard has no scan: its matched docs are the sum of its group counts (k_compact_count)
     if (fin) stats.num_docs_scanned = docs;
     for (int k = 0; k < nagg; ++k) {
